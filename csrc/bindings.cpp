@@ -1,0 +1,427 @@
+// Python bindings of the gfx950 kernel library (module `_C` of the framework package).
+//
+// Thin, checked wrappers: validate device/dtype/shape/alignment, allocate outputs, launch on the
+// current HIP stream. The kernels themselves live in csrc/kernels/*.hip and are built with
+// hipcc --offload-arch=gfx950; this translation unit is host-only C++ against libtorch.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+
+#include <string>
+#include <vector>
+
+#include "host/tokenizer.h"
+#include "host/ivf_host.h"
+
+extern "C" {
+int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
+               long, int, int, int, int, int, hipStream_t);
+int rt_norm_fwd(int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
+                hipStream_t);
+int rt_norm_bwd(int, const void*, const void*, const void*, const float*, const float*, const void*, void*, float*,
+                float*, int, int, hipStream_t);
+int rt_rope_qkv(void*, long, const int*, const float*, const float*, int, int, int, int, int, float, void*, void*,
+                const int*, int, int, hipStream_t);
+int rt_swiglu_fwd(const void*, void*, long, int, hipStream_t);
+int rt_swiglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
+int rt_embed(const void*, const long*, const void*, const long*, void*, long, int, hipStream_t);
+int rt_attn_fwd(const void*, long, const void*, long, const void*, long, void*, long, float*, const int*, const int*,
+                const float*, int, int, int, int, int, int, int, int, int, float, hipStream_t);
+int rt_attn_decode(const void*, long, const void*, const void*, int, const int*, const int*, int, float*, int, int,
+                   void*, long, int, int, int, int, float, hipStream_t);
+int rt_attn_bwd(const void*, long, const void*, long, const void*, long, const void*, long, const void*, long,
+                const float*, float*, float*, void*, long, void*, long, void*, long, const int*, int, int, int, int,
+                int, int, int, float, hipStream_t);
+int rt_logprob_fwd(const void*, int, long, const long*, float, long, int, float*, float*, float*, float*, hipStream_t);
+int rt_logprob_bwd(const void*, int, long, const long*, float, long, int, const float*, const float*, const float*,
+                   const float*, void*, long, hipStream_t);
+int rt_sample(const void*, int, long, long, int, float, int, float, int, uint64_t, const int64_t*, const uint8_t*, long*,
+              float*, hipStream_t);
+int rt_grad_sumsq(const float*, long, float*, int, hipStream_t);
+int rt_adamw(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, float, float,
+             const float*, int, float*, int*, hipStream_t);
+int rt_pool_norm(const void*, const int*, int, int, int, int, float*, hipStream_t);
+int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*, hipStream_t);
+int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const void*, const long*, int, float*, long*,
+                hipStream_t);
+int rt_gae(const float*, const float*, const float*, int, int, float, float, float*, float*, hipStream_t);
+int rt_decode_update(const long*, long*, int, float*, const float*, float*, const float*, uint8_t*, int*, int*, long*,
+                     int*, int64_t*, int64_t*, int, const long*, int, long, hipStream_t);
+}
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " launch failed (code ", rc, ")");
+}
+
+#define CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+#define CHECK_I64(t) TORCH_CHECK((t).scalar_type() == at::kLong, #t " must be int64")
+#define CHECK_ROWS(t) TORCH_CHECK((t).dim() == 2 && (t).stride(1) == 1, #t " must be 2-D with unit column stride")
+#define CHECK_ALIGN16(t)                                                                             \
+  TORCH_CHECK(reinterpret_cast<uintptr_t>((t).data_ptr()) % 16 == 0, #t " must be 16-byte aligned")
+
+const void* opt_ptr(const optional<Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
+
+// ---------------------------------------------------------------------------------------------
+Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const optional<Tensor>& ub,
+            const optional<Tensor>& bias, int64_t act, bool out_f32, optional<Tensor> out) {
+  CHECK_CUDA(a); CHECK_CUDA(w); CHECK_BF16(a); CHECK_BF16(w); CHECK_ROWS(a); CHECK_ROWS(w);
+  CHECK_ALIGN16(a); CHECK_ALIGN16(w);
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm: K mismatch ", w.size(1), " vs ", K);
+  TORCH_CHECK(K % 64 == 0, "gemm: K must be a multiple of 64, got ", K);
+  TORCH_CHECK(N % 8 == 0, "gemm: N must be a multiple of 8, got ", N);
+  TORCH_CHECK(a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm: row strides must be multiples of 8");
+  int Rp = 0;
+  if (u.has_value() && u->defined()) {
+    TORCH_CHECK(ub.has_value() && ub->defined(), "gemm: LoRA U given without UB");
+    CHECK_BF16(*u); CHECK_BF16(*ub); CHECK_ROWS(*u); CHECK_ROWS(*ub); CHECK_ALIGN16(*u); CHECK_ALIGN16(*ub);
+    TORCH_CHECK(u->size(0) == M && ub->size(0) == N && u->size(1) == ub->size(1), "gemm: LoRA shape mismatch");
+    Rp = (int)u->size(1);
+    TORCH_CHECK(Rp % 64 == 0, "gemm: LoRA rank must be padded to a multiple of 64");
+    TORCH_CHECK(u->stride(0) % 8 == 0 && ub->stride(0) % 8 == 0, "gemm: LoRA row strides must be multiples of 8");
+  }
+  if (bias.has_value() && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N && bias->is_contiguous()); }
+  Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1, "gemm: bad out shape");
+    TORCH_CHECK(c.scalar_type() == (out_f32 ? at::kFloat : at::kBFloat16), "gemm: bad out dtype");
+    TORCH_CHECK(c.stride(0) % 8 == 0, "gemm: out row stride must be a multiple of 8");
+    CHECK_ALIGN16(c);
+  } else {
+    c = at::empty({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  }
+  if (M == 0) return c;
+  check_rc(rt_gemm_nt(a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), opt_ptr(u), Rp ? u->stride(0) : 0,
+                      opt_ptr(ub), Rp ? ub->stride(0) : 0, Rp, opt_ptr(bias), c.data_ptr(), c.stride(0), (int)M,
+                      (int)N, (int)K, (int)act, out_f32 ? 1 : 0, cur_stream()),
+           "gemm");
+  return c;
+}
+
+// ---------------------------------------------------------------------------------------------
+std::vector<Tensor> norm_fwd(bool layernorm, const Tensor& x, const optional<Tensor>& res, const Tensor& w,
+                             const optional<Tensor>& b, double eps) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w);
+  TORCH_CHECK(x.is_contiguous(), "norm: x must be contiguous");
+  const int64_t H = x.size(-1), T = x.numel() / H;
+  auto y = at::empty_like(x);
+  Tensor h;
+  if (res.has_value() && res->defined()) {
+    CHECK_BF16(*res);
+    TORCH_CHECK(res->is_contiguous() && res->numel() == x.numel(), "norm: residual shape");
+    h = at::empty_like(x);
+  }
+  auto rstd = at::empty({T}, x.options().dtype(at::kFloat));
+  Tensor mean = layernorm ? at::empty({T}, x.options().dtype(at::kFloat)) : Tensor();
+  check_rc(rt_norm_fwd(layernorm, x.data_ptr(), opt_ptr(res), w.data_ptr(), opt_ptr(b), y.data_ptr(),
+                       h.defined() ? h.data_ptr() : nullptr, rstd.data_ptr<float>(),
+                       layernorm ? mean.data_ptr<float>() : nullptr, (int)T, (int)H, (float)eps, cur_stream()),
+           "norm_fwd");
+  return {y, h, rstd, mean};
+}
+
+std::vector<Tensor> norm_bwd(bool layernorm, const Tensor& dy, const Tensor& h, const Tensor& w, const Tensor& rstd,
+                             const optional<Tensor>& mean, const optional<Tensor>& dh_res, bool need_dw, bool need_db) {
+  CHECK_CUDA(dy); CHECK_BF16(dy); CHECK_BF16(h);
+  TORCH_CHECK(dy.is_contiguous() && h.is_contiguous(), "norm_bwd: contiguous inputs required");
+  const int64_t H = dy.size(-1), T = dy.numel() / H;
+  auto dh = at::empty_like(dy);
+  Tensor dw = need_dw ? at::zeros({H}, dy.options().dtype(at::kFloat)) : Tensor();
+  Tensor db = need_db ? at::zeros({H}, dy.options().dtype(at::kFloat)) : Tensor();
+  if (dh_res.has_value() && dh_res->defined()) {
+    CHECK_BF16(*dh_res);
+    TORCH_CHECK(dh_res->is_contiguous(), "norm_bwd: dh_res contiguous");
+  }
+  check_rc(rt_norm_bwd(layernorm, dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(),
+                       layernorm ? (const float*)mean->data_ptr() : nullptr, opt_ptr(dh_res), dh.data_ptr(),
+                       need_dw ? dw.data_ptr<float>() : nullptr, need_db ? db.data_ptr<float>() : nullptr, (int)T,
+                       (int)H, cur_stream()),
+           "norm_bwd");
+  return {dh, dw, db};
+}
+
+// ---------------------------------------------------------------------------------------------
+void rope_qkv(Tensor qkv, const Tensor& pos, const optional<Tensor>& cos, const optional<Tensor>& sin, int64_t S,
+              int64_t Hq, int64_t Hkv, int64_t D, double sign, const optional<Tensor>& kc, const optional<Tensor>& vc,
+              const optional<Tensor>& slot_base, bool rope_q) {
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_ROWS(qkv); CHECK_I32(pos);
+  TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * D, "rope: qkv too narrow");
+  int Smax = 0;
+  if (kc.has_value() && kc->defined()) {
+    CHECK_BF16(*kc); CHECK_BF16(*vc);
+    TORCH_CHECK(kc->dim() == 4 && kc->size(1) == Hkv && kc->size(3) == D && kc->is_contiguous(), "rope: cache layout");
+    Smax = (int)kc->size(2);
+  }
+  if (cos.has_value() && cos->defined()) { CHECK_F32(*cos); CHECK_F32(*sin); }
+  if (slot_base.has_value() && slot_base->defined()) CHECK_I32(*slot_base);
+  check_rc(rt_rope_qkv(qkv.data_ptr(), qkv.stride(0), pos.data_ptr<int>(),
+                       (const float*)opt_ptr(cos), (const float*)opt_ptr(sin), (int)qkv.size(0), (int)S, (int)Hq,
+                       (int)Hkv, (int)D, (float)sign, (void*)opt_ptr(kc), (void*)opt_ptr(vc),
+                       (const int*)opt_ptr(slot_base), Smax, rope_q ? 1 : 0, cur_stream()),
+           "rope_qkv");
+}
+
+Tensor swiglu_fwd(const Tensor& gu) {
+  CHECK_CUDA(gu); CHECK_BF16(gu); TORCH_CHECK(gu.is_contiguous());
+  const int64_t F2 = gu.size(-1), T = gu.numel() / F2;
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F2 / 2;
+  auto y = at::empty(sizes, gu.options());
+  check_rc(rt_swiglu_fwd(gu.data_ptr(), y.data_ptr(), T, (int)(F2 / 2), cur_stream()), "swiglu_fwd");
+  return y;
+}
+
+Tensor swiglu_bwd(const Tensor& gu, const Tensor& dy) {
+  CHECK_CUDA(gu); CHECK_BF16(gu); CHECK_BF16(dy); TORCH_CHECK(gu.is_contiguous() && dy.is_contiguous());
+  const int64_t F2 = gu.size(-1), T = gu.numel() / F2;
+  auto dgu = at::empty_like(gu);
+  check_rc(rt_swiglu_bwd(gu.data_ptr(), dy.data_ptr(), dgu.data_ptr(), T, (int)(F2 / 2), cur_stream()), "swiglu_bwd");
+  return dgu;
+}
+
+Tensor embed(const Tensor& table, const Tensor& ids, const optional<Tensor>& ptable, const optional<Tensor>& pids) {
+  CHECK_CUDA(table); CHECK_BF16(table); CHECK_I64(ids); TORCH_CHECK(table.is_contiguous() && ids.is_contiguous());
+  const int64_t H = table.size(1), T = ids.numel();
+  auto sizes = ids.sizes().vec();
+  sizes.push_back(H);
+  auto out = at::empty(sizes, table.options());
+  check_rc(rt_embed(table.data_ptr(), ids.data_ptr<int64_t>() ? (const long*)ids.data_ptr() : nullptr, opt_ptr(ptable),
+                    (const long*)opt_ptr(pids), out.data_ptr(), T, (int)H, cur_stream()),
+           "embed");
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------
+std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, int64_t B, int64_t Sq, int64_t Sk,
+                             int64_t Hq, int64_t Hkv, int64_t D, bool causal, int64_t window, double scale,
+                             const optional<Tensor>& kv_start, const optional<Tensor>& kv_len,
+                             const optional<Tensor>& rel_bias, int64_t rb_L, bool need_lse) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_BF16(k); CHECK_BF16(v); CHECK_ROWS(q); CHECK_ROWS(k); CHECK_ROWS(v);
+  TORCH_CHECK(q.size(0) == B * Sq && k.size(0) == B * Sk && v.size(0) == B * Sk, "attn_fwd: row counts");
+  TORCH_CHECK(Hq % Hkv == 0, "attn_fwd: Hq % Hkv");
+  TORCH_CHECK(q.stride(0) % 8 == 0 && k.stride(0) % 8 == 0 && v.stride(0) % 8 == 0, "attn_fwd: strides % 8");
+  auto o = at::empty({B * Sq, Hq * D}, q.options());
+  Tensor lse = need_lse ? at::empty({B, Hq, Sq}, q.options().dtype(at::kFloat)) : Tensor();
+  if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
+  if (kv_len.has_value() && kv_len->defined()) CHECK_I32(*kv_len);
+  if (rel_bias.has_value() && rel_bias->defined()) {
+    CHECK_F32(*rel_bias);
+    TORCH_CHECK(rel_bias->size(0) == Hq && rel_bias->size(1) == 2 * rb_L - 1 && rb_L >= std::max(Sq, Sk));
+  }
+  check_rc(rt_attn_fwd(q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0), o.data_ptr(),
+                       o.stride(0), need_lse ? lse.data_ptr<float>() : nullptr, (const int*)opt_ptr(kv_start),
+                       (const int*)opt_ptr(kv_len), (const float*)opt_ptr(rel_bias), (int)rb_L, (int)B, (int)Sq,
+                       (int)Sk, (int)Hq, (int)Hkv, (int)D, causal ? 1 : 0, (int)window, (float)scale, cur_stream()),
+           "attn_fwd");
+  return {o, lse};
+}
+
+void attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, const Tensor& kv_len,
+                 const optional<Tensor>& kv_start, int64_t window, double scale, int64_t Hq, Tensor part, int64_t PS,
+                 Tensor out) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_ROWS(q); CHECK_BF16(kc); CHECK_BF16(vc); CHECK_I32(kv_len); CHECK_F32(part);
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous(), "attn_decode: cache layout");
+  const int64_t B = kc.size(0), Hkv = kc.size(1), Smax = kc.size(2), D = kc.size(3);
+  const int64_t NP = (Smax + PS - 1) / PS, G = Hq / Hkv;
+  TORCH_CHECK(part.numel() >= B * Hkv * NP * G * (D + 2), "attn_decode: partial workspace too small");
+  TORCH_CHECK(q.size(0) == B && out.size(0) == B, "attn_decode: batch");
+  if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
+  check_rc(rt_attn_decode(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(), (int)Smax, kv_len.data_ptr<int>(),
+                          (const int*)opt_ptr(kv_start), (int)window, part.data_ptr<float>(), (int)NP, (int)PS,
+                          out.data_ptr(), out.stride(0), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
+                          cur_stream()),
+           "attn_decode");
+}
+
+void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout, const Tensor& lse,
+              Tensor dq, Tensor dk, Tensor dv, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D, bool causal,
+              int64_t window, double scale, const optional<Tensor>& kv_start) {
+  CHECK_CUDA(q); CHECK_ROWS(q); CHECK_ROWS(k); CHECK_ROWS(v); CHECK_ROWS(o); CHECK_ROWS(dout);
+  CHECK_ROWS(dq); CHECK_ROWS(dk); CHECK_ROWS(dv); CHECK_F32(lse);
+  auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
+  auto dq32 = at::empty({B * S, Hq * D}, q.options().dtype(at::kFloat));
+  if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
+  check_rc(rt_attn_bwd(q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0), o.data_ptr(),
+                       o.stride(0), dout.data_ptr(), dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                       dq32.data_ptr<float>(), dq.data_ptr(), dq.stride(0), dk.data_ptr(), dk.stride(0),
+                       dv.data_ptr(), dv.stride(0), (const int*)opt_ptr(kv_start), (int)B, (int)S, (int)Hq, (int)Hkv,
+                       (int)D, causal ? 1 : 0, (int)window, (float)scale, cur_stream()),
+           "attn_bwd");
+}
+
+// ---------------------------------------------------------------------------------------------
+std::vector<Tensor> logprob_fwd(const Tensor& logits, const optional<Tensor>& targets, double inv_temp, bool need_ent) {
+  CHECK_CUDA(logits); CHECK_ROWS(logits); CHECK_ALIGN16(logits);
+  const bool f32 = logits.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || logits.scalar_type() == at::kBFloat16, "logprob: logits must be bf16 or f32");
+  TORCH_CHECK((logits.stride(0) * logits.element_size()) % 16 == 0, "logprob: row stride must be 16-B aligned");
+  const int64_t T = logits.size(0), V = logits.size(1);
+  auto opts = logits.options().dtype(at::kFloat);
+  auto logp = at::empty({T}, opts), lse = at::empty({T}, opts), ex = at::empty({T}, opts);
+  Tensor ent = need_ent ? at::empty({T}, opts) : Tensor();
+  if (targets.has_value() && targets->defined()) { CHECK_I64(*targets); TORCH_CHECK(targets->numel() == T); }
+  check_rc(rt_logprob_fwd(logits.data_ptr(), f32, logits.stride(0), (const long*)opt_ptr(targets), (float)inv_temp, T,
+                          (int)V, logp.data_ptr<float>(), need_ent ? ent.data_ptr<float>() : nullptr,
+                          lse.data_ptr<float>(), ex.data_ptr<float>(), cur_stream()),
+           "logprob_fwd");
+  return {logp, ent, lse, ex};
+}
+
+Tensor logprob_bwd(const Tensor& logits, const optional<Tensor>& targets, double inv_temp, const Tensor& lse,
+                   const Tensor& ex, const optional<Tensor>& g_logp, const optional<Tensor>& g_ent) {
+  CHECK_CUDA(logits); CHECK_ROWS(logits);
+  const bool f32 = logits.scalar_type() == at::kFloat;
+  const int64_t T = logits.size(0), V = logits.size(1);
+  auto d = at::empty({T, V}, logits.options().dtype(at::kBFloat16));
+  check_rc(rt_logprob_bwd(logits.data_ptr(), f32, logits.stride(0), (const long*)opt_ptr(targets), (float)inv_temp, T,
+                          (int)V, lse.data_ptr<float>(), ex.data_ptr<float>(), (const float*)opt_ptr(g_logp),
+                          (const float*)opt_ptr(g_ent), d.data_ptr(), d.stride(0), cur_stream()),
+           "logprob_bwd");
+  return d;
+}
+
+void sample(const Tensor& logits, double inv_temp, int64_t top_k, double top_p, bool greedy, int64_t seed,
+            const optional<Tensor>& offset, const optional<Tensor>& active, Tensor out_tok,
+            const optional<Tensor>& out_logp) {
+  CHECK_CUDA(logits); CHECK_ROWS(logits); CHECK_I64(out_tok);
+  const bool f32 = logits.scalar_type() == at::kFloat;
+  if (offset.has_value() && offset->defined()) CHECK_I64(*offset);
+  check_rc(rt_sample(logits.data_ptr(), f32, logits.stride(0), logits.size(0), (int)logits.size(1), (float)inv_temp,
+                     (int)top_k, (float)top_p, greedy ? 1 : 0, (uint64_t)seed, (const int64_t*)opt_ptr(offset),
+                     (const uint8_t*)opt_ptr(active), (long*)out_tok.data_ptr(), (float*)opt_ptr(out_logp),
+                     cur_stream()),
+           "sample");
+}
+
+// ---------------------------------------------------------------------------------------------
+void adamw(Tensor p, const Tensor& g, Tensor m, Tensor v, const optional<Tensor>& pbf, double lr, double b1, double b2,
+           double eps, double wd, int64_t step, double max_norm, Tensor partials, Tensor norm_out, Tensor skipped) {
+  CHECK_CUDA(p); CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(partials);
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous());
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adamw: sizes");
+  if (pbf.has_value() && pbf->defined()) { CHECK_BF16(*pbf); TORCH_CHECK(pbf->numel() == n); }
+  const int nparts = (int)partials.numel();
+  const float bc1 = 1.f - (float)std::pow(b1, (double)step), bc2 = 1.f - (float)std::pow(b2, (double)step);
+  check_rc(rt_grad_sumsq(g.data_ptr<float>(), n, partials.data_ptr<float>(), nparts, cur_stream()), "grad_sumsq");
+  check_rc(rt_adamw(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                    (void*)opt_ptr(pbf), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, bc1, bc2,
+                    (float)max_norm, partials.data_ptr<float>(), nparts, norm_out.data_ptr<float>(),
+                    skipped.data_ptr<int>(), cur_stream()),
+           "adamw");
+}
+
+Tensor grad_norm(const Tensor& g, Tensor partials) {
+  CHECK_CUDA(g); CHECK_F32(g);
+  check_rc(rt_grad_sumsq(g.data_ptr<float>(), g.numel(), partials.data_ptr<float>(), (int)partials.numel(),
+                         cur_stream()),
+           "grad_sumsq");
+  return partials.sum().sqrt();
+}
+
+// ---------------------------------------------------------------------------------------------
+Tensor pool_norm(const Tensor& x, const optional<Tensor>& lengths, bool normalize) {
+  CHECK_CUDA(x); CHECK_BF16(x); TORCH_CHECK(x.dim() == 3 && x.is_contiguous());
+  const int64_t B = x.size(0), S = x.size(1), H = x.size(2);
+  auto out = at::empty({B, H}, x.options().dtype(at::kFloat));
+  if (lengths.has_value() && lengths->defined()) CHECK_I32(*lengths);
+  check_rc(rt_pool_norm(x.data_ptr(), (const int*)opt_ptr(lengths), (int)B, (int)S, (int)H, normalize ? 1 : 0,
+                        out.data_ptr<float>(), cur_stream()),
+           "pool_norm");
+  return out;
+}
+
+std::vector<Tensor> topk(const Tensor& scores, int64_t k, const optional<Tensor>& idmap) {
+  CHECK_CUDA(scores); CHECK_F32(scores); CHECK_ROWS(scores);
+  const int64_t nq = scores.size(0), N = scores.size(1);
+  auto vals = at::empty({nq, k}, scores.options());
+  auto ids = at::empty({nq, k}, scores.options().dtype(at::kLong));
+  if (idmap.has_value() && idmap->defined()) { CHECK_I64(*idmap); CHECK_ROWS(*idmap); }
+  check_rc(rt_topk(scores.data_ptr<float>(), scores.stride(0), nq, (int)N, (int)k, (const long*)opt_ptr(idmap),
+                   idmap.has_value() && idmap->defined() ? idmap->stride(0) : 0, vals.data_ptr<float>(),
+                   (long*)ids.data_ptr(), cur_stream()),
+           "topk");
+  return {vals, ids};
+}
+
+std::vector<Tensor> ivf_scan(const Tensor& q, const Tensor& probes, const Tensor& offsets, const Tensor& vecs,
+                             const Tensor& ids, int64_t maxlen) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_I32(probes); CHECK_I32(offsets); CHECK_BF16(vecs); CHECK_I64(ids);
+  TORCH_CHECK(q.is_contiguous() && probes.is_contiguous() && vecs.is_contiguous());
+  const int64_t nq = q.size(0), d = q.size(1), nprobe = probes.size(1);
+  auto cand = at::empty({nq, nprobe * maxlen}, q.options().dtype(at::kFloat));
+  auto cid = at::empty({nq, nprobe * maxlen}, q.options().dtype(at::kLong));
+  check_rc(rt_ivf_scan(q.data_ptr(), (int)nq, (int)d, probes.data_ptr<int>(), (int)nprobe, offsets.data_ptr<int>(),
+                       vecs.data_ptr(), (const long*)ids.data_ptr(), (int)maxlen, cand.data_ptr<float>(),
+                       (long*)cid.data_ptr(), cur_stream()),
+           "ivf_scan");
+  return {cand, cid};
+}
+
+std::vector<Tensor> gae(const Tensor& rewards, const Tensor& values, const Tensor& mask, double gamma, double lam) {
+  CHECK_CUDA(rewards); CHECK_F32(rewards); CHECK_F32(values); CHECK_F32(mask);
+  TORCH_CHECK(rewards.is_contiguous() && values.is_contiguous() && mask.is_contiguous() && rewards.dim() == 2);
+  auto adv = at::empty_like(rewards), ret = at::empty_like(rewards);
+  check_rc(rt_gae(rewards.data_ptr<float>(), values.data_ptr<float>(), mask.data_ptr<float>(), (int)rewards.size(0),
+                  (int)rewards.size(1), (float)gamma, (float)lam, adv.data_ptr<float>(), ret.data_ptr<float>(),
+                  cur_stream()),
+           "gae");
+  return {adv, ret};
+}
+
+void decode_update(const Tensor& tok, Tensor out_tokens, const optional<Tensor>& out_logp,
+                   const optional<Tensor>& logp, const optional<Tensor>& out_values, const optional<Tensor>& values,
+                   Tensor active, Tensor kv_len, Tensor pos, Tensor next_input, Tensor gen_len, Tensor step,
+                   Tensor rng_offset, const Tensor& eos_ids, int64_t pad_id) {
+  CHECK_I64(tok); CHECK_I64(out_tokens); CHECK_I32(kv_len); CHECK_I32(pos); CHECK_I64(next_input); CHECK_I32(gen_len);
+  CHECK_I64(step); CHECK_I64(rng_offset); CHECK_I64(eos_ids);
+  TORCH_CHECK(active.scalar_type() == at::kByte || active.scalar_type() == at::kBool);
+  check_rc(rt_decode_update((const long*)tok.data_ptr(), (long*)out_tokens.data_ptr(), (int)out_tokens.size(1),
+                            (float*)opt_ptr(out_logp), (const float*)opt_ptr(logp), (float*)opt_ptr(out_values),
+                            (const float*)opt_ptr(values), (uint8_t*)active.data_ptr(), kv_len.data_ptr<int>(),
+                            pos.data_ptr<int>(), (long*)next_input.data_ptr(), gen_len.data_ptr<int>(),
+                            (int64_t*)step.data_ptr(), (int64_t*)rng_offset.data_ptr(), (int)tok.numel(),
+                            (const long*)eos_ids.data_ptr(), (int)eos_ids.numel(), (long)pad_id, cur_stream()),
+           "decode_update");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 (MI355X) HIP kernels + native host runtime";
+  m.def("gemm", &gemm, "bf16 MFMA GEMM C = act(A W^T + U UB^T + bias)", py::arg("a"), py::arg("w"),
+        py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0,
+        py::arg("out_f32") = false, py::arg("out") = py::none());
+  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_bwd", &norm_bwd);
+  m.def("rope_qkv", &rope_qkv);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("embed", &embed);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_decode", &attn_decode);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("logprob_fwd", &logprob_fwd);
+  m.def("logprob_bwd", &logprob_bwd);
+  m.def("sample", &sample);
+  m.def("adamw", &adamw);
+  m.def("grad_norm", &grad_norm);
+  m.def("pool_norm", &pool_norm);
+  m.def("topk", &topk);
+  m.def("ivf_scan", &ivf_scan);
+  m.def("gae", &gae);
+  m.def("decode_update", &decode_update);
+  ragtl::bind_tokenizer(m);
+  ragtl::bind_ivf_host(m);
+}

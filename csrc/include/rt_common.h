@@ -1,0 +1,135 @@
+// Common device helpers for the gfx950 (CDNA4, MI355X) kernels of this framework.
+//
+// Everything here is written for wave64: lane ids are threadIdx.x & 63, cross-lane
+// reductions walk offsets 32..1, block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define RT_WAVE 64
+
+#define RT_HIP_CHECK(expr)                                                        \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) return (int)_e;                                         \
+  } while (0)
+
+#define RT_LAUNCH_CHECK() RT_HIP_CHECK(hipGetLastError())
+
+namespace rt {
+
+typedef uint16_t bf16_t;  // raw bf16 bits; storage type for every bf16 tensor
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;   // MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4;     // 16x16 accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16;   // 32x32 accumulator
+typedef __attribute__((ext_vector_type(8))) uint16_t u16x8;
+typedef __attribute__((ext_vector_type(4))) uint16_t u16x4;
+
+__device__ __forceinline__ float bf2f(bf16_t x) {
+  return __uint_as_float(((uint32_t)x) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 through the compiler's cast (lowers to
+// v_cvt_pk_bf16_f32 on gfx950 and keeps NaN a NaN).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// 16-byte vector of 8 bf16 <-> 8 floats
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2bf(f[0], f[1]);
+  v.y = pack2bf(f[2], f[3]);
+  v.z = pack2bf(f[4], f[5]);
+  v.w = pack2bf(f[6], f[7]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum; `sbuf` must hold blockDim.x/64 floats. Result broadcast to all threads.
+__device__ __forceinline__ float block_sum(float v, float* sbuf) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sbuf[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += sbuf[i];
+  return r;
+}
+
+__device__ __forceinline__ float block_max(float v, float* sbuf) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) sbuf[wid] = v;
+  __syncthreads();
+  float r = -INFINITY;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, sbuf[i]);
+  return r;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, T1):
+// blocks dealt round-robin over 8 XCDs are renumbered so each XCD gets a contiguous
+// chunk of the tile grid (neighbouring tiles share operand panels in that XCD's L2).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / 8;
+}
+
+// Philox4x32-10 counter-based RNG (graph-replay safe: state = (seed, offset) in memory).
+struct Philox {
+  __device__ static inline uint4 round(uint4 c, uint2 k) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    return make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+  }
+  __device__ static inline uint4 gen(uint64_t seed, uint64_t subseq, uint64_t offset) {
+    uint4 c = make_uint4((uint32_t)offset, (uint32_t)(offset >> 32), (uint32_t)subseq,
+                         (uint32_t)(subseq >> 32));
+    uint2 k = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      c = round(c, k);
+      k.x += 0x9E3779B9u;
+      k.y += 0xBB67AE85u;
+    }
+    return c;
+  }
+};
+
+__device__ __forceinline__ float u32_to_unit(uint32_t x) {
+  // uniform in (0, 1]
+  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+}  // namespace rt

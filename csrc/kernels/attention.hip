@@ -1,0 +1,745 @@
+// Attention kernels for gfx950 (SURVEY K4 flash prefill fwd/bwd, K5 decode, K11 encoder attention).
+//
+// Layout convention: activations are token-major rows ([B*S, ld]) with head h at column h*D, so
+// q/k/v are read straight out of the fused qkv projection output and O feeds o_proj directly.
+//
+// Forward (attn_fwd_kernel<D>): one workgroup = 128 query rows of one (batch, head), 4 waves x 32
+// rows. S^T = K·Q^T is computed "swapped" (key on the MFMA row, query on the lane): the S^T
+// accumulator of mfma_f32_16x16x32_bf16 is then, after bf16 packing, exactly the A operand of
+// P·V (cdna_hip_programming.md §3 'An accumulator tile as the next MFMA's operand'), so P never
+// touches LDS; V's B operand comes from ds_read_b64_tr_b16 (T10). K is XOR-swizzled for
+// conflict-free ds_read_b128 (T2), V for conflict-free transposed reads. K/V tiles are register-
+// prefetched one tile ahead (T14 split: issue before compute, LDS write after the barrier).
+// Masks: causal, sliding window, per-batch key start (left padding) and key length (encoder
+// padding), plus an optional additive relative-position bias LUT (MPNet).
+//
+// Decode (attn_decode_kernel + attn_decode_combine_kernel): split-K over the KV cache; one
+// workgroup = (partition of keys, kv head, batch) and computes all G = Hq/Hkv query heads that
+// share the kv head (the KV cache is read once); per-partition (m, l, o) partials combined by a
+// second kernel. Fixed grid sized for the cache capacity -> safe under hipGraph replay with
+// device-side lengths.
+//
+// Backward (attn_bwd_kernel<D>): FA2-style. One workgroup = 64 keys of one (batch, kv head);
+// waves own 16 keys each and keep dK^T, dV^T in accumulators while sweeping the group's query
+// heads x 64-row query tiles. S and dP are computed with the key on the lane so their
+// accumulators are directly the B operands of dV^T = dO^T·P and dK^T = Q^T·dS; only dS crosses
+// LDS (once) for dQ = dS·K, which is accumulated with fp32 atomics.
+#include "rt_common.h"
+
+namespace rt {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x4 ds_tr16(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+}
+
+__device__ __forceinline__ bf16x8 pack_bf16x8(const f32x4& a, const f32x4& b) {
+  uint4 v;
+  v.x = pack2bf(a[0], a[1]);
+  v.y = pack2bf(a[2], a[3]);
+  v.z = pack2bf(b[0], b[1]);
+  v.w = pack2bf(b[2], b[3]);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+struct AttnArgs {
+  const bf16_t* q; long ldq;
+  const bf16_t* k; long ldk;
+  const bf16_t* v; long ldv;
+  bf16_t* o; long ldo;
+  float* lse;                 // [B, Hq, Sq] (may be null)
+  const int* kv_start;        // [B] or null
+  const int* kv_len;          // [B] or null
+  const float* rel_bias;      // [Hq, 2*rb_L - 1] (log2-domain scaled on host) or null
+  int rb_L;
+  int B, Sq, Sk, Hq, Hkv;
+  int causal, window;
+  float scale_log2;           // softmax scale * log2(e)
+};
+
+// byte offset of 16-B chunk c of row r in a K-style (row-read) tile image
+template <int D>
+__device__ __forceinline__ int k_off(int r, int c) {
+  constexpr int NCH = D / 8;
+  return r * (D * 2) + ((c ^ (r & (NCH - 1))) << 4);
+}
+// byte offset of 16-B chunk c of row r in a V-style (transposed-read) tile image
+template <int D>
+__device__ __forceinline__ int v_off(int r, int c) {
+  constexpr int NCH = D / 8;
+  constexpr int RPB = 128 / D;
+  return r * (D * 2) + ((c ^ (((r / RPB) & (NCH / 2 - 1)) << 1)) << 4);
+}
+
+// ---------------------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
+  constexpr int TILE_BYTES = 64 * D * 2;
+  constexpr int OROW = D + 8;  // O staging row stride (elements)
+  constexpr int SMEM = (2 * TILE_BYTES > 128 * OROW * 2) ? 2 * TILE_BYTES : 128 * OROW * 2;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  char* Ks = smem;
+  char* Vs = smem + TILE_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int hk = h / (a.Hq / a.Hkv);
+  const int qblk0 = blockIdx.x * 128;
+  const int q0 = qblk0 + wid * 32;
+
+  const int start = a.kv_start ? a.kv_start[b] : 0;
+  int kend = a.kv_len ? min(a.kv_len[b], a.Sk) : a.Sk;
+  const int qlast = min(qblk0 + 127, a.Sq - 1);
+  if (a.causal) kend = min(kend, qlast + 1);
+  int kbeg = start;
+  if (a.window > 0) kbeg = max(kbeg, qblk0 - a.window + 1);
+  kbeg = max(kbeg, 0) & ~63;
+
+  // Q fragments (B operand of S^T = K·Q^T): lane holds Q[q0+16u+r16][32s + 8g .. +8]
+  bf16x8 qf[2][DS];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int qrow = min(q0 + 16 * u + r16, a.Sq - 1);
+    const bf16_t* qp = a.q + ((long)b * a.Sq + qrow) * a.ldq + (long)h * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < DS; ++s) qf[u][s] = *(const bf16x8*)(qp + 32 * s);
+  }
+
+  f32x4 o[2][DT];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int c = 0; c < DT; ++c) o[u][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+
+  // register prefetch of one K/V tile: 64 rows x NCH chunks each, spread over 256 threads
+  constexpr int CPT = 64 * NCH / 256;  // chunks per thread per tensor (4 for D=128)
+  uint4 kreg[CPT], vreg[CPT];
+  auto load_tile = [&](int kv0) {
+#pragma unroll
+    for (int r = 0; r < CPT; ++r) {
+      const int e = tid + 256 * r;
+      const int key = e / NCH, c = e % NCH;
+      const int kk = min(kv0 + key, a.Sk - 1);
+      kreg[r] = *(const uint4*)(a.k + ((long)b * a.Sk + kk) * a.ldk + (long)hk * D + c * 8);
+      vreg[r] = *(const uint4*)(a.v + ((long)b * a.Sk + kk) * a.ldv + (long)hk * D + c * 8);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int r = 0; r < CPT; ++r) {
+      const int e = tid + 256 * r;
+      const int key = e / NCH, c = e % NCH;
+      *(uint4*)(Ks + k_off<D>(key, c)) = kreg[r];
+      *(uint4*)(Vs + v_off<D>(key, c)) = vreg[r];
+    }
+  };
+
+  if (kbeg < kend) {
+    load_tile(kbeg);
+    store_tile();
+  }
+  __syncthreads();
+
+  for (int kv0 = kbeg; kv0 < kend; kv0 += 64) {
+    const bool has_next = kv0 + 64 < kend;
+    if (has_next) load_tile(kv0 + 64);
+
+    // ---- S^T[t][u] = K[16t..][:] · Q[u]^T ----
+    f32x4 st[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) st[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < DS; ++s) {
+        const bf16x8 kf = *(const bf16x8*)(Ks + k_off<D>(16 * t + r16, 4 * s + g));
+#pragma unroll
+        for (int u = 0; u < 2; ++u) st[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[u][s], st[t][u], 0, 0, 0);
+      }
+
+    // ---- scale + mask ----
+    const bool full = kv0 >= start && kv0 + 63 < kend && (!a.causal || kv0 + 63 <= q0) &&
+                      (a.window <= 0 || (q0 + 31) - kv0 < a.window) && !a.rel_bias;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float x = st[t][u][i] * a.scale_log2;
+          if (!full) {
+            const int kk = kv0 + 16 * t + 4 * g + i;
+            const int qq = q0 + 16 * u + r16;
+            bool ok = kk >= start && kk < kend;
+            if (a.causal) ok = ok && kk <= qq;
+            if (a.window > 0) ok = ok && (qq - kk) < a.window;
+            ok = ok && qq < a.Sq;
+            if (a.rel_bias && ok) x += a.rel_bias[(long)h * (2 * a.rb_L - 1) + (kk - qq) + a.rb_L - 1];
+            x = ok ? x : -INFINITY;
+          }
+          st[t][u][i] = x;
+        }
+
+    // ---- online softmax (per q column = lane r16 of each u) ----
+    float alpha[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[t][u][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[u], mx);
+      const float mu = mn == -INFINITY ? 0.f : mn;
+      alpha[u] = exp2f(m[u] - mu);
+      m[u] = mn;
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float pv = exp2f(st[t][u][i] - mu);
+          st[t][u][i] = pv;
+          rs += pv;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l[u] = l[u] * alpha[u] + rs;
+    }
+    // rescale O rows (row q = 16u + 4g + i lives in lane 4g+i's alpha)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float al = __shfl(alpha[u], 4 * g + i, 64);
+#pragma unroll
+        for (int c = 0; c < DT; ++c) o[u][c][i] *= al;
+      }
+
+    // ---- O += P · V ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 pa[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) pa[u] = pack_bf16x8(st[2 * ks][u], st[2 * ks + 1][u]);
+      const int qrow = lane >> 2 & 3, pcol = lane & 3;  // tr-read addressing within the 16-lane group
+#pragma unroll
+      for (int c = 0; c < DT; ++c) {
+        const int key_a = 32 * ks + 4 * g + qrow;
+        const int col = 16 * c + 4 * pcol;  // element column
+        const s16x4 lo = ds_tr16(Vs + v_off<D>(key_a, col >> 3) + ((col & 7) << 1));
+        const s16x4 hi = ds_tr16(Vs + v_off<D>(key_a + 16, col >> 3) + ((col & 7) << 1));
+        const bf16x8 vf = cat_tr(lo, hi);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) o[u][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[u], vf, o[u][c], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (has_next) store_tile();
+    __syncthreads();
+  }
+
+  // ---- finalize ----
+  if (a.lse && g == 0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qq = q0 + 16 * u + r16;
+      if (qq < a.Sq) {
+        const float v = l[u] > 0.f ? (m[u] + __log2f(l[u])) * 0.69314718055994531f : INFINITY;
+        a.lse[((long)b * a.Hq + h) * a.Sq + qq] = v;
+      }
+    }
+  }
+  bf16_t* Os = (bf16_t*)smem;  // [128][OROW]
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float lr = __shfl(l[u], 4 * g + i, 64);
+      const float inv = lr > 0.f ? 1.f / lr : 0.f;
+      const int row = wid * 32 + 16 * u + 4 * g + i;
+#pragma unroll
+      for (int c = 0; c < DT; ++c) Os[row * OROW + 16 * c + r16] = f2bf(o[u][c][i] * inv);
+    }
+  __syncthreads();
+  for (int e = tid; e < 128 * NCH; e += 256) {
+    const int row = e / NCH, c = e % NCH;
+    const int qq = qblk0 + row;
+    if (qq < a.Sq)
+      *(uint4*)(a.o + ((long)b * a.Sq + qq) * a.ldo + (long)h * D + c * 8) = *(const uint4*)(Os + row * OROW + c * 8);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// decode (one query token per sequence, KV cache [B, Hkv, Smax, D])
+// ---------------------------------------------------------------------------------------------
+struct DecodeArgs {
+  const bf16_t* q; long ldq;        // [B, ldq], head h at h*D
+  const bf16_t* kc; const bf16_t* vc;
+  int Smax;
+  const int* kv_len;                // [B] valid keys (incl. current token)
+  const int* kv_start;              // [B] or null
+  int window;
+  float* part;                      // [B, Hkv, NP, G, D+2]
+  bf16_t* o; long ldo;
+  int B, Hq, Hkv, NP, PS;
+  float scale_log2;
+};
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void attn_decode_kernel(DecodeArgs a) {
+  constexpr int LPK = D / 8;       // lanes per key (8 d each)
+  constexpr int KPW = 64 / LPK;    // keys per wave-step
+  extern __shared__ __attribute__((aligned(16))) float dsm[];  // scores [G][PS] + reduce
+  float* sc = dsm;
+  float* red = dsm + G * a.PS;     // [4 waves][G][D]
+  __shared__ float wstat[4][G][2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int part = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int len = a.kv_len[b];
+  int kbeg = a.kv_start ? a.kv_start[b] : 0;
+  if (a.window > 0) kbeg = max(kbeg, len - a.window);
+  const int p0 = max(part * a.PS, kbeg), p1 = min((part + 1) * a.PS, len);
+  float* outp = a.part + ((((long)b * a.Hkv + hk) * a.NP + part) * G) * (D + 2);
+  if (p0 >= p1) {
+    if (tid < G) { outp[tid * (D + 2) + D] = -INFINITY; outp[tid * (D + 2) + D + 1] = 0.f; }
+    return;
+  }
+  const int sub = lane / LPK, dl = lane % LPK;
+  float qv[G][8];
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg) unpack8(*(const uint4*)(a.q + (long)b * a.ldq + (long)(hk * G + gg) * D + dl * 8), qv[gg]);
+
+  const bf16_t* kbase = a.kc + ((long)b * a.Hkv + hk) * a.Smax * D;
+  const bf16_t* vbase = a.vc + ((long)b * a.Hkv + hk) * a.Smax * D;
+  // pass 1: scores
+  float wmax[G];
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg) wmax[gg] = -INFINITY;
+  for (int key = p0 + wid * KPW + sub; key - sub < p1; key += 4 * KPW) {
+    float kv[8];
+    const int kk = min(key, p1 - 1);
+    unpack8(*(const uint4*)(kbase + (long)kk * D + dl * 8), kv);
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += qv[gg][e] * kv[e];
+#pragma unroll
+      for (int off = LPK / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+      s *= a.scale_log2;
+      if (key < p1) {
+        if (dl == 0) sc[gg * a.PS + (key - p0)] = s;
+        wmax[gg] = fmaxf(wmax[gg], s);
+      }
+    }
+  }
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg) {
+    const float mx = wave_max(wmax[gg]);
+    if (lane == 0) wstat[wid][gg][0] = mx;
+  }
+  __syncthreads();
+  float mrow[G];
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg)
+    mrow[gg] = fmaxf(fmaxf(wstat[0][gg][0], wstat[1][gg][0]), fmaxf(wstat[2][gg][0], wstat[3][gg][0]));
+  // pass 2: p = exp2(s - m), o += p v
+  float acc[G][8], lsum[G];
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg) {
+    lsum[gg] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[gg][e] = 0.f;
+  }
+  for (int key = p0 + wid * KPW + sub; key - sub < p1; key += 4 * KPW) {
+    if (key < p1) {
+      float vv[8];
+      unpack8(*(const uint4*)(vbase + (long)key * D + dl * 8), vv);
+#pragma unroll
+      for (int gg = 0; gg < G; ++gg) {
+        const float p = exp2f(sc[gg * a.PS + (key - p0)] - mrow[gg]);
+        lsum[gg] += p;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[gg][e] += p * vv[e];
+      }
+    }
+  }
+  // reduce over the KPW key sub-groups of the wave
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg) {
+#pragma unroll
+    for (int off = LPK; off < 64; off <<= 1) {
+      lsum[gg] += __shfl_xor(lsum[gg], off, 64);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[gg][e] += __shfl_xor(acc[gg][e], off, 64);
+    }
+  }
+  if (sub == 0) {
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(wid * G + gg) * D + dl * 8 + e] = acc[gg][e];
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) wstat[wid][gg][1] = lsum[gg];
+  __syncthreads();
+  for (int e = tid; e < G * D; e += 256) {
+    const int gg = e / D, d = e % D;
+    outp[gg * (D + 2) + d] = red[(0 * G + gg) * D + d] + red[(1 * G + gg) * D + d] + red[(2 * G + gg) * D + d] +
+                             red[(3 * G + gg) * D + d];
+  }
+  if (tid < G) {
+    outp[tid * (D + 2) + D] = mrow[tid];
+    outp[tid * (D + 2) + D + 1] = wstat[0][tid][1] + wstat[1][tid][1] + wstat[2][tid][1] + wstat[3][tid][1];
+  }
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void attn_decode_combine_kernel(DecodeArgs a) {
+  // one workgroup per (b, hk); threads over G*D outputs
+  const int hk = blockIdx.x, b = blockIdx.y;
+  const float* pp = a.part + (((long)b * a.Hkv + hk) * a.NP) * G * (D + 2);
+  for (int e = threadIdx.x; e < G * D; e += blockDim.x) {
+    const int gg = e / D, d = e % D;
+    float M = -INFINITY;
+    for (int p = 0; p < a.NP; ++p) M = fmaxf(M, pp[(p * G + gg) * (D + 2) + D]);
+    float L = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+      for (int p = 0; p < a.NP; ++p) {
+        const float* q = pp + (p * G + gg) * (D + 2);
+        if (q[D] == -INFINITY) continue;  // empty partition: its o[] was never written
+        const float w = exp2f(q[D] - M);
+        L += w * q[D + 1];
+        O += w * q[d];
+      }
+    }
+    a.o[(long)b * a.ldo + (long)(hk * G + gg) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------------------------
+struct AttnBwdArgs {
+  const bf16_t* q; long ldq;
+  const bf16_t* k; long ldk;
+  const bf16_t* v; long ldv;
+  const bf16_t* o; long ldo;
+  const bf16_t* dout; long lddo;
+  const float* lse;            // [B, Hq, S]
+  float* delta;                // [B, Hq, S]
+  float* dq;                   // fp32 [B*S, Hq*D] (zeroed)
+  bf16_t* dk; long lddk;       // may alias into a d_qkv buffer
+  bf16_t* dv; long lddv;
+  const int* kv_start;
+  int B, S, Hq, Hkv;
+  int causal, window;
+  float scale_log2;            // scale * log2 e
+  float scale;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
+  // delta[b,h,q] = sum_d dO*O ; one wave per (b,q,h) row
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long total = (long)a.B * a.S * a.Hq;
+  if (row >= total) return;
+  const int h = row % a.Hq;
+  const long t = row / a.Hq;  // b*S + q
+  float s = 0.f;
+  for (int d = lane * 2; d < D; d += 128) {
+    const float o0 = bf2f(a.o[t * a.ldo + (long)h * D + d]), o1 = bf2f(a.o[t * a.ldo + (long)h * D + d + 1]);
+    const float g0 = bf2f(a.dout[t * a.lddo + (long)h * D + d]), g1 = bf2f(a.dout[t * a.lddo + (long)h * D + d + 1]);
+    s += o0 * g0 + o1 * g1;
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    const long b = t / a.S, q = t % a.S;
+    a.delta[(b * a.Hq + h) * a.S + q] = s;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnBwdArgs a) {
+  constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
+  constexpr int TB = 64 * D * 2;
+  // LDS: K tile (block keys) | Q tile | dO tile | dS tile [64 q][64 keys] | lse[64] | delta[64]
+  __shared__ __attribute__((aligned(16))) char smem[3 * TB + 64 * 64 * 2 + 2 * 64 * 4];
+  char* Ks = smem;
+  char* Qs = smem + TB;
+  char* Os = smem + 2 * TB;  // dO
+  char* dSs = smem + 3 * TB;
+  float* lse_s = (float*)(dSs + 64 * 64 * 2);
+  float* del_s = lse_s + 64;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int b = blockIdx.z, hk = blockIdx.y;
+  const int kb0 = blockIdx.x * 64;
+  const int G = a.Hq / a.Hkv;
+  const int start = a.kv_start ? a.kv_start[b] : 0;
+  const int mykey = kb0 + wid * 16 + r16;  // this lane's key column
+  constexpr int CPT = 64 * NCH / 256;
+
+  // block K tile -> LDS (for dQ), and this wave's K, V fragments (B operands) -> registers
+#pragma unroll
+  for (int r = 0; r < CPT; ++r) {
+    const int e = tid + 256 * r;
+    const int key = e / NCH, c = e % NCH;
+    const int kk = min(kb0 + key, a.S - 1);
+    *(uint4*)(Ks + v_off<D>(key, c)) = *(const uint4*)(a.k + ((long)b * a.S + kk) * a.ldk + (long)hk * D + c * 8);
+  }
+  bf16x8 kf[DS], vf[DS];
+  {
+    const int kk = min(mykey, a.S - 1);
+#pragma unroll
+    for (int s = 0; s < DS; ++s) {
+      kf[s] = *(const bf16x8*)(a.k + ((long)b * a.S + kk) * a.ldk + (long)hk * D + 32 * s + 8 * g);
+      vf[s] = *(const bf16x8*)(a.v + ((long)b * a.S + kk) * a.ldv + (long)hk * D + 32 * s + 8 * g);
+    }
+  }
+  f32x4 dk[DT], dvv[DT];
+#pragma unroll
+  for (int c = 0; c < DT; ++c) { dk[c] = f32x4{0.f, 0.f, 0.f, 0.f}; dvv[c] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+  int qbeg = a.causal ? kb0 : 0;
+  qbeg = max(qbeg, start) & ~63;
+  int qend = a.S;
+  if (a.window > 0) qend = min(qend, kb0 + 63 + a.window);
+  const bool key_valid = mykey >= start && mykey < a.S;
+
+  for (int hh = 0; hh < G; ++hh) {
+    const int h = hk * G + hh;
+    for (int qt = qbeg; qt < qend; qt += 64) {
+      __syncthreads();  // previous users of Q/dO/dS tiles are done
+      // stage Q and dO tile (64 rows) + lse/delta
+#pragma unroll
+      for (int r = 0; r < CPT; ++r) {
+        const int e = tid + 256 * r;
+        const int row = e / NCH, c = e % NCH;
+        const int qq = min(qt + row, a.S - 1);
+        *(uint4*)(Qs + k_off<D>(row, c)) = *(const uint4*)(a.q + ((long)b * a.S + qq) * a.ldq + (long)h * D + c * 8);
+        *(uint4*)(Os + k_off<D>(row, c)) =
+            *(const uint4*)(a.dout + ((long)b * a.S + qq) * a.lddo + (long)h * D + c * 8);
+      }
+      if (tid < 64) {
+        const int qq = qt + tid;
+        const bool ok = qq < a.S;
+        lse_s[tid] = ok ? a.lse[((long)b * a.Hq + h) * a.S + qq] * 1.4426950408889634f : INFINITY;
+        del_s[tid] = ok ? a.delta[((long)b * a.Hq + h) * a.S + qq] : 0.f;
+      }
+      __syncthreads();
+
+      // S[q][key] and dP[q][key] for 4 q-subtiles (key on lane)
+      f32x4 sp[4], dp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        sp[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+          const bf16x8 qa = *(const bf16x8*)(Qs + k_off<D>(16 * u + r16, 4 * s + g));
+          const bf16x8 oa = *(const bf16x8*)(Os + k_off<D>(16 * u + r16, 4 * s + g));
+          sp[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[s], sp[u], 0, 0, 0);
+          dp[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[s], dp[u], 0, 0, 0);
+        }
+      }
+      // P and dS (element (u,i) <-> q = qt + 16u + 4g + i, key = mykey)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ql = 16 * u + 4 * g + i;
+          const int qq = qt + ql;
+          bool ok = key_valid && qq < a.S;
+          if (a.causal) ok = ok && mykey <= qq;
+          if (a.window > 0) ok = ok && (qq - mykey) < a.window;
+          const float p = ok ? exp2f(sp[u][i] * a.scale_log2 - lse_s[ql]) : 0.f;
+          sp[u][i] = p;
+          dp[u][i] = p * (dp[u][i] - del_s[ql]);
+        }
+      // dV^T += dO^T · P ; dK^T += Q^T · dS  (A via transposed reads, B = accumulators)
+      const int qrow = lane >> 2 & 3, pcol = lane & 3;
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        const bf16x8 pb = pack_bf16x8(sp[2 * qs], sp[2 * qs + 1]);
+        const bf16x8 db = pack_bf16x8(dp[2 * qs], dp[2 * qs + 1]);
+#pragma unroll
+        for (int c = 0; c < DT; ++c) {
+          const int rowa = 32 * qs + 4 * g + qrow;
+          const int col = 16 * c + 4 * pcol;
+          // Q and dO tiles use the K-style image: tr reads address it with the same k_off
+          const bf16x8 oT = cat_tr(ds_tr16(Os + k_off<D>(rowa, col >> 3) + ((col & 7) << 1)),
+                                   ds_tr16(Os + k_off<D>(rowa + 16, col >> 3) + ((col & 7) << 1)));
+          const bf16x8 qT = cat_tr(ds_tr16(Qs + k_off<D>(rowa, col >> 3) + ((col & 7) << 1)),
+                                   ds_tr16(Qs + k_off<D>(rowa + 16, col >> 3) + ((col & 7) << 1)));
+          dvv[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oT, pb, dvv[c], 0, 0, 0);
+          dk[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qT, db, dk[c], 0, 0, 0);
+        }
+      }
+      // dS -> LDS as [q][key] (16-B chunk swizzle by q&7) for dQ = dS · K
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ql = 16 * u + 4 * g + i;
+          const int kl = wid * 16 + r16;
+          const int off = ql * 128 + (((kl >> 3) ^ (ql & 7)) << 4) + ((kl & 7) << 1);
+          *(bf16_t*)(dSs + off) = f2bf(dp[u][i]);
+        }
+      __syncthreads();
+      // dQ[q][d] for this wave's 16 q rows over the block's 64 keys
+      {
+        f32x4 dq[DT];
+#pragma unroll
+        for (int c = 0; c < DT; ++c) dq[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int ql = wid * 16 + r16;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int ch = 4 * ks + g;
+          const bf16x8 da = *(const bf16x8*)(dSs + ql * 128 + ((ch ^ (ql & 7)) << 4));
+#pragma unroll
+          for (int c = 0; c < DT; ++c) {
+            // B[k = key slot][col = d]: keys 32ks + 8g + j -> tr read rows 32ks + 8g + {0..3}, {4..7}
+            const int rowa = 32 * ks + 8 * g + qrow;
+            const int col = 16 * c + 4 * pcol;
+            const bf16x8 kb = cat_tr(ds_tr16(Ks + v_off<D>(rowa, col >> 3) + ((col & 7) << 1)),
+                                     ds_tr16(Ks + v_off<D>(rowa + 4, col >> 3) + ((col & 7) << 1)));
+            dq[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, kb, dq[c], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < DT; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int qq = qt + wid * 16 + 4 * g + i;
+            if (qq < a.S)
+              atomicAdd(a.dq + ((long)b * a.S + qq) * ((long)a.Hq * D) + (long)h * D + 16 * c + r16,
+                        dq[c][i] * a.scale);
+          }
+      }
+    }
+  }
+  // write dK, dV (lane holds dX^T[d = 16c + 4g + i][key = mykey])
+  if (mykey < a.S) {
+#pragma unroll
+    for (int c = 0; c < DT; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = 16 * c + 4 * g + i;
+        a.dk[((long)b * a.S + mykey) * a.lddk + (long)hk * D + d] = f2bf(dk[c][i] * a.scale);
+        a.dv[((long)b * a.S + mykey) * a.lddv + (long)hk * D + d] = f2bf(dvv[c][i]);
+      }
+  }
+}
+
+__global__ void f32_to_bf16_strided_kernel(const float* __restrict__ x, long n_cols, bf16_t* __restrict__ y, long ldy,
+                                           long rows) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= rows * n_cols) return;
+  const long r = gid / n_cols, c = gid % n_cols;
+  y[r * ldy + c] = f2bf(x[gid]);
+}
+
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" int rt_attn_fwd(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv, void* o, long ldo,
+                           float* lse, const int* kv_start, const int* kv_len, const float* rel_bias, int rb_L, int B,
+                           int Sq, int Sk, int Hq, int Hkv, int D, int causal, int window, float scale,
+                           hipStream_t stream) {
+  AttnArgs a;
+  a.q = (const bf16_t*)q; a.ldq = ldq; a.k = (const bf16_t*)k; a.ldk = ldk; a.v = (const bf16_t*)v; a.ldv = ldv;
+  a.o = (bf16_t*)o; a.ldo = ldo; a.lse = lse; a.kv_start = kv_start; a.kv_len = kv_len; a.rel_bias = rel_bias;
+  a.rb_L = rb_L; a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.window = window;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  if (B == 0 || Sq == 0) return 0;
+  dim3 grid((Sq + 127) / 128, Hq, B), block(256);
+  switch (D) {
+    case 32: hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, block, 0, stream, a); break;
+    case 64: hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, block, 0, stream, a); break;
+    case 128: hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, block, 0, stream, a); break;
+    default: return -1;
+  }
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int rt_attn_decode(const void* q, long ldq, const void* kc, const void* vc, int Smax, const int* kv_len,
+                              const int* kv_start, int window, float* part, int NP, int PS, void* o, long ldo, int B,
+                              int Hq, int Hkv, int D, float scale, hipStream_t stream) {
+  DecodeArgs a;
+  a.q = (const bf16_t*)q; a.ldq = ldq; a.kc = (const bf16_t*)kc; a.vc = (const bf16_t*)vc; a.Smax = Smax;
+  a.kv_len = kv_len; a.kv_start = kv_start; a.window = window; a.part = part; a.o = (bf16_t*)o; a.ldo = ldo;
+  a.B = B; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
+  const int G = Hq / Hkv;
+  if (B == 0) return 0;
+  dim3 grid(NP, Hkv, B), block(256);
+  const size_t shm = (size_t)(G * PS + 4 * G * D) * sizeof(float);
+#define DEC_CASE(DD, GG)                                                                      \
+  if (D == DD && G == GG) {                                                                   \
+    hipLaunchKernelGGL((attn_decode_kernel<DD, GG>), grid, block, shm, stream, a);            \
+    hipLaunchKernelGGL((attn_decode_combine_kernel<DD, GG>), dim3(Hkv, B), dim3(256), 0, stream, a); \
+    RT_LAUNCH_CHECK();                                                                        \
+    return 0;                                                                                 \
+  }
+  DEC_CASE(128, 1) DEC_CASE(128, 2) DEC_CASE(128, 4) DEC_CASE(128, 8)
+  DEC_CASE(64, 1) DEC_CASE(64, 2) DEC_CASE(64, 4) DEC_CASE(64, 8)
+  DEC_CASE(32, 1)
+#undef DEC_CASE
+  return -1;
+}
+
+extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv, const void* o,
+                           long ldo, const void* dout, long lddo, const float* lse, float* delta, float* dq_f32,
+                           void* dq, long lddq, void* dk, long lddk, void* dv, long lddv, const int* kv_start, int B,
+                           int S, int Hq, int Hkv, int D, int causal, int window, float scale, hipStream_t stream) {
+  AttnBwdArgs a;
+  a.q = (const bf16_t*)q; a.ldq = ldq; a.k = (const bf16_t*)k; a.ldk = ldk; a.v = (const bf16_t*)v; a.ldv = ldv;
+  a.o = (const bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.lse = lse; a.delta = delta;
+  a.dq = dq_f32; a.dk = (bf16_t*)dk; a.lddk = lddk; a.dv = (bf16_t*)dv; a.lddv = lddv; a.kv_start = kv_start;
+  a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.window = window;
+  a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
+  if (B == 0 || S == 0) return 0;
+  RT_HIP_CHECK(hipMemsetAsync(dq_f32, 0, (size_t)B * S * Hq * D * sizeof(float), stream));
+  const long rows = (long)B * S * Hq;
+  dim3 pgrid((unsigned)((rows + 3) / 4)), grid((S + 63) / 64, Hkv, B);
+  switch (D) {
+    case 64:
+      hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, pgrid, dim3(256), 0, stream, a);
+      hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, stream, a);
+      break;
+    case 128:
+      hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, pgrid, dim3(256), 0, stream, a);
+      hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, stream, a);
+      break;
+    default: return -1;
+  }
+  const long n = (long)B * S * Hq * D;
+  hipLaunchKernelGGL(f32_to_bf16_strided_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_f32,
+                     (long)Hq * D, (bf16_t*)dq, lddq, (long)B * S);
+  RT_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,197 @@
+// On-device token sampler: temperature, top-k, top-p (nucleus), greedy, and the
+// log-prob of the drawn token under the full tempered distribution (PPO's behaviour log-prob, so
+// rollout needs no separate "old log-prob" forward). One workgroup per row.
+//
+//  * top-k threshold: exact 4-pass 8-bit radix select of the k-th largest logit (ties kept, as the
+//    reference's HF TopK warper keeps every logit >= the k-th value).
+//  * top-p threshold: the same radix walk but histogramming probability MASS: the smallest set of
+//    highest-probability tokens whose mass reaches p (ties at the threshold kept).
+//  * draw: Gumbel-max over the kept set with a counter-based Philox stream keyed by
+//    (seed, row, offset + token id); `offset` is read from device memory so a hipGraph-captured
+//    decode step stays random across replays (the decode epilogue kernel advances it).
+// Reference behaviour being replaced: HF generate(do_sample=True, temperature=0.7)
+// (reinforcement_learning_optimization_after_rag.py:38-44).
+#include "rt_common.h"
+
+namespace rt {
+
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+template <typename T> __device__ __forceinline__ float ld1(const T* p);
+template <> __device__ __forceinline__ float ld1<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
+
+template <typename T>
+__global__ __launch_bounds__(256) void sample_kernel(const T* __restrict__ logits, long ld, int V, float inv_temp,
+                                                     int top_k, float top_p, int greedy, uint64_t seed,
+                                                     const int64_t* __restrict__ offset_ptr,
+                                                     const uint8_t* __restrict__ row_active, long* __restrict__ out_tok,
+                                                     float* __restrict__ out_logp) {
+  __shared__ float hist_f[256];
+  __shared__ unsigned hist_c[256];
+  __shared__ float redf[8];
+  __shared__ int redi[8];
+  __shared__ uint32_t sh_key;
+  __shared__ float sh_f;
+
+  const long row = blockIdx.x;
+  const T* x = logits + row * ld;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // pass 1: max of tempered logits (and argmax for greedy)
+  float mx = -INFINITY;
+  int amx = 0;
+  for (int i = tid; i < V; i += 256) {
+    const float f = ld1<T>(x + i) * inv_temp;
+    if (f > mx) { mx = f; amx = i; }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float om = __shfl_xor(mx, off, 64);
+    const int oi = __shfl_xor(amx, off, 64);
+    if (om > mx || (om == mx && oi < amx)) { mx = om; amx = oi; }
+  }
+  if (lane == 0) { redf[wid] = mx; redi[wid] = amx; }
+  __syncthreads();
+  float M = redf[0];
+  int AM = redi[0];
+  for (int w = 1; w < 4; ++w)
+    if (redf[w] > M || (redf[w] == M && redi[w] < AM)) { M = redf[w]; AM = redi[w]; }
+  __syncthreads();
+  // pass 2: sum of exp
+  float s = 0.f;
+  for (int i = tid; i < V; i += 256) s += __expf(ld1<T>(x + i) * inv_temp - M);
+  const float S = block_sum(s, redf);
+  const float lse = M + __logf(S);
+
+  int tok = AM;
+  const bool active = row_active ? row_active[row] != 0 : true;
+  if (!greedy && active) {
+    // ---- top-k threshold (key space of raw logits; order == tempered order for inv_temp > 0) ----
+    uint32_t kth = 0;  // keep key >= kth
+    if (top_k > 0 && top_k < V) {
+      uint32_t prefix = 0, mask = 0;
+      unsigned remaining = top_k;
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        hist_c[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < V; i += 256) {
+          const uint32_t k = fkey(ld1<T>(x + i));
+          if ((k & mask) == prefix) atomicAdd(&hist_c[(k >> shift) & 255], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          unsigned cum = 0;
+          int bsel = 0;
+          for (int bb = 255; bb >= 0; --bb) {
+            if (cum + hist_c[bb] >= remaining) { bsel = bb; break; }
+            cum += hist_c[bb];
+          }
+          remaining -= cum;
+          sh_key = bsel;
+        }
+        __syncthreads();
+        prefix |= sh_key << shift;
+        mask |= 255u << shift;
+        __syncthreads();
+      }
+      kth = prefix;
+    }
+    // ---- top-p threshold by probability mass among the top-k survivors ----
+    uint32_t pth = kth;
+    if (top_p < 1.f) {
+      float sk = 0.f;
+      for (int i = tid; i < V; i += 256) {
+        const float f = ld1<T>(x + i);
+        if (fkey(f) >= kth) sk += __expf(f * inv_temp - M);
+      }
+      const float Sk = block_sum(sk, redf);
+      const float target = top_p * Sk;
+      uint32_t prefix = 0, mask = 0;
+      float above = 0.f;
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        hist_f[tid] = 0.f;
+        __syncthreads();
+        for (int i = tid; i < V; i += 256) {
+          const float f = ld1<T>(x + i);
+          const uint32_t k = fkey(f);
+          if (k >= kth && (k & mask) == prefix) atomicAdd(&hist_f[(k >> shift) & 255], __expf(f * inv_temp - M));
+        }
+        __syncthreads();
+        if (tid == 0) {
+          int bsel = 0;
+          float a = above;
+          for (int bb = 255; bb >= 0; --bb) {
+            if (a + hist_f[bb] >= target || bb == 0) { bsel = bb; break; }
+            a += hist_f[bb];
+          }
+          sh_key = bsel;
+          sh_f = a;
+        }
+        __syncthreads();
+        prefix |= sh_key << shift;
+        mask |= 255u << shift;
+        above = sh_f;
+        __syncthreads();
+      }
+      pth = prefix > kth ? prefix : kth;
+    }
+    // ---- Gumbel-max draw over kept tokens ----
+    const uint64_t off = offset_ptr ? (uint64_t)offset_ptr[0] : 0ull;
+    float best = -INFINITY;
+    int bi = AM;
+    for (int i = tid; i < V; i += 256) {
+      const float f = ld1<T>(x + i);
+      if (fkey(f) >= pth) {
+        const uint4 r = Philox::gen(seed, (uint64_t)row, off * (uint64_t)V + (uint64_t)i);
+        const float u = u32_to_unit(r.x);
+        const float gmb = -__logf(-__logf(u));
+        const float sc = f * inv_temp + gmb;
+        if (sc > best || (sc == best && i < bi)) { best = sc; bi = i; }
+      }
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+      const float ob = __shfl_xor(best, o2, 64);
+      const int oi = __shfl_xor(bi, o2, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    __syncthreads();
+    if (lane == 0) { redf[wid] = best; redi[wid] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      float B = redf[0];
+      int BI = redi[0];
+      for (int w = 1; w < 4; ++w)
+        if (redf[w] > B || (redf[w] == B && redi[w] < BI)) { B = redf[w]; BI = redi[w]; }
+      redi[0] = BI;
+    }
+    __syncthreads();
+    tok = redi[0];
+  }
+  if (tid == 0) {
+    out_tok[row] = tok;
+    if (out_logp) out_logp[row] = ld1<T>(x + tok) * inv_temp - lse;
+  }
+}
+
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" int rt_sample(const void* logits, int is_f32, long ld, long B, int V, float inv_temp, int top_k, float top_p,
+                         int greedy, uint64_t seed, const int64_t* offset_ptr, const uint8_t* row_active, long* out_tok,
+                         float* out_logp, hipStream_t stream) {
+  if (B == 0) return 0;
+  if (is_f32)
+    hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(256), 0, stream, (const float*)logits, ld, V, inv_temp,
+                       top_k, top_p, greedy, seed, offset_ptr, row_active, out_tok, out_logp);
+  else
+    hipLaunchKernelGGL(sample_kernel<bf16_t>, dim3(B), dim3(256), 0, stream, (const bf16_t*)logits, ld, V, inv_temp,
+                       top_k, top_p, greedy, seed, offset_ptr, row_active, out_tok, out_logp);
+  RT_LAUNCH_CHECK();
+  return 0;
+}

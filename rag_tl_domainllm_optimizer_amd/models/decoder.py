@@ -1,0 +1,278 @@
+"""Causal decoder LMs: Llama-2 / Mistral (RMSNorm, RoPE, GQA, SwiGLU, sliding window) and OPT
+(pre-LN, learned positions, biases, ReLU MLP, tied head), in one module with three entry points:
+
+* ``forward``  — full-sequence forward (training / scoring), flash attention, autograd-ready,
+  LoRA adapters fused into the projection GEMMs;
+* ``prefill``  — prompt forward that also appends K/V to a static cache;
+* ``decode``   — one token per sequence against the cache (graph-capturable: no host sync, no
+  allocation-dependent control flow).
+
+Parameters use a fused layout (``qkv_proj`` = q|k|v rows, ``gate_up_proj`` = gate|up rows) so each
+sub-layer is one GEMM; :mod:`.io` maps to/from the HF per-projection names. The reference loads
+the same architectures through ``AutoModelForCausalLM`` (reinforcement_learning_optimization_after_rag.py:23,140,171).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..ops import reference as ref
+from .config import ModelConfig
+
+LLAMA_LORA_TARGETS = ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj")
+OPT_LORA_TARGETS = ("q_proj", "k_proj", "v_proj", "out_proj", "fc1", "fc2")
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        H, F = cfg.hidden_size, cfg.intermediate_size
+        kw = dict(device=device, dtype=dtype)
+        self.cfg = cfg
+        self.ln1_w = nn.Parameter(torch.ones(H, **kw))
+        self.ln2_w = nn.Parameter(torch.ones(H, **kw))
+        self.qkv_w = nn.Parameter(torch.empty(cfg.qkv_dim, H, **kw))
+        self.o_w = nn.Parameter(torch.empty(H, cfg.num_heads * cfg.head_dim, **kw))
+        if cfg.arch == "opt":
+            self.ln1_b = nn.Parameter(torch.zeros(H, **kw))
+            self.ln2_b = nn.Parameter(torch.zeros(H, **kw))
+            self.qkv_b = nn.Parameter(torch.zeros(cfg.qkv_dim, **kw))
+            self.o_b = nn.Parameter(torch.zeros(H, **kw))
+            self.fc1_w = nn.Parameter(torch.empty(F, H, **kw))
+            self.fc1_b = nn.Parameter(torch.zeros(F, **kw))
+            self.fc2_w = nn.Parameter(torch.empty(H, F, **kw))
+            self.fc2_b = nn.Parameter(torch.zeros(H, **kw))
+        else:
+            self.gate_up_w = nn.Parameter(torch.empty(2 * F, H, **kw))
+            self.down_w = nn.Parameter(torch.empty(H, F, **kw))
+        # LoRA: projection name -> LoRAGroup ; parameters registered in lora_params for state tracking
+        self.lora: Dict[str, ops.LoRAGroup] = {}
+        self.lora_params = nn.ParameterDict()
+        self.lora_enabled = True
+
+    # ---------------------------------------------------------------- helpers
+    def _lg(self, name):
+        g = self.lora.get(name)
+        return g if (g is not None and self.lora_enabled) else None
+
+    def _b(self, name):
+        return getattr(self, name, None)
+
+    def attn_in(self, x, residual):
+        cfg = self.cfg
+        if cfg.arch == "opt":
+            h, residual = ops.layer_norm(x, self.ln1_w, self.ln1_b, cfg.norm_eps, residual)
+        else:
+            h, residual = ops.rms_norm(x, self.ln1_w, cfg.norm_eps, residual)
+        qkv = ops.linear(h, self.qkv_w, self._b("qkv_b"), lora=self._lg("qkv"))
+        return qkv, residual
+
+    def mlp(self, a, residual):
+        cfg = self.cfg
+        a = ops.linear(a, self.o_w, self._b("o_b"), lora=self._lg("o"))
+        if cfg.arch == "opt":
+            h, residual = ops.layer_norm(a, self.ln2_w, self.ln2_b, cfg.norm_eps, residual)
+            f = ops.linear(h, self.fc1_w, self.fc1_b, act=cfg.hidden_act, lora=self._lg("fc1"))
+            d = ops.linear(f, self.fc2_w, self.fc2_b, lora=self._lg("fc2"))
+        else:
+            h, residual = ops.rms_norm(a, self.ln2_w, cfg.norm_eps, residual)
+            gu = ops.linear(h, self.gate_up_w, lora=self._lg("gate_up"))
+            d = ops.linear(ops.swiglu(gu), self.down_w, lora=self._lg("down"))
+        return d, residual
+
+
+class CausalLM(nn.Module):
+    def __init__(self, cfg: ModelConfig, device=None, dtype=torch.bfloat16, init: bool = True, seed: int = 0):
+        super().__init__()
+        assert cfg.is_decoder, cfg.arch
+        self.cfg = cfg
+        self.dtype = dtype
+        kw = dict(device=device, dtype=dtype)
+        self.embed = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden_size, **kw))
+        if cfg.arch == "opt":
+            self.pos_embed = nn.Parameter(torch.empty(cfg.max_position + cfg.position_offset, cfg.hidden_size, **kw))
+            self.norm_b = nn.Parameter(torch.zeros(cfg.hidden_size, **kw))
+        self.norm_w = nn.Parameter(torch.ones(cfg.hidden_size, **kw))
+        self.layers = nn.ModuleList([DecoderLayer(cfg, device, dtype) for _ in range(cfg.num_layers)])
+        if not cfg.tie_embeddings:
+            self.lm_head = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden_size, **kw))
+        self._rope = None
+        if init:
+            self.reset_parameters(seed)
+
+    # ------------------------------------------------------------------ init
+    @torch.no_grad()
+    def reset_parameters(self, seed: int = 0):
+        """Random init (HF-style normal(0, initializer_range)); seeded -> identical on every DP rank."""
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        std = self.cfg.initializer_range
+        for name, p in self.named_parameters():
+            if "lora" in name:
+                continue
+            if name.endswith("_w") and ("ln" in name or "norm" in name):
+                p.fill_(1.0)
+            elif name.endswith("_b") or name == "norm_b":
+                p.zero_()
+            else:
+                _normal_(p, std, g)
+
+    # ------------------------------------------------------------------ utils
+    @property
+    def head_weight(self):
+        return self.embed if self.cfg.tie_embeddings else self.lm_head
+
+    def rope(self, device):
+        if self.cfg.arch == "opt":
+            return None, None
+        if self._rope is None or self._rope[0].device != torch.device(device):
+            self._rope = ref.rope_tables(self.cfg.head_dim, self.cfg.max_position, self.cfg.rope_theta, device)
+        return self._rope
+
+    def positions(self, B, S, kv_start, device):
+        ar = torch.arange(S, device=device)[None, :].expand(B, S)
+        if kv_start is not None:
+            ar = (ar - kv_start.long()[:, None]).clamp(min=0)
+        return ar.reshape(-1).to(torch.int32)
+
+    def embed_tokens(self, ids_flat, pos_flat):
+        if self.cfg.arch == "opt":
+            return ops.embedding(self.embed, ids_flat, self.pos_embed, pos_flat.long() + self.cfg.position_offset)
+        return ops.embedding(self.embed, ids_flat)
+
+    def final_norm(self, d, residual):
+        cfg = self.cfg
+        if cfg.arch == "opt":
+            return ops.layer_norm(d, self.norm_w, self.norm_b, cfg.norm_eps, residual)[0]
+        return ops.rms_norm(d, self.norm_w, cfg.norm_eps, residual)[0]
+
+    def logits(self, hidden, out_f32: bool = False):
+        return ops.gemm(hidden.contiguous(), self.head_weight, out_f32=out_f32) if not torch.is_grad_enabled() or \
+            not hidden.requires_grad else ops.linear(hidden, self.head_weight)
+
+    # ------------------------------------------------------------------ full forward
+    def forward(self, input_ids: torch.Tensor, kv_start: Optional[torch.Tensor] = None,
+                gradient_checkpointing: bool = False) -> torch.Tensor:
+        """input_ids [B, S] (left-padded; kv_start[b] = first real token) -> final hidden [B*S, H]."""
+        cfg = self.cfg
+        B, S = input_ids.shape
+        dev = input_ids.device
+        pos = self.positions(B, S, kv_start, dev)
+        cos, sin = self.rope(dev)
+        ks = kv_start.to(torch.int32) if kv_start is not None else None
+        x = self.embed_tokens(input_ids.reshape(-1), pos)
+        residual = None
+        for layer in self.layers:
+            if gradient_checkpointing and torch.is_grad_enabled():
+                x, residual = torch.utils.checkpoint.checkpoint(self._layer_fwd, layer, x, residual, pos, cos, sin,
+                                                                B, S, ks, use_reentrant=False)
+            else:
+                x, residual = self._layer_fwd(layer, x, residual, pos, cos, sin, B, S, ks)
+        return self.final_norm(x, residual)
+
+    def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks):
+        cfg = self.cfg
+        qkv, residual = layer.attn_in(x, residual)
+        if cos is not None:
+            qkv = ops.rope_qkv(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim)
+        o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
+                                    cfg.sliding_window, kv_start=ks)
+        return layer.mlp(o, residual)
+
+    # ------------------------------------------------------------------ generation
+    @torch.no_grad()
+    def prefill(self, input_ids, kv_start, cache) -> torch.Tensor:
+        """Prompt forward writing K/V into ``cache`` slots [0, S); returns final hidden at the last
+        position of every row [B, H] (rows are left-padded so all end at S-1)."""
+        cfg = self.cfg
+        B, S = input_ids.shape
+        dev = input_ids.device
+        pos = self.positions(B, S, kv_start, dev)
+        cos, sin = self.rope(dev)
+        ks = kv_start.to(torch.int32)
+        x = self.embed_tokens(input_ids.reshape(-1), pos)
+        residual = None
+        for li, layer in enumerate(self.layers):
+            qkv, residual = layer.attn_in(x, residual)
+            ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S,
+                          k_cache=cache.k[li], v_cache=cache.v[li], slot_base=None)
+            o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
+                                        cfg.sliding_window, kv_start=ks)
+            x, residual = layer.mlp(o, residual)
+        last = torch.arange(B, device=dev) * S + (S - 1)
+        return self.final_norm(x[last].contiguous(), residual[last].contiguous())
+
+    @torch.no_grad()
+    def decode(self, tokens, pos, slot, attn_len, kv_start, cache, workspace=None) -> torch.Tensor:
+        """One step: tokens [B] at rotary position pos [B] written to cache slot ``slot`` [B];
+        attention over ``attn_len`` [B] keys. Returns final hidden [B, H]."""
+        cfg = self.cfg
+        cos, sin = self.rope(tokens.device)
+        x = self.embed_tokens(tokens, pos)
+        residual = None
+        for li, layer in enumerate(self.layers):
+            qkv, residual = layer.attn_in(x, residual)
+            ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=1,
+                          k_cache=cache.k[li], v_cache=cache.v[li], slot_base=slot)
+            o = ops.decode_attention(qkv, cache.k[li], cache.v[li], attn_len, cfg.num_heads, kv_start,
+                                     cfg.sliding_window, workspace=workspace)
+            x, residual = layer.mlp(o, residual)
+        return self.final_norm(x, residual)
+
+    # ------------------------------------------------------------------ LoRA
+    def add_lora(self, r: int = 16, alpha: float = 32.0, targets=None, dropout: float = 0.0, seed: int = 0):
+        """Attach PEFT-style LoRA adapters (A kaiming-uniform, B zero) to the target projections."""
+        from .lora import attach_lora
+
+        return attach_lora(self, r, alpha, targets, dropout, seed)
+
+    def lora_parameters(self) -> List[nn.Parameter]:
+        out = []
+        for layer in self.layers:
+            out += list(layer.lora_params.values())
+        return out
+
+    def set_lora_enabled(self, on: bool):
+        for layer in self.layers:
+            layer.lora_enabled = on
+
+    def refresh_lora(self):
+        for layer in self.layers:
+            for g in layer.lora.values():
+                g.refresh(dtype=self.dtype)
+
+    def freeze_base(self):
+        for n, p in self.named_parameters():
+            if "lora" not in n:
+                p.requires_grad_(False)
+
+
+def _normal_(p: torch.Tensor, std: float, g: torch.Generator):
+    # generate in chunks on CPU for reproducibility across devices, then copy
+    flat = p.view(-1)
+    n = flat.numel()
+    chunk = 1 << 26
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        flat[s:e].copy_(torch.randn(e - s, generator=g) * std)
+
+
+def fast_random_init_(model: nn.Module, seed: int = 0, std: float = 0.02):
+    """Device-side random init for large models (bench/smoke): identical for every rank with the
+    same seed. Norm weights 1, biases 0, LoRA untouched."""
+    gen = None
+    for name, p in model.named_parameters():
+        if "lora" in name:
+            continue
+        with torch.no_grad():
+            if name.endswith("_w") and ("ln" in name or "norm" in name):
+                p.fill_(1.0)
+            elif name.endswith("_b"):
+                p.zero_()
+            else:
+                if gen is None or gen.device != p.device:
+                    gen = torch.Generator(device=p.device).manual_seed(seed)
+                p.normal_(0.0, std, generator=gen)

@@ -1,0 +1,157 @@
+"""Linear projections: frozen/trainable base weight + fused LoRA adapters + bias/activation.
+
+GPU forward is one MFMA GEMM (``_C.gemm``) in which the LoRA term rides on the same accumulators
+as extra K-steps:  ``Y = act(X W^T + U UB^T + b)`` with ``U = X A_pad^T`` (A_pad = scaling * A,
+zero-padded to a multiple of 64 rows) computed by a small GEMM first. Several adapters on one
+fused projection (q|k|v, gate|up) share one padded rank dimension, with UB block-diagonal.
+
+Backward (training): dX = dY W + dU A_pad, dA = s dU^T X, dB = dY^T U, dW = dY^T X (full FT) are
+plain library GEMMs (torch.matmul -> hipBLASLt); only the forward carries fused epilogues.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from . import reference as ref
+from ._ext import native, on_gpu
+
+ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new": 3, "silu": 4}
+
+
+def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None):
+    """Raw (non-autograd) fused GEMM on 2-D row-major operands."""
+    if on_gpu(x):
+        return native().gemm(x, w, u, ub, bias, act, out_f32, out)
+    y = ref.gemm(x, w, u, ub, bias, act, out_f32)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+@dataclass
+class LoRAGroup:
+    """Adapters attached to one (possibly fused) projection.
+
+    ``a[i]`` [r_i, K] and ``b[i]`` [n_i, r_i] are the trainable fp32 parameters of adapter i,
+    which writes output columns ``[col0[i], col0[i] + n_i)`` with scale ``scale[i]``.
+    ``a_pad`` [Rp, K] and ``ub`` [N, Rp] are the bf16 compute images (rebuilt by ``refresh``).
+    """
+
+    names: List[str]
+    a: List[torch.nn.Parameter]
+    b: List[torch.nn.Parameter]
+    col0: List[int]
+    scale: List[float]
+    n_out: int
+    a_pad: Optional[torch.Tensor] = None
+    ub: Optional[torch.Tensor] = None
+    r0: List[int] = field(default_factory=list)
+    enabled: bool = True
+
+    @property
+    def rank_total(self) -> int:
+        return sum(int(a.shape[0]) for a in self.a)
+
+    @property
+    def rp(self) -> int:
+        return max(64, (self.rank_total + 63) // 64 * 64)
+
+    @torch.no_grad()
+    def refresh(self, dtype=torch.bfloat16):
+        """Rebuild the padded bf16 images from the fp32 parameters (after each optimizer step)."""
+        K = self.a[0].shape[1]
+        dev = self.a[0].device
+        rp = self.rp
+        if self.a_pad is None or self.a_pad.shape != (rp, K) or self.a_pad.device != dev:
+            self.a_pad = torch.zeros(rp, K, dtype=dtype, device=dev)
+            self.ub = torch.zeros(self.n_out, rp, dtype=dtype, device=dev)
+        self.r0 = []
+        r = 0
+        for a, b, c0, s in zip(self.a, self.b, self.col0, self.scale):
+            ri = a.shape[0]
+            self.r0.append(r)
+            self.a_pad[r:r + ri].copy_(a.detach() * s)
+            self.ub[c0:c0 + b.shape[0], r:r + ri].copy_(b.detach())
+            r += ri
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], *lora_params):
+        u = ub = None
+        if lora is not None:
+            u = gemm(x2, lora.a_pad)  # [M, Rp] = X (s*A)^T
+            ub = lora.ub
+        y = gemm(x2, w, u, ub, bias, act)
+        ctx.act = act
+        ctx.lora = lora
+        ctx.has_bias = bias is not None
+        # with an activation epilogue the pre-activation is recomputed in backward (no extra
+        # activation-sized tensor is kept alive)
+        ctx.save_for_backward(x2, w, u if u is not None else torch.empty(0), bias if bias is not None else torch.empty(0))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, u, bias = ctx.saved_tensors
+        lora = ctx.lora
+        dy = dy.contiguous()
+        if ctx.act != 0:
+            # recompute pre-activation and apply the activation derivative
+            ub = lora.ub if lora is not None else None
+            pre = gemm(x2, w, u if lora is not None else None, ub, bias if ctx.has_bias else None, 0, out_f32=True)
+            with torch.enable_grad():
+                p = pre.detach().requires_grad_(True)
+                yact = ref.apply_act(p, ctx.act)
+                (g,) = torch.autograd.grad(yact, p, dy.float())
+            dy = g.to(dy.dtype)
+        needs = ctx.needs_input_grad
+        dx = dw = db = None
+        if needs[0]:
+            dx = dy @ w
+        if needs[1]:
+            dw = (dy.t() @ x2).to(w.dtype)
+        if ctx.has_bias and needs[2]:
+            db = dy.float().sum(0).to(bias.dtype)
+        lora_grads = []
+        if lora is not None:
+            du = dy @ lora.ub  # [M, Rp]  (= dL/dU)
+            if needs[0]:
+                dx = dx + du @ lora.a_pad
+            for a, b, r0, c0, s in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
+                ri, ni = a.shape[0], b.shape[0]
+                ga = (du[:, r0:r0 + ri].t().float() @ x2.float()) * s
+                gb = dy[:, c0:c0 + ni].t().float() @ u[:, r0:r0 + ri].float()
+                lora_grads.append(ga.to(a.dtype))
+                lora_grads.append(gb.to(b.dtype))
+            # parameter order in forward(*lora_params) is a0, b0, a1, b1, ...
+        return (dx, dw, db, None, None, *lora_grads)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional[LoRAGroup] = None):
+    """y = act(x W^T (+ LoRA) + b) over the last dim of x."""
+    act_id = ACT_IDS[act] if not isinstance(act, int) else act
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    use_lora = lora is not None and lora.enabled
+    if use_lora and (lora.a_pad is None or lora.a_pad.device != x.device):
+        lora.refresh(dtype=w.dtype)
+    grad_needed = torch.is_grad_enabled() and (
+        x2.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)
+        or (use_lora and any(p.requires_grad for p in lora.a + lora.b)))
+    if not grad_needed:
+        u = gemm(x2, lora.a_pad) if use_lora else None
+        y = gemm(x2, w, u, lora.ub if use_lora else None, bias, act_id)
+    else:
+        params = []
+        if use_lora:
+            for a, b in zip(lora.a, lora.b):
+                params += [a, b]
+        y = _LinearFn.apply(x2, w, bias, act_id, lora if use_lora else None, *params)
+    return y.reshape(*shp[:-1], w.shape[0])

@@ -1,0 +1,145 @@
+"""SwiGLU, embedding gather, token log-probs / entropy, sampler, retrieval and RL kernels."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import reference as ref
+from ._ext import native, on_gpu
+
+
+# ------------------------------------------------------------------------------------ SwiGLU
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return native().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (gu,) = ctx.saved_tensors
+        return native().swiglu_bwd(gu, dy.contiguous())
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    """silu(gate) * up for gu = [gate | up] along the last dim."""
+    if not on_gpu(gu):
+        F2 = gu.shape[-1]
+        return F.silu(gu[..., : F2 // 2]) * gu[..., F2 // 2:]
+    if torch.is_grad_enabled() and gu.requires_grad:
+        return _SwiGLUFn.apply(gu)
+    return native().swiglu_fwd(gu.contiguous())
+
+
+# --------------------------------------------------------------------------------- embedding
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, table, ids):
+        ctx.save_for_backward(ids)
+        ctx.shape = table.shape
+        return native().embed(table, ids.contiguous(), None, None)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        d = torch.zeros(ctx.shape, dtype=torch.float32, device=g.device)
+        d.index_add_(0, ids.reshape(-1), g.reshape(-1, ctx.shape[1]).float())
+        return d.to(g.dtype), None
+
+
+def embedding(table: torch.Tensor, ids: torch.Tensor, pos_table=None, pos_ids=None) -> torch.Tensor:
+    if not on_gpu(table):
+        out = F.embedding(ids, table)
+        if pos_table is not None:
+            out = out + F.embedding(pos_ids, pos_table)
+        return out
+    if torch.is_grad_enabled() and table.requires_grad:
+        out = _EmbedFn.apply(table, ids.long())
+        if pos_table is not None:
+            out = out + _EmbedFn.apply(pos_table, pos_ids.long()) if pos_table.requires_grad else \
+                out + native().embed(pos_table, pos_ids.long().contiguous(), None, None)
+        return out
+    return native().embed(table, ids.long().contiguous(), pos_table,
+                          pos_ids.long().contiguous() if pos_ids is not None else None)
+
+
+# --------------------------------------------------------------------------- token log-probs
+class _LogProbFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, inv_temp):
+        logp, ent, lse, ex = native().logprob_fwd(logits, targets, inv_temp, True)
+        ctx.save_for_backward(logits, targets if targets is not None else torch.empty(0, dtype=torch.long), lse, ex)
+        ctx.inv_temp = inv_temp
+        ctx.has_t = targets is not None
+        return logp, ent
+
+    @staticmethod
+    def backward(ctx, g_lp, g_ent):
+        logits, targets, lse, ex = ctx.saved_tensors
+        gl = g_lp.float().contiguous() if g_lp is not None else None
+        ge = g_ent.float().contiguous() if g_ent is not None else None
+        d = native().logprob_bwd(logits, targets if ctx.has_t else None, ctx.inv_temp, lse, ex, gl, ge)
+        return d.to(logits.dtype), None, None
+
+
+def token_logprobs(logits: torch.Tensor, targets, inv_temp: float = 1.0):
+    """Per-row (log p(target), entropy) of softmax(logits * inv_temp); logits [T, V]."""
+    if not on_gpu(logits):
+        lp, ent, _, _ = ref.logprob(logits, targets, inv_temp)
+        return lp, ent
+    if logits.stride(-1) != 1:
+        logits = logits.contiguous()
+    if torch.is_grad_enabled() and logits.requires_grad:
+        return _LogProbFn.apply(logits, targets, inv_temp)
+    lp, ent, _, _ = native().logprob_fwd(logits, targets, inv_temp, True)
+    return lp, ent
+
+
+# --------------------------------------------------------------------------------- sampler
+def sample(logits, inv_temp=1.0, top_k=0, top_p=1.0, greedy=False, seed=0, offset=None, active=None,
+           out_tok=None, out_logp=None, generator=None):
+    """Draw one token per row; returns (tokens int64 [B], logp of drawn token [B])."""
+    B = logits.shape[0]
+    if not on_gpu(logits):
+        tok, lp = ref.sample(logits, inv_temp, top_k, top_p, greedy, generator)
+        if out_tok is not None:
+            out_tok.copy_(tok)
+            tok = out_tok
+        if out_logp is not None:
+            out_logp.copy_(lp)
+            lp = out_logp
+        return tok, lp
+    if out_tok is None:
+        out_tok = torch.empty(B, dtype=torch.long, device=logits.device)
+    if out_logp is None:
+        out_logp = torch.empty(B, dtype=torch.float32, device=logits.device)
+    native().sample(logits, inv_temp, top_k, top_p, greedy, seed, offset, active, out_tok, out_logp)
+    return out_tok, out_logp
+
+
+# ------------------------------------------------------------------------------- retrieval
+def pool_normalize(x: torch.Tensor, lengths=None, normalize: bool = True) -> torch.Tensor:
+    """Masked mean over tokens + L2 normalisation: [B, S, H] -> [B, H] fp32."""
+    if on_gpu(x):
+        return native().pool_norm(x.contiguous(), lengths.int() if lengths is not None else None, normalize)
+    return ref.pool_norm(x, lengths, normalize)
+
+
+def topk(scores: torch.Tensor, k: int, idmap=None):
+    """Row-wise top-k (descending) of fp32 scores [nq, N] -> (values, ids)."""
+    if on_gpu(scores) and k <= 512:
+        return native().topk(scores.float().contiguous(), k, idmap)
+    return ref.topk(scores, k, idmap)
+
+
+def ivf_scan(q, probes, offsets, vecs, ids, maxlen):
+    return native().ivf_scan(q.contiguous(), probes.int().contiguous(), offsets, vecs, ids, maxlen)
+
+
+# ---------------------------------------------------------------------------------------- RL
+def gae(rewards, values, mask, gamma: float, lam: float):
+    if on_gpu(rewards):
+        return native().gae(rewards.float().contiguous(), values.float().contiguous(), mask.float().contiguous(),
+                            gamma, lam)
+    return ref.gae(rewards.float(), values.float(), mask.float(), gamma, lam)

@@ -1,0 +1,328 @@
+"""Numerics of every HIP kernel against the plain-PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from rag_tl_domainllm_optimizer_amd import ops
+from rag_tl_domainllm_optimizer_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, rtol=2e-2, atol=2e-2):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= atol + rtol * scale, f"max err {err} (scale {scale})"
+
+
+def setup_module(_):
+    torch.manual_seed(0)
+    assert ops.native_available(), "native extension must load on the GPU box"
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (300, 1000, 512), (1024, 6144, 1024), (1, 4096, 4096),
+                                   (37, 2048, 1024), (64, 512, 384), (129, 136, 128)])
+def test_gemm(M, N, K):
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / math.sqrt(K)
+    _close(ops.gemm(a, w), ref.gemm(a, w, out_f32=True))
+
+
+@pytest.mark.parametrize("M", [8, 200])
+def test_gemm_lora_bias_act(M):
+    K, N, R = 512, 384, 64
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / math.sqrt(K)
+    u = torch.randn(M, R, device=DEV, dtype=torch.bfloat16)
+    ub = torch.randn(N, R, device=DEV, dtype=torch.bfloat16) * 0.1
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    for act in (0, 1, 2, 3, 4):
+        _close(ops.gemm(a, w, u, ub, b, act), ref.gemm(a, w, u, ub, b, act, out_f32=True))
+    y32 = ops.gemm(a, w, u, ub, b, 0, out_f32=True)
+    assert y32.dtype == torch.float32
+    _close(y32, ref.gemm(a, w, u, ub, b, 0, out_f32=True), rtol=5e-3, atol=5e-3)
+
+
+def test_gemm_asymmetric_identity():
+    # A = I with asymmetric B catches transposed C writes (cdna_hip_programming.md §3)
+    n = 128
+    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    w = (torch.arange(n * n, device=DEV).reshape(n, n) % 97).to(torch.bfloat16)
+    out = ops.gemm(a, w)
+    assert torch.equal(out.float(), w.t().float())
+
+
+def test_linear_lora_autograd():
+    torch.manual_seed(1)
+    M, K, N, r = 96, 256, 192, 8
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(N, K, device=DEV) / 16).to(torch.bfloat16)
+    a1 = torch.nn.Parameter(torch.randn(r, K, device=DEV) * 0.05)
+    b1 = torch.nn.Parameter(torch.randn(N // 2, r, device=DEV) * 0.05)
+    a2 = torch.nn.Parameter(torch.randn(r, K, device=DEV) * 0.05)
+    b2 = torch.nn.Parameter(torch.randn(N // 2, r, device=DEV) * 0.05)
+    grp = ops.LoRAGroup(["q", "v"], [a1, a2], [b1, b2], [0, N // 2], [2.0, 2.0], N)
+    y = ops.linear(x, w, lora=grp)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    # reference
+    xr = x.detach().float().requires_grad_(True)
+    a1r, b1r, a2r, b2r = [p.detach().clone().requires_grad_(True) for p in (a1, b1, a2, b2)]
+    yr = xr @ w.float().t()
+    yr = yr + torch.cat([2.0 * (xr @ a1r.t()) @ b1r.t(), 2.0 * (xr @ a2r.t()) @ b2r.t()], 1)
+    (yr * g.float()).sum().backward()
+    _close(y, yr)
+    _close(x.grad, xr.grad)
+    for p, pr in ((a1, a1r), (b1, b1r), (a2, a2r), (b2, b2r)):
+        _close(p.grad, pr.grad, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("H", [384, 768, 4096, 5120])
+@pytest.mark.parametrize("layernorm", [False, True])
+def test_norm(H, layernorm):
+    T = 67
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16) if layernorm else None
+    y, h, rstd, mean = ops.native().norm_fwd(layernorm, x, r, w, b, 1e-5)
+    yr, hr, rstdr, meanr = ref.norm(x, w, b, 1e-5, r, layernorm)
+    _close(y, yr)
+    assert torch.equal(h, hr)
+    # backward through the autograd path
+    xg = x.clone().requires_grad_(True)
+    rg = r.clone().requires_grad_(True)
+    wg = w.clone().requires_grad_(True)
+    if layernorm:
+        y1, h1 = ops.layer_norm(xg, wg, b, 1e-5, rg)
+    else:
+        y1, h1 = ops.rms_norm(xg, wg, 1e-5, rg)
+    gy, gh = torch.randn_like(y1), torch.randn_like(h1)
+    (y1.float() * gy.float()).sum().add((h1.float() * gh.float()).sum()).backward()
+    xf = x.float().requires_grad_(True)
+    rf = r.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    hf = xf + rf
+    if layernorm:
+        yf = torch.nn.functional.layer_norm(hf, (H,), wf, b.float(), 1e-5)
+    else:
+        yf = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    (yf * gy.float()).sum().add((hf * gh.float()).sum()).backward()
+    _close(xg.grad, xf.grad)
+    _close(rg.grad, rf.grad)
+    _close(wg.grad, wf.grad, rtol=3e-2, atol=5e-2)
+
+
+def test_rope_and_cache():
+    B, S, Hq, Hkv, D = 2, 5, 4, 2, 128
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    cos, sin = ref.rope_tables(D, 64, device=DEV)
+    pos = (torch.arange(S, device=DEV).repeat(B) + 3).int()
+    kc = torch.zeros(B, Hkv, 16, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    slot = torch.tensor([2, 7], device=DEV, dtype=torch.int32)
+    expect = ref.rope_qkv(qkv, pos, cos, sin, Hq, Hkv, D)
+    got = ops.rope_qkv_(qkv.clone(), pos, cos, sin, Hq, Hkv, D, S=S, k_cache=kc, v_cache=vc, slot_base=slot)
+    _close(got, expect, rtol=1e-2, atol=1e-2)
+    k = expect[:, Hq * D:(Hq + Hkv) * D].reshape(B, S, Hkv, D)
+    v = expect[:, (Hq + Hkv) * D:].reshape(B, S, Hkv, D)
+    for b in range(B):
+        s0 = int(slot[b])
+        _close(kc[b, :, s0:s0 + S], k[b].transpose(0, 1), rtol=1e-2, atol=1e-2)
+        assert torch.equal(vc[b, :, s0:s0 + S], v[b].transpose(0, 1))
+    # inverse rotation recovers the input
+    back = ops.rope_qkv_(got.clone(), pos, cos, sin, Hq, Hkv, D, sign=-1.0)
+    _close(back, qkv, rtol=2e-2, atol=2e-2)
+
+
+def test_swiglu():
+    gu = torch.randn(33, 2 * 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.swiglu(gu)
+    gy = torch.randn_like(y)
+    (y.float() * gy.float()).sum().backward()
+    gf = gu.detach().float().requires_grad_(True)
+    yf = torch.nn.functional.silu(gf[:, :1024]) * gf[:, 1024:]
+    (yf * gy.float()).sum().backward()
+    _close(y, yf)
+    _close(gu.grad, gf.grad)
+
+
+def test_embed():
+    table = torch.randn(1000, 256, device=DEV, dtype=torch.bfloat16)
+    ptable = torch.randn(64, 256, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, 1000, (3, 17), device=DEV)
+    pids = torch.randint(0, 64, (3, 17), device=DEV)
+    out = ops.embedding(table, ids, ptable, pids)
+    _close(out, (table[ids].float() + ptable[pids].float()), rtol=1e-2, atol=1e-2)
+
+
+def _qkv(B, S, Hq, Hkv, D):
+    return torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+
+
+@pytest.mark.parametrize("S,causal,window,left", [(64, True, 0, False), (200, True, 0, True), (384, True, 100, False),
+                                                  (130, False, 0, False)])
+def test_flash_fwd_bwd(S, causal, window, left):
+    B, Hq, Hkv, D = 2, 8, 2, 128
+    qkv = _qkv(B, S, Hq, Hkv, D)
+    kv_start = torch.tensor([0, 37], device=DEV, dtype=torch.int32) if left else None
+    x = qkv.clone().requires_grad_(True)
+    o = ops.flash_attention_qkv(x, B, S, Hq, Hkv, D, causal, window, kv_start=kv_start)
+    go = torch.randn_like(o)
+    (o.float() * go.float()).sum().backward()
+    xr = qkv.float().requires_grad_(True)
+    q, k, v = xr[:, :Hq * D], xr[:, Hq * D:(Hq + Hkv) * D], xr[:, (Hq + Hkv) * D:]
+    orf, lse = ref.attention(q, k, v, B, S, S, Hq, Hkv, D, causal, window, None, kv_start)
+    valid = torch.ones(B * S, dtype=torch.bool, device=DEV)
+    if left:
+        valid = (torch.arange(S, device=DEV)[None, :] >= kv_start[:, None]).reshape(-1)
+    _close(o[valid], orf[valid])
+    (orf[valid].float() * go[valid].float()).sum().backward()
+    gx = x.grad.float()
+    gr = xr.grad
+    _close(gx[:, :Hq * D][valid], gr[:, :Hq * D][valid], rtol=3e-2, atol=3e-2)
+    _close(gx[:, Hq * D:], gr[:, Hq * D:], rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("D,H", [(32, 12), (64, 12)])
+def test_encoder_attention_relbias(D, H):
+    B, S = 3, 70
+    qkv = _qkv(B, S, H, H, D)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    lens = torch.tensor([70, 31, 5], device=DEV, dtype=torch.int32)
+    L = 128
+    lut = torch.randn(H, 2 * L - 1, device=DEV) * 0.5
+    o = ops.attention(q, k, v, B, S, S, H, H, D, False, kv_len=lens, rel_bias_lut=lut, rb_L=L)
+    orf, _ = ref.attention(q, k, v, B, S, S, H, H, D, False, 0, None, None, lens, lut, L)
+    _close(o, orf)
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,D,Smax", [(3, 32, 8, 128, 300), (64, 32, 8, 128, 520), (2, 12, 12, 64, 90)])
+def test_decode_attention(B, Hq, Hkv, D, Smax):
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    kc = torch.randn(B, Hkv, Smax, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    lens = torch.randint(1, Smax + 1, (B,), device=DEV, dtype=torch.int32)
+    start = (torch.rand(B, device=DEV) * lens.float() * 0.3).int()
+    for window in (0, 50):
+        o = ops.decode_attention(q, kc, vc, lens, Hq, start, window)
+        orf = ref.decode_attention(q, kc, vc, lens, Hq, start, window)
+        _close(o, orf)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_logprob_entropy(dtype):
+    T, V = 45, 32000
+    logits = (torch.randn(T, V, device=DEV) * 3).to(dtype).requires_grad_(True)
+    tgt = torch.randint(0, V, (T,), device=DEV)
+    tgt[3] = -100
+    lp, ent = ops.token_logprobs(logits, tgt, 1 / 0.7)
+    g1, g2 = torch.randn(T, device=DEV), torch.randn(T, device=DEV)
+    ((lp * g1).sum() + (ent * g2).sum()).backward()
+    lf = logits.detach().float().requires_grad_(True)
+    lpr, entr, _, _ = ref.logprob(lf, tgt, 1 / 0.7)
+    ((lpr * g1).sum() + (entr * g2).sum()).backward()
+    _close(lp, lpr, rtol=1e-3, atol=1e-3)
+    _close(ent, entr, rtol=1e-3, atol=1e-3)
+    _close(logits.grad, lf.grad, rtol=2e-2, atol=1e-4)
+
+
+def test_sampler_greedy_and_topk1():
+    logits = torch.randn(16, 32000, device=DEV, dtype=torch.bfloat16)
+    tok, lp = ops.sample(logits, 1.0, greedy=True)
+    assert torch.equal(tok, logits.float().argmax(-1))
+    off = torch.zeros(1, dtype=torch.long, device=DEV)
+    tok2, lp2 = ops.sample(logits, 1 / 0.7, top_k=1, seed=5, offset=off)
+    assert torch.equal(tok2, logits.float().argmax(-1))
+    _, lpr, _, _ = ref.logprob(logits, tok2, 1 / 0.7)
+    _close(lp2, lpr, rtol=1e-3, atol=1e-3)
+
+
+def test_sampler_distribution_and_filters():
+    V, B = 8, 20000
+    base = torch.tensor([2.0, 1.5, 1.0, 0.5, 0.0, -0.5, -1.0, -3.0], device=DEV)
+    logits = base.repeat(B, 1)
+    off = torch.zeros(1, dtype=torch.long, device=DEV)
+    tok, _ = ops.sample(logits, 1.0, seed=123, offset=off)
+    freq = torch.bincount(tok, minlength=V).float() / B
+    p = torch.softmax(base, -1)
+    assert (freq - p).abs().max().item() < 0.02
+    tok, _ = ops.sample(logits, 1.0, top_k=3, seed=7, offset=off)
+    assert int(tok.max()) <= 2
+    freq = torch.bincount(tok, minlength=V).float() / B
+    pk = torch.softmax(base[:3], -1)
+    assert (freq[:3] - pk).abs().max().item() < 0.02
+    # top-p 0.6: smallest prefix with mass >= 0.6
+    tok, _ = ops.sample(logits, 1.0, top_p=0.6, seed=9, offset=off)
+    keep = ref.filter_logits(base[None], 1.0, 0, 0.6)[0]
+    assert bool(keep[tok].all())
+    # different offsets give different draws
+    off1 = torch.ones(1, dtype=torch.long, device=DEV)
+    t0, _ = ops.sample(logits[:256], 1.0, seed=3, offset=off)
+    t1, _ = ops.sample(logits[:256], 1.0, seed=3, offset=off1)
+    assert not torch.equal(t0, t1)
+
+
+def test_adamw_matches_torch():
+    n = 10007
+    p0 = torch.randn(n, device=DEV)
+    params = [torch.nn.Parameter(p0[:5000].clone()), torch.nn.Parameter(p0[5000:].clone())]
+    flat = ops.FlatParams(params)
+    opt = ops.FusedAdamW(flat, lr=1e-2, weight_decay=0.01, max_grad_norm=0.5)
+    tp = [torch.nn.Parameter(p0[:5000].clone()), torch.nn.Parameter(p0[5000:].clone())]
+    topt = torch.optim.AdamW(tp, lr=1e-2, weight_decay=0.01)
+    for _ in range(3):
+        g = torch.randn(n, device=DEV)
+        opt.zero_grad()
+        params[0].grad.copy_(g[:5000])
+        params[1].grad.copy_(g[5000:])
+        opt.step()
+        tp[0].grad = g[:5000].clone()
+        tp[1].grad = g[5000:].clone()
+        torch.nn.utils.clip_grad_norm_(tp, 0.5)
+        topt.step()
+    _close(params[0].detach(), tp[0].detach(), rtol=1e-4, atol=1e-5)
+    _close(params[1].detach(), tp[1].detach(), rtol=1e-4, atol=1e-5)
+    # non-finite gradients skip the update
+    before = flat.data.clone()
+    opt.zero_grad()
+    params[0].grad.fill_(float("nan"))
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.equal(before, flat.data) and int(opt.skipped) == 1
+
+
+def test_pool_topk_ivf_gae():
+    x = torch.randn(4, 33, 384, device=DEV, dtype=torch.bfloat16)
+    lens = torch.tensor([33, 10, 1, 20], device=DEV, dtype=torch.int32)
+    _close(ops.pool_normalize(x, lens), ref.pool_norm(x, lens), rtol=1e-3, atol=1e-3)
+    scores = torch.randn(5, 100003, device=DEV)
+    v, i = ops.topk(scores, 10)
+    vr, ir = torch.topk(scores, 10)
+    assert torch.equal(i, ir) and torch.allclose(v, vr)
+    # ivf scan over 3 lists
+    d = 64
+    vecs = torch.randn(50, d, device=DEV, dtype=torch.bfloat16)
+    ids = torch.arange(50, device=DEV) + 1000
+    offsets = torch.tensor([0, 10, 35, 50], device=DEV, dtype=torch.int32)
+    q = torch.randn(2, d, device=DEV, dtype=torch.bfloat16)
+    probes = torch.tensor([[2, 0], [1, 2]], device=DEV, dtype=torch.int32)
+    cand, cid = ops.ivf_scan(q, probes, offsets, vecs, ids, 32)
+    full = q.float() @ vecs.float().t()
+    for qi in range(2):
+        for p in range(2):
+            L = int(probes[qi, p])
+            a, b = int(offsets[L]), int(offsets[L + 1])
+            n = min(b - a, 32)
+            _close(cand[qi, p * 32:p * 32 + n], full[qi, a:a + n], rtol=1e-2, atol=1e-2)
+            assert torch.equal(cid[qi, p * 32:p * 32 + n], ids[a:a + n])
+    r = torch.randn(3, 17, device=DEV)
+    val = torch.randn(3, 17, device=DEV)
+    mask = (torch.arange(17, device=DEV)[None] < torch.tensor([17, 9, 1], device=DEV)[:, None]).float()
+    a1, r1 = ops.gae(r, val, mask, 0.99, 0.95)
+    a2, r2 = ref.gae(r, val, mask, 0.99, 0.95)
+    _close(a1, a2, rtol=1e-4, atol=1e-5)
+    _close(r1, r2, rtol=1e-4, atol=1e-5)

@@ -1,0 +1,105 @@
+"""Model parity vs the installed HF transformers (weights copied across), CPU, fp32."""
+import os
+
+import pytest
+import torch
+
+from rag_tl_domainllm_optimizer_amd import models
+from rag_tl_domainllm_optimizer_amd.models import io
+from rag_tl_domainllm_optimizer_amd.models.config import PRESETS, config_to_hf
+
+transformers = pytest.importorskip("transformers")
+
+
+def _hf_causal(cfg):
+    d = config_to_hf(cfg)
+    d.pop("architectures", None)
+    mt = d.pop("model_type")
+    conf = transformers.AutoConfig.for_model(mt, **d)
+    conf._attn_implementation = "eager"
+    return transformers.AutoModelForCausalLM.from_config(conf).float().eval()
+
+
+def _hf_encoder(cfg):
+    d = config_to_hf(cfg)
+    d.pop("architectures", None)
+    mt = d.pop("model_type")
+    conf = transformers.AutoConfig.for_model(mt, **d)
+    conf._attn_implementation = "eager"
+    return transformers.AutoModel.from_config(conf, add_pooling_layer=False).float().eval() if mt == "bert" else \
+        transformers.AutoModel.from_config(conf, add_pooling_layer=False).float().eval()
+
+
+@pytest.mark.parametrize("preset", ["tiny-llama", "tiny-mistral", "tiny-opt"])
+def test_decoder_logits_match_hf(preset):
+    torch.manual_seed(0)
+    cfg = PRESETS[preset]
+    ours = models.CausalLM(cfg, dtype=torch.float32, seed=1)
+    hf = _hf_causal(cfg)
+    io.load_hf_state_dict(hf, {}, strict=False) if False else None
+    # ours -> HF
+    sd = io.to_hf_state_dict(ours)
+    missing, unexpected = hf.load_state_dict(sd, strict=False)
+    assert not [k for k in missing if "lm_head" not in k and "rotary" not in k], missing
+    if cfg.tie_embeddings:
+        hf.tie_weights()
+    ids = torch.randint(3, cfg.vocab_size, (2, 37))
+    with torch.no_grad():
+        h = ours(ids)
+        lg = ours.logits(h).view(2, 37, -1)
+        ref = hf(input_ids=ids).logits
+    torch.testing.assert_close(lg, ref, rtol=1e-3, atol=1e-3)
+
+
+def test_decoder_left_padding_matches_unpadded():
+    cfg = PRESETS["tiny-llama"]
+    m = models.CausalLM(cfg, dtype=torch.float32, seed=2)
+    ids = torch.randint(3, cfg.vocab_size, (1, 20))
+    padded = torch.cat([torch.zeros(1, 5, dtype=torch.long), ids], 1)
+    with torch.no_grad():
+        h1 = m(ids).view(1, 20, -1)
+        h2 = m(padded, kv_start=torch.tensor([5], dtype=torch.int32)).view(1, 25, -1)[:, 5:]
+    torch.testing.assert_close(h1, h2, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("preset", ["tiny-bert", "tiny-mpnet"])
+def test_encoder_matches_hf(preset):
+    torch.manual_seed(0)
+    cfg = PRESETS[preset]
+    ours = models.SentenceEncoder(cfg, dtype=torch.float32, seed=3)
+    hf = _hf_encoder(cfg)
+    missing, unexpected = hf.load_state_dict(io.to_hf_state_dict(ours), strict=False)
+    assert not [k for k in missing if "pooler" not in k and "position_ids" not in k], missing
+    B, S = 3, 19
+    ids = torch.randint(5, cfg.vocab_size, (B, S))
+    lens = torch.tensor([19, 7, 12])
+    mask = (torch.arange(S)[None] < lens[:, None]).long()
+    ids = torch.where(mask.bool(), ids, torch.full_like(ids, cfg.pad_token_id))
+    with torch.no_grad():
+        ours_h = ours(ids, lens).view(B, S, -1)
+        ref = hf(input_ids=ids, attention_mask=mask).last_hidden_state
+    for b in range(B):
+        n = int(lens[b])
+        torch.testing.assert_close(ours_h[b, :n], ref[b, :n], rtol=2e-3, atol=2e-3)
+
+
+def test_save_load_roundtrip_and_hf_from_pretrained(tmp_path):
+    cfg = PRESETS["tiny-llama"]
+    m = models.CausalLM(cfg, dtype=torch.float32, seed=4)
+    io.save_pretrained(m, str(tmp_path / "p"), dtype=torch.float32)
+    m2 = io.from_pretrained(str(tmp_path / "p"), dtype=torch.float32)
+    for (a, pa), (b, pb) in zip(m.named_parameters(), m2.named_parameters()):
+        assert torch.equal(pa, pb), a
+    hf = transformers.AutoModelForCausalLM.from_pretrained(str(tmp_path / "p"), torch_dtype=torch.float32)
+    ids = torch.randint(3, cfg.vocab_size, (1, 9))
+    with torch.no_grad():
+        torch.testing.assert_close(m.logits(m(ids)).view(1, 9, -1), hf(input_ids=ids).logits, rtol=1e-3, atol=1e-3)
+
+
+def test_sharded_save(tmp_path):
+    cfg = PRESETS["tiny-llama"]
+    m = models.CausalLM(cfg, dtype=torch.float32, seed=5)
+    io.save_pretrained(m, str(tmp_path / "s"), max_shard_bytes=200_000, dtype=torch.float32)
+    assert os.path.exists(tmp_path / "s" / "model.safetensors.index.json")
+    m2 = io.from_pretrained(str(tmp_path / "s"), dtype=torch.float32)
+    assert torch.equal(m.layers[1].down_w, m2.layers[1].down_w)
