@@ -1,0 +1,296 @@
+"""Batched generation: static KV cache, prefill, and a hipGraph-captured decode step.
+
+Replaces HF ``generate`` as used by the reference (rollouts rl.py:38-44, evaluation rl.py:411-417):
+prompts are left-padded into one batch, prefilled with the flash kernel (K/V appended to a static
+cache by the fused RoPE kernel), then every decode step — embedding, 32 x (norm, LoRA-fused
+projections, RoPE+append, split-K decode attention, SwiGLU), final norm, LM head, on-device
+sampler (which also emits the behaviour log-prob), value head, and the bookkeeping kernel — is one
+graph replay with zero host synchronisation. Finished rows are masked on device; the host polls
+completion only every ``sync_every`` steps.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import torch
+
+from .. import ops
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 128
+    temperature: float = 0.7            # reference rl.py:41
+    top_k: int = 50                     # HF 4.x generate default the reference ran with
+    top_p: float = 1.0
+    do_sample: bool = True              # reference rl.py:42
+    max_length: Optional[int] = None    # reference semantics: prompt + new tokens (rl.py:40)
+    stop_token_ids: Sequence[int] = ()
+    seed: int = 0
+
+    @property
+    def greedy(self) -> bool:
+        return (not self.do_sample) or self.temperature <= 0
+
+    @property
+    def inv_temp(self) -> float:
+        return 1.0 if self.greedy else 1.0 / self.temperature
+
+
+@dataclass
+class GenerationOutput:
+    tokens: torch.Tensor        # [B, T] generated ids (pad after finish)
+    lengths: torch.Tensor       # [B] number of generated tokens
+    logprobs: torch.Tensor      # [B, T] behaviour log-probs of the drawn tokens (tempered dist.)
+    values: Optional[torch.Tensor]  # [B, T] value-head outputs at each generating state
+    prompt_ids: torch.Tensor    # [B, S] left-padded prompts
+    prompt_start: torch.Tensor  # [B] first real prompt token
+    timings: dict = field(default_factory=dict)
+
+
+class KVCache:
+    def __init__(self, num_layers, B, Hkv, Smax, D, device, dtype=torch.bfloat16):
+        alloc = torch.empty if torch.device(device).type == "cuda" else torch.zeros
+        self.k = alloc(num_layers, B, Hkv, Smax, D, device=device, dtype=dtype)
+        self.v = alloc(num_layers, B, Hkv, Smax, D, device=device, dtype=dtype)
+        self.B, self.Smax = B, Smax
+
+    @property
+    def nbytes(self):
+        return 2 * self.k.numel() * self.k.element_size()
+
+
+class Generator:
+    """Owns the cache and captured graph for one (model, max_batch, max_seq) configuration."""
+
+    def __init__(self, model, max_batch: int, max_seq: int, device=None, use_graph: bool = True,
+                 value_head=None, sync_every: int = 16):
+        self.model = model
+        cfg = model.cfg
+        self.cfg = cfg
+        self.device = torch.device(device or model.embed.device)
+        self.max_batch, self.max_seq = max_batch, max_seq
+        self.use_graph = use_graph and self.device.type == "cuda"
+        self.value_head = value_head
+        self.sync_every = sync_every
+        self.cache = KVCache(cfg.num_layers, max_batch, cfg.num_kv_heads, max_seq, cfg.head_dim, self.device,
+                             model.dtype)
+        dev = self.device
+        B = max_batch
+        self.workspace = ops.decode_workspace(B, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, max_seq, dev) \
+            if dev.type == "cuda" else None
+        # device-resident decode state (static addresses for graph replay)
+        self.tok_in = torch.zeros(B, dtype=torch.long, device=dev)
+        self.kv_len = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.kv_start = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.pos = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.attn_len = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.active = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.gen_len = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.step = torch.zeros(1, dtype=torch.long, device=dev)
+        self.rng_offset = torch.zeros(1, dtype=torch.long, device=dev)
+        self.sampled = torch.zeros(B, dtype=torch.long, device=dev)
+        self.sampled_lp = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.values = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.out_tokens = None
+        self.graph = None
+        self._graph_key = None
+
+    # ------------------------------------------------------------------ one decode step (device only)
+    def _step(self, params: SamplingParams, eos_ids: torch.Tensor, pad_id: int):
+        torch.add(self.kv_len, 1, out=self.attn_len)
+        torch.sub(self.kv_len, self.kv_start, out=self.pos)
+        h = self.model.decode(self.tok_in, self.pos, self.kv_len, self.attn_len, self.kv_start, self.cache,
+                              self.workspace)
+        self._emit(h, params, eos_ids, pad_id)
+
+    def _emit(self, h, params: SamplingParams, eos_ids, pad_id):
+        logits = self.model.logits(h)
+        ops.sample(logits, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed,
+                   self.rng_offset, self.active, self.sampled, self.sampled_lp)
+        if self.value_head is not None:
+            self.values.copy_(self.value_head(h))
+        if h.is_cuda:
+            ops.native().decode_update(self.sampled, self.out_tokens, self.out_logp, self.sampled_lp,
+                                       self.out_values if self.value_head is not None else None,
+                                       self.values if self.value_head is not None else None, self.active,
+                                       self.kv_len, self.pos, self.tok_in, self.gen_len, self.step, self.rng_offset,
+                                       eos_ids, pad_id)
+        else:
+            self._update_cpu(eos_ids, pad_id)
+
+    def _update_cpu(self, eos_ids, pad_id):
+        s = int(self.step.item())
+        T = self.out_tokens.shape[1]
+        act = self.active.bool()
+        if s < T:
+            self.out_tokens[act, s] = self.sampled[act]
+            self.out_logp[act, s] = self.sampled_lp[act]
+            if self.value_head is not None:
+                self.out_values[act, s] = self.values[act]
+            self.gen_len[act] = s + 1
+            fin = torch.isin(self.sampled, eos_ids) | torch.full_like(act, s + 1 >= T)
+            self.kv_len[act] += 1
+            self.pos[act] += 1
+            self.tok_in.copy_(torch.where(act, self.sampled, torch.full_like(self.sampled, pad_id)))
+            self.active[act & fin] = 0
+        self.step += 1
+        self.rng_offset += 1
+
+    # ------------------------------------------------------------------ public
+    @torch.no_grad()
+    def generate(self, prompts: List[List[int]], params: SamplingParams, pad_id: int = 0,
+                 eos_ids: Sequence[int] = ()) -> GenerationOutput:
+        """Synchronous generation with early exit once every row has finished."""
+        return self.generate_async(prompts, params, pad_id, eos_ids, early_stop=True).result()
+
+    @torch.no_grad()
+    def generate_async(self, prompts: List[List[int]], params: SamplingParams, pad_id: int = 0,
+                       eos_ids: Sequence[int] = (), early_stop: bool = False) -> "_Pending":
+        """Enqueue prefill + all decode steps on the current stream and return without waiting
+        (unless ``early_stop``, which polls completion every ``sync_every`` steps)."""
+        import time
+
+        cfg = self.cfg
+        dev = self.device
+        B = len(prompts)
+        assert 0 < B <= self.max_batch, f"batch {B} > max_batch {self.max_batch}"
+        S = max(len(p) for p in prompts)
+        T = params.max_new_tokens
+        if params.max_length is not None:
+            T = max(1, min(T, params.max_length - S))
+        assert S + T <= self.max_seq, f"prompt {S} + new {T} exceeds cache {self.max_seq}"
+        t0 = time.perf_counter()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if dev.type == "cuda" else None
+        if ev:
+            ev[0].record()
+        ids = torch.full((B, S), pad_id, dtype=torch.long)
+        start = torch.zeros(B, dtype=torch.int32)
+        for b, p in enumerate(prompts):
+            ids[b, S - len(p):] = torch.tensor(p, dtype=torch.long)
+            start[b] = S - len(p)
+        ids = ids.to(dev, non_blocking=True)
+        MB = self.max_batch
+        # reset device state (rows >= B stay inactive)
+        self.kv_start.zero_()
+        self.kv_start[:B].copy_(start.to(dev))
+        self.active.zero_()
+        self.active[:B] = 1
+        self.gen_len.zero_()
+        self.step.zero_()
+        self.tok_in.fill_(pad_id)
+        if self.out_tokens is None or self.out_tokens.shape[1] != T:
+            self.out_tokens = torch.full((MB, T), pad_id, dtype=torch.long, device=dev)
+            self.out_logp = torch.zeros(MB, T, dtype=torch.float32, device=dev)
+            self.out_values = torch.zeros(MB, T, dtype=torch.float32, device=dev)
+            self.graph = None
+        else:
+            self.out_tokens.fill_(pad_id)
+            self.out_logp.zero_()
+            self.out_values.zero_()
+        eos_list = list(eos_ids) or [cfg.eos_token_id]
+        eos = torch.tensor(eos_list, dtype=torch.long, device=dev)
+        # prefill on the first B rows of the cache
+        sub = _SubCache(self.cache, B)
+        h_last = self.model.prefill(ids, self.kv_start[:B], sub)
+        h = torch.zeros(MB, cfg.hidden_size, dtype=h_last.dtype, device=dev)
+        h[:B] = h_last
+        # the first sampled token is not in the cache yet: the bookkeeping kernel advances kv_len
+        # to S, so the first decode step writes it at slot S
+        self.kv_len.fill_(S - 1)
+        self._emit(h, params, eos, pad_id)
+        if ev:
+            ev[1].record()
+        key = (T, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed, tuple(eos_list), pad_id)
+        steps = T - 1
+        if steps > 0:
+            if self.use_graph:
+                if self.graph is None or self._graph_key != key:
+                    self._capture(params, eos, pad_id)
+                    self._graph_key = key
+                done = 0
+                while done < steps:
+                    n = min(self.sync_every, steps - done) if early_stop else steps - done
+                    for _ in range(n):
+                        self.graph.replay()
+                    done += n
+                    if early_stop and done < steps and int(self.active.sum().item()) == 0:
+                        break
+            else:
+                for i in range(steps):
+                    self._step(params, eos, pad_id)
+                    if early_stop and (i + 1) % self.sync_every == 0 and int(self.active.sum().item()) == 0:
+                        break
+        if ev:
+            ev[2].record()
+        return _Pending(self, B, ids, start, t0, ev)
+
+    def _capture(self, params, eos, pad_id):
+        # snapshot the state the warm-up step mutates, then restore it after capture
+        saved = [t.clone() for t in self._state()]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._step(params, eos, pad_id)  # warm-up (allocations, lazy init)
+        torch.cuda.current_stream().wait_stream(s)
+        for t, v in zip(self._state(), saved):
+            t.copy_(v)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step(params, eos, pad_id)
+        for t, v in zip(self._state(), saved):
+            t.copy_(v)
+        torch.cuda.synchronize()
+        self.graph = g
+
+    def _state(self):
+        return [self.tok_in, self.kv_len, self.pos, self.attn_len, self.active, self.gen_len, self.step,
+                self.rng_offset, self.sampled, self.sampled_lp, self.values, self.out_tokens, self.out_logp,
+                self.out_values]
+
+
+class _Pending:
+    """Handle of an enqueued generation; ``result()`` waits and copies the outputs out."""
+
+    def __init__(self, gen: "Generator", B, ids, start, t0, ev):
+        self.gen, self.B, self.ids, self.start, self.t0, self.ev = gen, B, ids, start, t0, ev
+
+    def result(self) -> GenerationOutput:
+        import time
+
+        g, B = self.gen, self.B
+        if self.ev:
+            self.ev[2].synchronize()
+        t_total = time.perf_counter() - self.t0
+        tim = {"total_s": t_total}
+        if self.ev:
+            tim["prefill_s"] = self.ev[0].elapsed_time(self.ev[1]) / 1e3
+            tim["decode_s"] = self.ev[1].elapsed_time(self.ev[2]) / 1e3
+        return GenerationOutput(g.out_tokens[:B].clone(), g.gen_len[:B].clone().long(), g.out_logp[:B].clone(),
+                                g.out_values[:B].clone() if g.value_head is not None else None, self.ids,
+                                self.start.to(g.device).long(), tim)
+
+
+class _SubCache:
+    """View of the first B batch rows of a KVCache (prefill of a partial batch)."""
+
+    def __init__(self, cache: KVCache, B: int):
+        self.k = [cache.k[l, :B] for l in range(cache.k.shape[0])]
+        self.v = [cache.v[l, :B] for l in range(cache.v.shape[0])]
+
+
+def generate_text(model, tokenizer, prompts: List[str], params: SamplingParams, generator: Optional[Generator] = None,
+                  max_prompt_tokens: Optional[int] = None) -> List[str]:
+    enc = tokenizer.encode_batch(prompts)
+    if max_prompt_tokens:
+        enc = [e[-max_prompt_tokens:] for e in enc]
+    if generator is None:
+        S = max(len(e) for e in enc)
+        generator = Generator(model, len(enc), S + params.max_new_tokens + 1)
+    out = generator.generate(enc, params, pad_id=tokenizer.pad_token_id, eos_ids=[tokenizer.eos_token_id])
+    res = []
+    for b in range(len(prompts)):
+        n = int(out.lengths[b])
+        res.append(tokenizer.decode(out.tokens[b, :n].tolist()))
+    return res

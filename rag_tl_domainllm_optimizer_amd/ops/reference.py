@@ -145,6 +145,7 @@ def decode_attention(q, kc, vc, kv_len, Hq, kv_start=None, window=0, scale=None)
         lo = torch.maximum(lo, kv_len.long() - window)
     mask = (ki >= lo[:, None]) & (ki < kv_len.long()[:, None])
     s = s.masked_fill(~mask[:, None, :], float("-inf"))
+    vh = vh.masked_fill(~mask[:, None, :, None], 0.0)  # never touch unwritten cache slots
     p = torch.softmax(s, -1)
     p = torch.nan_to_num(p, nan=0.0)
     return torch.einsum("bhk,bhkd->bhd", p, vh).reshape(B, Hq * D).to(q.dtype)

@@ -1,0 +1,110 @@
+"""Process-group setup for one-process-per-GPU data parallelism.
+
+``torch.distributed`` with backend "nccl" is RCCL on ROCm (collectives over xGMI between the 8
+MI355X of a node); "gloo" is used for CPU runs and the multi-process CPU tests. Rank/world come
+from torchrun-style environment variables (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT). The
+reference is single-process, single-device (reinforcement_learning_optimization_after_rag.py:166).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: Optional[str] = None
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1 and dist.is_initialized()
+
+
+_INFO = DistInfo()
+
+
+def info() -> DistInfo:
+    return _INFO
+
+
+def init(backend: Optional[str] = None, timeout_s: float = 900.0, device: Optional[str] = None) -> DistInfo:
+    """Initialise from env (no-op for a single process). Sets the current GPU to LOCAL_RANK."""
+    global _INFO
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_cuda = (device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda")
+    if use_cuda:
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    be = backend or ("nccl" if use_cuda else "gloo")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    _INFO = DistInfo(rank, world, local, be if world > 1 else None, dev)
+    return _INFO
+
+
+def barrier():
+    if _INFO.enabled:
+        if _INFO.backend == "nccl":
+            dist.barrier(device_ids=[_INFO.device.index])
+        else:
+            dist.barrier()
+
+
+def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    if _INFO.enabled:
+        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
+    return t
+
+
+def reduce_metrics(values: dict, device=None) -> dict:
+    """Mean of scalar metrics over ranks in ONE packed all-reduce."""
+    if not _INFO.enabled or not values:
+        return dict(values)
+    keys = sorted(values)
+    vec = torch.tensor([float(values[k]) for k in keys], dtype=torch.float64,
+                       device=device or _INFO.device)
+    dist.all_reduce(vec)
+    vec /= _INFO.world
+    return {k: float(v) for k, v in zip(keys, vec.tolist())}
+
+
+def broadcast_module_(module: torch.nn.Module, src: int = 0):
+    if not _INFO.enabled:
+        return
+    for p in module.parameters():
+        dist.broadcast(p.data, src)
+
+
+def all_gather_object(obj):
+    if not _INFO.enabled:
+        return [obj]
+    out = [None] * _INFO.world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def shutdown():
+    if dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,78 @@
+"""Runtime helpers: HIP streams for overlapped phases, event timers, roctx ranges."""
+from __future__ import annotations
+
+import contextlib
+import time
+from collections import defaultdict
+
+import torch
+
+
+def _roctx():
+    try:
+        return torch.cuda.nvtx  # maps to roctx on ROCm builds
+    except Exception:  # pragma: no cover
+        return None
+
+
+@contextlib.contextmanager
+def range_(name: str):
+    """roctx range (visible in rocprofv3 --marker-trace) around a phase."""
+    nv = _roctx() if torch.cuda.is_available() else None
+    if nv is not None:
+        try:
+            nv.range_push(name)
+        except Exception:
+            nv = None
+    try:
+        yield
+    finally:
+        if nv is not None:
+            nv.range_pop()
+
+
+class PhaseTimer:
+    """Wall-clock phase timer (synchronises the device at phase boundaries when asked)."""
+
+    def __init__(self, sync: bool = True):
+        self.sync = sync and torch.cuda.is_available()
+        self.totals = defaultdict(float)
+
+    @contextlib.contextmanager
+    def phase(self, name: str):
+        if self.sync:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with range_(name):
+            yield
+        if self.sync:
+            torch.cuda.synchronize()
+        self.totals[name] += time.perf_counter() - t0
+
+    def reset(self):
+        self.totals.clear()
+
+    def as_dict(self, prefix: str = "time/"):
+        return {prefix + k: v for k, v in self.totals.items()}
+
+
+class StreamPair:
+    """A main stream and a side stream (e.g. rollout generation vs reward scoring)."""
+
+    def __init__(self, device=None):
+        self.enabled = torch.cuda.is_available() and (device is None or torch.device(device).type == "cuda")
+        self.main = torch.cuda.current_stream() if self.enabled else None
+        self.side = torch.cuda.Stream() if self.enabled else None
+
+    @contextlib.contextmanager
+    def on_side(self):
+        if not self.enabled:
+            yield
+            return
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            yield
+
+    def join(self):
+        if self.enabled:
+            torch.cuda.current_stream().wait_stream(self.side)

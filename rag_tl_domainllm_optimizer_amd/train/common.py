@@ -1,0 +1,69 @@
+"""Shared training pieces: sequence scoring (token log-probs / entropy / values in one forward),
+masked reductions, LR schedules."""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .. import ops
+
+
+def masked_mean(x: torch.Tensor, mask: torch.Tensor, dim=None) -> torch.Tensor:
+    m = mask.to(x.dtype)
+    if dim is None:
+        return (x * m).sum() / m.sum().clamp(min=1.0)
+    return (x * m).sum(dim) / m.sum(dim).clamp(min=1.0)
+
+
+def masked_whiten(x: torch.Tensor, mask: torch.Tensor, shift_mean: bool = True, eps: float = 1e-8) -> torch.Tensor:
+    mean = masked_mean(x, mask)
+    var = masked_mean((x - mean) ** 2, mask)
+    w = (x - mean) * torch.rsqrt(var + eps)
+    if not shift_mean:
+        w = w + mean
+    return w * mask.to(x.dtype)
+
+
+def response_mask(lengths: torch.Tensor, T: int) -> torch.Tensor:
+    return torch.arange(T, device=lengths.device)[None, :] < lengths[:, None]
+
+
+def score_sequences(model, prompt_ids: torch.Tensor, start: torch.Tensor, resp: torch.Tensor,
+                    resp_len: torch.Tensor, inv_temp: float = 1.0, value_head=None,
+                    gradient_checkpointing: bool = False):
+    """One forward over [prompt | response] -> per-response-token (logp, entropy, values).
+
+    The hidden state at position S-1+t produces the distribution of response token t and is also
+    the state whose value is V_t (the reference instead runs two forwards and scores a response
+    against a different prompt)."""
+    B, S = prompt_ids.shape
+    T = resp.shape[1]
+    seq = torch.cat([prompt_ids, resp], 1)
+    h = model(seq, kv_start=start.to(torch.int32), gradient_checkpointing=gradient_checkpointing)
+    H = h.shape[-1]
+    h = h.view(B, S + T, H)[:, S - 1:S + T - 1].reshape(B * T, H)
+    mask = response_mask(resp_len, T)
+    tgt = torch.where(mask, resp, torch.full_like(resp, -100)).reshape(-1)
+    logits = ops.linear(h, model.head_weight) if (torch.is_grad_enabled() and h.requires_grad) else \
+        ops.gemm(h.contiguous(), model.head_weight)
+    logp, ent = ops.token_logprobs(logits, tgt, inv_temp)
+    values = value_head(h).view(B, T) if value_head is not None else None
+    return logp.view(B, T), ent.view(B, T), values, mask
+
+
+def lr_at(step: int, base: float, schedule: str = "constant", warmup: int = 0, total: int = 0,
+          min_ratio: float = 0.0) -> float:
+    """constant / linear / cosine with linear warmup (the reference imports get_scheduler but never
+    uses it, rl.py:11)."""
+    if warmup and step < warmup:
+        return base * (step + 1) / warmup
+    if schedule == "constant" or total <= warmup:
+        return base
+    p = min(1.0, (step - warmup) / max(1, total - warmup))
+    if schedule == "linear":
+        return base * (min_ratio + (1 - min_ratio) * (1 - p))
+    if schedule == "cosine":
+        return base * (min_ratio + (1 - min_ratio) * 0.5 * (1 + math.cos(math.pi * p)))
+    raise ValueError(schedule)

@@ -1,0 +1,360 @@
+"""PPO after RAG (config 4): rollout -> reward -> frozen-reference KL -> token GAE -> clipped update.
+
+Reference: PPOTrainer / RLTrainer (reinforcement_learning_optimization_after_rag.py:127-363). Kept:
+hyper-parameter defaults (lr 5e-5, gamma 0.99, clip 0.2, value coef 0.5, entropy coef 0.01,
+max grad norm 0.5, GAE lambda 0.95, AdamW wd 0.01), the reward, the 10 logged metric keys and the
+checkpoint artifacts. Fixed: rollouts come from the current policy on the GPU (B2)
+with the same RAG prompt that is trained on (B3); log-probs are per response token (B1); the
+frozen reference enters as a per-token KL penalty (B4; the reference is the base weights with LoRA
+disabled, no third model copy); "entropy" is the true token entropy (B5); values are read at the
+last real position (B6) from the same forward as the log-probs (B7); GAE runs over tokens (B8).
+
+Device flow per step (one process per GPU, DP over RCCL):
+  generate (hipGraph decode, behaviour log-probs + values emitted by the sampler step)
+  || reward encoder on a side stream (overlapped with the next rollout chunk)
+  -> reference log-probs (LoRA off, no grad) -> token rewards / GAE kernel
+  -> ppo_epochs x minibatches of (forward, backward with bucketed all-reduce, fused AdamW).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..generation import Generator, SamplingParams
+from ..models import ValueHead
+from ..parallel import GradSync, info as dist_info, reduce_metrics
+from ..rag.prompt import build_prompt, extract_answer
+from ..runtime import PhaseTimer, StreamPair
+from ..utils import MetricsSink, maybe_inject_fault
+from .common import lr_at, masked_mean, masked_whiten, response_mask, score_sequences
+
+
+@dataclass
+class PPOConfig:
+    lr: float = 5e-5                     # rl.py:132
+    gamma: float = 0.99                  # rl.py:133
+    lam: float = 0.95                    # rl.py:188 (hard-coded there)
+    clip_range: float = 0.2              # rl.py:134
+    value_coef: float = 0.5              # rl.py:135
+    entropy_coef: float = 0.01           # rl.py:136
+    max_grad_norm: float = 0.5           # rl.py:137
+    weight_decay: float = 0.01           # torch AdamW default (rl.py:153)
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+    value_clip: Optional[float] = None
+    kl_coef: float = 0.05
+    adaptive_kl: bool = False
+    target_kl: float = 6.0
+    kl_horizon: int = 10000
+    ppo_epochs: int = 1                  # reference: one update per batch (rl.py:328)
+    minibatch_size: int = 16
+    whiten_advantages: bool = True
+    # generation (rl.py:38-44)
+    max_new_tokens: int = 128
+    temperature: float = 0.7
+    top_k: int = 50
+    top_p: float = 1.0
+    max_prompt_tokens: int = 384
+    # adapters
+    lora_r: int = 16
+    lora_alpha: float = 32.0
+    lora_targets: Sequence[str] = ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj")
+    full_finetune: bool = False
+    gradient_checkpointing: bool = False
+    overlap_reward: bool = True
+    rollout_chunks: int = 2
+    lr_schedule: str = "constant"
+    warmup_steps: int = 0
+    total_steps: int = 0
+    seed: int = 0
+
+
+class AdaptiveKL:
+    """TRL-style proportional KL controller."""
+
+    def __init__(self, init: float, target: float, horizon: int):
+        self.value, self.target, self.horizon = init, target, horizon
+
+    def update(self, current_kl: float, n_steps: int):
+        err = float(np.clip(current_kl / self.target - 1, -0.2, 0.2))
+        self.value *= 1 + err * n_steps / self.horizon
+
+
+@dataclass
+class Rollout:
+    prompt_ids: torch.Tensor
+    start: torch.Tensor
+    resp: torch.Tensor
+    resp_len: torch.Tensor
+    old_logp: torch.Tensor
+    old_values: torch.Tensor
+    scores: torch.Tensor
+    components: dict
+    responses: List[str]
+    queries: List[str]
+    ref_logp: Optional[torch.Tensor] = None
+    adv: Optional[torch.Tensor] = None
+    returns: Optional[torch.Tensor] = None
+    rewards_tok: Optional[torch.Tensor] = None
+    n_tokens: int = 0
+
+
+class PPOTrainer:
+    def __init__(self, policy, tokenizer, reward_model, cfg: Optional[PPOConfig] = None, value_head=None,
+                 sink: Optional[MetricsSink] = None, max_batch: int = 64):
+        self.cfg = cfg or PPOConfig()
+        c = self.cfg
+        self.policy = policy
+        self.tok = tokenizer
+        self.reward_model = reward_model
+        self.device = policy.embed.device
+        self.sink = sink or MetricsSink(enabled=False)
+        if c.full_finetune:
+            raise NotImplementedError("PPO trains LoRA adapters + value head; full-parameter fine-tuning is "
+                                      "provided by train.sft.SFTTrainer(full_finetune=True)")
+        if getattr(policy, "lora_config", None) is None:
+            policy.add_lora(c.lora_r, c.lora_alpha, list(c.lora_targets), seed=c.seed)
+        policy.freeze_base()
+        self.value_head = value_head or ValueHead(policy.cfg.hidden_size, device=self.device)
+        # LoRA A/B + value head re-homed into one flat fp32 buffer (fused AdamW, bucketed all-reduce)
+        self.flat = ops.FlatParams(list(policy.lora_parameters()) + list(self.value_head.parameters()))
+        policy.refresh_lora()
+        self.opt = ops.FusedAdamW(self.flat, lr=c.lr, betas=c.betas, eps=c.eps, weight_decay=c.weight_decay,
+                                  max_grad_norm=c.max_grad_norm)
+        self.sync = GradSync(self.flat)
+        self.kl = AdaptiveKL(c.kl_coef, c.target_kl, c.kl_horizon) if c.adaptive_kl else None
+        self.max_batch = max_batch
+        self.gen = Generator(policy, max_batch, c.max_prompt_tokens + c.max_new_tokens + 8, self.device,
+                             value_head=self.value_head)
+        self.sampling = SamplingParams(max_new_tokens=c.max_new_tokens, temperature=c.temperature, top_k=c.top_k,
+                                       top_p=c.top_p, do_sample=True, seed=c.seed + 1000 * dist_info().rank)
+        self.streams = StreamPair(self.device)
+        self.timer = PhaseTimer(sync=self.device.type == "cuda")
+        self.global_step = 0
+
+    @property
+    def kl_coef(self):
+        return self.kl.value if self.kl is not None else self.cfg.kl_coef
+
+    # ------------------------------------------------------------------ prompts
+    def encode_prompts(self, queries: Sequence[str], docs: Sequence[Sequence[str]]) -> List[List[int]]:
+        out = []
+        budget = self.cfg.max_prompt_tokens
+        for q, ds in zip(queries, docs):
+            ids = self.tok.encode(build_prompt(q, ds))
+            if len(ids) > budget:  # drop lowest-ranked docs until the prompt fits (SURVEY 5.7 d)
+                ds = list(ds)
+                while ds and len(ids) > budget:
+                    ds.pop()
+                    ids = self.tok.encode(build_prompt(q, ds))
+                ids = ids[-budget:]
+            out.append(ids)
+        return out
+
+    # ------------------------------------------------------------------ rollout + reward
+    @torch.no_grad()
+    def rollout(self, batch: Dict[str, list]) -> Rollout:
+        c = self.cfg
+        queries, docs = batch["query"], batch["retrieved_docs"]
+        gts = batch.get("ground_truth") or [None] * len(queries)
+        prompts = self.encode_prompts(queries, docs)
+        B = len(prompts)
+        n_chunks = max(1, min(c.rollout_chunks if c.overlap_reward else 1, B))
+        bounds = [(i * B // n_chunks, (i + 1) * B // n_chunks) for i in range(n_chunks)]
+        outs, texts, pending = [], [None] * B, []
+        scores = torch.zeros(B, device=self.device)
+        comps_all = {}
+
+        def finish_reward(lo, hi, out):
+            toks = out.tokens.cpu()
+            lens = out.lengths.cpu()
+            resp_txt = [extract_answer(self.tok.decode(toks[b, :int(lens[b])].tolist())) for b in range(hi - lo)]
+            for i, t in enumerate(resp_txt):
+                texts[lo + i] = t
+            with self.streams.on_side():
+                r, comp = self.reward_model.score(resp_txt, queries[lo:hi], docs[lo:hi], gts[lo:hi])
+            pending.append((lo, hi, r, comp))
+
+        with self.timer.phase("rollout"):
+            prev = None
+            for ci, (lo, hi) in enumerate(bounds):
+                # enqueue chunk ci (prefill + graph replays, no host sync) on the main stream ...
+                handle = self.gen.generate_async(prompts[lo:hi], self.sampling, pad_id=self.tok.pad_token_id,
+                                                 eos_ids=[self.tok.eos_token_id])
+                # ... and score chunk ci-1 on the side stream while it decodes
+                if prev is not None:
+                    finish_reward(*prev)
+                out = handle.result()
+                outs.append(out)
+                prev = (lo, hi, out)
+            finish_reward(*prev)
+            self.streams.join()
+        for lo, hi, r, comp in pending:
+            scores[lo:hi] = r
+            for k, v in comp.items():
+                comps_all.setdefault(k, []).append(v)
+        T = max(o.tokens.shape[1] for o in outs)
+        S = max(o.prompt_ids.shape[1] for o in outs)
+        pad = self.tok.pad_token_id
+
+        def cat_pad(ts, width, left, value):
+            res = []
+            for t in ts:
+                d = width - t.shape[1]
+                if d:
+                    p = torch.full((t.shape[0], d), value, dtype=t.dtype, device=t.device)
+                    t = torch.cat([p, t], 1) if left else torch.cat([t, p], 1)
+                res.append(t)
+            return torch.cat(res, 0)
+
+        prompt_ids = cat_pad([o.prompt_ids for o in outs], S, True, pad)
+        start = torch.cat([o.prompt_start + (S - o.prompt_ids.shape[1]) for o in outs], 0)
+        resp = cat_pad([o.tokens for o in outs], T, False, pad)
+        resp_len = torch.cat([o.lengths for o in outs], 0)
+        old_logp = cat_pad([o.logprobs for o in outs], T, False, 0.0)
+        old_values = cat_pad([o.values for o in outs], T, False, 0.0)
+        comps = {k: (torch.cat(v) if isinstance(v[0], torch.Tensor) else sum(v, [])) for k, v in comps_all.items()}
+        return Rollout(prompt_ids, start, resp, resp_len, old_logp, old_values, scores, comps, texts,
+                       list(queries), n_tokens=int(resp_len.sum()))
+
+    # ------------------------------------------------------------------ reference KL, GAE
+    @torch.no_grad()
+    def prepare(self, ro: Rollout):
+        c = self.cfg
+        with self.timer.phase("ref_logprobs"):
+            self.policy.set_lora_enabled(False)
+            try:
+                ref_lp = []
+                mb = c.minibatch_size
+                for s in range(0, ro.resp.shape[0], mb):
+                    lp, _, _, _ = score_sequences(self.policy, ro.prompt_ids[s:s + mb], ro.start[s:s + mb],
+                                                  ro.resp[s:s + mb], ro.resp_len[s:s + mb],
+                                                  1.0 / c.temperature)
+                    ref_lp.append(lp)
+                ro.ref_logp = torch.cat(ref_lp, 0)
+            finally:
+                self.policy.set_lora_enabled(True)
+        mask = response_mask(ro.resp_len, ro.resp.shape[1])
+        kl = (ro.old_logp - ro.ref_logp) * mask
+        rewards = -self.kl_coef * kl
+        last = (ro.resp_len - 1).clamp(min=0)
+        rewards[torch.arange(len(last), device=rewards.device), last] += ro.scores
+        rewards = rewards * mask
+        adv, ret = ops.gae(rewards, ro.old_values * mask, mask.float(), c.gamma, c.lam)
+        if c.whiten_advantages:
+            adv = masked_whiten(adv, mask)
+        ro.adv, ro.returns, ro.rewards_tok = adv, ret, rewards
+        ro.kl_ref = float(kl.sum(-1).mean())
+        return ro
+
+    # ------------------------------------------------------------------ update
+    def update(self, ro: Rollout) -> dict:
+        c = self.cfg
+        B = ro.resp.shape[0]
+        stats = {"policy_loss": [], "value_loss": [], "entropy_loss": [], "total_loss": [], "approx_kl": [],
+                 "clipfrac": [], "entropy": []}
+        inv_t = 1.0 / c.temperature
+        g = torch.Generator(device="cpu").manual_seed(c.seed + self.global_step)
+        with self.timer.phase("update"):
+            for _ in range(c.ppo_epochs):
+                perm = torch.randperm(B, generator=g).tolist()
+                for s in range(0, B, c.minibatch_size):
+                    idx = torch.tensor(perm[s:s + c.minibatch_size], device=self.device)
+                    lp, ent, vals, mask = score_sequences(self.policy, ro.prompt_ids[idx], ro.start[idx],
+                                                          ro.resp[idx], ro.resp_len[idx], inv_t, self.value_head,
+                                                          c.gradient_checkpointing)
+                    old = ro.old_logp[idx]
+                    adv = ro.adv[idx]
+                    ratio = torch.exp(lp - old)
+                    s1 = ratio * adv
+                    s2 = torch.clamp(ratio, 1 - c.clip_range, 1 + c.clip_range) * adv
+                    pg = masked_mean(-torch.min(s1, s2), mask)
+                    ret = ro.returns[idx]
+                    if c.value_clip is not None:
+                        ov = ro.old_values[idx]
+                        vc = ov + torch.clamp(vals - ov, -c.value_clip, c.value_clip)
+                        vl = 0.5 * masked_mean(torch.max((vals - ret) ** 2, (vc - ret) ** 2), mask)
+                    else:
+                        vl = 0.5 * masked_mean((vals - ret) ** 2, mask)
+                    ent_m = masked_mean(ent, mask)
+                    ent_loss = -c.entropy_coef * ent_m
+                    loss = pg + c.value_coef * vl + ent_loss
+                    self.opt.zero_grad()
+                    self.sync.start()
+                    loss.backward()
+                    self.sync.finish()
+                    lr = lr_at(self.opt.step_count, c.lr, c.lr_schedule, c.warmup_steps, c.total_steps)
+                    self.opt.step(lr)
+                    self.policy.refresh_lora()
+                    with torch.no_grad():
+                        stats["policy_loss"].append(pg.detach())
+                        stats["value_loss"].append(vl.detach())
+                        stats["entropy_loss"].append(ent_loss.detach())
+                        stats["total_loss"].append(loss.detach())
+                        stats["approx_kl"].append(masked_mean(old - lp.detach(), mask))
+                        stats["clipfrac"].append(masked_mean(((ratio.detach() - 1).abs() > c.clip_range).float(), mask))
+                        stats["entropy"].append(ent_m.detach())
+        out = {k: float(torch.stack(v).mean()) for k, v in stats.items()}
+        out["grad_norm"] = float(self.opt.last_norm)
+        out["lr"] = lr
+        return out
+
+    # ------------------------------------------------------------------ one PPO iteration
+    def step(self, batch: Dict[str, list]) -> dict:
+        self.timer.reset()
+        t0 = time.perf_counter()
+        maybe_inject_fault(self.global_step)
+        ro = self.rollout(batch)
+        self.prepare(ro)
+        upd = self.update(ro)
+        dt = time.perf_counter() - t0
+        comps = ro.components
+        m = {
+            "reward_mean": float(ro.scores.mean()), "reward_std": float(ro.scores.std(unbiased=False)),
+            "factual_accuracy": float(comps["factual_accuracy"].mean()), "relevance": float(comps["relevance"].mean()),
+            "conciseness": float(comps["conciseness"].mean()),
+            **upd, "kl_ref": ro.kl_ref, "kl_coef": self.kl_coef, "rollout_tokens": float(ro.n_tokens),
+            "response_len": float(ro.resp_len.float().mean()), "step_time_s": dt,
+        }
+        m.update(self.timer.as_dict())
+        m = reduce_metrics(m)
+        m["rollout_tokens_per_s"] = m["rollout_tokens"] * dist_info().world / max(m["step_time_s"], 1e-9)
+        if self.kl is not None:
+            self.kl.update(m["kl_ref"], len(batch["query"]))
+        self.global_step += 1
+        if dist_info().is_main:
+            self.sink.log(m, step=self.global_step)
+        self.last_rollout = ro
+        return m
+
+    # ------------------------------------------------------------------ checkpoints
+    def trainer_state(self, epoch: int = 0, best: float = -math.inf):
+        from ..utils import rng_state
+
+        return {"global_step": self.global_step, "epoch": epoch, "best_reward": best, "config": asdict(self.cfg),
+                "kl_coef": self.kl_coef, "rng": rng_state()}
+
+    def save_checkpoint(self, prefix: str, epoch: int = 0, best: float = -math.inf, full_policy: bool = True):
+        from .checkpoint import save_checkpoint
+
+        if dist_info().is_main:
+            save_checkpoint(prefix, self.policy, self.tok, self.value_head, self.opt,
+                            self.trainer_state(epoch, best), save_full_policy=full_policy)
+
+    def load_checkpoint(self, prefix: str) -> dict:
+        from ..utils import set_rng_state
+        from .checkpoint import load_checkpoint
+
+        st = load_checkpoint(prefix, self.policy, self.value_head, self.opt)
+        self.global_step = int(st.get("global_step", 0))
+        if self.kl is not None and "kl_coef" in st:
+            self.kl.value = st["kl_coef"]
+        if "rng" in st:
+            set_rng_state(st["rng"])
+        return st
