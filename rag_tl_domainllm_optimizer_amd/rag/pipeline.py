@@ -1,0 +1,100 @@
+"""End-to-end RAG answering: embed query -> index top-k -> reference prompt template -> generate.
+
+The minimum end-to-end slice of SURVEY §7.3 and config 2 ("Mistral-7B bf16 RAG answer on 1 MI355X,
+100k-doc IVF index in HBM"). Per-stage wall-clock latency is reported for every answer; this is
+the "p50 RAG answer latency" half of the headline metric (README.md:38 publishes 2.4 s / 3.1 s).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..generation import Generator, SamplingParams
+from .prompt import build_prompt, extract_answer
+
+
+@dataclass
+class RagAnswer:
+    query: str
+    answer: str
+    doc_ids: List[int]
+    docs: List[str]
+    scores: List[float]
+    timings: dict = field(default_factory=dict)
+
+
+class RagPipeline:
+    def __init__(self, encoder, index, docs: Sequence[str], model, tokenizer, top_k: int = 3,
+                 sampling: Optional[SamplingParams] = None, max_prompt_tokens: int = 1024, max_batch: int = 1,
+                 use_graph: bool = True):
+        self.encoder, self.index, self.docs = encoder, index, list(docs)
+        self.model, self.tok = model, tokenizer
+        self.top_k = top_k
+        self.sampling = sampling or SamplingParams(max_new_tokens=128)
+        self.max_prompt_tokens = max_prompt_tokens
+        self.gen = Generator(model, max_batch, max_prompt_tokens + self.sampling.max_new_tokens + 8,
+                             use_graph=use_graph)
+        self.max_batch = max_batch
+
+    @property
+    def device(self):
+        return self.model.embed.device
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    def retrieve(self, queries: Sequence[str], k: Optional[int] = None):
+        q = self.encoder.encode(list(queries))
+        return self.index.search(q, k or self.top_k)
+
+    def _prompt_ids(self, query: str, docs: List[str]) -> List[int]:
+        docs = list(docs)
+        ids = self.tok.encode(build_prompt(query, docs))
+        while len(ids) > self.max_prompt_tokens and docs:
+            docs.pop()
+            ids = self.tok.encode(build_prompt(query, docs))
+        return ids[-self.max_prompt_tokens:]
+
+    @torch.no_grad()
+    def answer(self, queries: Sequence[str]) -> List[RagAnswer]:
+        out: List[RagAnswer] = []
+        for s in range(0, len(queries), self.max_batch):
+            qs = list(queries[s:s + self.max_batch])
+            t0 = time.perf_counter()
+            scores, ids = self.retrieve(qs)
+            ids_l = ids.tolist()
+            self._sync()
+            t1 = time.perf_counter()
+            docs = [[self.docs[i] for i in row if i >= 0] for row in ids_l]
+            prompts = [self._prompt_ids(q, d) for q, d in zip(qs, docs)]
+            t2 = time.perf_counter()
+            g = self.gen.generate(prompts, self.sampling, pad_id=self.tok.pad_token_id,
+                                  eos_ids=[self.tok.eos_token_id])
+            t3 = time.perf_counter()
+            for b, q in enumerate(qs):
+                n = int(g.lengths[b])
+                text = extract_answer(self.tok.decode(g.tokens[b, :n].tolist()))
+                t4 = time.perf_counter()
+                out.append(RagAnswer(q, text, ids_l[b], docs[b], scores[b].tolist(),
+                                     {"retrieve_s": t1 - t0, "prompt_s": t2 - t1, "generate_s": t3 - t2,
+                                      "prefill_s": g.timings.get("prefill_s", 0.0),
+                                      "decode_s": g.timings.get("decode_s", 0.0),
+                                      "new_tokens": n, "total_s": t4 - t0}))
+        return out
+
+    def latency_stats(self, queries: Sequence[str], warmup: int = 2) -> dict:
+        for q in queries[:warmup]:
+            self.answer([q])
+        lat, toks = [], []
+        for q in queries:
+            a = self.answer([q])[0]
+            lat.append(a.timings["total_s"])
+            toks.append(a.timings["new_tokens"])
+        lat = np.array(lat)
+        return {"p50_s": float(np.percentile(lat, 50)), "p90_s": float(np.percentile(lat, 90)),
+                "mean_s": float(lat.mean()), "n": len(lat), "mean_new_tokens": float(np.mean(toks))}

@@ -70,6 +70,7 @@ class PPOConfig:
     overlap_reward: bool = True
     rollout_chunks: int = 2
     lr_schedule: str = "constant"
+    bucket_mb: float = 64.0
     warmup_steps: int = 0
     total_steps: int = 0
     seed: int = 0
@@ -127,7 +128,7 @@ class PPOTrainer:
         policy.refresh_lora()
         self.opt = ops.FusedAdamW(self.flat, lr=c.lr, betas=c.betas, eps=c.eps, weight_decay=c.weight_decay,
                                   max_grad_norm=c.max_grad_norm)
-        self.sync = GradSync(self.flat)
+        self.sync = GradSync(self.flat, bucket_bytes=int(c.bucket_mb * (1 << 20)))
         self.kl = AdaptiveKL(c.kl_coef, c.target_kl, c.kl_horizon) if c.adaptive_kl else None
         self.max_batch = max_batch
         self.gen = Generator(policy, max_batch, c.max_prompt_tokens + c.max_new_tokens + 8, self.device,

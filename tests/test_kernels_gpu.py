@@ -237,7 +237,7 @@ def test_sampler_greedy_and_topk1():
     off = torch.zeros(1, dtype=torch.long, device=DEV)
     tok2, lp2 = ops.sample(logits, 1 / 0.7, top_k=1, seed=5, offset=off)
     assert torch.equal(tok2, logits.float().argmax(-1))
-    _, lpr, _, _ = ref.logprob(logits, tok2, 1 / 0.7)
+    lpr, _, _, _ = ref.logprob(logits, tok2, 1 / 0.7)
     _close(lp2, lpr, rtol=1e-3, atol=1e-3)
 
 
