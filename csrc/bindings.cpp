@@ -7,7 +7,9 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "host/tokenizer.h"
@@ -15,7 +17,7 @@
 
 extern "C" {
 int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
-               long, int, int, int, int, int, hipStream_t);
+               long, int, int, int, int, int, float*, unsigned*, hipStream_t);
 int rt_norm_fwd(int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
                 hipStream_t);
 int rt_norm_bwd(int, const void*, const void*, const void*, const float*, const float*, const void*, void*, float*,
@@ -71,6 +73,26 @@ void check_rc(int rc, const char* what) {
 
 const void* opt_ptr(const optional<Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
 
+// Split-K workspace of the decode GEMM (fp32 slabs + self-resetting arrival tickets), one per
+// (device, stream) so GEMMs on concurrent streams never share tickets. Allocated on first use
+// (eager warm-up precedes graph capture); intentionally never freed.
+struct DecodeWS {
+  Tensor slabs, tickets;
+};
+DecodeWS& decode_ws(const Tensor& like, hipStream_t st) {
+  static std::mutex mu;
+  static auto* map = new std::unordered_map<uint64_t, DecodeWS*>();
+  std::lock_guard<std::mutex> g(mu);
+  const uint64_t key = (uint64_t)like.get_device() << 56 ^ (uint64_t)(uintptr_t)st;
+  auto it = map->find(key);
+  if (it != map->end()) return *it->second;
+  auto* w = new DecodeWS();
+  w->slabs = at::empty({1 << 22}, like.options().dtype(at::kFloat));
+  w->tickets = at::zeros({1 << 16}, like.options().dtype(at::kInt));
+  (*map)[key] = w;
+  return *w;
+}
+
 // ---------------------------------------------------------------------------------------------
 Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const optional<Tensor>& ub,
             const optional<Tensor>& bias, int64_t act, bool out_f32, optional<Tensor> out) {
@@ -102,9 +124,18 @@ Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const o
     c = at::empty({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   }
   if (M == 0) return c;
+  hipStream_t st = cur_stream();
+  float* slabs = nullptr;
+  unsigned* tickets = nullptr;
+  if (M <= 64) {
+    DecodeWS& ws = decode_ws(a, st);
+    slabs = ws.slabs.data_ptr<float>();
+    tickets = (unsigned*)ws.tickets.data_ptr<int>();
+    TORCH_CHECK((N + 63) / 64 <= ws.tickets.numel(), "gemm: N too large for the decode workspace");
+  }
   check_rc(rt_gemm_nt(a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), opt_ptr(u), Rp ? u->stride(0) : 0,
                       opt_ptr(ub), Rp ? ub->stride(0) : 0, Rp, opt_ptr(bias), c.data_ptr(), c.stride(0), (int)M,
-                      (int)N, (int)K, (int)act, out_f32 ? 1 : 0, cur_stream()),
+                      (int)N, (int)K, (int)act, out_f32 ? 1 : 0, slabs, tickets, st),
            "gemm");
   return c;
 }

@@ -14,10 +14,8 @@
 //    mfma_f32_16x16x32_bf16 accumulators), global_load_lds (16 B/lane) into an XOR-swizzled
 //    lane-linear LDS image (source-address swizzle, cdna_hip_programming.md rule 21), two LDS
 //    stages, XCD-aware bijective block remap + grouped tile order, LDS-staged coalesced epilogue.
-//  * gemm_skinny_kernel — M <= 64 (decode / small batch): weight streaming. One block = 16 output
-//    columns x all M rows; its 4 waves split K and stream W straight to VGPRs with a deep
-//    unrolled prefetch (LDS would be pure overhead: W is read once, cdna_hip_programming.md §5,
-//    'GEMV / M <= 16 decode weights'), cross-wave reduction through LDS.
+//  * gemm_decode_kernel — M <= 64 (decode / small batch): weight streaming, 64 columns per wave,
+//    split-K over waves and workgroups with an in-launch last-arriver reduction (see below).
 //
 // Replaces every projection GEMM of the reference's HF forward passes (reference
 // call sites reinforcement_learning_optimization_after_rag.py:38,200,207,313,318).
@@ -216,111 +214,186 @@ __global__ __launch_bounds__(256, 2) void gemm_tile_kernel(GemmArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Skinny (M <= 64) weight-streaming kernel
+// Decode GEMM (M <= 64): weight streaming with split-K and an in-launch last-arriver reduction
 // ---------------------------------------------------------------------------------------------
-// Each wave: 16 output columns (one MFMA B fragment), all MT*16 rows, a contiguous range of
-// 64-deep K chunks. Per 64-chunk, lane group g = lane>>4 owns k in [16g, 16g+16) (k-slot
-// permutation: MFMA step s uses k = 16g + 8s + j, identical for A and B, so the sum is exact) so
-// each W row is read as 4 lanes x 32 contiguous bytes = one full 128-B line per k-chunk.
-constexpr int SK_PREF = 4;  // 64-chunks in flight per wave
+// Work unit: one column group of 64 output columns (4 MFMA B fragments) x a K range. A wave owns
+// 64 columns x (K / (4*split)), so every X fragment feeds 4 MFMAs (X:W traffic 1:1 at M = 64
+// instead of 4:1 with 16-column waves). Its W rows stream straight to VGPRs (read once: no LDS,
+// cdna_hip_programming.md §5 'GEMV / M <= 16'), one 64-deep k-chunk ahead in two named register
+// sets (no runtime-indexed register arrays). Per 64-chunk, lane group g = lane>>4 owns
+// k in [16g, 16g+16): MFMA step s uses k = 16g + 8s + j for BOTH operands (exact reordering of the
+// sum), so each W row is read as one full 128-B line per chunk.
+// Reduction: the 4 waves of a block sum through LDS; the `split` blocks of a column group publish
+// fp32 slabs and the LAST arriver (agent-scope release -> relaxed ticket -> agent-scope acquire,
+// §6 Guideline 16 / §5 'In-launch split-K reduction') sums them and runs the epilogue (LoRA U*UB^T,
+// bias, activation, bf16/fp32 store), then re-arms the ticket for the next launch (graph replay).
+constexpr int DG_COLS = 64;
 
-template <int MT, bool OUT_F32>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmArgs p) {
-  __shared__ float red[4][MT * 16][17];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int n0 = blockIdx.x * 16;
-  const int frow = lane & 15, g = lane >> 4;
+template <int MT>
+struct DGRegs {
+  uint4 w[4][2];
+  uint4 x[MT][2];
+};
 
-  const int nc_main = p.K / 64;
-  const int c_begin = (wid * nc_main) / 4, c_end = ((wid + 1) * nc_main) / 4;
-
-  const int wn = min(n0 + frow, p.N - 1);
-  const bf16_t* wrow = p.B + (long)wn * p.ldb + g * 16;
-  const bf16_t* xrow[MT];
+template <int MT>
+__device__ __forceinline__ void dg_load(DGRegs<MT>& r, const bf16_t* const* wrow, const bf16_t* const* xrow, long c) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m) xrow[m] = p.A + (long)min(m * 16 + frow, p.M - 1) * p.lda + g * 16;
-
-  f32x4 acc[MT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // software pipeline: W for SK_PREF chunks ahead in registers
-  uint4 wbuf[SK_PREF][2];
-#pragma unroll
-  for (int s = 0; s < SK_PREF; ++s) {
-    const int c = c_begin + s;
-    if (c < c_end) {
-      wbuf[s][0] = *(const uint4*)(wrow + (long)c * 64);
-      wbuf[s][1] = *(const uint4*)(wrow + (long)c * 64 + 8);
-    }
+  for (int j = 0; j < 4; ++j) {
+    r.w[j][0] = *(const uint4*)(wrow[j] + c * 64);
+    r.w[j][1] = *(const uint4*)(wrow[j] + c * 64 + 8);
   }
-  for (int c0 = c_begin; c0 < c_end; c0 += SK_PREF) {
 #pragma unroll
-    for (int s = 0; s < SK_PREF; ++s) {
-      const int c = c0 + s;
-      if (c < c_end) {
-        const uint4 w0 = wbuf[s][0], w1 = wbuf[s][1];
-        const int cn = c + SK_PREF;
-        if (cn < c_end) {
-          wbuf[s][0] = *(const uint4*)(wrow + (long)cn * 64);
-          wbuf[s][1] = *(const uint4*)(wrow + (long)cn * 64 + 8);
-        }
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const uint4 x0 = *(const uint4*)(xrow[m] + (long)c * 64);
-          const uint4 x1 = *(const uint4*)(xrow[m] + (long)c * 64 + 8);
-          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x0),
-                                                           __builtin_bit_cast(bf16x8, w0), acc[m], 0, 0, 0);
-          acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x1),
-                                                           __builtin_bit_cast(bf16x8, w1), acc[m], 0, 0, 0);
-        }
-      }
-    }
+  for (int m = 0; m < MT; ++m) {
+    r.x[m][0] = *(const uint4*)(xrow[m] + c * 64);
+    r.x[m][1] = *(const uint4*)(xrow[m] + c * 64 + 8);
   }
-  // LoRA extension chunks: handled by wave 3 (its main range is last to start, roughly balanced)
-  if (p.Rp > 0 && wid == 3) {
-    const bf16_t* ubrow = p.UB + (long)wn * p.ldub + g * 16;
-    for (int c = 0; c < p.Rp / 64; ++c) {
-      const uint4 w0 = *(const uint4*)(ubrow + c * 64);
-      const uint4 w1 = *(const uint4*)(ubrow + c * 64 + 8);
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const bf16_t* urow = p.U + (long)min(m * 16 + frow, p.M - 1) * p.ldu + g * 16;
-        const uint4 x0 = *(const uint4*)(urow + c * 64);
-        const uint4 x1 = *(const uint4*)(urow + c * 64 + 8);
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x0),
-                                                         __builtin_bit_cast(bf16x8, w0), acc[m], 0, 0, 0);
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x1),
-                                                         __builtin_bit_cast(bf16x8, w1), acc[m], 0, 0, 0);
-      }
-    }
-  }
-  // acc[m] lane holds C[row = m*16 + 4g + r][col = frow]
+}
+
+template <int MT>
+__device__ __forceinline__ void dg_mma(const DGRegs<MT>& r, f32x4 (&acc)[MT][4]) {
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[wid][m * 16 + g * 4 + r][frow] = acc[m][r];
+    for (int j = 0; j < 4; ++j) {
+      acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x[m][0]),
+                                                          __builtin_bit_cast(bf16x8, r.w[j][0]), acc[m][j], 0, 0, 0);
+      acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x[m][1]),
+                                                          __builtin_bit_cast(bf16x8, r.w[j][1]), acc[m][j], 0, 0, 0);
+    }
+}
+
+template <int MT, bool OUT_F32>
+__global__ __launch_bounds__(256) void gemm_decode_kernel(GemmArgs p, float* __restrict__ slabs,
+                                                          unsigned* __restrict__ tickets, int split) {
+  constexpr int ROWS = MT * 16;
+  constexpr int LDR = DG_COLS + 1;
+  __shared__ float red[4 * ROWS * LDR];  // the ONLY __shared__ object (also carries the last-flag)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cg = blockIdx.x / split, sp = blockIdx.x % split;
+  const int n0 = cg * DG_COLS;
+  const int frow = lane & 15, g = lane >> 4;
+
+  const int nc = p.K / 64;
+  const int part = sp * 4 + wid, nparts = split * 4;
+  const int c_begin = (int)((long)part * nc / nparts), c_end = (int)((long)(part + 1) * nc / nparts);
+
+  const bf16_t* wrow[4];
+  const bf16_t* xrow[MT];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wrow[j] = p.B + (long)min(n0 + j * 16 + frow, p.N - 1) * p.ldb + g * 16;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) xrow[m] = p.A + (long)min(m * 16 + frow, p.M - 1) * p.lda + g * 16;
+
+  f32x4 acc[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  DGRegs<MT> ra, rb;
+  if (c_begin < c_end) dg_load<MT>(ra, wrow, xrow, c_begin);
+  for (int c = c_begin; c < c_end; c += 2) {
+    if (c + 1 < c_end) dg_load<MT>(rb, wrow, xrow, c + 1);
+    dg_mma<MT>(ra, acc);
+    if (c + 2 < c_end) dg_load<MT>(ra, wrow, xrow, c + 2);
+    if (c + 1 < c_end) dg_mma<MT>(rb, acc);
+  }
+
+  // ---- intra-block reduction: acc[m][j] lane holds C[m*16 + 4g + r][j*16 + frow] ----
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(wid * ROWS + m * 16 + g * 4 + r) * LDR + j * 16 + frow] = acc[m][j][r];
   __syncthreads();
-  for (int e = tid; e < MT * 16 * 16; e += 256) {
-    const int row = e >> 4, col = e & 15;
+  constexpr int NE = ROWS * DG_COLS / 256;  // elements per thread
+  float v[NE];
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int e = tid + 256 * i;
+    const int row = e / DG_COLS, col = e % DG_COLS;
+    v[i] = red[(0 * ROWS + row) * LDR + col] + red[(1 * ROWS + row) * LDR + col] + red[(2 * ROWS + row) * LDR + col] +
+           red[(3 * ROWS + row) * LDR + col];
+  }
+
+  if (split > 1) {
+    // publish this block's slab, take a ticket; the last arriver of the column group reduces
+    float* slab = slabs + ((long)cg * split + sp) * (ROWS * DG_COLS);
+#pragma unroll
+    for (int i = 0; i < NE; ++i) slab[tid + 256 * i] = v[i];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old = __hip_atomic_fetch_add(tickets + cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      red[0] = (old == (unsigned)(split - 1)) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    const bool last = red[0] != 0.f;
+    if (!last) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const float* base = slabs + (long)cg * split * (ROWS * DG_COLS);
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      float t = 0.f;
+      for (int s2 = 0; s2 < split; ++s2) t += base[(long)s2 * (ROWS * DG_COLS) + tid + 256 * i];
+      v[i] = t;
+    }
+    if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  // ---- epilogue: LoRA K-extension (U UB^T), bias, activation, store ----
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int e = tid + 256 * i;
+    const int row = e / DG_COLS, col = e % DG_COLS;
     const int grow = row, gcol = n0 + col;
     if (grow < p.M && gcol < p.N) {
-      float v = red[0][row][col] + red[1][row][col] + red[2][row][col] + red[3][row][col];
-      if (p.bias) v += bf2f(p.bias[gcol]);
-      v = apply_act(v, p.act);
-      if constexpr (OUT_F32) ((float*)p.C)[(long)grow * p.ldc + gcol] = v;
-      else ((bf16_t*)p.C)[(long)grow * p.ldc + gcol] = f2bf(v);
+      float y = v[i];
+      if (p.Rp > 0) {
+        const bf16_t* ur = p.U + (long)grow * p.ldu;
+        const bf16_t* br = p.UB + (long)gcol * p.ldub;
+        for (int k = 0; k < p.Rp; k += 8) {
+          float a8[8], b8[8];
+          unpack8(*(const uint4*)(ur + k), a8);
+          unpack8(*(const uint4*)(br + k), b8);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) y += a8[q] * b8[q];
+        }
+      }
+      if (p.bias) y += bf2f(p.bias[gcol]);
+      y = apply_act(y, p.act);
+      if constexpr (OUT_F32) ((float*)p.C)[(long)grow * p.ldc + gcol] = y;
+      else ((bf16_t*)p.C)[(long)grow * p.ldc + gcol] = f2bf(y);
     }
   }
+}
+
+// split so that the grid has >= ~2 blocks per CU while each wave keeps >= 2 k-chunks
+static int decode_split(int N, int K) {
+  const int groups = (N + DG_COLS - 1) / DG_COLS;
+  const int nc = K / 64;
+  int split = 1;
+  while (groups * split < 512 && nc / (4 * split * 2) >= 2 && split < 16) split *= 2;
+  return split;
 }
 
 }  // namespace rt
 
 using namespace rt;
 
+extern "C" int rt_gemm_decode_split(int N, int K) { return decode_split(N, K); }
+
 extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, const void* U, long ldu,
                           const void* UB, long ldub, int Rp, const void* bias, void* C, long ldc, int M,
-                          int N, int K, int act, int out_f32, hipStream_t stream) {
+                          int N, int K, int act, int out_f32, float* slabs, unsigned* tickets,
+                          hipStream_t stream) {
   GemmArgs p;
   p.A = (const bf16_t*)A; p.lda = lda;
   p.B = (const bf16_t*)B; p.ldb = ldb;
@@ -333,14 +406,15 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   if (M <= 0 || N <= 0) return 0;
   if (M <= 64) {
     const int MT = (M + 15) / 16;
-    dim3 grid((N + 15) / 16), block(256);
-#define SK_CASE(mt)                                                                              \
-  case mt:                                                                                       \
-    if (out_f32) hipLaunchKernelGGL((gemm_skinny_kernel<mt, true>), grid, block, 0, stream, p);  \
-    else hipLaunchKernelGGL((gemm_skinny_kernel<mt, false>), grid, block, 0, stream, p);         \
+    const int split = (slabs && tickets) ? decode_split(N, K) : 1;
+    dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
+#define DG_CASE(mt)                                                                                        \
+  case mt:                                                                                                 \
+    if (out_f32) hipLaunchKernelGGL((gemm_decode_kernel<mt, true>), grid, block, 0, stream, p, slabs, tickets, split); \
+    else hipLaunchKernelGGL((gemm_decode_kernel<mt, false>), grid, block, 0, stream, p, slabs, tickets, split);       \
     break;
-    switch (MT) { SK_CASE(1) SK_CASE(2) SK_CASE(3) SK_CASE(4) default: return -1; }
-#undef SK_CASE
+    switch (MT) { DG_CASE(1) DG_CASE(2) DG_CASE(3) DG_CASE(4) default: return -1; }
+#undef DG_CASE
   } else {
     const int tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     dim3 grid(tiles), block(256);

@@ -178,6 +178,185 @@ __global__ __launch_bounds__(256) void sample_kernel(const T* __restrict__ logit
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// bf16 fast path: the row (<= 80k tokens) is staged ONCE in LDS as 16-bit order-preserving keys;
+// top-k / top-p thresholds are 2-pass 8-bit radix selects over those keys with per-wave
+// histograms (no cross-wave atomic contention); Philox noise only for surviving tokens.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t key16(uint16_t b) {  // bf16 bits -> ascending unsigned key
+  return (b & 0x8000u) ? (uint32_t)(~b & 0xFFFFu) : (uint32_t)(b | 0x8000u);
+}
+__device__ __forceinline__ float key16_to_f(uint32_t k) {
+  const uint16_t b = (k & 0x8000u) ? (uint16_t)(k & 0x7FFFu) : (uint16_t)(~k & 0xFFFFu);
+  return bf2f(b);
+}
+
+__global__ __launch_bounds__(256) void sample_bf16_lds_kernel(const bf16_t* __restrict__ logits, long ld, int V,
+                                                              float inv_temp, int top_k, float top_p, int greedy,
+                                                              uint64_t seed, const int64_t* __restrict__ offset_ptr,
+                                                              const uint8_t* __restrict__ row_active,
+                                                              long* __restrict__ out_tok, float* __restrict__ out_logp) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t keys[];   // [V] (+ pad) 16-bit keys
+  __shared__ float hist[4][256];
+  __shared__ float redf[8];
+  __shared__ int redi[8];
+  __shared__ uint32_t sh_sel;
+  __shared__ float sh_f;
+  const long row = blockIdx.x;
+  const bf16_t* x = logits + row * ld;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nv = V / 8;
+
+  // stage + max/argmax (keys are monotone in the logit value)
+  uint32_t kmax = 0;
+  int amx = 0;
+  for (int c = tid; c < nv; c += 256) {
+    const uint4 v = *(const uint4*)(x + (long)c * 8);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t k0 = key16((uint16_t)(w[q] & 0xFFFF)), k1 = key16((uint16_t)(w[q] >> 16));
+      keys[c * 8 + 2 * q] = (uint16_t)k0;
+      keys[c * 8 + 2 * q + 1] = (uint16_t)k1;
+      if (k0 > kmax) { kmax = k0; amx = c * 8 + 2 * q; }
+      if (k1 > kmax) { kmax = k1; amx = c * 8 + 2 * q + 1; }
+    }
+  }
+  for (int i = nv * 8 + tid; i < V; i += 256) {
+    const uint32_t k = key16(x[i]);
+    keys[i] = (uint16_t)k;
+    if (k > kmax) { kmax = k; amx = i; }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t ok = __shfl_xor(kmax, off, 64);
+    const int oi = __shfl_xor(amx, off, 64);
+    if (ok > kmax || (ok == kmax && oi < amx)) { kmax = ok; amx = oi; }
+  }
+  if (lane == 0) { redi[wid] = amx; redf[wid] = __uint_as_float(kmax); }
+  __syncthreads();
+  uint32_t KM = __float_as_uint(redf[0]);
+  int AM = redi[0];
+  for (int w2 = 1; w2 < 4; ++w2) {
+    const uint32_t k = __float_as_uint(redf[w2]);
+    if (k > KM || (k == KM && redi[w2] < AM)) { KM = k; AM = redi[w2]; }
+  }
+  const float M = key16_to_f(KM) * inv_temp;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = tid; i < V; i += 256) s += __expf(key16_to_f(keys[i]) * inv_temp - M);
+  const float S = block_sum(s, redf);
+  const float lse = M + __logf(S);
+
+  int tok = AM;
+  const bool active = row_active ? row_active[row] != 0 : true;
+  if (!greedy && active) {
+    uint32_t kth = 0;
+    if (top_k > 0 && top_k < V) {
+      uint32_t prefix = 0;
+      unsigned remaining = top_k;
+      for (int shift = 8; shift >= 0; shift -= 8) {
+        for (int i = tid; i < 1024; i += 256) (&hist[0][0])[i] = 0.f;
+        __syncthreads();
+        const uint32_t mask = shift == 8 ? 0u : 0xFF00u;
+        for (int i = tid; i < V; i += 256) {
+          const uint32_t k = keys[i];
+          if ((k & mask) == prefix) atomicAdd(&hist[wid][(k >> shift) & 255], 1.f);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          unsigned cum = 0;
+          int bsel = 0;
+          for (int bb = 255; bb >= 0; --bb) {
+            const unsigned h = (unsigned)(hist[0][bb] + hist[1][bb] + hist[2][bb] + hist[3][bb]);
+            if (cum + h >= remaining) { bsel = bb; break; }
+            cum += h;
+          }
+          remaining -= cum;
+          sh_sel = bsel;
+        }
+        __syncthreads();
+        prefix |= sh_sel << shift;
+        __syncthreads();
+      }
+      kth = prefix;
+    }
+    uint32_t pth = kth;
+    if (top_p < 1.f) {
+      float sk = 0.f;
+      for (int i = tid; i < V; i += 256) {
+        const uint32_t k = keys[i];
+        if (k >= kth) sk += __expf(key16_to_f(k) * inv_temp - M);
+      }
+      const float target = top_p * block_sum(sk, redf);
+      uint32_t prefix = 0;
+      float above = 0.f;
+      for (int shift = 8; shift >= 0; shift -= 8) {
+        for (int i = tid; i < 1024; i += 256) (&hist[0][0])[i] = 0.f;
+        __syncthreads();
+        const uint32_t mask = shift == 8 ? 0u : 0xFF00u;
+        for (int i = tid; i < V; i += 256) {
+          const uint32_t k = keys[i];
+          if (k >= kth && (k & mask) == prefix)
+            atomicAdd(&hist[wid][(k >> shift) & 255], __expf(key16_to_f(k) * inv_temp - M));
+        }
+        __syncthreads();
+        if (tid == 0) {
+          int bsel = 0;
+          float a = above;
+          for (int bb = 255; bb >= 0; --bb) {
+            const float h = hist[0][bb] + hist[1][bb] + hist[2][bb] + hist[3][bb];
+            if (a + h >= target || bb == 0) { bsel = bb; break; }
+            a += h;
+          }
+          sh_sel = bsel;
+          sh_f = a;
+        }
+        __syncthreads();
+        prefix |= sh_sel << shift;
+        above = sh_f;
+        __syncthreads();
+      }
+      pth = prefix > kth ? prefix : kth;
+    }
+    const uint64_t off = offset_ptr ? (uint64_t)offset_ptr[0] : 0ull;
+    float best = -INFINITY;
+    int bi = AM;
+    for (int i = tid; i < V; i += 256) {
+      const uint32_t k = keys[i];
+      if (k >= pth) {
+        const uint4 r = Philox::gen(seed, (uint64_t)row, off * (uint64_t)V + (uint64_t)i);
+        const float gmb = -__logf(-__logf(u32_to_unit(r.x)));
+        const float sc = key16_to_f(k) * inv_temp + gmb;
+        if (sc > best || (sc == best && i < bi)) { best = sc; bi = i; }
+      }
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+      const float ob = __shfl_xor(best, o2, 64);
+      const int oi = __shfl_xor(bi, o2, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    __syncthreads();
+    if (lane == 0) { redf[wid] = best; redi[wid] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      float Bv = redf[0];
+      int BI = redi[0];
+      for (int w2 = 1; w2 < 4; ++w2)
+        if (redf[w2] > Bv || (redf[w2] == Bv && redi[w2] < BI)) { Bv = redf[w2]; BI = redi[w2]; }
+      redi[0] = BI;
+    }
+    __syncthreads();
+    tok = redi[0];
+  }
+  if (tid == 0) {
+    out_tok[row] = tok;
+    if (out_logp) out_logp[row] = key16_to_f(keys[tok]) * inv_temp - lse;
+  }
+}
+
 }  // namespace rt
 
 using namespace rt;
@@ -186,6 +365,13 @@ extern "C" int rt_sample(const void* logits, int is_f32, long ld, long B, int V,
                          int greedy, uint64_t seed, const int64_t* offset_ptr, const uint8_t* row_active, long* out_tok,
                          float* out_logp, hipStream_t stream) {
   if (B == 0) return 0;
+  if (!is_f32 && V % 8 == 0 && ld % 8 == 0 && (size_t)V * 2 <= 96 * 1024) {
+    const size_t shm = ((size_t)V * 2 + 15) / 16 * 16;
+    hipLaunchKernelGGL(sample_bf16_lds_kernel, dim3(B), dim3(256), shm, stream, (const bf16_t*)logits, ld, V, inv_temp,
+                       top_k, top_p, greedy, seed, offset_ptr, row_active, out_tok, out_logp);
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
   if (is_f32)
     hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(256), 0, stream, (const float*)logits, ld, V, inv_temp,
                        top_k, top_p, greedy, seed, offset_ptr, row_active, out_tok, out_logp);

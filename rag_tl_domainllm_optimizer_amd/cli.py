@@ -1,0 +1,249 @@
+"""Command line: ``python -m rag_tl_domainllm_optimizer_amd <command> [--config f.yaml] [--preset p]
+[--section.key=value ...]``.
+
+Commands: index | rag | sft | ppo | eval | pipeline | serve | bench | launch.
+Multi-GPU: ``python -m rag_tl_domainllm_optimizer_amd launch --nproc 8 ppo ...`` starts one process
+per GPU through torch.distributed.run (RCCL over xGMI) as a child process.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from typing import List, Optional
+
+import torch
+
+from . import config as C
+
+
+def _device():
+    from . import parallel
+
+    di = parallel.init()
+    return di
+
+
+def build_stack(cfg: C.RunConfig, device, need_policy=True, need_index=True):
+    """Tokenizer, policy, encoder, documents, index according to the config."""
+    from .data import SyntheticCorpus
+    from .models import build_model
+    from .retrieval import Encoder, FlatIndex, IVFIndex, chunk_documents, load_index
+    from .retrieval.chunking import read_text_file
+    from .tokenizer import load_tokenizer
+
+    dtype = getattr(torch, cfg.model.dtype) if device.type == "cuda" else torch.float32
+    out = {}
+    policy = build_model(cfg.model.policy, device=device, dtype=dtype, seed=cfg.model.seed,
+                         fast_init=device.type == "cuda") if need_policy else None
+    pcfg = policy.cfg if policy is not None else None
+    from .models import resolve_preset
+
+    if pcfg is None:
+        pcfg = resolve_preset(cfg.model.policy)
+    tok = load_tokenizer(cfg.model.policy, pcfg.vocab_size if pcfg else None, pcfg.arch if pcfg else "llama")
+    enc_model = build_model(cfg.model.encoder, device=device, dtype=dtype, seed=cfg.model.seed + 1,
+                            fast_init=device.type == "cuda").eval()
+    enc_tok = load_tokenizer(cfg.model.encoder, enc_model.cfg.vocab_size, enc_model.cfg.arch)
+    encoder = Encoder(enc_model, enc_tok)
+    corpus = None
+    if cfg.data.docs_path:
+        p = cfg.data.docs_path
+        raw = [read_text_file(os.path.join(p, f)) for f in sorted(os.listdir(p))] if os.path.isdir(p) else \
+            [l.strip() for l in open(p) if l.strip()]
+        docs, _ = chunk_documents(raw, cfg.retrieval.chunk_words, cfg.retrieval.chunk_overlap)
+    else:
+        corpus = SyntheticCorpus(tok.words(), n_docs=cfg.data.synthetic_docs, doc_words=cfg.data.doc_words,
+                                 seed=cfg.model.seed + 7)
+        docs = corpus.docs
+    index = None
+    if need_index:
+        if cfg.retrieval.index_path and os.path.exists(os.path.join(cfg.retrieval.index_path, "index.json")):
+            index = load_index(cfg.retrieval.index_path, device)
+        else:
+            emb = encoder.encode(docs)
+            if cfg.retrieval.index == "flat":
+                index = FlatIndex(encoder.dim, cfg.retrieval.metric, device)
+            else:
+                index = IVFIndex(encoder.dim, min(cfg.retrieval.nlist, max(1, len(docs) // 8)), cfg.retrieval.metric,
+                                 device, cfg.retrieval.nprobe)
+                index.train(emb)
+            index.add(emb)
+            if cfg.retrieval.index_path:
+                index.save(cfg.retrieval.index_path)
+    out.update(policy=policy, tokenizer=tok, encoder=encoder, docs=docs, corpus=corpus, index=index)
+    return out
+
+
+def _records(cfg: C.RunConfig, stack, n: int):
+    from .data import load_records
+
+    if cfg.data.train_path:
+        return load_records(cfg.data.train_path)
+    corpus, index, enc = stack["corpus"], stack["index"], stack["encoder"]
+    items = corpus.sample_queries(n, seed=cfg.model.seed + 11)
+    qs = [it.query for it in items]
+    recs = []
+    for s in range(0, len(qs), 256):
+        _, ids = index.search(enc.encode(qs[s:s + 256]), cfg.retrieval.top_k)
+        for it, row in zip(items[s:s + 256], ids.tolist()):
+            recs.append({"query": it.query, "retrieved_docs": [stack["docs"][i] for i in row if i >= 0],
+                         "ground_truth": it.ground_truth, "gold_doc": it.gold_doc})
+    return recs
+
+
+def cmd_index(cfg, args):
+    di = _device()
+    st = build_stack(cfg, di.device, need_policy=False)
+    path = cfg.retrieval.index_path or os.path.join(cfg.out_dir, cfg.name, "index")
+    st["index"].save(path)
+    print(json.dumps({"index": path, "ntotal": st["index"].ntotal, "kind": st["index"].kind}))
+
+
+def cmd_rag(cfg, args):
+    from .generation import SamplingParams
+    from .rag import RagPipeline
+
+    di = _device()
+    st = build_stack(cfg, di.device)
+    sp = SamplingParams(max_new_tokens=cfg.ppo.max_new_tokens, temperature=cfg.eval.temperature,
+                        do_sample=cfg.eval.do_sample, top_k=cfg.eval.top_k)
+    rag = RagPipeline(st["encoder"], st["index"], st["docs"], st["policy"], st["tokenizer"], cfg.retrieval.top_k, sp,
+                      cfg.ppo.max_prompt_tokens)
+    queries = args.query or [it.query for it in st["corpus"].sample_queries(4)] if st["corpus"] else args.query
+    for a in rag.answer(queries):
+        print(json.dumps({"query": a.query, "answer": a.answer, "doc_ids": a.doc_ids, "timings": a.timings}))
+
+
+def cmd_sft(cfg, args):
+    from .train import SFTTrainer, build_raft_examples
+    from .utils import MetricsSink
+
+    di = _device()
+    st = build_stack(cfg, di.device)
+    recs = _records(cfg, st, cfg.data.n_queries)
+    items = [r for r in recs if "gold_doc" in r] or recs
+    examples = build_raft_examples(items, st["docs"], cfg.raft) if "gold_doc" in items[0] else \
+        [{"prompt": __import__("rag_tl_domainllm_optimizer_amd.rag", fromlist=["build_prompt"]).build_prompt(
+            r["query"], r["retrieved_docs"]), "answer": r["ground_truth"] or ""} for r in recs]
+    run_dir = os.path.join(cfg.out_dir, cfg.name)
+    sink = MetricsSink(run_dir if di.is_main else None, config=C.to_dict(cfg), use_wandb=cfg.use_wandb)
+    tr = SFTTrainer(st["policy"], st["tokenizer"], cfg.sft, sink)
+    hist = tr.fit(examples, epochs=cfg.data.epochs)
+    tr.save(os.path.join(run_dir, "sft"))
+    if di.is_main:
+        print(json.dumps({"final_loss": hist[-1]["loss"] if hist else None, "steps": len(hist)}))
+    return tr
+
+
+def cmd_ppo(cfg, args, policy=None):
+    from .data import RecordLoader
+    from .rewards import RewardModel
+    from .train import PPOTrainer
+    from .utils import MetricsSink
+
+    di = _device()
+    st = build_stack(cfg, di.device, need_policy=policy is None)
+    if policy is not None:
+        st["policy"] = policy
+    recs = _records(cfg, st, cfg.data.n_queries)
+    run_dir = os.path.join(cfg.out_dir, cfg.name)
+    sink = MetricsSink(run_dir if di.is_main else None, config=C.to_dict(cfg), use_wandb=cfg.use_wandb)
+    tr = PPOTrainer(st["policy"], st["tokenizer"], RewardModel(st["encoder"], cfg.reward), cfg.ppo, sink=sink,
+                    max_batch=cfg.data.batch_size)
+    loader = RecordLoader(recs, cfg.data.batch_size, seed=cfg.model.seed, rank=di.rank, world=di.world)
+    best = -float("inf")
+    for ep in range(cfg.data.epochs):
+        loader.set_epoch(ep)
+        rewards = []
+        for batch in loader:
+            m = tr.step(batch)
+            rewards.append(m["reward_mean"])
+            if di.is_main:
+                print(json.dumps({k: m[k] for k in ("reward_mean", "total_loss", "kl_ref", "rollout_tokens_per_s")}),
+                      flush=True)
+        avg = sum(rewards) / max(len(rewards), 1)
+        if di.is_main:
+            print(f"Epoch {ep + 1}/{cfg.data.epochs}: Average Reward = {avg:.4f}")
+        if avg > best:
+            best = avg
+            tr.save_checkpoint(os.path.join(run_dir, "best_model"), ep, best)
+        tr.save_checkpoint(os.path.join(run_dir, f"epoch_{ep + 1}"), ep, best)
+    return tr
+
+
+def cmd_eval(cfg, args):
+    from .eval import Evaluator
+    from .models import build_model
+    from .rewards import RewardModel
+
+    di = _device()
+    st = build_stack(cfg, di.device)
+    recs = _records(cfg, st, min(cfg.data.n_queries, 64))
+    ev = Evaluator(RewardModel(st["encoder"], cfg.reward), cfg.eval)
+    models = {"Base Model": (st["policy"], st["tokenizer"])}
+    for p in args.checkpoint or []:
+        models[os.path.basename(p.rstrip("/"))] = (build_model(p, device=di.device), st["tokenizer"])
+    report = ev.compare_models(models, recs)
+    out = os.path.join(cfg.out_dir, cfg.name, "model_comparison_results.csv")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    report.to_csv(out)
+    print("Model Comparison Report:")
+    print(report)
+
+
+def cmd_pipeline(cfg, args):
+    """Config 5: RAG index -> RAFT LoRA SFT -> PPO, chained through the SFT adapter checkpoint."""
+    tr = cmd_sft(cfg, args)
+    cmd_ppo(cfg, args, policy=tr.model)
+
+
+def cmd_serve(cfg, args):
+    from .serve import serve
+
+    serve(cfg, host=args.host, port=args.port)
+
+
+def cmd_bench(cfg, args, rest):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *rest])
+    sys.exit(r.returncode)
+
+
+def cmd_launch(args, rest):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={args.port}", "-m", "rag_tl_domainllm_optimizer_amd", *rest]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.run(cmd, env=env).returncode)
+
+
+def main(argv: Optional[List[str]] = None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    ap = argparse.ArgumentParser(prog="rag_tl_domainllm_optimizer_amd")
+    ap.add_argument("command", choices=["index", "rag", "sft", "ppo", "eval", "pipeline", "serve", "bench", "launch"])
+    ap.add_argument("--config", default=None)
+    ap.add_argument("--preset", default=None, choices=sorted(C.PRESETS))
+    ap.add_argument("--query", action="append")
+    ap.add_argument("--checkpoint", action="append")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--nproc", type=int, default=1)
+    if argv and argv[0] == "launch":
+        a, rest = ap.parse_known_args(argv)
+        return cmd_launch(a, [x for x in rest])
+    if argv and argv[0] == "bench":
+        return cmd_bench(None, None, argv[1:])
+    args, rest = ap.parse_known_args(argv)
+    overrides = [r for r in rest if r.startswith("--") and "=" in r]
+    cfg = C.load(args.config, args.preset, overrides)
+    fn = {"index": cmd_index, "rag": cmd_rag, "sft": cmd_sft, "ppo": cmd_ppo, "eval": cmd_eval,
+          "pipeline": cmd_pipeline, "serve": cmd_serve}[args.command]
+    return fn(cfg, args)
+
+
+if __name__ == "__main__":
+    main()

@@ -239,6 +239,12 @@ class CausalLM(nn.Module):
         for layer in self.layers:
             layer.lora_enabled = on
 
+    def set_lora_merged(self, on: bool):
+        """Inference with merged adapter weights (W + s B A, kept in sync lazily after updates)."""
+        for layer in self.layers:
+            for g in layer.lora.values():
+                g.use_merged = on
+
     def refresh_lora(self):
         for layer in self.layers:
             for g in layer.lora.values():

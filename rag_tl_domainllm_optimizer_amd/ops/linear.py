@@ -51,6 +51,11 @@ class LoRAGroup:
     ub: Optional[torch.Tensor] = None
     r0: List[int] = field(default_factory=list)
     enabled: bool = True
+    # inference mode: W' = W + UB A_pad materialised once per adapter update (decode / prefill of
+    # rollouts read one merged weight stream instead of running the rank-Rp K-extension)
+    use_merged: bool = False
+    merged: Optional[torch.Tensor] = None
+    merged_dirty: bool = True
 
     @property
     def rank_total(self) -> int:
@@ -77,6 +82,21 @@ class LoRAGroup:
             self.a_pad[r:r + ri].copy_(a.detach() * s)
             self.ub[c0:c0 + b.shape[0], r:r + ri].copy_(b.detach())
             r += ri
+        self.merged_dirty = True
+
+    @torch.no_grad()
+    def merged_weight(self, w: torch.Tensor, rows_per_chunk: int = 4096) -> torch.Tensor:
+        """W + UB A_pad (fp32 accumulate, bf16 result), updated IN PLACE so captured graphs that
+        read it stay valid across adapter updates."""
+        if self.merged is None or self.merged.shape != w.shape or self.merged.device != w.device:
+            self.merged = torch.empty_like(w)
+            self.merged_dirty = True
+        if self.merged_dirty:
+            for r0 in range(0, w.shape[0], rows_per_chunk):
+                r1 = min(w.shape[0], r0 + rows_per_chunk)
+                self.merged[r0:r1].copy_(torch.addmm(w[r0:r1].float(), self.ub[r0:r1].float(), self.a_pad.float()))
+            self.merged_dirty = False
+        return self.merged
 
 
 class _LinearFn(torch.autograd.Function):
@@ -142,6 +162,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
     use_lora = lora is not None and lora.enabled
     if use_lora and (lora.a_pad is None or lora.a_pad.device != x.device):
         lora.refresh(dtype=w.dtype)
+    if use_lora and lora.use_merged and not torch.is_grad_enabled():
+        y = gemm(x2, lora.merged_weight(w), None, None, bias, act_id)
+        return y.reshape(*shp[:-1], w.shape[0])
     grad_needed = torch.is_grad_enabled() and (
         x2.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)
         or (use_lora and any(p.requires_grad for p in lora.a + lora.b)))

@@ -65,11 +65,15 @@ class StreamPair:
         self.side = torch.cuda.Stream() if self.enabled else None
 
     @contextlib.contextmanager
-    def on_side(self):
+    def on_side(self, wait: bool = False):
+        """Run on the side stream. ``wait=True`` orders it after everything already enqueued on the
+        main stream; leave it False when the side work only consumes host-produced inputs (then it
+        truly overlaps the main stream's queued kernels)."""
         if not self.enabled:
             yield
             return
-        self.side.wait_stream(torch.cuda.current_stream())
+        if wait:
+            self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
             yield
 

@@ -68,7 +68,8 @@ class PPOConfig:
     full_finetune: bool = False
     gradient_checkpointing: bool = False
     overlap_reward: bool = True
-    rollout_chunks: int = 2
+    rollout_chunks: int = 1          # >1: score chunk i while chunk i+1 decodes
+    merged_lora_rollout: bool = True  # decode/prefill rollouts on W + sBA (refreshed per update)
     lr_schedule: str = "constant"
     bucket_mb: float = 64.0
     warmup_steps: int = 0
@@ -104,6 +105,7 @@ class Rollout:
     returns: Optional[torch.Tensor] = None
     rewards_tok: Optional[torch.Tensor] = None
     n_tokens: int = 0
+    kl_ref: float = 0.0
 
 
 class PPOTrainer:
@@ -161,45 +163,42 @@ class PPOTrainer:
     # ------------------------------------------------------------------ rollout + reward
     @torch.no_grad()
     def rollout(self, batch: Dict[str, list]) -> Rollout:
+        """Generate responses. With ``rollout_chunks > 1`` the reward of chunk i is scored on the side
+        stream while chunk i+1 decodes; with one chunk the reward is deferred to ``prepare`` where
+        it overlaps the reference forward (one full-batch decode reads the weights half as often)."""
         c = self.cfg
         queries, docs = batch["query"], batch["retrieved_docs"]
         gts = batch.get("ground_truth") or [None] * len(queries)
         prompts = self.encode_prompts(queries, docs)
         B = len(prompts)
-        n_chunks = max(1, min(c.rollout_chunks if c.overlap_reward else 1, B))
+        n_chunks = max(1, min(c.rollout_chunks, B))
         bounds = [(i * B // n_chunks, (i + 1) * B // n_chunks) for i in range(n_chunks)]
-        outs, texts, pending = [], [None] * B, []
-        scores = torch.zeros(B, device=self.device)
-        comps_all = {}
+        outs, pending = [], []
 
-        def finish_reward(lo, hi, out):
-            toks = out.tokens.cpu()
-            lens = out.lengths.cpu()
-            resp_txt = [extract_answer(self.tok.decode(toks[b, :int(lens[b])].tolist())) for b in range(hi - lo)]
-            for i, t in enumerate(resp_txt):
-                texts[lo + i] = t
+        def score_chunk(lo, hi, out):
+            texts = self._texts(out)
             with self.streams.on_side():
-                r, comp = self.reward_model.score(resp_txt, queries[lo:hi], docs[lo:hi], gts[lo:hi])
-            pending.append((lo, hi, r, comp))
+                r, comp = self.reward_model.score(texts, queries[lo:hi], docs[lo:hi], gts[lo:hi])
+            pending.append((lo, hi, texts, r, comp))
 
-        with self.timer.phase("rollout"):
-            prev = None
-            for ci, (lo, hi) in enumerate(bounds):
-                # enqueue chunk ci (prefill + graph replays, no host sync) on the main stream ...
-                handle = self.gen.generate_async(prompts[lo:hi], self.sampling, pad_id=self.tok.pad_token_id,
-                                                 eos_ids=[self.tok.eos_token_id])
-                # ... and score chunk ci-1 on the side stream while it decodes
-                if prev is not None:
-                    finish_reward(*prev)
-                out = handle.result()
-                outs.append(out)
-                prev = (lo, hi, out)
-            finish_reward(*prev)
-            self.streams.join()
-        for lo, hi, r, comp in pending:
-            scores[lo:hi] = r
-            for k, v in comp.items():
-                comps_all.setdefault(k, []).append(v)
+        if c.merged_lora_rollout:
+            self.policy.set_lora_merged(True)
+        try:
+            with self.timer.phase("rollout"):
+                prev = None
+                for lo, hi in bounds:
+                    handle = self.gen.generate_async(prompts[lo:hi], self.sampling, pad_id=self.tok.pad_token_id,
+                                                     eos_ids=[self.tok.eos_token_id])
+                    if prev is not None:
+                        score_chunk(*prev)
+                    out = handle.result()
+                    outs.append(out)
+                    prev = (lo, hi, out)
+                if n_chunks > 1:
+                    score_chunk(*prev)
+                    self.streams.join()
+        finally:
+            self.policy.set_lora_merged(False)
         T = max(o.tokens.shape[1] for o in outs)
         S = max(o.prompt_ids.shape[1] for o in outs)
         pad = self.tok.pad_token_id
@@ -214,21 +213,47 @@ class PPOTrainer:
                 res.append(t)
             return torch.cat(res, 0)
 
-        prompt_ids = cat_pad([o.prompt_ids for o in outs], S, True, pad)
-        start = torch.cat([o.prompt_start + (S - o.prompt_ids.shape[1]) for o in outs], 0)
-        resp = cat_pad([o.tokens for o in outs], T, False, pad)
-        resp_len = torch.cat([o.lengths for o in outs], 0)
-        old_logp = cat_pad([o.logprobs for o in outs], T, False, 0.0)
-        old_values = cat_pad([o.values for o in outs], T, False, 0.0)
-        comps = {k: (torch.cat(v) if isinstance(v[0], torch.Tensor) else sum(v, [])) for k, v in comps_all.items()}
-        return Rollout(prompt_ids, start, resp, resp_len, old_logp, old_values, scores, comps, texts,
-                       list(queries), n_tokens=int(resp_len.sum()))
+        ro = Rollout(cat_pad([o.prompt_ids for o in outs], S, True, pad),
+                     torch.cat([o.prompt_start + (S - o.prompt_ids.shape[1]) for o in outs], 0),
+                     cat_pad([o.tokens for o in outs], T, False, pad), torch.cat([o.lengths for o in outs], 0),
+                     cat_pad([o.logprobs for o in outs], T, False, 0.0),
+                     cat_pad([o.values for o in outs], T, False, 0.0), None, {}, [], list(queries))
+        ro.n_tokens = int(ro.resp_len.sum())
+        ro._outs, ro._pending, ro._batch = outs, pending, (queries, docs, gts)
+        return ro
+
+    def _texts(self, out) -> List[str]:
+        toks = out.tokens.cpu()
+        lens = out.lengths.cpu()
+        return [extract_answer(self.tok.decode(toks[b, :int(lens[b])].tolist())) for b in range(toks.shape[0])]
+
+    def _collect_rewards(self, ro: Rollout):
+        queries, docs, gts = ro._batch
+        if not ro._pending:  # single chunk: score now, on the side stream (caller overlaps it)
+            texts = sum((self._texts(o) for o in ro._outs), [])
+            with self.streams.on_side():
+                r, comp = self.reward_model.score(texts, queries, docs, gts)
+            ro._pending = [(0, len(texts), texts, r, comp)]
+        self.streams.join()
+        B = ro.resp.shape[0]
+        scores = torch.zeros(B, device=self.device)
+        comps_all, texts_all = {}, []
+        for lo, hi, texts, r, comp in ro._pending:
+            scores[lo:hi] = r
+            texts_all += texts
+            for k, v in comp.items():
+                comps_all.setdefault(k, []).append(v)
+        ro.scores = scores
+        ro.responses = texts_all
+        ro.components = {k: (torch.cat(v) if isinstance(v[0], torch.Tensor) else sum(v, [])) for k, v in comps_all.items()}
 
     # ------------------------------------------------------------------ reference KL, GAE
     @torch.no_grad()
     def prepare(self, ro: Rollout):
+        """Frozen-reference log-probs (main stream) overlapped with reward scoring (side stream),
+        then token rewards (score at the last token, -beta*KL per token) and GAE."""
         c = self.cfg
-        with self.timer.phase("ref_logprobs"):
+        with self.timer.phase("ref_logprobs+reward"):
             self.policy.set_lora_enabled(False)
             try:
                 ref_lp = []
@@ -241,6 +266,8 @@ class PPOTrainer:
                 ro.ref_logp = torch.cat(ref_lp, 0)
             finally:
                 self.policy.set_lora_enabled(True)
+            # host-side detokenisation + reward encoder run while the reference forward executes
+            self._collect_rewards(ro)
         mask = response_mask(ro.resp_len, ro.resp.shape[1])
         kl = (ro.old_logp - ro.ref_logp) * mask
         rewards = -self.kl_coef * kl

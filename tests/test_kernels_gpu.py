@@ -241,10 +241,11 @@ def test_sampler_greedy_and_topk1():
     _close(lp2, lpr, rtol=1e-3, atol=1e-3)
 
 
-def test_sampler_distribution_and_filters():
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sampler_distribution_and_filters(dtype):
     V, B = 8, 20000
     base = torch.tensor([2.0, 1.5, 1.0, 0.5, 0.0, -0.5, -1.0, -3.0], device=DEV)
-    logits = base.repeat(B, 1)
+    logits = base.repeat(B, 1).to(dtype)
     off = torch.zeros(1, dtype=torch.long, device=DEV)
     tok, _ = ops.sample(logits, 1.0, seed=123, offset=off)
     freq = torch.bincount(tok, minlength=V).float() / B
@@ -264,6 +265,33 @@ def test_sampler_distribution_and_filters():
     t0, _ = ops.sample(logits[:256], 1.0, seed=3, offset=off)
     t1, _ = ops.sample(logits[:256], 1.0, seed=3, offset=off1)
     assert not torch.equal(t0, t1)
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 28672, 4096), (16, 4096, 14336), (3, 32000, 4096), (64, 6144, 4096),
+                                   (1, 1152, 384), (50, 64, 4096)])
+def test_decode_gemm_split_k_repeated(M, N, K):
+    # split-K with in-launch last-arriver reduction; tickets must re-arm across launches
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / math.sqrt(K)
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    ref_ = ref.gemm(a, w, bias=b, act=4, out_f32=True)
+    for _ in range(3):
+        _close(ops.gemm(a, w, bias=b, act=4), ref_)
+    u = torch.randn(M, 64, device=DEV, dtype=torch.bfloat16)
+    ub = torch.randn(N, 64, device=DEV, dtype=torch.bfloat16) * 0.1
+    _close(ops.gemm(a, w, u, ub, out_f32=True), ref.gemm(a, w, u, ub, out_f32=True), rtol=5e-3, atol=5e-3)
+
+
+def test_sampler_bf16_topk_topp_vocab():
+    # LDS fast path on a realistic vocabulary: only top-k survivors are ever drawn
+    B, V = 64, 32000
+    logits = (torch.randn(B, V, device=DEV) * 2).to(torch.bfloat16)
+    off = torch.zeros(1, dtype=torch.long, device=DEV)
+    tok, lp = ops.sample(logits, 1 / 0.7, top_k=50, top_p=0.9, seed=11, offset=off)
+    keep = ref.filter_logits(logits.float(), 1 / 0.7, 50, 0.9)
+    assert bool(keep.gather(1, tok[:, None]).all())
+    lpr, _, _, _ = ref.logprob(logits, tok, 1 / 0.7)
+    _close(lp, lpr, rtol=2e-3, atol=2e-3)
 
 
 def test_adamw_matches_torch():
