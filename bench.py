@@ -96,7 +96,7 @@ def main():
 
     # ---- PPO trainer ----
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
-                   lora_r=16, lora_alpha=32.0, seed=0, rollout_chunks=2, overlap_reward=True)
+                   lora_r=16, lora_alpha=32.0, seed=0, rollout_chunks=1, overlap_reward=True)
     trainer = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
     if args.no_graph:
         trainer.gen.use_graph = False
@@ -120,8 +120,14 @@ def main():
         del rag
         torch.cuda.empty_cache()
         log(f"[bench] RAG latency p50={lat['p50_s']:.3f}s p90={lat['p90_s']:.3f}s "
-            f"({lat['mean_new_tokens']:.0f} new tokens)")
+            f"({lat['mean_new_tokens']:.0f} new tokens) stages={lat['stage_mean_s']}")
     log(f"[bench] setup {time.perf_counter() - t_setup:.1f}s")
+
+    if args.steps == 0:  # latency-only (profiling) mode
+        if di.is_main:
+            print(json.dumps({"p50_rag_latency_s": lat["p50_s"] if lat else None, "rag_stages": lat}), flush=True)
+        parallel.shutdown()
+        return
 
     # ---- PPO steps ----
     for w in range(args.warmup):

@@ -193,6 +193,17 @@ class Generator:
         eos = torch.tensor(eos_list, dtype=torch.long, device=dev)
         # prefill on the first B rows of the cache
         sub = _SubCache(self.cache, B)
+        # generation never differentiates: run adapters on merged weights (one weight stream per
+        # projection; the merged images are refreshed in place after each adapter update)
+        prev_merged = self.model.set_lora_merged(True) if hasattr(self.model, "set_lora_merged") else None
+        try:
+            return self._enqueue(params, B, S, T, ids, start, eos, eos_list, pad_id, sub, early_stop, t0, ev)
+        finally:
+            if prev_merged is not None:
+                self.model.set_lora_merged(prev_merged)
+
+    def _enqueue(self, params, B, S, T, ids, start, eos, eos_list, pad_id, sub, early_stop, t0, ev):
+        cfg, dev, MB = self.cfg, self.device, self.max_batch
         h_last = self.model.prefill(ids, self.kv_start[:B], sub)
         h = torch.zeros(MB, cfg.hidden_size, dtype=h_last.dtype, device=dev)
         h[:B] = h_last

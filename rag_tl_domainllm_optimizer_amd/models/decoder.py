@@ -240,10 +240,14 @@ class CausalLM(nn.Module):
             layer.lora_enabled = on
 
     def set_lora_merged(self, on: bool):
-        """Inference with merged adapter weights (W + s B A, kept in sync lazily after updates)."""
+        """Inference with merged adapter weights (W + s B A, kept in sync lazily after updates).
+        Returns the previous setting."""
+        prev = False
         for layer in self.layers:
             for g in layer.lora.values():
+                prev = prev or g.use_merged
                 g.use_merged = on
+        return prev
 
     def refresh_lora(self):
         for layer in self.layers:

@@ -10,6 +10,7 @@ plain library GEMMs (torch.matmul -> hipBLASLt); only the forward carries fused 
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -21,9 +22,16 @@ from ._ext import native, on_gpu
 ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new": 3, "silu": 4}
 
 
+# Skinny (M <= 64) plain GEMMs: "native" = split-K MFMA decode kernel, "lib" = hipBLASLt.
+SKINNY_BACKEND = os.environ.get("RAGTL_SKINNY", "lib")
+
+
 def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None):
     """Raw (non-autograd) fused GEMM on 2-D row-major operands."""
     if on_gpu(x):
+        if (SKINNY_BACKEND == "lib" and x.shape[0] <= 64 and u is None and bias is None and act == 0
+                and not out_f32):
+            return torch.matmul(x, w.t(), out=out)
         return native().gemm(x, w, u, ub, bias, act, out_f32, out)
     y = ref.gemm(x, w, u, ub, bias, act, out_f32)
     if out is not None:

@@ -90,11 +90,14 @@ class RagPipeline:
     def latency_stats(self, queries: Sequence[str], warmup: int = 2) -> dict:
         for q in queries[:warmup]:
             self.answer([q])
-        lat, toks = [], []
+        lat, toks, stages = [], [], {}
         for q in queries:
             a = self.answer([q])[0]
             lat.append(a.timings["total_s"])
             toks.append(a.timings["new_tokens"])
+            for k in ("retrieve_s", "prompt_s", "prefill_s", "decode_s"):
+                stages.setdefault(k, []).append(a.timings[k])
         lat = np.array(lat)
         return {"p50_s": float(np.percentile(lat, 50)), "p90_s": float(np.percentile(lat, 90)),
-                "mean_s": float(lat.mean()), "n": len(lat), "mean_new_tokens": float(np.mean(toks))}
+                "mean_s": float(lat.mean()), "n": len(lat), "mean_new_tokens": float(np.mean(toks)),
+                "stage_mean_s": {k: float(np.mean(v)) for k, v in stages.items()}}
