@@ -18,6 +18,7 @@
 extern "C" {
 int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
                long, int, int, int, int, int, float*, unsigned*, hipStream_t);
+void rt_gemm_set_variant(int);
 int rt_norm_fwd(int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
                 hipStream_t);
 int rt_norm_bwd(int, const void*, const void*, const void*, const float*, const float*, const void*, void*, float*,
@@ -434,6 +435,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM C = act(A W^T + U UB^T + bias)", py::arg("a"), py::arg("w"),
         py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out_f32") = false, py::arg("out") = py::none());
+  m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
   m.def("rope_qkv", &rope_qkv);

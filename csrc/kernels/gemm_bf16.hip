@@ -21,6 +21,8 @@
 // call sites reinforcement_learning_optimization_after_rag.py:38,200,207,313,318).
 #include "rt_common.h"
 
+#include <cmath>
+
 namespace rt {
 
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3, ACT_SILU = 4 };
@@ -52,6 +54,13 @@ struct GemmArgs {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// 16-B slot swizzle of a 128-B-row LDS tile read by ds_read_b128 in 16-row lane groups: two rows
+// share a 256-B bank row, so the XOR key must differ between rows r and r+8 of the same parity.
+// (r >> 1) & 7 makes any 16 consecutive rows hit 16 distinct slots (conflict-free); (r & 7)
+// would put rows r and r+8 on the same banks (2-way). Applied on the glds SOURCE address and on
+// the read (rule 21).
+__device__ __forceinline__ int lds_swz(int row) { return (row >> 1) & 7; }
+
 // ---------------------------------------------------------------------------------------------
 // Large-M tile kernel
 // ---------------------------------------------------------------------------------------------
@@ -79,13 +88,13 @@ __global__ __launch_bounds__(256, 2) void gemm_tile_kernel(GemmArgs p) {
 
   // Per-lane staging source rows (4 A chunks + 4 B chunks per wave, 8 rows x 128 B each).
   // LDS image is lane-linear: lane l of chunk c lands at row 8c + (l>>3), 16-B slot (l&7).
-  // It must hold k-chunk slot ^ (row&7)  ->  source k-chunk = (l&7) ^ (l>>3).
+  // It must hold k-chunk slot ^ lds_swz(row)  ->  source k-chunk = (l&7) ^ lds_swz(row).
   const int r_in_chunk = lane >> 3;
-  const int src_kc = (lane & 7) ^ r_in_chunk;
   long a_row_off[4], b_row_off[4], u_row_off[4], ub_row_off[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (wid * 4 + i) * 8 + r_in_chunk;
+    const int src_kc = (lane & 7) ^ lds_swz(row);
     const int ga = min(m0 + row, p.M - 1);
     const int gb = min(n0 + row, p.N - 1);
     a_row_off[i] = (long)ga * p.lda + src_kc * 8;
@@ -145,12 +154,12 @@ __global__ __launch_bounds__(256, 2) void gemm_tile_kernel(GemmArgs p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = wr * 64 + i * 16 + frow;
-        af[i] = *(const bf16x8*)(sA + row * 128 + ((kc ^ (row & 7)) << 4));
+        af[i] = *(const bf16x8*)(sA + row * 128 + ((kc ^ lds_swz(row)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = wc * 64 + j * 16 + frow;
-        bfr[j] = *(const bf16x8*)(sB + row * 128 + ((kc ^ (row & 7)) << 4));
+        bfr[j] = *(const bf16x8*)(sB + row * 128 + ((kc ^ lds_swz(row)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -210,6 +219,236 @@ __global__ __launch_bounds__(256, 2) void gemm_tile_kernel(GemmArgs p) {
         *(uint4*)(C + (long)grow * p.ldc + gcol) = v;
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Large GEMM: 256x256x64 tile, 8 waves, 4 phases per K-tile with LDS-DMA kept in flight across
+// raw barriers (cdna_hip_programming.md §5 'The 256² 8-phase template', T1-T5)
+// ---------------------------------------------------------------------------------------------
+// LDS: two K-tile buffers x {A rows 0-127, A rows 128-255, B rows 0-127, B rows 128-255}, each a
+// 128-row x 64-k "half-tile" of 16 KiB (128-B rows, 16-B slot = k-chunk ^ lds_swz(row), written
+// lane-linearly by global_load_lds with the swizzle applied to the SOURCE address).
+// Wave (wr, wc) in a 2x4 grid owns C rows [128wr, +128) x cols [64wc, +64) = acc[8][4] fragments,
+// computed per K-tile as four 64x32 quadrants, one per phase:
+//   q0: (a0,b0)  reads A-sub0 (8 ds_read_b128) + B-sub0 (4)      stages A_lo of tile t+1
+//   q1: (a0,b1)  reads B-sub1 (4)                                stages A_hi of tile t+1
+//   q2: (a1,b1)  reads A-sub1 (8)
+//   q3: (a1,b0)  no reads (both in registers)                    stages B_lo, B_hi of tile t+2,
+//                                                                then vmcnt(4): tile t+1 landed
+// The two wave groups (wr = 0 / 1) are staggered by one barrier (T3: one group's MFMAs overlap
+// the other's ds_reads). Phase q of group 1 retires its reads before global barrier 8t+2q+2,
+// while group 0 issues phase q' DMAs after global barrier 8t'+2q'-1, so a refill must trail the
+// last read of its region by >= 2 phases: A of buffer (t+1)&1 was last read in q2 of tile t-1
+// (refilled from q0 of tile t), B of buffer t&1 in q1 of tile t (refilled in q3). RAW: tile t+1
+// is retired by q3's counted wait (leaving tile t+2's two B half-tiles = 4 DMAs in flight) before
+// the barrier that precedes either group's first read of it in q0 of tile t+1.
+constexpr int G2_HALF = 128 * 64 * 2;     // 16 KiB
+constexpr int G2_BUF = 4 * G2_HALF;       // 64 KiB per K-tile
+constexpr int G2_GROUP_M = 4;
+
+#define G2_BARRIER() asm volatile("s_barrier" ::: "memory")
+
+template <bool OUT_F32, int ACT>
+__device__ __forceinline__ void g2_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], char* smem, int m0, int n0) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int frow = lane & 15, fq = lane >> 4;
+  float bcol[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wc * 64 + j * 16 + frow;
+    bcol[j] = (p.bias && col < p.N) ? bf2f(p.bias[col]) : 0.f;
+  }
+  if constexpr (OUT_F32) {
+    float* C = (float*)p.C;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wc * 64 + j * 16 + frow;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
+          if (row < p.M && col < p.N) C[(long)row * p.ldc + col] = apply_act(acc[i][j][r] + bcol[j], ACT);
+        }
+      }
+  } else {
+    constexpr int LDT = 256 + 8;
+    bf16_t* tile = (bf16_t*)smem;
+    bf16_t* C = (bf16_t*)p.C;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (wr == half) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int col = wc * 64 + j * 16 + frow;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = i * 16 + fq * 4 + r;
+              tile[row * LDT + col] = f2bf(apply_act(acc[i][j][r] + bcol[j], ACT));
+            }
+          }
+      }
+      __syncthreads();
+      const int cc = tid & 31;
+#pragma unroll
+      for (int pass = 0; pass < 8; ++pass) {
+        const int row = pass * 16 + (tid >> 5);
+        const int grow = m0 + half * 128 + row, gcol = n0 + cc * 8;
+        if (grow < p.M && gcol < p.N) *(uint4*)(C + (long)grow * p.ldc + gcol) = *(const uint4*)(tile + row * LDT + cc * 8);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <bool OUT_F32>
+__global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * G2_BUF];  // the only __shared__ object
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int group = bid / (G2_GROUP_M * tiles_n);
+  const int first_m = group * G2_GROUP_M;
+  const int gsz = min(tiles_m - first_m, G2_GROUP_M);
+  const int tm = first_m + (bid % gsz);
+  const int tn = (bid % (G2_GROUP_M * tiles_n)) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk_main = p.K / 64;
+  const int nk = nk_main + p.Rp / 64;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int frow = lane & 15, fq = lane >> 4;
+
+  const int srow = lane >> 3;
+
+  // one half-tile (operand op: 0 = A, 1 = B; half h) of K-tile t -> buffer t & 1: 2 DMAs per lane
+  auto stage = [&](int op, int h, int t) {
+    const bf16_t* base;
+    long ld;
+    int k0;
+    if (t < nk_main) {
+      base = op ? p.B : p.A;
+      ld = op ? p.ldb : p.lda;
+      k0 = t * 64;
+    } else {
+      base = op ? p.UB : p.U;
+      ld = op ? p.ldub : p.ldu;
+      k0 = (t - nk_main) * 64;
+    }
+    const int rmax = op ? p.N - 1 : p.M - 1;
+    const int r0 = (op ? n0 : m0) + h * 128;
+    char* dst = smem + (t & 1) * G2_BUF + (op * 2 + h) * G2_HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lr = (wid * 2 + j) * 8 + srow;
+      const int gr = min(r0 + lr, rmax);
+      const bf16_t* src = base + (long)gr * ld + k0 + ((lane & 7) ^ lds_swz(lr)) * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (wid * 2 + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+
+  auto read_a = [&](int buf, int s) {
+    const char* hb = smem + buf * G2_BUF + wr * G2_HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lr = s * 64 + i * 16 + frow;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + fq;
+        fa[i][kk] = *(const bf16x8*)(hb + lr * 128 + ((c ^ lds_swz(lr)) << 4));
+      }
+    }
+  };
+  auto read_b = [&](int buf, int s, bf16x8 (&fb)[2][2]) {
+    const char* hb = smem + buf * G2_BUF + (2 + (wc >> 1)) * G2_HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lr = (wc & 1) * 64 + s * 32 + j * 16 + frow;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + fq;
+        fb[j][kk] = *(const bf16x8*)(hb + lr * 128 + ((c ^ lds_swz(lr)) << 4));
+      }
+    }
+  };
+#define G2_MMA(SA, SB, FB)                                                                        \
+  do {                                                                                           \
+    G2_BARRIER();                                                                                \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    __builtin_amdgcn_s_setprio(1);                                                               \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
+        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
+          acc[(SA) * 4 + i][(SB) * 2 + j] =                                                      \
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], FB[j][kk], acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                               \
+    G2_BARRIER();                                                                                \
+  } while (0)
+
+  // prologue: tile 0 complete + tile 1's B in flight
+  if (nk > 0) {
+    stage(0, 0, 0); stage(0, 1, 0); stage(1, 0, 0); stage(1, 1, 0);
+  }
+  if (nk > 1) {
+    stage(1, 0, 1); stage(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  G2_BARRIER();
+
+  // Wave group 1 (wr = 1) runs one barrier behind group 0: each group's MFMA cluster then
+  // overlaps the other group's LDS reads and DMA issue on the same SIMD (waves w and w+4).
+  if (wr == 1) G2_BARRIER();
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    // q0
+    read_a(buf, 0);
+    read_b(buf, 0, fb0);
+    if (t + 1 < nk) stage(0, 0, t + 1);
+    G2_MMA(0, 0, fb0);
+    // q1
+    read_b(buf, 1, fb1);
+    if (t + 1 < nk) stage(0, 1, t + 1);
+    G2_MMA(0, 1, fb1);
+    // q2
+    read_a(buf, 1);
+    G2_MMA(1, 1, fb1);
+    // q3
+    if (t + 2 < nk) {
+      stage(1, 0, t + 2);
+      stage(1, 1, t + 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    G2_MMA(1, 0, fb0);
+  }
+  if (wr == 0) G2_BARRIER();
+#undef G2_MMA
+
+  // ---- epilogue: bias + activation (dispatched once), bf16 through LDS (two 128-row passes) ----
+  switch (p.act) {
+    case ACT_RELU: g2_epilogue<OUT_F32, ACT_RELU>(p, acc, smem, m0, n0); break;
+    case ACT_GELU: g2_epilogue<OUT_F32, ACT_GELU>(p, acc, smem, m0, n0); break;
+    case ACT_GELU_TANH: g2_epilogue<OUT_F32, ACT_GELU_TANH>(p, acc, smem, m0, n0); break;
+    case ACT_SILU: g2_epilogue<OUT_F32, ACT_SILU>(p, acc, smem, m0, n0); break;
+    default: g2_epilogue<OUT_F32, ACT_NONE>(p, acc, smem, m0, n0); break;
   }
 }
 
@@ -390,6 +629,24 @@ using namespace rt;
 
 extern "C" int rt_gemm_decode_split(int N, int K) { return decode_split(N, K); }
 
+// 0 = automatic, 1 = force the 128x128 tile kernel, 2 = force the 256x256 kernel (M > 64)
+static int g_gemm_variant = 0;
+extern "C" void rt_gemm_set_variant(int v) { g_gemm_variant = v; }
+
+// Wave quantisation decides between the kernels: the 256-tile kernel runs one workgroup per CU
+// (256 slots), the 128-tile kernel two (512 slots); the 256 kernel is ~10 % faster per FLOP
+// when both fill the chip.
+static bool use_256(int M, int N) {
+  if (g_gemm_variant == 1) return false;
+  if (g_gemm_variant == 2) return true;
+  if (M < 256 || N < 256) return false;
+  const double t256 = (double)((M + 255) / 256) * ((N + 255) / 256);
+  const double t128 = (double)((M + 127) / 128) * ((N + 127) / 128);
+  const double e256 = t256 / (std::ceil(t256 / 256.0) * 256.0);
+  const double e128 = t128 / (std::ceil(t128 / 512.0) * 512.0);
+  return 1.10 * e256 >= e128;
+}
+
 extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, const void* U, long ldu,
                           const void* UB, long ldub, int Rp, const void* bias, void* C, long ldc, int M,
                           int N, int K, int act, int out_f32, float* slabs, unsigned* tickets,
@@ -415,6 +672,11 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
     break;
     switch (MT) { DG_CASE(1) DG_CASE(2) DG_CASE(3) DG_CASE(4) default: return -1; }
 #undef DG_CASE
+  } else if (use_256(M, N) && (N % 8) == 0 && (ldc % 8) == 0) {
+    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    dim3 grid(tiles), block(512);
+    if (out_f32) hipLaunchKernelGGL((gemm_256_kernel<true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((gemm_256_kernel<false>), grid, block, 0, stream, p);
   } else {
     const int tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     dim3 grid(tiles), block(256);

@@ -22,16 +22,22 @@ from ._ext import native, on_gpu
 ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new": 3, "silu": 4}
 
 
-# Skinny (M <= 64) plain GEMMs: "native" = split-K MFMA decode kernel, "lib" = hipBLASLt.
-SKINNY_BACKEND = os.environ.get("RAGTL_SKINNY", "lib")
+# Plain GEMMs (no LoRA K-extension, bias or activation epilogue, bf16 out) are library GEMMs:
+# hipBLASLt by default ("lib"), or the hand-written kernels ("native": split-K MFMA decode
+# kernel for M <= 64, 128/256 tile kernels above). Everything with a fused epilogue or LoRA
+# term always runs on the hand-written kernels. Measured on MI355X (profiles/): hipBLASLt
+# ~1.5 PF/s on large plain GEMMs vs ~1.2 PF/s for the 256x256 8-phase kernel; equal on skinny.
+PLAIN_BACKEND = os.environ.get("RAGTL_PLAIN_GEMM", "lib")
+SKINNY_BACKEND = os.environ.get("RAGTL_SKINNY", PLAIN_BACKEND)
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None):
     """Raw (non-autograd) fused GEMM on 2-D row-major operands."""
     if on_gpu(x):
-        if (SKINNY_BACKEND == "lib" and x.shape[0] <= 64 and u is None and bias is None and act == 0
-                and not out_f32):
-            return torch.matmul(x, w.t(), out=out)
+        if u is None and bias is None and act == 0 and not out_f32:
+            backend = SKINNY_BACKEND if x.shape[0] <= 64 else PLAIN_BACKEND
+            if backend == "lib":
+                return torch.matmul(x, w.t(), out=out)
         return native().gemm(x, w, u, ub, bias, act, out_f32, out)
     y = ref.gemm(x, w, u, ub, bias, act, out_f32)
     if out is not None:

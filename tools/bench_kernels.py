@@ -32,25 +32,63 @@ def timeit(fn, iters=20, warmup=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, help="comma list of kinds: gemm,lora,attn,decode,norm,loss,sample")
     args = ap.parse_args()
+    only = set(args.only.split(",")) if args.only else None
+
+    def want(k):
+        return only is None or k in only
+
+    from rag_tl_domainllm_optimizer_amd.ops import linear as _lin
+
+    _lin.SKINNY_BACKEND = _lin.PLAIN_BACKEND = "native"  # time the hand-written kernels
+    C = ops.native()
     dev = "cuda"
     res = []
     H, F, NQKV, V = 4096, 14336, 6144, 32000
     gemms = [("qkv", NQKV, H), ("o", H, H), ("gate_up", 2 * F, H), ("down", H, F), ("lm_head", V, H)]
-    for M in (1, 16, 64, 2048, 8192):
+    for M in (1, 16, 64, 512, 2048, 7168, 20480):
+        if not want("gemm"):
+            break
         for name, N, K in gemms:
             a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-            w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
-            t_ours = timeit(lambda: ops.gemm(a, w))
+            w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) / math.sqrt(K)
             t_lib = timeit(lambda: a @ w.t())
             flops = 2 * M * N * K
             byts = 2 * (N * K + M * K + M * N)
-            r = dict(kind="gemm", name=name, M=M, N=N, K=K, us=t_ours, lib_us=t_lib,
-                     tflops=flops / t_ours / 1e6, lib_tflops=flops / t_lib / 1e6, gbs=byts / t_ours / 1e3)
+            variants = [("auto", 0)] if M <= 64 else [("t128", 1), ("t256", 2), ("auto", 0)]
+            for vname, v in variants:
+                C.gemm_set_variant(v)
+                t_ours = timeit(lambda: ops.gemm(a, w))
+                r = dict(kind="gemm", variant=vname, name=name, M=M, N=N, K=K, us=t_ours, lib_us=t_lib,
+                         tflops=flops / t_ours / 1e6, lib_tflops=flops / t_lib / 1e6, gbs=byts / t_ours / 1e3)
+                res.append(r)
+                print(json.dumps(r), flush=True)
+            C.gemm_set_variant(0)
+    # skinny GEMMs with the weights streamed from HBM (rotating copies > the 256 MB Infinity
+    # Cache), which is what a decode step sees
+    for M in ((1, 8, 64) if want("cold") else ()):
+        for name, N, K in gemms:
+            ncopy = max(2, int(1.2e9 // (N * K * 2)))
+            ws_ = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) / math.sqrt(K) for _ in range(ncopy)]
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            it = [0]
+
+            def run(fn):
+                it[0] = (it[0] + 1) % ncopy
+                return fn(ws_[it[0]])
+
+            t_n = timeit(lambda: run(lambda w_: ops.gemm(a, w_)), iters=ncopy * 2)
+            t_l = timeit(lambda: run(lambda w_: a @ w_.t()), iters=ncopy * 2)
+            byts = 2 * N * K
+            r = dict(kind="gemm_cold", name=name, M=M, N=N, K=K, us=t_n, lib_us=t_l, gbs=byts / t_n / 1e3,
+                     lib_gbs=byts / t_l / 1e3)
             res.append(r)
             print(json.dumps(r), flush=True)
+            del ws_
+        torch.cuda.empty_cache()
     # LoRA-fused vs separate
-    for M in (2048, 8192):
+    for M in ((2048, 8192) if want("lora") else ()):
         N, K, R = NQKV, H, 64
         a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
@@ -62,7 +100,7 @@ def main():
         res.append(r)
         print(json.dumps(r), flush=True)
     # attention prefill fwd
-    for B, S in ((16, 384), (4, 2048)):
+    for B, S in (((16, 384), (4, 2048)) if want("attn") else ()):
         Hq, Hkv, D = 32, 8, 128
         qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
         t = timeit(lambda: ops.flash_attention_qkv(qkv, B, S, Hq, Hkv, D, True))
@@ -82,7 +120,7 @@ def main():
         res.append(r)
         print(json.dumps(r), flush=True)
     # decode attention
-    for B, L in ((1, 512), (64, 512), (64, 2048)):
+    for B, L in (((1, 512), (64, 512), (64, 2048)) if want("decode") else ()):
         Hq, Hkv, D = 32, 8, 128
         q = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
         kc = torch.randn(B, Hkv, L, D, device=dev, dtype=torch.bfloat16)
@@ -96,6 +134,11 @@ def main():
         res.append(r)
         print(json.dumps(r), flush=True)
     # norm / logprob / sampler
+    if not want("misc"):
+        if args.json:
+            with open(args.json, "w") as f:
+                json.dump(res, f, indent=1)
+        return
     x = torch.randn(8192, H, device=dev, dtype=torch.bfloat16)
     rr = torch.randn_like(x)
     w = torch.ones(H, device=dev, dtype=torch.bfloat16)
