@@ -31,6 +31,20 @@ PLAIN_BACKEND = os.environ.get("RAGTL_PLAIN_GEMM", "lib")
 SKINNY_BACKEND = os.environ.get("RAGTL_SKINNY", PLAIN_BACKEND)
 
 
+def set_gemm_backend(plain: Optional[str] = None, skinny: Optional[str] = None):
+    """Select "lib" (hipBLASLt) or "native" (hand-written kernels) for plain GEMMs; returns the
+    previous (plain, skinny) pair."""
+    global PLAIN_BACKEND, SKINNY_BACKEND
+    prev = (PLAIN_BACKEND, SKINNY_BACKEND)
+    if plain is not None:
+        assert plain in ("lib", "native")
+        PLAIN_BACKEND = plain
+    if skinny is not None:
+        assert skinny in ("lib", "native")
+        SKINNY_BACKEND = skinny
+    return prev
+
+
 def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None):
     """Raw (non-autograd) fused GEMM on 2-D row-major operands."""
     if on_gpu(x):

@@ -22,15 +22,12 @@ def setup_module(_):
     torch.manual_seed(0)
     assert ops.native_available(), "native extension must load on the GPU box"
     # plain GEMMs default to hipBLASLt in the framework; these tests exercise the HIP kernels
-    from rag_tl_domainllm_optimizer_amd.ops import linear
-
-    linear.PLAIN_BACKEND = linear.SKINNY_BACKEND = "native"
+    global _PREV_BACKEND
+    _PREV_BACKEND = ops.set_gemm_backend("native", "native")
 
 
 def teardown_module(_):
-    from rag_tl_domainllm_optimizer_amd.ops import linear
-
-    linear.PLAIN_BACKEND = linear.SKINNY_BACKEND = "lib"
+    ops.set_gemm_backend(*_PREV_BACKEND)
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (300, 1000, 512), (1024, 6144, 1024), (1, 4096, 4096),

@@ -39,9 +39,7 @@ def main():
     def want(k):
         return only is None or k in only
 
-    from rag_tl_domainllm_optimizer_amd.ops import linear as _lin
-
-    _lin.SKINNY_BACKEND = _lin.PLAIN_BACKEND = "native"  # time the hand-written kernels
+    ops.set_gemm_backend("native", "native")  # time the hand-written kernels, not hipBLASLt
     C = ops.native()
     dev = "cuda"
     res = []
