@@ -32,6 +32,10 @@ int rt_attn_fwd(const void*, long, const void*, long, const void*, long, void*, 
                 const float*, int, int, int, int, int, int, int, int, int, float, hipStream_t);
 int rt_attn_decode(const void*, long, const void*, const void*, int, const int*, const int*, int, float*, int, int,
                    void*, long, int, int, int, int, float, hipStream_t);
+int rt_attn_decode_fused(const void*, long, void*, void*, int, const int*, const int*, const int*, const int*,
+                         const float*, const float*, float, int, float*, unsigned*, int, int, void*, long, int, int, int,
+                         int, float, hipStream_t);
+int rt_attn_decode_fused_ps(int, int);
 int rt_attn_bwd(const void*, long, const void*, long, const void*, long, const void*, long, const void*, long,
                 const float*, float*, float*, void*, long, void*, long, void*, long, const int*, int, int, int, int,
                 int, int, int, float, hipStream_t);
@@ -276,6 +280,40 @@ void attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, const Tens
            "attn_decode");
 }
 
+void attn_decode_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& slot, const Tensor& attn_len,
+                       const optional<Tensor>& kv_start, const optional<Tensor>& pos, const optional<Tensor>& cos,
+                       const optional<Tensor>& sin, double sign, int64_t window, double scale, int64_t Hq, Tensor part,
+                       Tensor tickets, int64_t PS, Tensor out) {
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_ROWS(qkv); CHECK_BF16(kc); CHECK_BF16(vc); CHECK_I32(slot);
+  CHECK_I32(attn_len); CHECK_F32(part); CHECK_I32(tickets); CHECK_BF16(out); CHECK_ROWS(out);
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes(),
+              "attn_decode_fused: cache layout");
+  const int64_t B = kc.size(0), Hkv = kc.size(1), Smax = kc.size(2), D = kc.size(3);
+  const int64_t NP = (Smax + PS - 1) / PS, G = Hq / Hkv;
+  TORCH_CHECK(G * Hkv == Hq, "attn_decode_fused: Hq must be a multiple of Hkv");
+  TORCH_CHECK(qkv.size(0) == B && out.size(0) == B && slot.numel() == B && attn_len.numel() == B,
+              "attn_decode_fused: batch");
+  TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * D && out.size(1) >= Hq * D, "attn_decode_fused: widths");
+  TORCH_CHECK(part.numel() >= B * Hkv * NP * G * (D + 2), "attn_decode_fused: partial workspace too small");
+  TORCH_CHECK(tickets.numel() >= B * Hkv, "attn_decode_fused: ticket workspace too small");
+  const bool rot = cos.has_value() && cos->defined();
+  if (rot) {
+    CHECK_F32(*cos); CHECK_F32(*sin);
+    TORCH_CHECK(pos.has_value() && pos->defined(), "attn_decode_fused: rotary needs pos");
+    CHECK_I32(*pos);
+    TORCH_CHECK(cos->size(-1) == D / 2 && cos->is_contiguous() && sin->is_contiguous(), "attn_decode_fused: tables");
+  }
+  if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
+  check_rc(rt_attn_decode_fused(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), (int)Smax,
+                                slot.data_ptr<int>(), attn_len.data_ptr<int>(), (const int*)opt_ptr(kv_start),
+                                rot ? pos->data_ptr<int>() : nullptr, rot ? cos->data_ptr<float>() : nullptr,
+                                rot ? sin->data_ptr<float>() : nullptr, (float)sign, (int)window,
+                                part.data_ptr<float>(), (unsigned*)tickets.data_ptr<int>(), (int)NP, (int)PS,
+                                out.data_ptr(), out.stride(0), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
+                                cur_stream()),
+           "attn_decode_fused");
+}
+
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout, const Tensor& lse,
               Tensor dq, Tensor dk, Tensor dv, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D, bool causal,
               int64_t window, double scale, const optional<Tensor>& kv_start) {
@@ -436,6 +474,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out_f32") = false, py::arg("out") = py::none());
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
+  m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
+  m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
   m.def("rope_qkv", &rope_qkv);

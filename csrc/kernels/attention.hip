@@ -438,6 +438,297 @@ __global__ __launch_bounds__(256) void attn_decode_combine_kernel(DecodeArgs a) 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Fused decode step: RoPE(q, k_new) + KV-cache append + split-K attention + in-launch combine
+// ---------------------------------------------------------------------------------------------
+// Replaces rope_qkv + attn_decode + attn_decode_combine (three launches, each a dependent global
+// round trip at decode sizes) by one. Grid (NP partitions, Hkv, B); partition p owns keys
+// [p*PS, (p+1)*PS). Every lane issues ALL of its K and V loads for the partition up front (NK keys
+// each, 16 B per key per operand), so a block costs one memory round trip. The block owning the
+// new token's slot rotates k_new, writes k/v into the cache and uses them from registers. Partials
+// (m, l, o) go to a workspace; the last-arriving partition of (b, kv-head) merges them (agent-scope
+// release -> relaxed ticket -> acquire, as in gemm_decode_kernel) and re-arms the ticket for the
+// next graph replay.
+struct DecodeFusedArgs {
+  const bf16_t* qkv; long ldq;      // [B, ldq] = q heads | k heads | v heads of the new token (pre-RoPE)
+  bf16_t* kc; bf16_t* vc; int Smax; // [B, Hkv, Smax, D]
+  const int* slot;                  // [B] cache slot of the new token
+  const int* attn_len;              // [B] keys attended (normally slot + 1)
+  const int* kv_start;              // [B] first valid slot (left padding) or null
+  const int* pos;                   // [B] rotary position of the new token
+  const float* cosT; const float* sinT; float sign;  // [P, D/2] tables or null (no rotary)
+  int window;
+  float* part;                      // [B, Hkv, NP, G, D + 2]
+  unsigned* tickets;                // [B * Hkv], zero between launches
+  bf16_t* o; long ldo;
+  int B, Hq, Hkv, NP, PS;
+  float scale_log2;
+};
+
+template <int D>
+__device__ __forceinline__ void rope_chunk(const bf16_t* head, int dl, const DecodeFusedArgs& a, int p,
+                                           float (&out)[8]) {
+  constexpr int HALF = D / 16;  // chunks of 8 in half a head
+  float x[8];
+  unpack8(*(const uint4*)(head + dl * 8), x);
+  if (a.cosT) {
+    float y[8];
+    unpack8(*(const uint4*)(head + (dl ^ HALF) * 8), y);
+    const int j0 = (dl & (HALF - 1)) * 8;
+    const float* cr = a.cosT + (long)p * (D / 2) + j0;
+    const float* sr = a.sinT + (long)p * (D / 2) + j0;
+    const float4 c0 = *(const float4*)cr, c1 = *(const float4*)(cr + 4);
+    const float4 s0 = *(const float4*)sr, s1 = *(const float4*)(sr + 4);
+    const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const bool lo = dl < HALF;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float sv = a.sign * sn[k];
+      out[k] = lo ? x[k] * cs[k] - y[k] * sv : x[k] * cs[k] + y[k] * sv;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = x[k];
+  }
+  // the unfused path stores rotated rows in bf16: round identically
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = bf2f(f2bf(out[k]));
+}
+
+// One key chunk: CH = 4 waves x KPW keys x NK keys per lane. Loads of chunk j+1 are issued before
+// chunk j is consumed (two named register sets), softmax is online across chunks.
+template <int D, int NK>
+struct KVChunk {
+  uint4 k[NK], v[NK];
+};
+
+template <int D, int NK>
+__device__ __forceinline__ void load_chunk(KVChunk<D, NK>& c, const bf16_t* kbase, const bf16_t* vbase, int c0,
+                                           int p1, int wid, int sub, int dl) {
+  constexpr int KPW = 64 / (D / 8);
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    const int key = min(c0 + (i * 4 + wid) * KPW + sub, p1 - 1);
+    c.k[i] = *(const uint4*)(kbase + (long)key * D + dl * 8);
+    c.v[i] = *(const uint4*)(vbase + (long)key * D + dl * 8);
+  }
+}
+
+template <int D, int G, int NK>
+__device__ __forceinline__ void consume_chunk(KVChunk<D, NK>& c, int c0, int p1, int s_new, bool has_new,
+                                              const uint4& kp, const uint4& vp, const float (&qv)[G][8],
+                                              float (&m)[G], float (&l)[G], float (&acc)[G][8], int wid, int sub,
+                                              float scale_log2) {
+  constexpr int LPK = D / 8, KPW = 64 / LPK;
+  if (has_new) {
+#pragma unroll
+    for (int i = 0; i < NK; ++i)
+      if (c0 + (i * 4 + wid) * KPW + sub == s_new) { c.k[i] = kp; c.v[i] = vp; }
+  }
+  float sc[G][NK];
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    float kf[8];
+    unpack8(c.k[i], kf);
+    const bool ok = c0 + (i * 4 + wid) * KPW + sub < p1;
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      float sdot = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sdot += qv[gg][e] * kf[e];
+#pragma unroll
+      for (int off = LPK / 2; off > 0; off >>= 1) sdot += __shfl_xor(sdot, off, 64);
+      sc[gg][i] = ok ? sdot * scale_log2 : -INFINITY;
+    }
+  }
+  // per-lane online softmax over this lane's keys (cross-lane merge happens once at the end)
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg) {
+    float cm = sc[gg][0];
+#pragma unroll
+    for (int i = 1; i < NK; ++i) cm = fmaxf(cm, sc[gg][i]);
+    const float mn = fmaxf(m[gg], cm);
+    if (mn == -INFINITY) continue;  // nothing valid yet for this lane
+    const float r = exp2f(m[gg] - mn);
+    l[gg] *= r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[gg][e] *= r;
+    m[gg] = mn;
+  }
+#pragma unroll
+  for (int i = 0; i < NK; ++i) {
+    float vf[8];
+    unpack8(c.v[i], vf);
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      // masked key -> 0 (also when every key so far was masked: m = -inf would give NaN)
+      const float pr = sc[gg][i] == -INFINITY ? 0.f : exp2f(sc[gg][i] - m[gg]);
+      l[gg] += pr;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[gg][e] += pr * vf[e];
+    }
+  }
+}
+
+template <int D, int G, int NK>
+__global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs a) {
+  constexpr int LPK = D / 8;    // lanes per key
+  constexpr int KPW = 64 / LPK; // keys per wave-step
+  constexpr int CH = 4 * KPW * NK;
+  __shared__ float red[4 * G * D];
+  __shared__ float wst[4][G][2];
+  __shared__ int flag;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int part = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int len = a.attn_len[b];
+  const int s_new = a.slot[b];
+  int kbeg = a.kv_start ? a.kv_start[b] : 0;
+  if (a.window > 0) kbeg = max(kbeg, len - a.window);
+  const int p0 = max(part * a.PS, kbeg), p1 = min((part + 1) * a.PS, len);
+  const int sub = lane / LPK, dl = lane % LPK;
+  const bf16_t* row = a.qkv + (long)b * a.ldq;
+
+  float mrow[G], lrow[G];
+  const bool active = p0 < p1;
+  if (active) {
+    const int p = a.pos ? a.pos[b] : 0;
+    const bf16_t* kbase = a.kc + ((long)b * a.Hkv + hk) * a.Smax * D;
+    const bf16_t* vbase = a.vc + ((long)b * a.Hkv + hk) * a.Smax * D;
+    KVChunk<D, NK> ca, cb;
+    load_chunk<D, NK>(ca, kbase, vbase, p0, p1, wid, sub, dl);
+    float qv[G][8];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) rope_chunk<D>(row + (long)(hk * G + gg) * D, dl, a, p, qv[gg]);
+    const bool has_new = s_new >= p0 && s_new < p1;
+    uint4 kp = make_uint4(0, 0, 0, 0), vp = kp;
+    if (has_new) {
+      float kn[8], vn[8];
+      rope_chunk<D>(row + (long)(a.Hq + hk) * D, dl, a, p, kn);
+      unpack8(*(const uint4*)(row + (long)(a.Hq + a.Hkv + hk) * D + dl * 8), vn);
+      kp = pack8(kn);
+      vp = pack8(vn);
+      if (wid == 0 && sub == 0) {
+        *(uint4*)(a.kc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D + dl * 8) = kp;
+        *(uint4*)(a.vc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D + dl * 8) = vp;
+      }
+    }
+    float m[G], l[G], acc[G][8];
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      m[gg] = -INFINITY;
+      l[gg] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[gg][e] = 0.f;
+    }
+    for (int c0 = p0; c0 < p1; c0 += 2 * CH) {
+      if (c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl);
+      consume_chunk<D, G, NK>(ca, c0, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
+      if (c0 + CH < p1) {
+        if (c0 + 2 * CH < p1) load_chunk<D, NK>(ca, kbase, vbase, c0 + 2 * CH, p1, wid, sub, dl);
+        consume_chunk<D, G, NK>(cb, c0 + CH, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
+      }
+    }
+    // merge lanes holding the same d (different keys): over sub within the wave, then over waves
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      float mw = m[gg];
+#pragma unroll
+      for (int off = LPK; off < 64; off <<= 1) mw = fmaxf(mw, __shfl_xor(mw, off, 64));
+      const float r = (m[gg] == -INFINITY) ? 0.f : exp2f(m[gg] - mw);
+      l[gg] *= r;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[gg][e] *= r;
+      m[gg] = mw;
+      if (lane == 0) wst[wid][gg][0] = mw;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) {
+      mrow[gg] = fmaxf(fmaxf(wst[0][gg][0], wst[1][gg][0]), fmaxf(wst[2][gg][0], wst[3][gg][0]));
+      const float r = (m[gg] == -INFINITY) ? 0.f : exp2f(m[gg] - mrow[gg]);
+      float lsum = l[gg] * r;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[gg][e] *= r;
+#pragma unroll
+      for (int off = LPK; off < 64; off <<= 1) {
+        lsum += __shfl_xor(lsum, off, 64);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[gg][e] += __shfl_xor(acc[gg][e], off, 64);
+      }
+      if (sub == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[(wid * G + gg) * D + dl * 8 + e] = acc[gg][e];
+      }
+      if (lane == 0) wst[wid][gg][1] = lsum;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) lrow[gg] = wst[0][gg][1] + wst[1][gg][1] + wst[2][gg][1] + wst[3][gg][1];
+  }
+
+  if (a.NP == 1) {
+    for (int e = tid; e < G * D; e += 256) {
+      const int gg = e / D, d = e % D;
+      float ov = 0.f;
+      if (active && lrow[gg] > 0.f)
+        ov = (red[(0 * G + gg) * D + d] + red[(1 * G + gg) * D + d] + red[(2 * G + gg) * D + d] +
+              red[(3 * G + gg) * D + d]) / lrow[gg];
+      a.o[(long)b * a.ldo + (long)(hk * G + gg) * D + d] = f2bf(ov);
+    }
+    return;
+  }
+
+  // ---- publish the partial with write-through (agent-scope) stores, take a ticket; the last
+  // partition of (b, hk) merges with agent-scope loads. No L2 writeback / invalidate fences:
+  // cdna_hip_programming.md / MI355X_MICROARCH.md 'handoff-flag' (drained sc1 payload -> flag).
+  float* pp = a.part + (((long)b * a.Hkv + hk) * a.NP) * G * (D + 2);
+  float* outp = pp + (long)part * G * (D + 2);
+  for (int e = tid; e < G * D; e += 256) {
+    const int gg = e / D, d = e % D;
+    if (active)
+      __hip_atomic_store(outp + gg * (D + 2) + d,
+                         red[(0 * G + gg) * D + d] + red[(1 * G + gg) * D + d] + red[(2 * G + gg) * D + d] +
+                             red[(3 * G + gg) * D + d],
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid < G) {
+    __hip_atomic_store(outp + tid * (D + 2) + D, active ? mrow[tid] : -INFINITY, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(outp + tid * (D + 2) + D + 1, active ? lrow[tid] : 0.f, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(a.tickets + (long)b * a.Hkv + hk, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    flag = (old == (unsigned)(a.NP - 1));
+  }
+  __syncthreads();
+  if (!flag) return;
+  for (int e = tid; e < G * D; e += 256) {
+    const int gg = e / D, d = e % D;
+    float M = -INFINITY, L = 0.f, O = 0.f;
+#pragma unroll 4
+    for (int q = 0; q < a.NP; ++q) {
+      const float* r = pp + (q * G + gg) * (D + 2);
+      const float mq = __hip_atomic_load(r + D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float lq = __hip_atomic_load(r + D + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float oq = __hip_atomic_load(r + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (mq == -INFINITY) continue;  // empty partition: o[] never written
+      const float Mn = fmaxf(M, mq);
+      const float r0 = exp2f(M - Mn), r1 = exp2f(mq - Mn);
+      L = L * r0 + lq * r1;
+      O = O * r0 + oq * r1;
+      M = Mn;
+    }
+    a.o[(long)b * a.ldo + (long)(hk * G + gg) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+  }
+  if (tid == 0) __hip_atomic_store(a.tickets + (long)b * a.Hkv + hk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------------------
 struct AttnBwdArgs {
@@ -709,6 +1000,38 @@ extern "C" int rt_attn_decode(const void* q, long ldq, const void* kc, const voi
   DEC_CASE(64, 1) DEC_CASE(64, 2) DEC_CASE(64, 4) DEC_CASE(64, 8)
   DEC_CASE(32, 1)
 #undef DEC_CASE
+  return -1;
+}
+
+// keys per chunk of the fused kernel: 4 waves x (64 / (D/8)) keys per step x NK (= 4)
+extern "C" int rt_attn_decode_fused_ps(int D, int nk) { return 4 * (64 / (D / 8)) * nk; }
+
+extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* vc, int Smax, const int* slot,
+                                    const int* attn_len, const int* kv_start, const int* pos, const float* cosT,
+                                    const float* sinT, float sign, int window, float* part, unsigned* tickets, int NP,
+                                    int PS, void* o, long ldo, int B, int Hq, int Hkv, int D, float scale,
+                                    hipStream_t stream) {
+  DecodeFusedArgs a;
+  a.qkv = (const bf16_t*)qkv; a.ldq = ldq; a.kc = (bf16_t*)kc; a.vc = (bf16_t*)vc; a.Smax = Smax;
+  a.slot = slot; a.attn_len = attn_len; a.kv_start = kv_start; a.pos = pos; a.cosT = cosT; a.sinT = sinT;
+  a.sign = sign; a.window = window; a.part = part; a.tickets = tickets; a.o = (bf16_t*)o; a.ldo = ldo;
+  a.B = B; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
+  if (B == 0) return 0;
+  const int G = Hq / Hkv;
+  if (G * Hkv != Hq) return -1;
+  const int nk = 4;  // keys per lane per chunk; PS must be a multiple of the chunk
+  if (PS % (4 * (64 / (D / 8)) * nk) != 0) return -1;
+  dim3 grid(NP, Hkv, B), block(256);
+#define DF_CASE(DD, GG, NN)                                                                   \
+  if (D == DD && G == GG && nk == NN) {                                                       \
+    hipLaunchKernelGGL((attn_decode_fused_kernel<DD, GG, NN>), grid, block, 0, stream, a);    \
+    RT_LAUNCH_CHECK();                                                                        \
+    return 0;                                                                                 \
+  }
+#define DF_G(DD, NN) DF_CASE(DD, 1, NN) DF_CASE(DD, 2, NN) DF_CASE(DD, 4, NN) DF_CASE(DD, 8, NN)
+  DF_G(128, 4) DF_G(64, 4) DF_G(32, 4)
+#undef DF_G
+#undef DF_CASE
   return -1;
 }
 

@@ -215,10 +215,9 @@ class CausalLM(nn.Module):
         residual = None
         for li, layer in enumerate(self.layers):
             qkv, residual = layer.attn_in(x, residual)
-            ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=1,
-                          k_cache=cache.k[li], v_cache=cache.v[li], slot_base=slot)
-            o = ops.decode_attention(qkv, cache.k[li], cache.v[li], attn_len, cfg.num_heads, kv_start,
-                                     cfg.sliding_window, workspace=workspace)
+            # one fused kernel: RoPE(q, k_new) + cache append + split-K attention + combine
+            o = ops.decode_step_attention(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads, pos, cos, sin,
+                                          kv_start, cfg.sliding_window, workspace=workspace)
             x, residual = layer.mlp(o, residual)
         return self.final_norm(x, residual)
 

@@ -117,15 +117,64 @@ def attention(q, k, v, B, Sq, Sk, Hq, Hkv, D, causal=False, window=0, scale=None
 
 
 # ------------------------------------------------------------------------------ decode attention
-def decode_partition(batch_heads: int) -> int:
-    """Keys per split-K partition: small partitions when few (batch, kv-head) pairs exist."""
-    return 64 if batch_heads < 128 else 256
+def decode_partition(batch_heads: int, D: int = 128, Smax: int = 4096) -> int:
+    """Keys per split-K partition of the fused decode kernel. A partition is a whole number of
+    key chunks (4 waves x 64/(D/8) keys x 4 keys per lane). With >= 256 (batch, kv-head) pairs the
+    grid already fills the chip: one partition per pair (no cross-block combine); with fewer pairs
+    the keys are split so that ~256 workgroups run, merged in-launch by the last arriver."""
+    chunk = 4 * (64 // (D // 8)) * 4
+    nchunks = (Smax + chunk - 1) // chunk
+    if batch_heads >= 256:
+        return nchunks * chunk
+    want_np = max(1, -(-256 // batch_heads))
+    per = max(1, -(-nchunks // want_np))
+    return per * chunk
+
+
+class DecodeWorkspace(tuple):
+    """(partials fp32, keys per partition, tickets int32) — static buffers reused by graph replays.
+    Tickets are zero between launches (the merging partition re-arms them)."""
+
+    @property
+    def part(self):
+        return self[0]
+
+    @property
+    def PS(self):
+        return self[1]
+
+    @property
+    def tickets(self):
+        return self[2]
 
 
 def decode_workspace(B, Hq, Hkv, D, Smax, device, PS=None):
-    PS = PS or decode_partition(B * Hkv)
+    PS = PS or decode_partition(B * Hkv, D, Smax)
     NP = (Smax + PS - 1) // PS
-    return torch.empty(B * Hkv * NP * (Hq // Hkv) * (D + 2), dtype=torch.float32, device=device), PS
+    part = torch.empty(B * Hkv * NP * (Hq // Hkv) * (D + 2), dtype=torch.float32, device=device)
+    tickets = torch.zeros(B * Hkv, dtype=torch.int32, device=device)
+    return DecodeWorkspace((part, PS, tickets))
+
+
+def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, cos=None, sin=None, kv_start=None,
+                          window=0, scale=None, workspace=None, out=None, sign: float = 1.0):
+    """One decode step of a layer, fused: rotate q / k_new (if ``cos`` is given), append k_new and
+    v_new at cache slot ``slot[b]``, attend over ``attn_len[b]`` keys -> [B, Hq*D].
+    ``qkv`` [B, (Hq + 2 Hkv) D] is left unrotated (the fused kernel rotates in registers)."""
+    B, Hkv, Smax, D = k_cache.shape
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not on_gpu(qkv):
+        q = rope_qkv_(qkv.clone(), pos, cos, sin, Hq, Hkv, D, S=1, k_cache=k_cache, v_cache=v_cache,
+                      slot_base=slot, sign=sign)
+        return decode_attention(q, k_cache, v_cache, attn_len, Hq, kv_start, window, scale, out=out)
+    if workspace is None or len(workspace) < 3:
+        workspace = decode_workspace(B, Hq, Hkv, D, Smax, qkv.device)
+    part, PS, tickets = workspace[0], workspace[1], workspace[2]
+    if out is None:
+        out = torch.empty(B, Hq * D, dtype=qkv.dtype, device=qkv.device)
+    native().attn_decode_fused(qkv, k_cache, v_cache, slot, attn_len, kv_start, pos, cos, sin, sign, window, scale,
+                               Hq, part, tickets, PS, out)
+    return out
 
 
 def decode_attention(q, k_cache, v_cache, kv_len, Hq, kv_start=None, window=0, scale=None, workspace=None, out=None):
@@ -140,7 +189,7 @@ def decode_attention(q, k_cache, v_cache, kv_len, Hq, kv_start=None, window=0, s
         return o
     if workspace is None:
         workspace = decode_workspace(B, Hq, Hkv, D, Smax, q.device)
-    part, PS = workspace
+    part, PS = workspace[0], workspace[1]
     if out is None:
         out = torch.empty(B, Hq * D, dtype=q.dtype, device=q.device)
     native().attn_decode(q, k_cache, v_cache, kv_len, kv_start, window, scale, Hq, part, PS, out)

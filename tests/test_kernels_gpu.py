@@ -398,3 +398,30 @@ def test_gemm_256_identity():
         assert torch.equal(ops.gemm(a, w).float(), w.t().float())
     finally:
         C.gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,D,Smax,rot,window", [(1, 32, 8, 128, 456, True, 0), (64, 32, 8, 128, 456, True, 0),
+                                                        (3, 8, 8, 64, 200, False, 0), (5, 8, 2, 32, 300, True, 64),
+                                                        (2, 16, 2, 128, 64, True, 0)])
+def test_decode_step_fused(B, Hq, Hkv, D, Smax, rot, window):
+    """Fused RoPE + append + attention + in-launch combine == rope_qkv_ + decode_attention."""
+    torch.manual_seed(B + D)
+    W = (Hq + 2 * Hkv) * D
+    kc = torch.randn(B, Hkv, Smax, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    kv_start = torch.randint(0, 8, (B,), device=DEV, dtype=torch.int32)
+    slot = torch.randint(20, Smax - 1, (B,), device=DEV, dtype=torch.int32)
+    attn_len = slot + 1
+    pos = (slot - kv_start).to(torch.int32)
+    cos, sin = ref.rope_tables(D, 4096, 10000.0, DEV) if rot else (None, None)
+    ws = ops.decode_workspace(B, Hq, Hkv, D, Smax, DEV)
+    for it in range(3):  # repeated launches: tickets must re-arm
+        qkv = torch.randn(B, W, device=DEV, dtype=torch.bfloat16)
+        kc2, vc2 = kc.clone(), vc.clone()
+        out = ops.decode_step_attention(qkv, kc, vc, slot, attn_len, Hq, pos, cos, sin, kv_start, window,
+                                        workspace=ws)
+        q_ref = ops.rope_qkv_(qkv.clone(), pos, cos, sin, Hq, Hkv, D, S=1, k_cache=kc2, v_cache=vc2, slot_base=slot)
+        o_ref = ref.decode_attention(q_ref, kc2, vc2, attn_len, Hq, kv_start, window, 1.0 / math.sqrt(D))
+        assert torch.equal(kc, kc2) and torch.equal(vc, vc2), "cache append differs"
+        _close(out, o_ref)
+    assert int(ws.tickets.abs().sum()) == 0

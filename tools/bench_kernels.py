@@ -131,6 +131,20 @@ def main():
         r = dict(kind="attn_decode", B=B, L=L, us=t, gbs=byts / t / 1e3)
         res.append(r)
         print(json.dumps(r), flush=True)
+        # fused rope + append + attention + combine (Smax > L as in generation)
+        kc2 = torch.randn(B, Hkv, L + 64, D, device=dev, dtype=torch.bfloat16)
+        vc2 = torch.randn_like(kc2)
+        slot = torch.full((B,), L - 1, device=dev, dtype=torch.int32)
+        alen = slot + 1
+        cos, sin = ops.reference.rope_tables(D, 8192, 10000.0, dev)
+        ws2 = ops.decode_workspace(B, Hq, Hkv, D, L + 64, dev)
+        t2 = timeit(lambda: ops.decode_step_attention(q, kc2, vc2, slot, alen, Hq, slot, cos, sin, workspace=ws2,
+                                                      out=out))
+        t_rope = timeit(lambda: ops.rope_qkv_(q, slot, cos, sin, Hq, Hkv, D, S=1, k_cache=kc2, v_cache=vc2,
+                                              slot_base=slot))
+        r = dict(kind="attn_decode_fused", B=B, L=L, us=t2, unfused_us=t + t_rope, gbs=byts / t2 / 1e3)
+        res.append(r)
+        print(json.dumps(r), flush=True)
     # norm / logprob / sampler
     if not want("misc"):
         if args.json:
