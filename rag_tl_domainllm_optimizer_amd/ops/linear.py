@@ -127,6 +127,14 @@ class LoRAGroup:
         return self.merged
 
 
+def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b with an fp32 result; on the GPU bf16 operands go straight to hipBLASLt with fp32
+    output (no fp32 copies of the operands)."""
+    if a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    return a.float() @ b.float()
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], *lora_params):
@@ -169,13 +177,15 @@ class _LinearFn(torch.autograd.Function):
         if lora is not None:
             du = dy @ lora.ub  # [M, Rp]  (= dL/dU)
             if needs[0]:
-                dx = dx + du @ lora.a_pad
+                dx.addmm_(du, lora.a_pad)  # dX += dU A_pad in the GEMM epilogue (no temporary)
+            # all adapters of the projection in two GEMMs with fp32 output (bf16 in, fp32 accumulate):
+            # dA_all = dU^T X [Rp, K]; dB_all = dY^T U [N, Rp] (adapter i uses its diagonal block)
+            ga_all = _mm_f32(du.t(), x2)
+            gb_all = _mm_f32(dy.t(), u)
             for a, b, r0, c0, s in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
                 ri, ni = a.shape[0], b.shape[0]
-                ga = (du[:, r0:r0 + ri].t().float() @ x2.float()) * s
-                gb = dy[:, c0:c0 + ni].t().float() @ u[:, r0:r0 + ri].float()
-                lora_grads.append(ga.to(a.dtype))
-                lora_grads.append(gb.to(b.dtype))
+                lora_grads.append((ga_all[r0:r0 + ri] * s).to(a.dtype))
+                lora_grads.append(gb_all[c0:c0 + ni, r0:r0 + ri].to(b.dtype))
             # parameter order in forward(*lora_params) is a0, b0, a1, b1, ...
         return (dx, dw, db, None, None, *lora_grads)
 
