@@ -26,6 +26,13 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;     // 16x16 accumulato
 typedef __attribute__((ext_vector_type(16))) float f32x16;   // 32x32 accumulator
 typedef __attribute__((ext_vector_type(8))) uint16_t u16x8;
 typedef __attribute__((ext_vector_type(4))) uint16_t u16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+// 16-B non-temporal load (global_load_dwordx4 ... nt): for data read once per launch (weights)
+__device__ __forceinline__ uint4 load_nt16(const void* p) {
+  const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 __device__ __forceinline__ float bf2f(bf16_t x) {
   return __uint_as_float(((uint32_t)x) << 16);

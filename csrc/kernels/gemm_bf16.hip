@@ -478,8 +478,9 @@ template <int MT>
 __device__ __forceinline__ void dg_load(DGRegs<MT>& r, const bf16_t* const* wrow, const bf16_t* const* xrow, long c) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    r.w[j][0] = *(const uint4*)(wrow[j] + c * 64);
-    r.w[j][1] = *(const uint4*)(wrow[j] + c * 64 + 8);
+    // weights are read once per launch: non-temporal (MI355X_MICROARCH.md 'nt-weights')
+    r.w[j][0] = load_nt16(wrow[j] + c * 64);
+    r.w[j][1] = load_nt16(wrow[j] + c * 64 + 8);
   }
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -557,31 +558,33 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(GemmArgs p, float* __r
   }
 
   if (split > 1) {
-    // publish this block's slab, take a ticket; the last arriver of the column group reduces
+    // publish this block's slab with write-through (agent-scope) stores, drain them, take a
+    // ticket; the last arriver of the column group reduces with agent-scope loads. No L2
+    // writeback/invalidate fences (a per-block buffer_wbl2 flushes the whole XCD L2).
     float* slab = slabs + ((long)cg * split + sp) * (ROWS * DG_COLS);
 #pragma unroll
-    for (int i = 0; i < NE; ++i) slab[tid + 256 * i] = v[i];
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + 256 * i;
+      if (e / DG_COLS < p.M) __hip_atomic_store(slab + e, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned old = __hip_atomic_fetch_add(tickets + cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       red[0] = (old == (unsigned)(split - 1)) ? 1.f : 0.f;
     }
     __syncthreads();
     const bool last = red[0] != 0.f;
     if (!last) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
     const float* base = slabs + (long)cg * split * (ROWS * DG_COLS);
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
+      const int e = tid + 256 * i;
       float t = 0.f;
-      for (int s2 = 0; s2 < split; ++s2) t += base[(long)s2 * (ROWS * DG_COLS) + tid + 256 * i];
+      if (e / DG_COLS < p.M) {
+        for (int s2 = 0; s2 < split; ++s2)
+          t += __hip_atomic_load(base + (long)s2 * (ROWS * DG_COLS) + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       v[i] = t;
     }
     if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -614,12 +617,13 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(GemmArgs p, float* __r
   }
 }
 
-// split so that the grid has >= ~2 blocks per CU while each wave keeps >= 2 k-chunks
+// split-K so the grid reaches ~256 workgroups (one per CU) while every wave keeps >= 4 k-chunks of
+// 64 in flight-able work (short waves pay the reduction without amortising it)
 static int decode_split(int N, int K) {
   const int groups = (N + DG_COLS - 1) / DG_COLS;
   const int nc = K / 64;
   int split = 1;
-  while (groups * split < 512 && nc / (4 * split * 2) >= 2 && split < 16) split *= 2;
+  while (groups * split < 256 && nc / (4 * split * 2) >= 4 && split < 16) split *= 2;
   return split;
 }
 

@@ -22,26 +22,29 @@ from ._ext import native, on_gpu
 ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new": 3, "silu": 4}
 
 
-# Plain GEMMs (no LoRA K-extension, bias or activation epilogue, bf16 out) are library GEMMs:
-# hipBLASLt by default ("lib"), or the hand-written kernels ("native": split-K MFMA decode
-# kernel for M <= 64, 128/256 tile kernels above). Everything with a fused epilogue or LoRA
-# term always runs on the hand-written kernels. Measured on MI355X (profiles/): hipBLASLt
-# ~1.5 PF/s on large plain GEMMs vs ~1.2 PF/s for the 256x256 8-phase kernel; equal on skinny.
+# Plain GEMMs (no LoRA K-extension, bias or activation epilogue, bf16 out) pick a backend by M:
+#   M <= 16      SKINNY_BACKEND, default "native": split-K MFMA weight-streaming kernel, measured
+#                faster than hipBLASLt on cold (HBM-streamed) decode weights at batch 1-8
+#                (profiles/kernels_skinny_cold.log: qkv 16.5 vs 19.5 us, o 11.4 vs 19.0 us,
+#                gate_up 46.9 vs 56.0 us, lm_head 47.8 vs 57.4 us)
+#   16 < M <= 64 MID_BACKEND, default "lib" (hipBLASLt; the native kernel's 64-row variant loses)
+#   M > 64       PLAIN_BACKEND, default "lib" (hipBLASLt ~1.5 PF/s vs ~1.2 PF/s for the 256x256
+#                8-phase kernel on plain GEMMs)
+# Everything with a fused epilogue or a LoRA term always runs on the hand-written kernels.
 PLAIN_BACKEND = os.environ.get("RAGTL_PLAIN_GEMM", "lib")
-SKINNY_BACKEND = os.environ.get("RAGTL_SKINNY", PLAIN_BACKEND)
+MID_BACKEND = os.environ.get("RAGTL_MID_GEMM", PLAIN_BACKEND)
+SKINNY_BACKEND = os.environ.get("RAGTL_SKINNY", "native")
 
 
-def set_gemm_backend(plain: Optional[str] = None, skinny: Optional[str] = None):
-    """Select "lib" (hipBLASLt) or "native" (hand-written kernels) for plain GEMMs; returns the
-    previous (plain, skinny) pair."""
-    global PLAIN_BACKEND, SKINNY_BACKEND
-    prev = (PLAIN_BACKEND, SKINNY_BACKEND)
-    if plain is not None:
-        assert plain in ("lib", "native")
-        PLAIN_BACKEND = plain
-    if skinny is not None:
-        assert skinny in ("lib", "native")
-        SKINNY_BACKEND = skinny
+def set_gemm_backend(plain: Optional[str] = None, skinny: Optional[str] = None, mid: Optional[str] = None):
+    """Select "lib" (hipBLASLt) or "native" (hand-written kernels) for plain GEMMs by M range;
+    returns the previous (plain, skinny, mid) triple."""
+    global PLAIN_BACKEND, SKINNY_BACKEND, MID_BACKEND
+    prev = (PLAIN_BACKEND, SKINNY_BACKEND, MID_BACKEND)
+    for name, val in (("PLAIN_BACKEND", plain), ("SKINNY_BACKEND", skinny), ("MID_BACKEND", mid)):
+        if val is not None:
+            assert val in ("lib", "native")
+            globals()[name] = val
     return prev
 
 
@@ -49,7 +52,8 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
     """Raw (non-autograd) fused GEMM on 2-D row-major operands."""
     if on_gpu(x):
         if u is None and bias is None and act == 0 and not out_f32:
-            backend = SKINNY_BACKEND if x.shape[0] <= 64 else PLAIN_BACKEND
+            M = x.shape[0]
+            backend = SKINNY_BACKEND if M <= 16 else (MID_BACKEND if M <= 64 else PLAIN_BACKEND)
             if backend == "lib":
                 return torch.matmul(x, w.t(), out=out)
         return native().gemm(x, w, u, ub, bias, act, out_f32, out)

@@ -23,7 +23,7 @@ def setup_module(_):
     assert ops.native_available(), "native extension must load on the GPU box"
     # plain GEMMs default to hipBLASLt in the framework; these tests exercise the HIP kernels
     global _PREV_BACKEND
-    _PREV_BACKEND = ops.set_gemm_backend("native", "native")
+    _PREV_BACKEND = ops.set_gemm_backend("native", "native", "native")
 
 
 def teardown_module(_):

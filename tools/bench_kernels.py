@@ -39,7 +39,7 @@ def main():
     def want(k):
         return only is None or k in only
 
-    ops.set_gemm_backend("native", "native")  # time the hand-written kernels, not hipBLASLt
+    ops.set_gemm_backend("native", "native", "native")  # time the hand-written kernels, not hipBLASLt
     C = ops.native()
     dev = "cuda"
     res = []
