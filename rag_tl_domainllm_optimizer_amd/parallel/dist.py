@@ -30,7 +30,7 @@ class DistInfo:
 
     @property
     def enabled(self) -> bool:
-        return self.world > 1 and dist.is_initialized()
+        return dist.is_initialized()
 
 
 _INFO = DistInfo()
@@ -40,8 +40,11 @@ def info() -> DistInfo:
     return _INFO
 
 
-def init(backend: Optional[str] = None, timeout_s: float = 900.0, device: Optional[str] = None) -> DistInfo:
-    """Initialise from env (no-op for a single process). Sets the current GPU to LOCAL_RANK."""
+def init(backend: Optional[str] = None, timeout_s: float = 900.0, device: Optional[str] = None,
+         force_group: bool = False) -> DistInfo:
+    """Initialise from env (no process group for a single process unless ``force_group`` or
+    RAGTL_FORCE_PG=1). Sets the current GPU to LOCAL_RANK. The timeout makes a hung collective
+    (e.g. a dead peer) surface as an error instead of a silent hang."""
     global _INFO
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -53,14 +56,15 @@ def init(backend: Optional[str] = None, timeout_s: float = 900.0, device: Option
     else:
         dev = torch.device("cpu")
     be = backend or ("nccl" if use_cuda else "gloo")
-    if world > 1 and not dist.is_initialized():
+    force_group = force_group or os.environ.get("RAGTL_FORCE_PG", "0") == "1"
+    if (world > 1 or force_group) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
-    _INFO = DistInfo(rank, world, local, be if world > 1 else None, dev)
+    _INFO = DistInfo(rank, world, local, be if (world > 1 or dist.is_initialized()) else None, dev)
     return _INFO
 
 
