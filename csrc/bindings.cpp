@@ -19,6 +19,9 @@ extern "C" {
 int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
                long, int, int, int, int, int, float*, unsigned*, hipStream_t);
 void rt_gemm_set_variant(int);
+int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
+                int, int, int, float*, unsigned*, hipStream_t);
+int rt_quant_fp8_rows(const void*, long, void*, long, float*, long, int, hipStream_t);
 int rt_norm_fwd(int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
                 hipStream_t);
 int rt_norm_bwd(int, const void*, const void*, const void*, const float*, const float*, const void*, void*, float*,
@@ -142,6 +145,52 @@ Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const o
                       opt_ptr(ub), Rp ? ub->stride(0) : 0, Rp, opt_ptr(bias), c.data_ptr(), c.stride(0), (int)M,
                       (int)N, (int)K, (int)act, out_f32 ? 1 : 0, slabs, tickets, st),
            "gemm");
+  return c;
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp8 (OCP e4m3fn): per-row quantisation and the two fp8 GEMM forms
+std::vector<Tensor> quant_fp8(const Tensor& x) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_ROWS(x);
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0, "quant_fp8: [R, C] with C % 8 == 0");
+  auto q = at::empty({x.size(0), x.size(1)}, x.options().dtype(at::kByte));
+  auto s = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
+  check_rc(rt_quant_fp8_rows(x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0), s.data_ptr<float>(), x.size(0),
+                             (int)x.size(1), cur_stream()),
+           "quant_fp8");
+  return {q, s};
+}
+
+Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, const Tensor& sw,
+                const optional<Tensor>& bias, int64_t act, optional<Tensor> out) {
+  // a: bf16 [M, K] (W8A16, M <= 64) or uint8 e4m3fn [M, K] with sa [M] (W8A8)
+  CHECK_CUDA(a); CHECK_CUDA(wq); CHECK_ROWS(a); CHECK_ROWS(wq); CHECK_F32(sw);
+  TORCH_CHECK(wq.scalar_type() == at::kByte, "gemm_fp8: weight must be uint8 (e4m3fn bits)");
+  const bool a_bf16 = a.scalar_type() == at::kBFloat16;
+  const int64_t M = a.size(0), K = a.size(1), N = wq.size(0);
+  TORCH_CHECK(wq.size(1) == K && sw.numel() == N, "gemm_fp8: shapes");
+  if (a_bf16) {
+    TORCH_CHECK(M <= 64 && K % 64 == 0, "gemm_fp8: bf16 activations only for M <= 64");
+  } else {
+    TORCH_CHECK(a.scalar_type() == at::kByte && sa.has_value() && sa->numel() == M, "gemm_fp8: W8A8 needs sa [M]");
+    TORCH_CHECK(K % 128 == 0 && N % 8 == 0, "gemm_fp8: K % 128 == 0, N % 8 == 0");
+  }
+  if (bias.has_value() && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N); }
+  Tensor c = (out.has_value() && out->defined()) ? *out : at::empty({M, N}, a.options().dtype(at::kBFloat16));
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.scalar_type() == at::kBFloat16, "gemm_fp8: out");
+  if (M == 0) return c;
+  hipStream_t st = cur_stream();
+  float* slabs = nullptr;
+  unsigned* tickets = nullptr;
+  if (a_bf16) {
+    DecodeWS& ws = decode_ws(wq, st);
+    slabs = ws.slabs.data_ptr<float>();
+    tickets = (unsigned*)ws.tickets.data_ptr<int>();
+  }
+  check_rc(rt_gemm_fp8(a.data_ptr(), a.stride(0), sa.has_value() && sa->defined() ? sa->data_ptr<float>() : nullptr,
+                       wq.data_ptr(), wq.stride(0), sw.data_ptr<float>(), opt_ptr(bias), c.data_ptr(), c.stride(0),
+                       (int)M, (int)N, (int)K, (int)act, a_bf16 ? 1 : 0, slabs, tickets, st),
+           "gemm_fp8");
   return c;
 }
 
@@ -476,6 +525,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
   m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");
+  m.def("quant_fp8", &quant_fp8, "per-row absmax e4m3fn quantisation -> (uint8 [R,C], scale fp32 [R])");
+  m.def("gemm_fp8", &gemm_fp8, "fp8 GEMM: W8A8 (MX MFMA 256x256) or W8A16 (skinny, M <= 64)", py::arg("a"),
+        py::arg("sa") = py::none(), py::arg("wq"), py::arg("sw"), py::arg("bias") = py::none(), py::arg("act") = 0,
+        py::arg("out") = py::none());
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
   m.def("rope_qkv", &rope_qkv);

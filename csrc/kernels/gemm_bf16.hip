@@ -50,9 +50,20 @@ struct GemmArgs {
   void* C; long ldc;
   int M, N, K;
   int act;
+  // fp8 paths only: per-row scale of A (W8A8 tile kernel) and per-column scale of B (W8A8 and
+  // W8A16 skinny kernel); A / B then point to OCP e4m3fn bytes with lda / ldb in elements (= bytes)
+  const float* sa;
+  const float* sb;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+
+__device__ __forceinline__ i32x8 cat_frag(const bf16x8& lo, const bf16x8& hi) {
+  const i32x4_t a = __builtin_bit_cast(i32x4_t, lo), b = __builtin_bit_cast(i32x4_t, hi);
+  return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
 
 // 16-B slot swizzle of a 128-B-row LDS tile read by ds_read_b128 in 16-row lane groups: two rows
 // share a 256-B bank row, so the XOR key must differ between rows r and r+8 of the same parity.
@@ -305,7 +316,7 @@ __device__ __forceinline__ void g2_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
   }
 }
 
-template <bool OUT_F32>
+template <bool OUT_F32, bool FP8>
 __global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * G2_BUF];  // the only __shared__ object
 
@@ -319,8 +330,9 @@ __global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
   const int tm = first_m + (bid % gsz);
   const int tn = (bid % (G2_GROUP_M * tiles_n)) / gsz;
   const int m0 = tm * 256, n0 = tn * 256;
-  const int nk_main = p.K / 64;
-  const int nk = nk_main + p.Rp / 64;
+  constexpr int ESZ = FP8 ? 1 : 2;           // bytes per element; a K-tile is always 128 B per row
+  const int nk_main = p.K / (128 / ESZ);
+  const int nk = nk_main + (FP8 ? 0 : p.Rp / 64);
   const int wr = wid >> 2, wc = wid & 3;
   const int frow = lane & 15, fq = lane >> 4;
 
@@ -328,17 +340,17 @@ __global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
 
   // one half-tile (operand op: 0 = A, 1 = B; half h) of K-tile t -> buffer t & 1: 2 DMAs per lane
   auto stage = [&](int op, int h, int t) {
-    const bf16_t* base;
-    long ld;
-    int k0;
+    const char* base;
+    long ldb;
+    long k0;
     if (t < nk_main) {
-      base = op ? p.B : p.A;
-      ld = op ? p.ldb : p.lda;
-      k0 = t * 64;
+      base = (const char*)(op ? p.B : p.A);
+      ldb = (op ? p.ldb : p.lda) * ESZ;
+      k0 = (long)t * 128;
     } else {
-      base = op ? p.UB : p.U;
-      ld = op ? p.ldub : p.ldu;
-      k0 = (t - nk_main) * 64;
+      base = (const char*)(op ? p.UB : p.U);
+      ldb = (op ? p.ldub : p.ldu) * 2;
+      k0 = (long)(t - nk_main) * 128;
     }
     const int rmax = op ? p.N - 1 : p.M - 1;
     const int r0 = (op ? n0 : m0) + h * 128;
@@ -347,7 +359,7 @@ __global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
     for (int j = 0; j < 2; ++j) {
       const int lr = (wid * 2 + j) * 8 + srow;
       const int gr = min(r0 + lr, rmax);
-      const bf16_t* src = base + (long)gr * ld + k0 + ((lane & 7) ^ lds_swz(lr)) * 8;
+      const char* src = base + (long)gr * ldb + k0 + ((lane & 7) ^ lds_swz(lr)) * 16;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (wid * 2 + j) * 1024), 16, 0, 0);
     }
   };
@@ -358,43 +370,50 @@ __global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  // a lane's 32 B of one 64-deep (bf16) / 128-deep (fp8) K-tile row: two 16-B LDS chunks held as
+  // one 8-register tuple (fp8 feeds it whole to the MX MFMA, bf16 as two k-halves)
+  i32x8 fa[4], fb0[2], fb1[2];
 
+  auto ld2 = [&](const char* hb, int lr) -> i32x8 {
+    const i32x4_t lo = *(const i32x4_t*)(hb + lr * 128 + ((fq ^ lds_swz(lr)) << 4));
+    const i32x4_t hi = *(const i32x4_t*)(hb + lr * 128 + (((4 + fq) ^ lds_swz(lr)) << 4));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
   auto read_a = [&](int buf, int s) {
     const char* hb = smem + buf * G2_BUF + wr * G2_HALF;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int lr = s * 64 + i * 16 + frow;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int c = kk * 4 + fq;
-        fa[i][kk] = *(const bf16x8*)(hb + lr * 128 + ((c ^ lds_swz(lr)) << 4));
-      }
-    }
+    for (int i = 0; i < 4; ++i) fa[i] = ld2(hb, s * 64 + i * 16 + frow);
   };
-  auto read_b = [&](int buf, int s, bf16x8 (&fb)[2][2]) {
+  auto read_b = [&](int buf, int s, i32x8 (&fb)[2]) {
     const char* hb = smem + buf * G2_BUF + (2 + (wc >> 1)) * G2_HALF;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int lr = (wc & 1) * 64 + s * 32 + j * 16 + frow;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int c = kk * 4 + fq;
-        fb[j][kk] = *(const bf16x8*)(hb + lr * 128 + ((c ^ lds_swz(lr)) << 4));
-      }
-    }
+    for (int j = 0; j < 2; ++j) fb[j] = ld2(hb, (wc & 1) * 64 + s * 32 + j * 16 + frow);
   };
+  auto half = [](const i32x8& v, int h) -> bf16x8 {
+    return h == 0 ? __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 0, 1, 2, 3))
+                  : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
+  };
+// bf16: 2 k-halves x mfma_16x16x32; fp8: one MX-scaled mfma_16x16x128 (unit block scales, e8m0
+// 127 = 2^0; the per-row / per-column scales are applied in the epilogue). The 32 bytes of a lane
+// are the same two 16-B LDS chunks for A and B, so the k pairing is consistent.
 #define G2_MMA(SA, SB, FB)                                                                        \
   do {                                                                                           \
     G2_BARRIER();                                                                                \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
     __builtin_amdgcn_sched_barrier(0);                                                           \
     __builtin_amdgcn_s_setprio(1);                                                               \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
-        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
-          acc[(SA) * 4 + i][(SB) * 2 + j] =                                                      \
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kk], FB[j][kk], acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0); \
+    if constexpr (FP8) {                                                                         \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
+          acc[(SA) * 4 + i][(SB) * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(    \
+              fa[i], FB[j], acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0, 127, 0, 127);              \
+    } else {                                                                                     \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
+          _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                       \
+            acc[(SA) * 4 + i][(SB) * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(           \
+                half(fa[i], kk), half(FB[j], kk), acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0);     \
+    }                                                                                            \
     __builtin_amdgcn_s_setprio(0);                                                               \
     G2_BARRIER();                                                                                \
   } while (0)
@@ -442,7 +461,27 @@ __global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
   if (wr == 0) G2_BARRIER();
 #undef G2_MMA
 
-  // ---- epilogue: bias + activation (dispatched once), bf16 through LDS (two 128-row passes) ----
+  // ---- epilogue: fp8 row/column scales, bias + activation (dispatched once), bf16 through LDS ----
+  if constexpr (FP8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float sc = p.sb ? p.sb[min(n0 + wc * 64 + j * 16 + frow, p.N - 1)] : 1.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc;
+    }
+    if (p.sa) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sr = p.sa[min(m0 + wr * 128 + i * 16 + fq * 4 + r, p.M - 1)];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j][r] *= sr;
+        }
+    }
+  }
   switch (p.act) {
     case ACT_RELU: g2_epilogue<OUT_F32, ACT_RELU>(p, acc, smem, m0, n0); break;
     case ACT_GELU: g2_epilogue<OUT_F32, ACT_GELU>(p, acc, smem, m0, n0); break;
@@ -474,13 +513,20 @@ struct DGRegs {
   uint4 x[MT][2];
 };
 
-template <int MT>
-__device__ __forceinline__ void dg_load(DGRegs<MT>& r, const bf16_t* const* wrow, const bf16_t* const* xrow, long c) {
+// W8: the weight row is OCP e4m3fn bytes (W8A16): one 16-B load covers the lane's 16 k of a
+// 64-deep chunk and is widened to two bf16x8 fragments in registers (per-column scale applied in
+// the epilogue). The k order matches the bf16 X fragments (lane group g owns k [16g, 16g+16)).
+template <int MT, bool W8>
+__device__ __forceinline__ void dg_load(DGRegs<MT>& r, const char* const* wrow, const bf16_t* const* xrow, long c) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     // weights are read once per launch: non-temporal (MI355X_MICROARCH.md 'nt-weights')
-    r.w[j][0] = load_nt16(wrow[j] + c * 64);
-    r.w[j][1] = load_nt16(wrow[j] + c * 64 + 8);
+    if constexpr (W8) {
+      r.w[j][0] = load_nt16(wrow[j] + c * 64);
+    } else {
+      r.w[j][0] = load_nt16(wrow[j] + c * 128);
+      r.w[j][1] = load_nt16(wrow[j] + c * 128 + 16);
+    }
   }
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -489,20 +535,38 @@ __device__ __forceinline__ void dg_load(DGRegs<MT>& r, const bf16_t* const* wrow
   }
 }
 
-template <int MT>
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16(unsigned lo, unsigned hi) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+  const bf16x2_t a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.f, false);
+  const bf16x2_t b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.f, true);
+  const bf16x2_t c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.f, false);
+  const bf16x2_t d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.f, true);
+  return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+template <int MT, bool W8>
 __device__ __forceinline__ void dg_mma(const DGRegs<MT>& r, f32x4 (&acc)[MT][4]) {
+  bf16x8 w0[4], w1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if constexpr (W8) {
+      w0[j] = fp8x8_to_bf16(r.w[j][0].x, r.w[j][0].y);
+      w1[j] = fp8x8_to_bf16(r.w[j][0].z, r.w[j][0].w);
+    } else {
+      w0[j] = __builtin_bit_cast(bf16x8, r.w[j][0]);
+      w1[j] = __builtin_bit_cast(bf16x8, r.w[j][1]);
+    }
+  }
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x[m][0]),
-                                                          __builtin_bit_cast(bf16x8, r.w[j][0]), acc[m][j], 0, 0, 0);
-      acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x[m][1]),
-                                                          __builtin_bit_cast(bf16x8, r.w[j][1]), acc[m][j], 0, 0, 0);
+      acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x[m][0]), w0[j], acc[m][j], 0, 0, 0);
+      acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x[m][1]), w1[j], acc[m][j], 0, 0, 0);
     }
 }
 
-template <int MT, bool OUT_F32>
+template <int MT, bool OUT_F32, bool W8>
 __global__ __launch_bounds__(256) void gemm_decode_kernel(GemmArgs p, float* __restrict__ slabs,
                                                           unsigned* __restrict__ tickets, int split) {
   constexpr int ROWS = MT * 16;
@@ -517,10 +581,12 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(GemmArgs p, float* __r
   const int part = sp * 4 + wid, nparts = split * 4;
   const int c_begin = (int)((long)part * nc / nparts), c_end = (int)((long)(part + 1) * nc / nparts);
 
-  const bf16_t* wrow[4];
+  constexpr int WSZ = W8 ? 1 : 2;  // bytes per weight element
+  const char* wrow[4];
   const bf16_t* xrow[MT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) wrow[j] = p.B + (long)min(n0 + j * 16 + frow, p.N - 1) * p.ldb + g * 16;
+  for (int j = 0; j < 4; ++j)
+    wrow[j] = (const char*)p.B + ((long)min(n0 + j * 16 + frow, p.N - 1) * p.ldb + g * 16) * WSZ;
 #pragma unroll
   for (int m = 0; m < MT; ++m) xrow[m] = p.A + (long)min(m * 16 + frow, p.M - 1) * p.lda + g * 16;
 
@@ -531,12 +597,12 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(GemmArgs p, float* __r
     for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   DGRegs<MT> ra, rb;
-  if (c_begin < c_end) dg_load<MT>(ra, wrow, xrow, c_begin);
+  if (c_begin < c_end) dg_load<MT, W8>(ra, wrow, xrow, c_begin);
   for (int c = c_begin; c < c_end; c += 2) {
-    if (c + 1 < c_end) dg_load<MT>(rb, wrow, xrow, c + 1);
-    dg_mma<MT>(ra, acc);
-    if (c + 2 < c_end) dg_load<MT>(ra, wrow, xrow, c + 2);
-    if (c + 1 < c_end) dg_mma<MT>(rb, acc);
+    if (c + 1 < c_end) dg_load<MT, W8>(rb, wrow, xrow, c + 1);
+    dg_mma<MT, W8>(ra, acc);
+    if (c + 2 < c_end) dg_load<MT, W8>(ra, wrow, xrow, c + 2);
+    if (c + 1 < c_end) dg_mma<MT, W8>(rb, acc);
   }
 
   // ---- intra-block reduction: acc[m][j] lane holds C[m*16 + 4g + r][j*16 + frow] ----
@@ -609,6 +675,7 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(GemmArgs p, float* __r
           for (int q = 0; q < 8; ++q) y += a8[q] * b8[q];
         }
       }
+      if constexpr (W8) y *= p.sb[gcol];
       if (p.bias) y += bf2f(p.bias[gcol]);
       y = apply_act(y, p.act);
       if constexpr (OUT_F32) ((float*)p.C)[(long)grow * p.ldc + gcol] = y;
@@ -664,6 +731,7 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   p.bias = (const bf16_t*)bias;
   p.C = C; p.ldc = ldc;
   p.M = M; p.N = N; p.K = K; p.act = act;
+  p.sa = nullptr; p.sb = nullptr;
   if (M <= 0 || N <= 0) return 0;
   if (M <= 64) {
     const int MT = (M + 15) / 16;
@@ -671,21 +739,54 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
     dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
 #define DG_CASE(mt)                                                                                        \
   case mt:                                                                                                 \
-    if (out_f32) hipLaunchKernelGGL((gemm_decode_kernel<mt, true>), grid, block, 0, stream, p, slabs, tickets, split); \
-    else hipLaunchKernelGGL((gemm_decode_kernel<mt, false>), grid, block, 0, stream, p, slabs, tickets, split);       \
+    if (out_f32) hipLaunchKernelGGL((gemm_decode_kernel<mt, true, false>), grid, block, 0, stream, p, slabs, tickets, split); \
+    else hipLaunchKernelGGL((gemm_decode_kernel<mt, false, false>), grid, block, 0, stream, p, slabs, tickets, split);       \
     break;
     switch (MT) { DG_CASE(1) DG_CASE(2) DG_CASE(3) DG_CASE(4) default: return -1; }
 #undef DG_CASE
   } else if (use_256(M, N) && (N % 8) == 0 && (ldc % 8) == 0) {
     const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
     dim3 grid(tiles), block(512);
-    if (out_f32) hipLaunchKernelGGL((gemm_256_kernel<true>), grid, block, 0, stream, p);
-    else hipLaunchKernelGGL((gemm_256_kernel<false>), grid, block, 0, stream, p);
+    if (out_f32) hipLaunchKernelGGL((gemm_256_kernel<true, false>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((gemm_256_kernel<false, false>), grid, block, 0, stream, p);
   } else {
     const int tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     dim3 grid(tiles), block(256);
     if (out_f32) hipLaunchKernelGGL((gemm_tile_kernel<true>), grid, block, 0, stream, p);
     else hipLaunchKernelGGL((gemm_tile_kernel<false>), grid, block, 0, stream, p);
+  }
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+// fp8 GEMMs: C[M,N] (bf16) = act( (A_q B_q^T) * sa[row] * sb[col] + bias ), A_q / B_q OCP e4m3fn.
+//  * M > 64 : W8A8, 256x256 8-phase kernel on MX-scaled mfma_16x16x128_f8f6f4 (2x the bf16 rate)
+//  * M <= 64: W8A16 skinny kernel (A = bf16 activations, sa ignored): half the weight bytes
+extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void* B, long ldb, const float* sb,
+                           const void* bias, void* C, long ldc, int M, int N, int K, int act, int a_is_bf16,
+                           float* slabs, unsigned* tickets, hipStream_t stream) {
+  GemmArgs p;
+  p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
+  p.U = nullptr; p.ldu = 0; p.UB = nullptr; p.ldub = 0; p.Rp = 0;
+  p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K; p.act = act;
+  p.sa = sa; p.sb = sb;
+  if (M <= 0 || N <= 0) return 0;
+  if (a_is_bf16) {
+    if (M > 64 || K % 64) return -1;
+    const int MT = (M + 15) / 16;
+    const int split = (slabs && tickets) ? decode_split(N, K) : 1;
+    dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
+    switch (MT) {
+      case 1: hipLaunchKernelGGL((gemm_decode_kernel<1, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;
+      case 2: hipLaunchKernelGGL((gemm_decode_kernel<2, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;
+      case 3: hipLaunchKernelGGL((gemm_decode_kernel<3, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;
+      case 4: hipLaunchKernelGGL((gemm_decode_kernel<4, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;
+      default: return -1;
+    }
+  } else {
+    if (K % 128 || N % 8) return -1;
+    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    hipLaunchKernelGGL((gemm_256_kernel<false, true>), dim3(tiles), dim3(512), 0, stream, p);
   }
   RT_LAUNCH_CHECK();
   return 0;

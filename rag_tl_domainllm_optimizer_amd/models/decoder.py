@@ -53,6 +53,9 @@ class DecoderLayer(nn.Module):
         self.lora: Dict[str, ops.LoRAGroup] = {}
         self.lora_params = nn.ParameterDict()
         self.lora_enabled = True
+        # fp8 inference images of the projection weights (CausalLM.set_fp8)
+        self.fp8_enabled = False
+        self._fp8: Dict[str, ops.Fp8Cache] = {}
 
     # ---------------------------------------------------------------- helpers
     def _lg(self, name):
@@ -62,26 +65,31 @@ class DecoderLayer(nn.Module):
     def _b(self, name):
         return getattr(self, name, None)
 
+    def _f8(self, name):
+        if not self.fp8_enabled:
+            return None
+        return self._fp8.setdefault(name, ops.Fp8Cache())
+
     def attn_in(self, x, residual):
         cfg = self.cfg
         if cfg.arch == "opt":
             h, residual = ops.layer_norm(x, self.ln1_w, self.ln1_b, cfg.norm_eps, residual)
         else:
             h, residual = ops.rms_norm(x, self.ln1_w, cfg.norm_eps, residual)
-        qkv = ops.linear(h, self.qkv_w, self._b("qkv_b"), lora=self._lg("qkv"))
+        qkv = ops.linear(h, self.qkv_w, self._b("qkv_b"), lora=self._lg("qkv"), fp8=self._f8("qkv"))
         return qkv, residual
 
     def mlp(self, a, residual):
         cfg = self.cfg
-        a = ops.linear(a, self.o_w, self._b("o_b"), lora=self._lg("o"))
+        a = ops.linear(a, self.o_w, self._b("o_b"), lora=self._lg("o"), fp8=self._f8("o"))
         if cfg.arch == "opt":
             h, residual = ops.layer_norm(a, self.ln2_w, self.ln2_b, cfg.norm_eps, residual)
-            f = ops.linear(h, self.fc1_w, self.fc1_b, act=cfg.hidden_act, lora=self._lg("fc1"))
-            d = ops.linear(f, self.fc2_w, self.fc2_b, lora=self._lg("fc2"))
+            f = ops.linear(h, self.fc1_w, self.fc1_b, act=cfg.hidden_act, lora=self._lg("fc1"), fp8=self._f8("fc1"))
+            d = ops.linear(f, self.fc2_w, self.fc2_b, lora=self._lg("fc2"), fp8=self._f8("fc2"))
         else:
             h, residual = ops.rms_norm(a, self.ln2_w, cfg.norm_eps, residual)
-            gu = ops.linear(h, self.gate_up_w, lora=self._lg("gate_up"))
-            d = ops.linear(ops.swiglu(gu), self.down_w, lora=self._lg("down"))
+            gu = ops.linear(h, self.gate_up_w, lora=self._lg("gate_up"), fp8=self._f8("gate_up"))
+            d = ops.linear(ops.swiglu(gu), self.down_w, lora=self._lg("down"), fp8=self._f8("down"))
         return d, residual
 
 
@@ -246,6 +254,15 @@ class CausalLM(nn.Module):
             for g in layer.lora.values():
                 prev = prev or g.use_merged
                 g.use_merged = on
+        return prev
+
+    def set_fp8(self, on: bool = True):
+        """fp8 (e4m3fn) weights for no-grad forwards (prefill, decode, reference scoring):
+        W8A8 MX-MFMA GEMMs for M > 64, W8A16 weight streaming for decode. Training forwards
+        (autograd) keep the bf16 weights. Returns the previous setting."""
+        prev = any(layer.fp8_enabled for layer in self.layers)
+        for layer in self.layers:
+            layer.fp8_enabled = on
         return prev
 
     def refresh_lora(self):

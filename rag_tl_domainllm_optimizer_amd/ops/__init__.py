@@ -8,4 +8,5 @@ from .attention import (  # noqa: F401
 )
 from .misc import embedding, gae, ivf_scan, pool_normalize, sample, swiglu, token_logprobs, topk  # noqa: F401
 from .optim import FlatParams, FusedAdamW  # noqa: F401
+from .fp8 import Fp8Cache, dequantize_fp8, gemm_fp8, quantize_fp8  # noqa: F401
 from . import reference  # noqa: F401

@@ -1,0 +1,81 @@
+"""fp8 (OCP e4m3fn) inference path for frozen weights (BASELINE config 5).
+
+* weights: per-output-channel absmax scale, quantised once per adapter update (LoRA merged first);
+* M > 64 (prefill / reference-model scoring): W8A8 — activations quantised per token, one
+  MX-scaled ``mfma_f32_16x16x128_f8f6f4`` 256x256 GEMM (2x the bf16 MFMA rate), scales in the
+  epilogue;
+* M <= 64 (decode): W8A16 — bf16 activations, fp8 weights widened in registers by the split-K
+  skinny kernel: half the weight bytes streamed per token.
+gfx950 uses OCP e4m3fn (max 448), not the MI300 fnuz variant (cdna_hip_programming.md §3).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+from ._ext import native, on_gpu
+
+E4M3_MAX = 448.0
+
+
+def quantize_fp8(x: torch.Tensor):
+    """Per-row absmax quantisation -> (uint8 e4m3fn bits [R, C], fp32 scale [R])."""
+    if on_gpu(x):
+        q, s = native().quant_fp8(x.contiguous())
+        return q, s
+    xf = x.float()
+    amax = xf.abs().amax(1)
+    s = torch.where(amax > 0, amax / E4M3_MAX, torch.ones_like(amax))
+    q = (xf / s[:, None]).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q, s
+
+
+def dequantize_fp8(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    return q.view(torch.float8_e4m3fn).float() * s[:, None]
+
+
+def gemm_fp8(x: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor, bias=None, act=0, out=None) -> torch.Tensor:
+    """y = act(x W^T + b) with W given as fp8 (wq, sw). W8A16 for M <= 64, W8A8 above."""
+    M, K = x.shape
+    if on_gpu(x):
+        C = native()
+        if M <= 64:
+            return C.gemm_fp8(x, None, wq, sw, bias, act, out)
+        xq, sx = quantize_fp8(x)
+        return C.gemm_fp8(xq, sx, wq, sw, bias, act, out)
+    xf = x.float() if M <= 64 else dequantize_fp8(*quantize_fp8(x))
+    y = xf @ dequantize_fp8(wq, sw).t()
+    if bias is not None:
+        y = y + bias.float()
+    y = ref.apply_act(y, act).to(x.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def fp8_supported(w: torch.Tensor) -> bool:
+    return w.dim() == 2 and w.shape[1] % 128 == 0 and w.shape[0] % 8 == 0
+
+
+class Fp8Cache(dict):
+    """fp8 image of one weight, refreshed in place when the source tensor changes (address or
+    in-place version, e.g. a re-merged LoRA weight) so graph-captured decode steps stay valid."""
+
+    @torch.no_grad()
+    def get(self, w: torch.Tensor):
+        key = (w.data_ptr(), w._version)
+        if self.get_key() != key:
+            q, s = quantize_fp8(w)
+            if "q" in self and self["q"].shape == q.shape and self["q"].device == q.device:
+                self["q"].copy_(q)
+                self["s"].copy_(s)
+            else:
+                self["q"], self["s"] = q, s
+            self["key"] = key
+        return self["q"], self["s"]
+
+    def get_key(self):
+        return dict.get(self, "key")

@@ -194,8 +194,9 @@ class _LinearFn(torch.autograd.Function):
         return (dx, dw, db, None, None, *lora_grads)
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional[LoRAGroup] = None):
-    """y = act(x W^T (+ LoRA) + b) over the last dim of x."""
+def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional[LoRAGroup] = None, fp8=None):
+    """y = act(x W^T (+ LoRA) + b) over the last dim of x. ``fp8`` (an ``ops.fp8.Fp8Cache``)
+    enables the fp8 inference path for this weight (no-grad only; LoRA merged first)."""
     act_id = ACT_IDS[act] if not isinstance(act, int) else act
     shp = x.shape
     x2 = x.reshape(-1, shp[-1])
@@ -204,6 +205,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
     use_lora = lora is not None and lora.enabled
     if use_lora and (lora.a_pad is None or lora.a_pad.device != x.device):
         lora.refresh(dtype=w.dtype)
+    if fp8 is not None and not torch.is_grad_enabled():
+        from .fp8 import fp8_supported, gemm_fp8
+
+        w_eff = lora.merged_weight(w) if use_lora else w
+        if fp8_supported(w_eff) and (x2.shape[0] > 64 or x2.shape[1] % 64 == 0):
+            q, s = fp8.get(w_eff)
+            y = gemm_fp8(x2, q, s, bias, act_id)
+            return y.reshape(*shp[:-1], w.shape[0])
     if use_lora and lora.use_merged and not torch.is_grad_enabled():
         y = gemm(x2, lora.merged_weight(w), None, None, bias, act_id)
         return y.reshape(*shp[:-1], w.shape[0])

@@ -85,6 +85,40 @@ def main():
             print(json.dumps(r), flush=True)
             del ws_
         torch.cuda.empty_cache()
+    # fp8: W8A8 MX-MFMA tile kernel (large M, incl. per-token activation quantisation) and W8A16
+    # skinny decode (cold weights)
+    for M in ((7168, 20480) if want("fp8") else ()):
+        for name, N, K in gemms:
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            w = (torch.randn(N, K, device=dev) / math.sqrt(K)).to(torch.bfloat16)
+            wq, sw = ops.quantize_fp8(w)
+            xq, sx = ops.quantize_fp8(a)
+            t8 = timeit(lambda: C.gemm_fp8(xq, sx, wq, sw))
+            tq = timeit(lambda: ops.quantize_fp8(a))
+            tl = timeit(lambda: a @ w.t())
+            flops = 2 * M * N * K
+            r = dict(kind="gemm_fp8", name=name, M=M, N=N, K=K, us=t8, quant_us=tq, bf16_lib_us=tl,
+                     tflops=flops / t8 / 1e6, tflops_with_quant=flops / (t8 + tq) / 1e6, lib_tflops=flops / tl / 1e6)
+            res.append(r)
+            print(json.dumps(r), flush=True)
+    for M in ((1, 16, 64) if want("fp8") else ()):
+        for name, N, K in gemms:
+            ncopy = max(2, int(1.2e9 // (N * K)))
+            wqs = [ops.quantize_fp8((torch.randn(N, K, device=dev) / math.sqrt(K)).to(torch.bfloat16))
+                   for _ in range(ncopy)]
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            it = [0]
+
+            def run8():
+                it[0] = (it[0] + 1) % ncopy
+                return C.gemm_fp8(a, None, wqs[it[0]][0], wqs[it[0]][1])
+
+            t8 = timeit(run8, iters=ncopy * 2)
+            r = dict(kind="gemm_w8a16_cold", name=name, M=M, N=N, K=K, us=t8, gbs=N * K / t8 / 1e3)
+            res.append(r)
+            print(json.dumps(r), flush=True)
+            del wqs
+        torch.cuda.empty_cache()
     # LoRA-fused vs separate
     for M in ((2048, 8192) if want("lora") else ()):
         N, K, R = NQKV, H, 64
