@@ -14,6 +14,11 @@ value = generated rollout tokens summed over ranks / max-over-ranks wall time of
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
+
+Secondary modes (not the headline; each prints its own JSON line):
+  --mode sft       BASELINE config 3: RAFT-style LoRA r=16 SFT with distractor docs, tokens/s
+  --mode pipeline  BASELINE config 5: RAG index -> LoRA SFT -> PPO on one policy (default
+                   --model llama2-13b; --fp8 runs rollouts / reference scoring on e4m3fn weights)
 """
 from __future__ import annotations
 
@@ -57,7 +62,12 @@ def main():
     ap.add_argument("--skip-latency", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--mode", default="ppo", choices=["ppo", "sft", "pipeline"])
+    ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3fn) weights for no-grad forwards (config 5)")
+    ap.add_argument("--sft-batch", type=int, default=16, help="SFT sequences per GPU per step")
     args = ap.parse_args()
+    if args.mode == "pipeline" and args.model == "mistral-7b" and "--model" not in sys.argv:
+        args.model = "llama2-13b"
 
     from rag_tl_domainllm_optimizer_amd import models, parallel
     from rag_tl_domainllm_optimizer_amd.data import SyntheticCorpus
@@ -93,6 +103,9 @@ def main():
     del emb
     torch.cuda.synchronize()
     log(f"[bench] indexed {len(corpus)} docs (IVF nlist={index.nlist}) in {time.perf_counter() - t0:.1f}s")
+
+    if args.mode in ("sft", "pipeline"):
+        return run_sft_pipeline(args, di, policy, tok, encoder, corpus, index)
 
     # ---- PPO trainer ----
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
@@ -180,6 +193,95 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 json.dump(res, f, indent=2)
+    parallel.shutdown()
+
+
+def _timed(di, fn, steps):
+    from rag_tl_domainllm_optimizer_amd import parallel
+
+    parallel.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = [fn(i) for i in range(steps)]
+    torch.cuda.synchronize()
+    parallel.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=di.device)
+    parallel.all_reduce_(el, "max")
+    return float(el), out
+
+
+def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
+    """config 3 (--mode sft) and config 5 (--mode pipeline) on synthetic data / random weights."""
+    import random
+
+    from rag_tl_domainllm_optimizer_amd import parallel
+    from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
+    from rag_tl_domainllm_optimizer_amd.train import SFTConfig, SFTTrainer, build_raft_examples
+    from rag_tl_domainllm_optimizer_amd.train.ppo import PPOConfig, PPOTrainer
+
+    rng = random.Random(200 + di.rank)
+    items = corpus.sample_queries(args.sft_batch * (args.steps + args.warmup), seed=rng.randrange(1 << 30))
+    ex = build_raft_examples([{"query": i.query, "ground_truth": i.ground_truth, "gold_doc": i.gold_doc}
+                              for i in items], corpus.docs)
+    sft = SFTTrainer(policy, tok, SFTConfig(batch_size=args.sft_batch, lora_r=16, max_seq=args.max_prompt + 64,
+                                            warmup_steps=0, lr_schedule="constant"))
+    B = args.sft_batch
+    for w in range(args.warmup):
+        m = sft.step(ex[w * B:(w + 1) * B])
+        log(f"[bench] sft warmup {w}: {m['step_time_s']:.2f}s loss={m['loss']:.3f}")
+    seq_tok = []
+
+    def sft_step(i):
+        batch = ex[(args.warmup + i) * B:(args.warmup + i + 1) * B]
+        ids, start, _ = sft.encode([e["prompt"] for e in batch], [e["answer"] for e in batch])
+        seq_tok.append(int((ids.shape[1] - start).sum()))
+        return sft.step(batch)
+
+    el, ms = _timed(di, sft_step, args.steps)
+    sft_tok = sum(seq_tok) * di.world
+    res = {"metric": "RAFT LoRA SFT tokens/sec (node), " + args.model, "value": sft_tok / el, "unit": "tokens/s",
+           "n_gpus": di.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic (random-init weights, synthetic corpus)",
+           "config": {"model": args.model, "global_batch": B * di.world, "seq_len": args.max_prompt + 64,
+                      "parallelism": f"dp{di.world}", "lora_r": 16, "raft_distractors": 3},
+           "final_loss": ms[-1]["loss"] if ms else None}
+    if args.mode == "sft":
+        if di.is_main:
+            print(json.dumps(res), flush=True)
+        parallel.shutdown()
+        return
+    # ---- config 5: the SFT-adapted policy continues into PPO (same adapters, fp8 inference) ----
+    if args.fp8:
+        policy.set_fp8(True)
+    pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
+                   lora_r=16, lora_alpha=32.0, seed=0)
+    ppo = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
+
+    def make_batch():
+        its = corpus.sample_queries(args.rollout_batch, seed=rng.randrange(1 << 30))
+        qs = [it.query for it in its]
+        _, ids = index.search(encoder.encode(qs), args.top_k_docs)
+        return {"query": qs, "retrieved_docs": [[corpus.docs[i] for i in row if i >= 0] for row in ids.tolist()],
+                "ground_truth": [it.ground_truth for it in its]}
+
+    for w in range(args.warmup):
+        ppo.step(make_batch())
+    batches = [make_batch() for _ in range(args.steps)]
+    el2, pm = _timed(di, lambda i: ppo.step(batches[i]), args.steps)
+    toks = sum(m["rollout_tokens"] for m in pm) * di.world
+    res2 = {"metric": "RAG -> LoRA SFT -> PPO pipeline, " + args.model, "value": toks / el2, "unit": "tokens/s",
+            "n_gpus": di.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el2 / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp8-e4m3fn inference / bf16 training" if args.fp8 else "bf16",
+            "data": "synthetic (random-init weights, synthetic corpus)",
+            "config": {"model": args.model, "global_batch": args.rollout_batch * di.world,
+                       "seq_len": args.max_prompt + args.new_tokens, "parallelism": f"dp{di.world}",
+                       "lora_r": 16, "fp8": bool(args.fp8)},
+            "sft": res, "ppo_phase_s_per_step": {k: sum(m[k] for m in pm) / len(pm) for k in pm[0]
+                                                  if k.startswith("time/")}}
+    if di.is_main:
+        print(json.dumps(res2), flush=True)
     parallel.shutdown()
 
 
