@@ -567,7 +567,7 @@ __device__ __forceinline__ void dg_mma(const DGRegs<MT>& r, f32x4 (&acc)[MT][4])
 }
 
 template <int MT, bool OUT_F32, bool W8>
-__global__ __launch_bounds__(256) void gemm_decode_kernel(GemmArgs p, float* __restrict__ slabs,
+__global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* __restrict__ slabs,
                                                           unsigned* __restrict__ tickets, int split) {
   constexpr int ROWS = MT * 16;
   constexpr int LDR = DG_COLS + 1;
