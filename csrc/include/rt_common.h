@@ -17,6 +17,20 @@
 
 #define RT_LAUNCH_CHECK() RT_HIP_CHECK(hipGetLastError())
 
+// Device-side bounds checks of the debug build (python -m rag_tl_domainllm_optimizer_amd._build
+// --debug): a failed check prints the condition and traps the wave, which surfaces as
+// a launch error on the next synchronisation instead of a silent out-of-bounds access.
+#ifndef RAGTL_DEBUG
+#define RAGTL_DEBUG 0
+#endif
+#define RT_ASSERT(cond)                                                                 \
+  do {                                                                                  \
+    if (RAGTL_DEBUG && !(cond)) {                                                       \
+      printf("RT_ASSERT failed %s:%d: %s\n", __FILE__, __LINE__, #cond);               \
+      __builtin_trap();                                                                 \
+    }                                                                                   \
+  } while (0)
+
 namespace rt {
 
 typedef uint16_t bf16_t;  // raw bf16 bits; storage type for every bf16 tensor

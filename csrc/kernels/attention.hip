@@ -583,6 +583,7 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
   const int part = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int len = a.attn_len[b];
   const int s_new = a.slot[b];
+  RT_ASSERT(len <= a.Smax && s_new >= 0 && s_new < a.Smax);
   int kbeg = a.kv_start ? a.kv_start[b] : 0;
   if (a.window > 0) kbeg = max(kbeg, len - a.window);
   const int p0 = max(part * a.PS, kbeg), p1 = min((part + 1) * a.PS, len);

@@ -55,6 +55,7 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(bf16_t* __restrict__ qkv,
     const int bidx = t / S, s = t % S;
     const int hk = is_k ? head - Hq : head - Hq - Hkv;
     bf16_t* cache = is_k ? kc : vc;
+    RT_ASSERT((slot_base ? slot_base[bidx] : 0) + s < Smax);
     bf16_t* dst = cache + (((long)bidx * Hkv + hk) * Smax + (slot_base ? slot_base[bidx] : 0) + s) * D;
     *(uint4*)(dst + e1) = pack8(a);
     *(uint4*)(dst + e2) = pack8(b);
@@ -112,6 +113,7 @@ __global__ __launch_bounds__(256) void embed_kernel(const bf16_t* __restrict__ t
   if (gid >= T * nv) return;
   const long t = gid / nv;
   const int c = gid % nv;
+  RT_ASSERT(ids[t] >= 0);
   uint4 v = *(const uint4*)(table + ids[t] * H + c * 8);
   if (ptable) {
     float a[8], b[8];

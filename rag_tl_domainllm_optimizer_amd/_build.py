@@ -67,10 +67,14 @@ def kernel_flags(debug: bool = False):
     ]
 
 
-def host_flags(debug: bool = False):
+def host_flags(debug: bool = False, sanitize: bool = False):
     inc, _, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
-    flags = ["-O1", "-g"] if debug else ["-O2"]
+    flags = ["-O1", "-g"] if (debug or sanitize) else ["-O2"]
+    if sanitize:
+        # host-only AddressSanitizer + UBSan (tokenizer, IVF host code, bindings); the runtime is
+        # LD_PRELOADed into python, GPU code is never sanitized
+        flags += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
     flags += [
         "-fPIC", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
         f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-DTORCH_API_INCLUDE_EXTENSION_H", "-fopenmp",
@@ -82,14 +86,17 @@ def host_flags(debug: bool = False):
     return flags
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int | None = None, debug: bool = False) -> str:
-    """Compile every HIP kernel for gfx950 and link the extension. Returns the .so path."""
+def build(verbose: bool = False, force: bool = False, jobs: int | None = None, debug: bool = False,
+          sanitize: bool = False) -> str:
+    """Compile every HIP kernel for gfx950 and link the extension. Returns the .so path.
+    ``sanitize`` builds the host C++ with ASan/UBSan into build/asan/ (load it with
+    RAGTL_EXT_PATH=<path> and LD_PRELOAD of libasan / libubsan)."""
     os.makedirs(BUILD, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     headers = glob.glob(os.path.join(CSRC, "include", "*.h")) + glob.glob(os.path.join(CSRC, "host", "*.h"))
     kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hosts = [os.path.join(CSRC, "bindings.cpp")] + sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
-    kf, hf = kernel_flags(debug), host_flags(debug)
+    kf, hf = kernel_flags(debug), host_flags(debug, sanitize)
 
     jobs_list = []
     objs = []
@@ -113,8 +120,13 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None, d
                 fut.result()
 
     out = _ext_path()
-    link_key = hashlib.sha256("|".join(objs).encode()).hexdigest()[:16]
     stamp = os.path.join(BUILD, "link.stamp")
+    if sanitize:
+        adir = os.path.join(REPO, "build", "asan")
+        os.makedirs(adir, exist_ok=True)
+        out = os.path.join(adir, os.path.basename(out))
+        stamp = os.path.join(adir, "link.stamp")
+    link_key = hashlib.sha256("|".join(objs).encode()).hexdigest()[:16]
     prev = open(stamp).read().strip() if os.path.exists(stamp) else ""
     if force or jobs_list or prev != link_key or not os.path.exists(out):
         _, tlib, _ = _torch_paths()
@@ -130,4 +142,4 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None, d
 
 if __name__ == "__main__":
     force = "--force" in sys.argv
-    print(build(verbose="-v" in sys.argv, force=force, debug="--debug" in sys.argv))
+    print(build(verbose="-v" in sys.argv, force=force, debug="--debug" in sys.argv, sanitize="--sanitize" in sys.argv))

@@ -7,6 +7,7 @@ tensors use the eager reference implementations in :mod:`.reference`.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 
 _C = None
@@ -16,6 +17,12 @@ _err: Exception | None = None
 def _load():
     global _C, _err
     if _C is not None or _err is not None:
+        return
+    alt = os.environ.get("RAGTL_EXT_PATH")
+    if alt:  # e.g. the host-sanitizer build (python -m rag_tl_domainllm_optimizer_amd._build --sanitize)
+        spec = importlib.util.spec_from_file_location("rag_tl_domainllm_optimizer_amd._C", alt)
+        _C = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(_C)
         return
     try:
         _C = importlib.import_module("rag_tl_domainllm_optimizer_amd._C")

@@ -135,3 +135,24 @@ def test_rccl_process_group_world1():
                HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT, RAGTL_FORCE_PG="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_reward_stream_overlap_matches_serial():
+    """Reward scoring on the side HIP stream (overlapped with the reference forward) gives the same
+    rewards and losses as the serialized schedule (SURVEY §5.2 stream-overlap correctness)."""
+    from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
+    from rag_tl_domainllm_optimizer_amd.train.ppo import PPOConfig, PPOTrainer
+
+    res = []
+    for overlap in (True, False):
+        pol, tok, enc, corpus = _tiny_stack(5)
+        items = corpus.sample_queries(8, seed=1)
+        batch = {"query": [i.query for i in items], "retrieved_docs": [[corpus.docs[i.gold_doc]] for i in items],
+                 "ground_truth": [i.ground_truth for i in items]}
+        tr = PPOTrainer(pol, tok, RewardModel(enc), PPOConfig(max_new_tokens=8, max_prompt_tokens=96,
+                                                              minibatch_size=4, lora_r=8, overlap_reward=overlap,
+                                                              seed=3), max_batch=8)
+        res.append(tr.step(batch))
+    a, b = res
+    for k in ("reward_mean", "factual_accuracy", "relevance", "conciseness", "kl_ref", "total_loss"):
+        assert abs(a[k] - b[k]) < 1e-5, (k, a[k], b[k])

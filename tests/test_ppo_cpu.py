@@ -67,3 +67,42 @@ def test_ppo_resume_reproduces_next_step(tmp_path):
     for a, b in zip(params_a, params_b):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
     assert abs(m_a["total_loss"] - m_b["total_loss"]) < 1e-5
+
+
+def test_ppo_deterministic_across_runs():
+    """Same seeds -> identical rollouts, rewards and losses in two independent runs."""
+    outs = []
+    for _ in range(2):
+        tr, recs = _setup(seed=0)
+        loader = RecordLoader(recs, batch_size=8, seed=0)
+        b = next(iter(loader))
+        m = tr.step(b)
+        outs.append((m, [p.detach().clone() for p in tr.policy.lora_parameters()]))
+    (m1, p1), (m2, p2) = outs
+    for k in REF_KEYS + ["kl_ref"]:
+        assert m1[k] == m2[k], (k, m1[k], m2[k])
+    assert all(torch.equal(a, b) for a, b in zip(p1, p2))
+
+
+def test_fault_injection_then_resume_matches(tmp_path, monkeypatch):
+    """RAGTL_FAULT_AT_STEP raises mid-run; resuming from the last checkpoint reproduces the
+    uninterrupted run's next step."""
+    import pytest
+
+    tr, recs = _setup(seed=0)
+    batches = list(RecordLoader(recs, batch_size=8, seed=0))
+    tr.step(batches[0])
+    ck = str(tmp_path / "f" / "s1")
+    tr.save_checkpoint(ck, full_policy=False)
+    ref = tr.step(batches[1])
+    tr2, _ = _setup(seed=0)
+    tr2.load_checkpoint(ck)
+    monkeypatch.setenv("RAGTL_FAULT_AT_STEP", str(tr2.global_step))
+    with pytest.raises(RuntimeError):
+        tr2.step(batches[1])
+    monkeypatch.delenv("RAGTL_FAULT_AT_STEP")
+    tr3, _ = _setup(seed=0)
+    tr3.load_checkpoint(ck)
+    got = tr3.step(batches[1])
+    for k in ("reward_mean", "total_loss", "policy_loss", "kl_ref"):
+        assert abs(got[k] - ref[k]) < 1e-6, (k, got[k], ref[k])
