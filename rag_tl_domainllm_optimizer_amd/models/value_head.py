@@ -11,11 +11,13 @@ import torch.nn as nn
 
 
 class ValueHead(nn.Module):
-    def __init__(self, hidden_size: int, device=None):
+    def __init__(self, hidden_size: int, device=None, seed: int = 0):
         super().__init__()
         self.linear = nn.Linear(hidden_size, 1, device=device, dtype=torch.float32)
+        # explicit CPU generator: identical init on every DP rank and in every run
+        g = torch.Generator(device="cpu").manual_seed(seed)
         with torch.no_grad():
-            self.linear.weight.normal_(0.0, 1.0 / (hidden_size ** 0.5))
+            self.linear.weight.copy_(torch.randn(1, hidden_size, generator=g) / (hidden_size ** 0.5))
             self.linear.bias.zero_()
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:

@@ -124,7 +124,7 @@ class PPOTrainer:
         if getattr(policy, "lora_config", None) is None:
             policy.add_lora(c.lora_r, c.lora_alpha, list(c.lora_targets), seed=c.seed)
         policy.freeze_base()
-        self.value_head = value_head or ValueHead(policy.cfg.hidden_size, device=self.device)
+        self.value_head = value_head or ValueHead(policy.cfg.hidden_size, device=self.device, seed=c.seed + 17)
         # LoRA A/B + value head re-homed into one flat fp32 buffer (fused AdamW, bucketed all-reduce)
         self.flat = ops.FlatParams(list(policy.lora_parameters()) + list(self.value_head.parameters()))
         policy.refresh_lora()
