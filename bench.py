@@ -178,7 +178,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (random-init weights, synthetic 100k-doc corpus)",
+        "data": f"synthetic (random-init weights, synthetic {args.ndocs}-doc corpus)",
         "config": {"model": args.model, "global_batch": args.rollout_batch * di.world,
                    "seq_len": args.max_prompt + args.new_tokens, "parallelism": f"dp{di.world}",
                    "new_tokens": args.new_tokens, "lora_r": 16, "encoder": args.encoder, "ndocs": args.ndocs,

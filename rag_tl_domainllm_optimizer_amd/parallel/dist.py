@@ -55,7 +55,9 @@ def init(backend: Optional[str] = None, timeout_s: float = 900.0, device: Option
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    be = backend or ("nccl" if use_cuda else "gloo")
+    # RAGTL_DIST_BACKEND=gloo runs several ranks on one GPU (RCCL needs one GPU per rank): used to
+    # rehearse the multi-rank GPU code path on a single-GPU box
+    be = backend or os.environ.get("RAGTL_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     force_group = force_group or os.environ.get("RAGTL_FORCE_PG", "0") == "1"
     if (world > 1 or force_group) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
