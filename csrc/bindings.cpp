@@ -14,11 +14,13 @@
 
 #include "host/tokenizer.h"
 #include "host/ivf_host.h"
+#include "rt_workspace.h"
 
 extern "C" {
 int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
                long, int, int, int, int, int, float*, unsigned*, hipStream_t);
 void rt_gemm_set_variant(int);
+void rt_gemm_set_m64_split(int);
 int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
                 int, int, int, float*, unsigned*, hipStream_t);
 int rt_quant_fp8_rows(const void*, long, void*, long, float*, long, int, hipStream_t);
@@ -95,8 +97,8 @@ DecodeWS& decode_ws(const Tensor& like, hipStream_t st) {
   auto it = map->find(key);
   if (it != map->end()) return *it->second;
   auto* w = new DecodeWS();
-  w->slabs = at::empty({1 << 22}, like.options().dtype(at::kFloat));
-  w->tickets = at::zeros({1 << 16}, like.options().dtype(at::kInt));
+  w->slabs = at::empty({RT_SPLITK_SLAB_FLOATS}, like.options().dtype(at::kFloat));
+  w->tickets = at::zeros({RT_SPLITK_TICKETS}, like.options().dtype(at::kInt));
   (*map)[key] = w;
   return *w;
 }
@@ -522,6 +524,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM C = act(A W^T + U UB^T + bias)", py::arg("a"), py::arg("w"),
         py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out_f32") = false, py::arg("out") = py::none());
+  m.def("gemm_set_m64_split", &rt_gemm_set_m64_split, "tuning: fixed split-K of the M<=64 ring kernel (0 = auto)");
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
   m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");

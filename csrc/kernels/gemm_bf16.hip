@@ -20,6 +20,7 @@
 // Replaces every projection GEMM of the reference's HF forward passes (reference
 // call sites reinforcement_learning_optimization_after_rag.py:38,200,207,313,318).
 #include "rt_common.h"
+#include "rt_workspace.h"
 
 #include <cmath>
 
@@ -648,6 +649,7 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
       const int e = tid + 256 * i;
       float t = 0.f;
       if (e / DG_COLS < p.M) {
+#pragma unroll 8
         for (int s2 = 0; s2 < split; ++s2)
           t += __hip_atomic_load(base + (long)s2 * (ROWS * DG_COLS) + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -684,6 +686,154 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// M in (16, 64]: LDS-DMA ring GEMM (rollout decode at batch 64)
+// ---------------------------------------------------------------------------------------------
+// Block = 4 waves, 64 output columns x all (<= 64) rows x a K range (split-K over workgroups).
+// Each 64-deep K-step stages X[64 x 64] and W[64 x 64] (8 KiB each, 2 x 16-B global_load_lds
+// per lane per operand) into one slot of a 4-slot ring; three steps stay in flight (counted
+// vmcnt, raw s_barrier — never __syncthreads inside the loop, which would drain the DMA queue),
+// so ~96 KiB per CU of loads are outstanding at 2 blocks/CU without costing VGPRs. Wave w owns
+// rows [16w, 16w+16) x 64 columns (4 MFMA fragments). Split-K partials use the write-through
+// ticket hand-off of gemm_decode_kernel.
+constexpr int R64_SLOTS = 4;
+constexpr int R64_SLOT = 2 * 64 * 128;  // X + W, 64 rows x 128 B each
+
+template <bool OUT_F32>
+__global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __restrict__ slabs,
+                                                          unsigned* __restrict__ tickets, int split) {
+  __shared__ __attribute__((aligned(16))) char smem[R64_SLOTS * R64_SLOT];  // the only __shared__ object
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cg = blockIdx.x / split, sp = blockIdx.x % split;
+  const int n0 = cg * 64;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int nk = p.K / 64;
+  const int t0 = (int)((long)sp * nk / split), t1 = (int)((long)(sp + 1) * nk / split);
+  const int nt = t1 - t0;
+
+  // staging: lane -> (row within an 8-row piece, 16-B slot); 2 pieces per operand per wave
+  const int srow = lane >> 3;
+  auto stage = [&](int t) {  // K-step t (absolute) -> slot (t - t0) % R64_SLOTS
+    char* slot = smem + ((t - t0) % R64_SLOTS) * R64_SLOT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lr = (wid * 2 + j) * 8 + srow;  // 0..63
+      const int ck = (lane & 7) ^ lds_swz(lr);
+      const bf16_t* xa = p.A + (long)min(lr, p.M - 1) * p.lda + (long)t * 64 + ck * 8;
+      const bf16_t* wb = p.B + (long)min(n0 + lr, p.N - 1) * p.ldb + (long)t * 64 + ck * 8;
+      __builtin_amdgcn_global_load_lds((const void*)xa, (lds_void*)(slot + (wid * 2 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)wb, (lds_void*)(slot + 8192 + (wid * 2 + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: steps t0 .. t0+2 in flight
+#pragma unroll
+  for (int i = 0; i < R64_SLOTS - 1; ++i)
+    if (i < nt) stage(t0 + i);
+
+  for (int i = 0; i < nt; ++i) {
+    // retire step i (each step = 4 DMAs per lane); later steps stay in flight
+    const int ahead = min(R64_SLOTS - 2, nt - 1 - i);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    // refill the slot read in the previous iteration (every wave is past it: barrier above)
+    if (i + R64_SLOTS - 1 < nt) stage(t0 + i + R64_SLOTS - 1);
+    const char* slot = smem + (i % R64_SLOTS) * R64_SLOT;
+    bf16x8 a[2], b[4][2];
+    const int ar = wid * 16 + frow;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fq;
+      a[kk] = *(const bf16x8*)(slot + ar * 128 + ((c ^ lds_swz(ar)) << 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int br = j * 16 + frow;
+        b[j][kk] = *(const bf16x8*)(slot + 8192 + br * 128 + ((c ^ lds_swz(br)) << 4));
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk], b[j][kk], acc[j], 0, 0, 0);
+  }
+
+  // lane holds C[16 wid + 4 fq + r][16 j + frow]
+  if (split > 1) {
+    float* slab = slabs + ((long)cg * split + sp) * (64 * 64);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wid * 16 + fq * 4 + r;
+        if (row < p.M)
+          __hip_atomic_store(slab + row * 64 + j * 16 + frow, acc[j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)smem;
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(tickets + cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (old == (unsigned)(split - 1));
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const float* base = slabs + (long)cg * split * (64 * 64);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wid * 16 + fq * 4 + r;
+        float t = 0.f;
+        // unrolled: the partial loads are independent and must all be in flight at once (a
+        // rolled loop waits one L2/MALL round trip per split)
+        if (row < p.M) {
+#pragma unroll 8
+          for (int s2 = 0; s2 < split; ++s2)
+            t += __hip_atomic_load(base + (long)s2 * 4096 + row * 64 + j * 16 + frow, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        acc[j][r] = t;
+      }
+    if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + j * 16 + frow;
+    if (col >= p.N) continue;
+    const float bv = p.bias ? bf2f(p.bias[col]) : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = wid * 16 + fq * 4 + r;
+      if (row >= p.M) continue;
+      const float y = apply_act(acc[j][r] + bv, p.act);
+      if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
+      else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
+    }
+  }
+}
+
+// split-K for the ring kernel, from a cold-weight sweep on MI355X (profiles/kernels_m64_split.log,
+// M = 64): wide outputs (>= 256 column groups) stream best unsplit, long K / narrow N want 8-way
+// split, mid shapes 2-way.
+static int g_m64_split = 0;  // 0 = heuristic below; tuning override (rt_gemm_set_m64_split)
+
+static int m64_split(int N, int K) {
+  if (g_m64_split > 0) return g_m64_split;
+  const int groups = (N + 63) / 64, nk = K / 64;
+  int split;
+  if (groups >= 256) split = 1;
+  else if (nk >= 128 || groups <= 64) split = 8;
+  else split = 2;
+  while (split > 1 && nk / split < 4) split >>= 1;
+  return split;
+}
+
 // split-K so the grid reaches ~256 workgroups (one per CU) while every wave keeps >= 4 k-chunks of
 // 64 in flight-able work (short waves pay the reduction without amortising it)
 static int decode_split(int N, int K) {
@@ -700,9 +850,18 @@ using namespace rt;
 
 extern "C" int rt_gemm_decode_split(int N, int K) { return decode_split(N, K); }
 
+// never let a split-K launch write past the workspace (slabs: groups x split x slab floats;
+// tickets: one per column group)
+static int fit_split(int split, int groups, long slab_floats) {
+  if (groups > RT_SPLITK_TICKETS) return 1;
+  while (split > 1 && (long)groups * split * slab_floats > RT_SPLITK_SLAB_FLOATS) split >>= 1;
+  return split;
+}
+
 // 0 = automatic, 1 = force the 128x128 tile kernel, 2 = force the 256x256 kernel (M > 64)
 static int g_gemm_variant = 0;
 extern "C" void rt_gemm_set_variant(int v) { g_gemm_variant = v; }
+extern "C" void rt_gemm_set_m64_split(int s) { g_m64_split = s; }
 
 // Wave quantisation decides between the kernels: the 256-tile kernel runs one workgroup per CU
 // (256 slots), the 128-tile kernel two (512 slots); the 256 kernel is ~10 % faster per FLOP
@@ -733,9 +892,14 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   p.M = M; p.N = N; p.K = K; p.act = act;
   p.sa = nullptr; p.sb = nullptr;
   if (M <= 0 || N <= 0) return 0;
-  if (M <= 64) {
+  if (M > 16 && M <= 64 && p.Rp == 0 && g_gemm_variant != 1) {
+    const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64) : 1;
+    dim3 grid(((N + 63) / 64) * split), block(256);
+    if (out_f32) hipLaunchKernelGGL((gemm_m64_kernel<true>), grid, block, 0, stream, p, slabs, tickets, split);
+    else hipLaunchKernelGGL((gemm_m64_kernel<false>), grid, block, 0, stream, p, slabs, tickets, split);
+  } else if (M <= 64) {
     const int MT = (M + 15) / 16;
-    const int split = (slabs && tickets) ? decode_split(N, K) : 1;
+    const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * DG_COLS) : 1;
     dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
 #define DG_CASE(mt)                                                                                        \
   case mt:                                                                                                 \
@@ -774,7 +938,7 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
   if (a_is_bf16) {
     if (M > 64 || K % 64) return -1;
     const int MT = (M + 15) / 16;
-    const int split = (slabs && tickets) ? decode_split(N, K) : 1;
+    const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * DG_COLS) : 1;
     dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
     switch (MT) {
       case 1: hipLaunchKernelGGL((gemm_decode_kernel<1, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;

@@ -27,12 +27,14 @@ ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new":
 #                faster than hipBLASLt on cold (HBM-streamed) decode weights at batch 1-8
 #                (profiles/kernels_skinny_cold.log: qkv 16.5 vs 19.5 us, o 11.4 vs 19.0 us,
 #                gate_up 46.9 vs 56.0 us, lm_head 47.8 vs 57.4 us)
-#   16 < M <= 64 MID_BACKEND, default "lib" (hipBLASLt; the native kernel's 64-row variant loses)
+#   16 < M <= 64 MID_BACKEND, default "auto": the LDS-DMA ring kernel for wide or deep weights
+#                (N >= 16384 or K >= 8192: gate_up 52 vs 55 us, down 36 vs 41 us, lm_head 54 vs
+#                60 us cold at M = 64), hipBLASLt for the rest (qkv / o: 20 vs 25 / 20 us)
 #   M > 64       PLAIN_BACKEND, default "lib" (hipBLASLt ~1.5 PF/s vs ~1.2 PF/s for the 256x256
 #                8-phase kernel on plain GEMMs)
 # Everything with a fused epilogue or a LoRA term always runs on the hand-written kernels.
 PLAIN_BACKEND = os.environ.get("RAGTL_PLAIN_GEMM", "lib")
-MID_BACKEND = os.environ.get("RAGTL_MID_GEMM", PLAIN_BACKEND)
+MID_BACKEND = os.environ.get("RAGTL_MID_GEMM", "auto")
 SKINNY_BACKEND = os.environ.get("RAGTL_SKINNY", "native")
 
 
@@ -43,7 +45,7 @@ def set_gemm_backend(plain: Optional[str] = None, skinny: Optional[str] = None, 
     prev = (PLAIN_BACKEND, SKINNY_BACKEND, MID_BACKEND)
     for name, val in (("PLAIN_BACKEND", plain), ("SKINNY_BACKEND", skinny), ("MID_BACKEND", mid)):
         if val is not None:
-            assert val in ("lib", "native")
+            assert val in ("lib", "native", "auto")
             globals()[name] = val
     return prev
 
@@ -54,6 +56,8 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
         if u is None and bias is None and act == 0 and not out_f32:
             M = x.shape[0]
             backend = SKINNY_BACKEND if M <= 16 else (MID_BACKEND if M <= 64 else PLAIN_BACKEND)
+            if backend == "auto":
+                backend = "native" if (w.shape[0] >= 16384 or w.shape[1] >= 8192) else "lib"
             if backend == "lib":
                 return torch.matmul(x, w.t(), out=out)
         return native().gemm(x, w, u, ub, bias, act, out_f32, out)

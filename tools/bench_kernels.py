@@ -65,7 +65,7 @@ def main():
             C.gemm_set_variant(0)
     # skinny GEMMs with the weights streamed from HBM (rotating copies > the 256 MB Infinity
     # Cache), which is what a decode step sees
-    for M in ((1, 8, 64) if want("cold") else ()):
+    for M in ((1, 8, 32, 64) if want("cold") else ()):
         for name, N, K in gemms:
             ncopy = max(2, int(1.2e9 // (N * K * 2)))
             ws_ = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) / math.sqrt(K) for _ in range(ncopy)]
@@ -118,6 +118,29 @@ def main():
             res.append(r)
             print(json.dumps(r), flush=True)
             del wqs
+        torch.cuda.empty_cache()
+    # split-K sweep of the M <= 64 ring kernel (cold weights)
+    for M in ((64,) if want("m64sweep") else ()):
+        for name, N, K in gemms:
+            ncopy = max(2, int(1.2e9 // (N * K * 2)))
+            ws_ = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) / math.sqrt(K) for _ in range(ncopy)]
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            it = [0]
+
+            def run_m64():
+                it[0] = (it[0] + 1) % ncopy
+                return ops.gemm(a, ws_[it[0]])
+
+            for sp in (0, 1, 2, 4, 8, 16):
+                if (K // 64) // max(sp, 1) < 2:
+                    continue
+                C.gemm_set_m64_split(sp)
+                t = timeit(run_m64, iters=ncopy * 2)
+                r = dict(kind="m64_split", name=name, M=M, split=sp, us=t, gbs=2 * N * K / t / 1e3)
+                res.append(r)
+                print(json.dumps(r), flush=True)
+            C.gemm_set_m64_split(0)
+            del ws_
         torch.cuda.empty_cache()
     # LoRA-fused vs separate
     for M in ((2048, 8192) if want("lora") else ()):
