@@ -123,15 +123,19 @@ Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const o
     TORCH_CHECK(u->stride(0) % 8 == 0 && ub->stride(0) % 8 == 0, "gemm: LoRA row strides must be multiples of 8");
   }
   if (bias.has_value() && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N && bias->is_contiguous()); }
+  // act 5 = SwiGLU pair mode: w = [gate; up] (2F rows), output [M, F] (skinny kernels, M <= 64)
+  const bool pair = act == 5;
+  if (pair) TORCH_CHECK(M <= 64 && N % 64 == 0 && Rp == 0, "gemm: SwiGLU pair mode needs M <= 64, N % 64 == 0, no LoRA");
+  const int64_t Nout = pair ? N / 2 : N;
   Tensor c;
   if (out.has_value() && out->defined()) {
     c = *out;
-    TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1, "gemm: bad out shape");
+    TORCH_CHECK(c.size(0) == M && c.size(1) == Nout && c.stride(1) == 1, "gemm: bad out shape");
     TORCH_CHECK(c.scalar_type() == (out_f32 ? at::kFloat : at::kBFloat16), "gemm: bad out dtype");
     TORCH_CHECK(c.stride(0) % 8 == 0, "gemm: out row stride must be a multiple of 8");
     CHECK_ALIGN16(c);
   } else {
-    c = at::empty({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+    c = at::empty({M, Nout}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   }
   if (M == 0) return c;
   hipStream_t st = cur_stream();
@@ -178,8 +182,11 @@ Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, c
     TORCH_CHECK(K % 128 == 0 && N % 8 == 0, "gemm_fp8: K % 128 == 0, N % 8 == 0");
   }
   if (bias.has_value() && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N); }
-  Tensor c = (out.has_value() && out->defined()) ? *out : at::empty({M, N}, a.options().dtype(at::kBFloat16));
-  TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.scalar_type() == at::kBFloat16, "gemm_fp8: out");
+  const bool pair = act == 5;  // SwiGLU pair mode (W8A16 skinny only)
+  if (pair) TORCH_CHECK(a_bf16 && N % 64 == 0, "gemm_fp8: SwiGLU pair mode needs bf16 activations, N % 64 == 0");
+  const int64_t Nout = pair ? N / 2 : N;
+  Tensor c = (out.has_value() && out->defined()) ? *out : at::empty({M, Nout}, a.options().dtype(at::kBFloat16));
+  TORCH_CHECK(c.size(0) == M && c.size(1) == Nout && c.stride(1) == 1 && c.scalar_type() == at::kBFloat16, "gemm_fp8: out");
   if (M == 0) return c;
   hipStream_t st = cur_stream();
   float* slabs = nullptr;

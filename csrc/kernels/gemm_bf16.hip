@@ -26,7 +26,11 @@
 
 namespace rt {
 
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3, ACT_SILU = 4 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3, ACT_SILU = 4,
+           // skinny kernels only: B = fused [gate; up] weight (2F rows), C[M, F] = silu(X gate^T) * (X up^T).
+           // Column group g reads gate rows [32g, 32g+32) and up rows [F+32g, F+32g+32), so the pair of
+           // every output lands in one lane (SwiGLU fused into the gate/up GEMM of a decode step)
+           ACT_SWIGLU = 5 };
 
 __device__ __forceinline__ float apply_act(float x, int act) {
   switch (act) {
@@ -583,11 +587,16 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
   const int c_begin = (int)((long)part * nc / nparts), c_end = (int)((long)(part + 1) * nc / nparts);
 
   constexpr int WSZ = W8 ? 1 : 2;  // bytes per weight element
+  const bool pair = p.act == ACT_SWIGLU;
+  const int F = p.N / 2;
   const char* wrow[4];
   const bf16_t* xrow[MT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    wrow[j] = (const char*)p.B + ((long)min(n0 + j * 16 + frow, p.N - 1) * p.ldb + g * 16) * WSZ;
+  for (int j = 0; j < 4; ++j) {
+    const int wr_ = pair ? (j < 2 ? cg * 32 + j * 16 + frow : F + cg * 32 + (j - 2) * 16 + frow)
+                         : min(n0 + j * 16 + frow, p.N - 1);
+    wrow[j] = (const char*)p.B + ((long)wr_ * p.ldb + g * 16) * WSZ;
+  }
 #pragma unroll
   for (int m = 0; m < MT; ++m) xrow[m] = p.A + (long)min(m * 16 + frow, p.M - 1) * p.lda + g * 16;
 
@@ -658,6 +667,31 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
     if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
+  if (pair) {
+    // stage the 64 sums of this group (32 gate | 32 up) through LDS, then pair them up
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = tid + 256 * i;
+      const int row = e / DG_COLS, col = e % DG_COLS;
+      const int wcol = col < 32 ? cg * 32 + col : F + cg * 32 + col - 32;
+      float y = v[i];
+      if constexpr (W8) y *= p.sb[wcol];
+      if (p.bias) y += bf2f(p.bias[wcol]);
+      red[row * LDR + col] = y;
+    }
+    __syncthreads();
+    for (int e = tid; e < ROWS * 32; e += 256) {
+      const int row = e / 32, c = e % 32;
+      if (row >= p.M) continue;
+      const float gt = red[row * LDR + c], up = red[row * LDR + c + 32];
+      const float y = gt / (1.f + __expf(-gt)) * up;
+      if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + cg * 32 + c] = y;
+      else ((bf16_t*)p.C)[(long)row * p.ldc + cg * 32 + c] = f2bf(y);
+    }
+    return;
+  }
+
   // ---- epilogue: LoRA K-extension (U UB^T), bias, activation, store ----
 #pragma unroll
   for (int i = 0; i < NE; ++i) {
@@ -710,6 +744,8 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
   const int nk = p.K / 64;
   const int t0 = (int)((long)sp * nk / split), t1 = (int)((long)(sp + 1) * nk / split);
   const int nt = t1 - t0;
+  const bool pair = p.act == ACT_SWIGLU;
+  const int F = p.N / 2;
 
   // staging: lane -> (row within an 8-row piece, 16-B slot); 2 pieces per operand per wave
   const int srow = lane >> 3;
@@ -720,7 +756,8 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
       const int lr = (wid * 2 + j) * 8 + srow;  // 0..63
       const int ck = (lane & 7) ^ lds_swz(lr);
       const bf16_t* xa = p.A + (long)min(lr, p.M - 1) * p.lda + (long)t * 64 + ck * 8;
-      const bf16_t* wb = p.B + (long)min(n0 + lr, p.N - 1) * p.ldb + (long)t * 64 + ck * 8;
+      const int wrow_ = pair ? (lr < 32 ? cg * 32 + lr : F + cg * 32 + lr - 32) : min(n0 + lr, p.N - 1);
+      const bf16_t* wb = p.B + (long)wrow_ * p.ldb + (long)t * 64 + ck * 8;
       __builtin_amdgcn_global_load_lds((const void*)xa, (lds_void*)(slot + (wid * 2 + j) * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)wb, (lds_void*)(slot + 8192 + (wid * 2 + j) * 1024), 16, 0, 0);
     }
@@ -801,6 +838,23 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
         acc[j][r] = t;
       }
     if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (pair) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = cg * 32 + j * 16 + frow;
+      const float bg = p.bias ? bf2f(p.bias[col]) : 0.f, bu = p.bias ? bf2f(p.bias[F + col]) : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wid * 16 + fq * 4 + r;
+        if (row >= p.M) continue;
+        const float gt = acc[j][r] + bg, up = acc[j + 2][r] + bu;
+        const float y = gt / (1.f + __expf(-gt)) * up;
+        if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
+        else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
+      }
+    }
+    return;
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -892,6 +946,7 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   p.M = M; p.N = N; p.K = K; p.act = act;
   p.sa = nullptr; p.sb = nullptr;
   if (M <= 0 || N <= 0) return 0;
+  if (act == ACT_SWIGLU && (M > 64 || N % 64 != 0 || (U && UB))) return -2;
   if (M > 16 && M <= 64 && p.Rp == 0 && g_gemm_variant != 1) {
     const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64) : 1;
     dim3 grid(((N + 63) / 64) * split), block(256);

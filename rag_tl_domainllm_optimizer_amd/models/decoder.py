@@ -88,8 +88,9 @@ class DecoderLayer(nn.Module):
             d = ops.linear(f, self.fc2_w, self.fc2_b, lora=self._lg("fc2"), fp8=self._f8("fc2"))
         else:
             h, residual = ops.rms_norm(a, self.ln2_w, cfg.norm_eps, residual)
-            gu = ops.linear(h, self.gate_up_w, lora=self._lg("gate_up"), fp8=self._f8("gate_up"))
-            d = ops.linear(ops.swiglu(gu), self.down_w, lora=self._lg("down"), fp8=self._f8("down"))
+            # act="swiglu": one fused skinny GEMM in no-grad decode, GEMM + SwiGLU kernel otherwise
+            f = ops.linear(h, self.gate_up_w, act="swiglu", lora=self._lg("gate_up"), fp8=self._f8("gate_up"))
+            d = ops.linear(f, self.down_w, lora=self._lg("down"), fp8=self._f8("down"))
         return d, residual
 
 

@@ -19,7 +19,8 @@ import torch
 from . import reference as ref
 from ._ext import native, on_gpu
 
-ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new": 3, "silu": 4}
+ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new": 3, "silu": 4, "swiglu": 5}
+ACT_SWIGLU = 5  # w = [gate; up] (2F rows) -> silu(x gate^T) * (x up^T), [.., F]
 
 
 # Plain GEMMs (no LoRA K-extension, bias or activation epilogue, bf16 out) pick a backend by M:
@@ -209,6 +210,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
     use_lora = lora is not None and lora.enabled
     if use_lora and (lora.a_pad is None or lora.a_pad.device != x.device):
         lora.refresh(dtype=w.dtype)
+    if act_id == ACT_SWIGLU:
+        # fused into the skinny gate/up GEMM when it can run there (no-grad decode on the GPU)
+        if (on_gpu(x2) and not torch.is_grad_enabled() and x2.shape[0] <= 64 and bias is None
+                and w.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0):
+            w_eff = lora.merged_weight(w) if use_lora else w
+            if fp8 is not None:
+                from .fp8 import fp8_supported
+
+                if fp8_supported(w_eff):
+                    q, sc = fp8.get(w_eff)
+                    y = native().gemm_fp8(x2, None, q, sc, None, ACT_SWIGLU, None)
+                    return y.reshape(*shp[:-1], w.shape[0] // 2)
+            y = native().gemm(x2, w_eff, None, None, None, ACT_SWIGLU, False, None)
+            return y.reshape(*shp[:-1], w.shape[0] // 2)
+        from .misc import swiglu
+
+        return swiglu(linear(x, w, bias, None, lora, fp8))
     if fp8 is not None and not torch.is_grad_enabled():
         from .fp8 import fp8_supported, gemm_fp8
 

@@ -474,3 +474,25 @@ def test_model_fp8_generation_gpu():
     out = gen.generate([list(range(5, 40)), list(range(7, 30))], SamplingParams(max_new_tokens=12, do_sample=False))
     assert out.tokens.shape == (2, 12)
     m.set_fp8(False)
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("F,K", [(512, 256), (14336, 4096)])
+def test_gemm_swiglu_pair(M, F, K):
+    """SwiGLU fused into the skinny gate/up GEMM (decode) == silu(x g^T) * (x u^T); bf16 and W8."""
+    torch.manual_seed(M + F)
+    w = (torch.randn(2 * F, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    g = x.float() @ w[:F].float().t()
+    u = x.float() @ w[F:].float().t()
+    yr = torch.nn.functional.silu(g) * u
+    y = ops.native().gemm(x, w, None, None, None, 5, False, None)
+    assert y.shape == (M, F)
+    _close(y, yr)
+    wq, sw = ops.quantize_fp8(w)
+    wd = ops.dequantize_fp8(wq, sw)
+    yr8 = torch.nn.functional.silu(x.float() @ wd[:F].t()) * (x.float() @ wd[F:].t())
+    _close(ops.native().gemm_fp8(x, None, wq, sw, None, 5, None), yr8)
+    # through the layer API (no-grad, GPU)
+    with torch.no_grad():
+        _close(ops.linear(x, w, act="swiglu"), yr)
