@@ -18,11 +18,11 @@
 
 extern "C" {
 int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
-               long, int, int, int, int, int, float*, unsigned*, hipStream_t);
+               long, int, int, int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
 void rt_gemm_set_variant(int);
 void rt_gemm_set_m64_split(int);
 int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
-                int, int, int, float*, unsigned*, hipStream_t);
+                int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
 int rt_quant_fp8_rows(const void*, long, void*, long, float*, long, int, hipStream_t);
 int rt_norm_fwd(int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
                 hipStream_t);
@@ -105,7 +105,8 @@ DecodeWS& decode_ws(const Tensor& like, hipStream_t st) {
 
 // ---------------------------------------------------------------------------------------------
 Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const optional<Tensor>& ub,
-            const optional<Tensor>& bias, int64_t act, bool out_f32, optional<Tensor> out) {
+            const optional<Tensor>& bias, int64_t act, bool out_f32, optional<Tensor> out,
+            const optional<Tensor>& residual, double norm_eps) {
   CHECK_CUDA(a); CHECK_CUDA(w); CHECK_BF16(a); CHECK_BF16(w); CHECK_ROWS(a); CHECK_ROWS(w);
   CHECK_ALIGN16(a); CHECK_ALIGN16(w);
   const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
@@ -138,6 +139,14 @@ Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const o
     c = at::empty({M, Nout}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   }
   if (M == 0) return c;
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res || norm_eps > 0) {
+    TORCH_CHECK(M <= 64, "gemm: residual / in-GEMM norm are decode (M <= 64) features");
+    if (has_res) {
+      CHECK_BF16(*residual);
+      TORCH_CHECK(residual->size(0) == M && residual->size(1) == Nout && residual->stride(1) == 1, "gemm: residual shape");
+    }
+  }
   hipStream_t st = cur_stream();
   float* slabs = nullptr;
   unsigned* tickets = nullptr;
@@ -149,7 +158,8 @@ Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const o
   }
   check_rc(rt_gemm_nt(a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), opt_ptr(u), Rp ? u->stride(0) : 0,
                       opt_ptr(ub), Rp ? ub->stride(0) : 0, Rp, opt_ptr(bias), c.data_ptr(), c.stride(0), (int)M,
-                      (int)N, (int)K, (int)act, out_f32 ? 1 : 0, slabs, tickets, st),
+                      (int)N, (int)K, (int)act, out_f32 ? 1 : 0, slabs, tickets,
+                      has_res ? residual->data_ptr() : nullptr, has_res ? residual->stride(0) : 0, (float)norm_eps, st),
            "gemm");
   return c;
 }
@@ -168,7 +178,8 @@ std::vector<Tensor> quant_fp8(const Tensor& x) {
 }
 
 Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, const Tensor& sw,
-                const optional<Tensor>& bias, int64_t act, optional<Tensor> out) {
+                const optional<Tensor>& bias, int64_t act, optional<Tensor> out, const optional<Tensor>& residual,
+                double norm_eps) {
   // a: bf16 [M, K] (W8A16, M <= 64) or uint8 e4m3fn [M, K] with sa [M] (W8A8)
   CHECK_CUDA(a); CHECK_CUDA(wq); CHECK_ROWS(a); CHECK_ROWS(wq); CHECK_F32(sw);
   TORCH_CHECK(wq.scalar_type() == at::kByte, "gemm_fp8: weight must be uint8 (e4m3fn bits)");
@@ -188,6 +199,12 @@ Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, c
   Tensor c = (out.has_value() && out->defined()) ? *out : at::empty({M, Nout}, a.options().dtype(at::kBFloat16));
   TORCH_CHECK(c.size(0) == M && c.size(1) == Nout && c.stride(1) == 1 && c.scalar_type() == at::kBFloat16, "gemm_fp8: out");
   if (M == 0) return c;
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res || norm_eps > 0) TORCH_CHECK(a_bf16, "gemm_fp8: residual / in-GEMM norm need the W8A16 (M <= 64) form");
+  if (has_res) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == Nout && residual->stride(1) == 1, "gemm_fp8: residual shape");
+  }
   hipStream_t st = cur_stream();
   float* slabs = nullptr;
   unsigned* tickets = nullptr;
@@ -198,7 +215,8 @@ Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, c
   }
   check_rc(rt_gemm_fp8(a.data_ptr(), a.stride(0), sa.has_value() && sa->defined() ? sa->data_ptr<float>() : nullptr,
                        wq.data_ptr(), wq.stride(0), sw.data_ptr<float>(), opt_ptr(bias), c.data_ptr(), c.stride(0),
-                       (int)M, (int)N, (int)K, (int)act, a_bf16 ? 1 : 0, slabs, tickets, st),
+                       (int)M, (int)N, (int)K, (int)act, a_bf16 ? 1 : 0, slabs, tickets,
+                       has_res ? residual->data_ptr() : nullptr, has_res ? residual->stride(0) : 0, (float)norm_eps, st),
            "gemm_fp8");
   return c;
 }
@@ -528,9 +546,10 @@ void decode_update(const Tensor& tok, Tensor out_tokens, const optional<Tensor>&
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels + native host runtime";
-  m.def("gemm", &gemm, "bf16 MFMA GEMM C = act(A W^T + U UB^T + bias)", py::arg("a"), py::arg("w"),
+  m.def("gemm", &gemm, "bf16 MFMA GEMM C = act(rstd(A) A W^T + U UB^T + bias) + R", py::arg("a"), py::arg("w"),
         py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0,
-        py::arg("out_f32") = false, py::arg("out") = py::none());
+        py::arg("out_f32") = false, py::arg("out") = py::none(), py::arg("residual") = py::none(),
+        py::arg("norm_eps") = 0.0);
   m.def("gemm_set_m64_split", &rt_gemm_set_m64_split, "tuning: fixed split-K of the M<=64 ring kernel (0 = auto)");
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
@@ -538,7 +557,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_fp8", &quant_fp8, "per-row absmax e4m3fn quantisation -> (uint8 [R,C], scale fp32 [R])");
   m.def("gemm_fp8", &gemm_fp8, "fp8 GEMM: W8A8 (MX MFMA 256x256) or W8A16 (skinny, M <= 64)", py::arg("a"),
         py::arg("sa") = py::none(), py::arg("wq"), py::arg("sw"), py::arg("bias") = py::none(), py::arg("act") = 0,
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("norm_eps") = 0.0);
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
   m.def("rope_qkv", &rope_qkv);

@@ -59,6 +59,11 @@ struct GemmArgs {
   // W8A16 skinny kernel); A / B then point to OCP e4m3fn bytes with lda / ldb in elements (= bytes)
   const float* sa;
   const float* sb;
+  // skinny kernels only (decode): residual added after the activation (C = act(..) + R, the new
+  // residual stream) and RMS-normalised input (C = rstd(X) * X B'^T with the norm weight folded
+  // into B'; rstd(X_row) = rsqrt(mean(X_row^2) + eps) is computed inside the GEMM, 0 = off)
+  const bf16_t* R; long ldr;
+  float norm_eps;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -576,7 +581,7 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
                                                           unsigned* __restrict__ tickets, int split) {
   constexpr int ROWS = MT * 16;
   constexpr int LDR = DG_COLS + 1;
-  __shared__ float red[4 * ROWS * LDR];  // the ONLY __shared__ object (also carries the last-flag)
+  __shared__ float red[4 * ROWS * LDR + 4 * ROWS];  // the ONLY __shared__ object (+ per-wave row sum-of-squares)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int cg = blockIdx.x / split, sp = blockIdx.x % split;
   const int n0 = cg * DG_COLS;
@@ -606,13 +611,34 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const bool normed = p.norm_eps > 0.f;
+  float sq[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) sq[m] = 0.f;
+  auto xsq = [&](const DGRegs<MT>& r) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float f[8];
+      unpack8(r.x[m][0], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sq[m] += f[e] * f[e];
+      unpack8(r.x[m][1], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sq[m] += f[e] * f[e];
+    }
+  };
+
   DGRegs<MT> ra, rb;
   if (c_begin < c_end) dg_load<MT, W8>(ra, wrow, xrow, c_begin);
   for (int c = c_begin; c < c_end; c += 2) {
     if (c + 1 < c_end) dg_load<MT, W8>(rb, wrow, xrow, c + 1);
     dg_mma<MT, W8>(ra, acc);
+    if (normed) xsq(ra);
     if (c + 2 < c_end) dg_load<MT, W8>(ra, wrow, xrow, c + 2);
-    if (c + 1 < c_end) dg_mma<MT, W8>(rb, acc);
+    if (c + 1 < c_end) {
+      dg_mma<MT, W8>(rb, acc);
+      if (normed) xsq(rb);
+    }
   }
 
   // ---- intra-block reduction: acc[m][j] lane holds C[m*16 + 4g + r][j*16 + frow] ----
@@ -622,6 +648,17 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[(wid * ROWS + m * 16 + g * 4 + r) * LDR + j * 16 + frow] = acc[m][j][r];
+  // row sums of squares of X over this wave's k range: lanes of one row differ in g (xor 16, 32)
+  float* rsq = red + 4 * ROWS * LDR;
+  if (normed) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float t = sq[m];
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      if (g == 0) rsq[wid * ROWS + m * 16 + frow] = t;
+    }
+  }
   __syncthreads();
   constexpr int NE = ROWS * DG_COLS / 256;  // elements per thread
   float v[NE];
@@ -632,17 +669,22 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
     v[i] = red[(0 * ROWS + row) * LDR + col] + red[(1 * ROWS + row) * LDR + col] + red[(2 * ROWS + row) * LDR + col] +
            red[(3 * ROWS + row) * LDR + col];
   }
+  // block-level row sum of squares (split-K blocks publish it after their slab)
+  float bsq = 0.f;  // thread tid < ROWS holds row tid
+  if (normed && tid < ROWS) bsq = rsq[tid] + rsq[ROWS + tid] + rsq[2 * ROWS + tid] + rsq[3 * ROWS + tid];
 
   if (split > 1) {
     // publish this block's slab with write-through (agent-scope) stores, drain them, take a
     // ticket; the last arriver of the column group reduces with agent-scope loads. No L2
     // writeback/invalidate fences (a per-block buffer_wbl2 flushes the whole XCD L2).
-    float* slab = slabs + ((long)cg * split + sp) * (ROWS * DG_COLS);
+    constexpr int SLAB = ROWS * DG_COLS + ROWS;
+    float* slab = slabs + ((long)cg * split + sp) * SLAB;
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
       const int e = tid + 256 * i;
       if (e / DG_COLS < p.M) __hip_atomic_store(slab + e, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (normed && tid < p.M) __hip_atomic_store(slab + ROWS * DG_COLS + tid, bsq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -652,7 +694,7 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
     __syncthreads();
     const bool last = red[0] != 0.f;
     if (!last) return;
-    const float* base = slabs + (long)cg * split * (ROWS * DG_COLS);
+    const float* base = slabs + (long)cg * split * SLAB;
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
       const int e = tid + 256 * i;
@@ -660,11 +702,27 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
       if (e / DG_COLS < p.M) {
 #pragma unroll 8
         for (int s2 = 0; s2 < split; ++s2)
-          t += __hip_atomic_load(base + (long)s2 * (ROWS * DG_COLS) + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          t += __hip_atomic_load(base + (long)s2 * SLAB + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       v[i] = t;
     }
+    if (normed && tid < p.M) {
+      float t = 0.f;
+#pragma unroll 8
+      for (int s2 = 0; s2 < split; ++s2)
+        t += __hip_atomic_load(base + (long)s2 * SLAB + ROWS * DG_COLS + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bsq = t;
+    }
     if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  // per-row rstd of the normalised input (rows < ROWS), shared through LDS
+  if (normed) {
+    __syncthreads();
+    if (tid < ROWS) rsq[tid] = rsqrtf(bsq / (float)p.K + p.norm_eps);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NE; ++i) v[i] *= rsq[(tid + 256 * i) / DG_COLS];
   }
 
   if (pair) {
@@ -714,6 +772,7 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
       if constexpr (W8) y *= p.sb[gcol];
       if (p.bias) y += bf2f(p.bias[gcol]);
       y = apply_act(y, p.act);
+      if (p.R) y += bf2f(p.R[(long)grow * p.ldr + gcol]);
       if constexpr (OUT_F32) ((float*)p.C)[(long)grow * p.ldc + gcol] = y;
       else ((bf16_t*)p.C)[(long)grow * p.ldc + gcol] = f2bf(y);
     }
@@ -766,6 +825,8 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool normed = p.norm_eps > 0.f;
+  float sq = 0.f;
 
   // prologue: steps t0 .. t0+2 in flight
 #pragma unroll
@@ -798,11 +859,28 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk], b[j][kk], acc[j], 0, 0, 0);
+    if (normed) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = (float)a[kk][e];
+          sq += f * f;
+        }
+    }
+  }
+  // lanes of row (16 wid + frow) differ in fq: the row's sum of squares over this block's K range
+  if (normed) {
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
   }
 
   // lane holds C[16 wid + 4 fq + r][16 j + frow]
   if (split > 1) {
-    float* slab = slabs + ((long)cg * split + sp) * (64 * 64);
+    constexpr int SLAB = 64 * 64 + 64;
+    float* slab = slabs + ((long)cg * split + sp) * SLAB;
+    if (normed && fq == 0 && wid * 16 + frow < p.M)
+      __hip_atomic_store(slab + 4096 + wid * 16 + frow, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -820,7 +898,17 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
     }
     __syncthreads();
     if (!*flag) return;
-    const float* base = slabs + (long)cg * split * (64 * 64);
+    const float* base = slabs + (long)cg * split * SLAB;
+    if (normed) {
+      float t = 0.f;
+      if (wid * 16 + frow < p.M) {
+#pragma unroll 8
+        for (int s2 = 0; s2 < split; ++s2)
+          t += __hip_atomic_load(base + (long)s2 * SLAB + 4096 + wid * 16 + frow, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+      sq = t;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -832,12 +920,22 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
         if (row < p.M) {
 #pragma unroll 8
           for (int s2 = 0; s2 < split; ++s2)
-            t += __hip_atomic_load(base + (long)s2 * 4096 + row * 64 + j * 16 + frow, __ATOMIC_RELAXED,
+            t += __hip_atomic_load(base + (long)s2 * SLAB + row * 64 + j * 16 + frow, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
         acc[j][r] = t;
       }
     if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (normed) {
+    // lane holds rows 16 wid + 4 fq + r; their sums of squares sit in lanes 4 fq + r of this wave
+    const float rs = rsqrtf(sq / (float)p.K + p.norm_eps);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float rr = __shfl(rs, fq * 4 + r, 64);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j][r] *= rr;
+    }
   }
   if (pair) {
 #pragma unroll
@@ -865,7 +963,8 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
     for (int r = 0; r < 4; ++r) {
       const int row = wid * 16 + fq * 4 + r;
       if (row >= p.M) continue;
-      const float y = apply_act(acc[j][r] + bv, p.act);
+      float y = apply_act(acc[j][r] + bv, p.act);
+      if (p.R) y += bf2f(p.R[(long)row * p.ldr + col]);
       if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
       else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
     }
@@ -934,7 +1033,7 @@ static bool use_256(int M, int N) {
 extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, const void* U, long ldu,
                           const void* UB, long ldub, int Rp, const void* bias, void* C, long ldc, int M,
                           int N, int K, int act, int out_f32, float* slabs, unsigned* tickets,
-                          hipStream_t stream) {
+                          const void* R, long ldr, float norm_eps, hipStream_t stream) {
   GemmArgs p;
   p.A = (const bf16_t*)A; p.lda = lda;
   p.B = (const bf16_t*)B; p.ldb = ldb;
@@ -945,16 +1044,18 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   p.C = C; p.ldc = ldc;
   p.M = M; p.N = N; p.K = K; p.act = act;
   p.sa = nullptr; p.sb = nullptr;
+  p.R = (const bf16_t*)R; p.ldr = ldr; p.norm_eps = norm_eps;
   if (M <= 0 || N <= 0) return 0;
   if (act == ACT_SWIGLU && (M > 64 || N % 64 != 0 || (U && UB))) return -2;
+  if ((R || norm_eps > 0.f) && M > 64) return -3;  // residual / in-GEMM norm: skinny kernels only
   if (M > 16 && M <= 64 && p.Rp == 0 && g_gemm_variant != 1) {
-    const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64) : 1;
+    const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64 + 64) : 1;
     dim3 grid(((N + 63) / 64) * split), block(256);
     if (out_f32) hipLaunchKernelGGL((gemm_m64_kernel<true>), grid, block, 0, stream, p, slabs, tickets, split);
     else hipLaunchKernelGGL((gemm_m64_kernel<false>), grid, block, 0, stream, p, slabs, tickets, split);
   } else if (M <= 64) {
     const int MT = (M + 15) / 16;
-    const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * DG_COLS) : 1;
+    const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * (DG_COLS + 1)) : 1;
     dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
 #define DG_CASE(mt)                                                                                        \
   case mt:                                                                                                 \
@@ -983,17 +1084,20 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
 //  * M <= 64: W8A16 skinny kernel (A = bf16 activations, sa ignored): half the weight bytes
 extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void* B, long ldb, const float* sb,
                            const void* bias, void* C, long ldc, int M, int N, int K, int act, int a_is_bf16,
-                           float* slabs, unsigned* tickets, hipStream_t stream) {
+                           float* slabs, unsigned* tickets, const void* R, long ldr, float norm_eps,
+                           hipStream_t stream) {
   GemmArgs p;
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
   p.U = nullptr; p.ldu = 0; p.UB = nullptr; p.ldub = 0; p.Rp = 0;
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K; p.act = act;
   p.sa = sa; p.sb = sb;
+  p.R = (const bf16_t*)R; p.ldr = ldr; p.norm_eps = norm_eps;
   if (M <= 0 || N <= 0) return 0;
+  if ((R || norm_eps > 0.f) && !a_is_bf16) return -3;
   if (a_is_bf16) {
     if (M > 64 || K % 64) return -1;
     const int MT = (M + 15) / 16;
-    const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * DG_COLS) : 1;
+    const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * (DG_COLS + 1)) : 1;
     dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
     switch (MT) {
       case 1: hipLaunchKernelGGL((gemm_decode_kernel<1, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;

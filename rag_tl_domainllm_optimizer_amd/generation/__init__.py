@@ -205,6 +205,8 @@ class Generator:
     def _enqueue(self, params, B, S, T, ids, start, eos, eos_list, pad_id, sub, early_stop, t0, ev):
         cfg, dev, MB = self.cfg, self.device, self.max_batch
         h_last = self.model.prefill(ids, self.kv_start[:B], sub)
+        if hasattr(self.model, "refresh_decode_weights"):
+            self.model.refresh_decode_weights()  # merged / folded / fp8 images used by graph replays
         h = torch.zeros(MB, cfg.hidden_size, dtype=h_last.dtype, device=dev)
         h[:B] = h_last
         # the first sampled token is not in the cache yet: the bookkeeping kernel advances kv_len

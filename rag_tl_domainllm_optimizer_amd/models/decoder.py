@@ -56,6 +56,8 @@ class DecoderLayer(nn.Module):
         # fp8 inference images of the projection weights (CausalLM.set_fp8)
         self.fp8_enabled = False
         self._fp8: Dict[str, ops.Fp8Cache] = {}
+        # norm-folded weights of the fused decode path (Llama/Mistral)
+        self._fold: Dict[str, ops.FoldCache] = {}
 
     # ---------------------------------------------------------------- helpers
     def _lg(self, name):
@@ -69,6 +71,44 @@ class DecoderLayer(nn.Module):
         if not self.fp8_enabled:
             return None
         return self._fp8.setdefault(name, ops.Fp8Cache())
+
+    # ---------------------------------------------------------------- fused decode step (M <= 64)
+    def _w_eff(self, wname: str, gname: str):
+        w = getattr(self, wname)
+        g = self._lg(gname)
+        if g is None:
+            return w
+        if g.a_pad is None or g.a_pad.device != w.device:
+            g.refresh(dtype=w.dtype)
+        return g.merged_weight(w)
+
+    @torch.no_grad()
+    def refresh_decode_weights(self):
+        """Bring the merged / folded / fp8 decode weights up to date eagerly (graph replays of a
+        captured decode step only read them)."""
+        if self.cfg.arch == "opt":
+            return
+        wq = self._fold.setdefault("qkv", ops.FoldCache()).get(self._w_eff("qkv_w", "qkv"), self.ln1_w)
+        wgu = self._fold.setdefault("gate_up", ops.FoldCache()).get(self._w_eff("gate_up_w", "gate_up"), self.ln2_w)
+        for name, w in (("qkv_folded", wq), ("gate_up_folded", wgu), ("o", self._w_eff("o_w", "o")),
+                        ("down", self._w_eff("down_w", "down"))):
+            c = self._f8(name)
+            if c is not None:
+                c.get(w)
+
+    def decode_fused(self, h, attend):
+        """One Llama/Mistral layer of a decode step in four kernels: [RMSNorm folded into the qkv
+        GEMM] -> attention (RoPE + append + split-K) -> [o GEMM + residual] -> [RMSNorm folded into
+        the gate/up GEMM + SwiGLU] -> [down GEMM + residual]. ``h`` is the bf16 residual stream."""
+        cfg = self.cfg
+        eps = cfg.norm_eps
+        wq = self._fold.setdefault("qkv", ops.FoldCache()).get(self._w_eff("qkv_w", "qkv"), self.ln1_w)
+        qkv = ops.gemm_decode(h, wq, norm_eps=eps, fp8=self._f8("qkv_folded"))
+        o = attend(qkv)
+        h = ops.gemm_decode(o, self._w_eff("o_w", "o"), residual=h, fp8=self._f8("o"))
+        wgu = self._fold.setdefault("gate_up", ops.FoldCache()).get(self._w_eff("gate_up_w", "gate_up"), self.ln2_w)
+        f = ops.gemm_decode(h, wgu, act=ops.ACT_SWIGLU, norm_eps=eps, fp8=self._f8("gate_up_folded"))
+        return ops.gemm_decode(f, self._w_eff("down_w", "down"), residual=h, fp8=self._f8("down"))
 
     def attn_in(self, x, residual):
         cfg = self.cfg
@@ -110,6 +150,8 @@ class CausalLM(nn.Module):
         if not cfg.tie_embeddings:
             self.lm_head = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden_size, **kw))
         self._rope = None
+        # decode steps run the fused 4-GEMM layer (norms folded into GEMMs, residual epilogues)
+        self.fused_decode = True
         if init:
             self.reset_parameters(seed)
 
@@ -221,6 +263,16 @@ class CausalLM(nn.Module):
         cfg = self.cfg
         cos, sin = self.rope(tokens.device)
         x = self.embed_tokens(tokens, pos)
+        if self.fused_decode and cfg.arch != "opt" and x.is_cuda and x.shape[0] <= 64 and not torch.is_grad_enabled():
+            h = x
+            for li, layer in enumerate(self.layers):
+                def attend(qkv, li=li):
+                    return ops.decode_step_attention(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads,
+                                                     pos, cos, sin, kv_start, cfg.sliding_window,
+                                                     workspace=workspace)
+                h = layer.decode_fused(h, attend)
+            y, _ = ops.rms_norm(h, self.norm_w, cfg.norm_eps)
+            return y
         residual = None
         for li, layer in enumerate(self.layers):
             qkv, residual = layer.attn_in(x, residual)
@@ -256,6 +308,11 @@ class CausalLM(nn.Module):
                 prev = prev or g.use_merged
                 g.use_merged = on
         return prev
+
+    def refresh_decode_weights(self):
+        if self.fused_decode:
+            for layer in self.layers:
+                layer.refresh_decode_weights()
 
     def set_fp8(self, on: bool = True):
         """fp8 (e4m3fn) weights for no-grad forwards (prefill, decode, reference scoring):

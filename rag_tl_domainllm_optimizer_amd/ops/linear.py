@@ -251,3 +251,47 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
                 params += [a, b]
         y = _LinearFn.apply(x2, w, bias, act_id, lora if use_lora else None, *params)
     return y.reshape(*shp[:-1], w.shape[0])
+
+
+def gemm_decode(x: torch.Tensor, w: torch.Tensor, act: int = 0, residual=None, norm_eps: float = 0.0, fp8=None):
+    """Decode-step GEMM (M <= 64) with the fused prologue/epilogue of the skinny kernels:
+    ``C = act(rstd(x) * x w^T) + residual`` where ``rstd`` (``norm_eps > 0``) is the RMS-norm of
+    each input row computed inside the GEMM (the norm weight must already be folded into ``w``)
+    and ``act`` may be ACT_SWIGLU (w = [gate; up]). ``fp8`` (Fp8Cache) streams e4m3fn weights."""
+    if on_gpu(x):
+        x = x.contiguous()
+        if fp8 is not None:
+            from .fp8 import fp8_supported
+
+            if fp8_supported(w):
+                q, sc = fp8.get(w)
+                return native().gemm_fp8(x, None, q, sc, None, act, None, residual, norm_eps)
+        return native().gemm(x, w, None, None, None, act, False, None, residual, norm_eps)
+    y = x.float() @ w.float().t()
+    if norm_eps > 0:
+        y = y * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + norm_eps)
+    if act == ACT_SWIGLU:
+        F = w.shape[0] // 2
+        y = torch.nn.functional.silu(y[:, :F]) * y[:, F:]
+    else:
+        y = ref.apply_act(y, act)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
+class FoldCache(dict):
+    """W diag(norm_w): the RMS-norm weight folded into the following projection for the fused
+    decode path, recomputed in place when either source changes (graph-safe addresses)."""
+
+    @torch.no_grad()
+    def get(self, w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
+        key = (w.data_ptr(), w._version, norm_w.data_ptr(), norm_w._version)
+        if dict.get(self, "key") != key:
+            buf = dict.get(self, "w")
+            if buf is None or buf.shape != w.shape or buf.device != w.device:
+                buf = torch.empty_like(w)
+                self["w"] = buf
+            torch.mul(w, norm_w.to(w.dtype)[None, :], out=buf)
+            self["key"] = key
+        return self["w"]

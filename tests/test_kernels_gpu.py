@@ -496,3 +496,32 @@ def test_gemm_swiglu_pair(M, F, K):
     # through the layer API (no-grad, GPU)
     with torch.no_grad():
         _close(ops.linear(x, w, act="swiglu"), yr)
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (512, 256)])
+def test_gemm_decode_norm_residual(M, N, K):
+    """In-GEMM RMS norm (norm weight folded into W) + residual epilogue == rms_norm -> GEMM -> add."""
+    torch.manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 3
+    lnw = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * lnw.float()
+    yr = xn @ w.float().t() + res.float()
+    wf = ops.FoldCache().get(w, lnw)
+    y = ops.gemm_decode(x, wf, residual=res, norm_eps=1e-5)
+    _close(y, yr)
+    # norm only / residual only / swiglu + norm
+    _close(ops.gemm_decode(x, wf, norm_eps=1e-5), xn @ w.float().t())
+    _close(ops.gemm_decode(x, w, residual=res), x.float() @ w.float().t() + res.float())
+    if N % 64 == 0:
+        F = N // 2
+        g, u = xn @ w[:F].float().t(), xn @ w[F:].float().t()
+        _close(ops.gemm_decode(x, wf, act=ops.ACT_SWIGLU, norm_eps=1e-5), torch.nn.functional.silu(g) * u)
+    # fp8 weights (W8A16)
+    c8 = ops.Fp8Cache()
+    q, s = c8.get(wf)
+    wd = ops.dequantize_fp8(q, s)
+    yr8 = (x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)) @ wd.t() + res.float()
+    _close(ops.gemm_decode(x, wf, residual=res, norm_eps=1e-5, fp8=c8), yr8)
