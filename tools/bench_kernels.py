@@ -119,6 +119,39 @@ def main():
             print(json.dumps(r), flush=True)
             del wqs
         torch.cuda.empty_cache()
+    # one decode layer: fused (norm folded, residual epilogues, SwiGLU epilogue) vs unfused
+    for M in ((1, 16, 32, 64) if want("layer") else ()):
+        Hs, Fs = H, F
+        x = torch.randn(M, Hs, device=dev, dtype=torch.bfloat16)
+        resid = torch.randn_like(x)
+        lnw = torch.ones(Hs, device=dev, dtype=torch.bfloat16)
+        wqkv = torch.randn(NQKV, Hs, device=dev, dtype=torch.bfloat16) / 64
+        wo = torch.randn(Hs, Hs, device=dev, dtype=torch.bfloat16) / 64
+        wgu = torch.randn(2 * Fs, Hs, device=dev, dtype=torch.bfloat16) / 64
+        wd = torch.randn(Hs, Fs, device=dev, dtype=torch.bfloat16) / 128
+        att = torch.randn(M, Hs, device=dev, dtype=torch.bfloat16)
+
+        def fused():
+            q = ops.gemm_decode(x, wqkv, norm_eps=1e-5)
+            h = ops.gemm_decode(att, wo, residual=x)
+            f = ops.gemm_decode(h, wgu, act=ops.ACT_SWIGLU, norm_eps=1e-5)
+            return ops.gemm_decode(f, wd, residual=h), q
+
+        def unfused():
+            y, h0 = ops.rms_norm(x, lnw, 1e-5, resid)
+            q = ops.gemm(y, wqkv)
+            a = ops.gemm(att, wo)
+            y2, h = ops.rms_norm(a, lnw, 1e-5, h0)
+            gu = ops.gemm(y2, wgu)
+            return ops.gemm(ops.swiglu(gu), wd), q
+
+        ops.set_gemm_backend("lib", "native", "auto")
+        tu = timeit(unfused)
+        tf = timeit(fused)
+        ops.set_gemm_backend("native", "native", "native")
+        r = dict(kind="decode_layer", M=M, fused_us=tf, unfused_us=tu)
+        res.append(r)
+        print(json.dumps(r), flush=True)
     # split-K sweep of the M <= 64 ring kernel (cold weights)
     for M in ((64,) if want("m64sweep") else ()):
         for name, N, K in gemms:
