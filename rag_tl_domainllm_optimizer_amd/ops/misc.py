@@ -90,6 +90,14 @@ def token_logprobs(logits: torch.Tensor, targets, inv_temp: float = 1.0):
         return lp, ent
     if logits.stride(-1) != 1:
         logits = logits.contiguous()
+    V = logits.shape[-1]
+    if V % 8 or logits.stride(0) % 8:
+        # the kernel streams 16-B row vectors: pad the vocabulary up to a multiple of 8 columns with a
+        # large negative logit (probability exactly 0 and p * x = 0 in the entropy; finite even after
+        # the temperature scaling, unlike finfo.min)
+        Vp = (V + 7) // 8 * 8
+        pad = torch.full((logits.shape[0], Vp - V), -1e30, dtype=logits.dtype, device=logits.device)
+        logits = torch.cat([logits, pad], 1)
     if torch.is_grad_enabled() and logits.requires_grad:
         return _LogProbFn.apply(logits, targets, inv_temp)
     lp, ent, _, _ = native().logprob_fwd(logits, targets, inv_temp, True)

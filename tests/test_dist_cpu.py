@@ -56,18 +56,17 @@ def _worker(rank, world, port, out_dir, bucket_bytes):
     parallel.shutdown()
 
 
-@pytest.mark.parametrize("bucket_bytes", [1 << 10, 64 << 20])
-def test_dp_allreduce_equals_single_process(tmp_path, bucket_bytes):
+@pytest.mark.parametrize("world,bucket_bytes", [(2, 1 << 10), (2, 64 << 20), (4, 1 << 12)])
+def test_dp_allreduce_equals_single_process(tmp_path, world, bucket_bytes):
     from rag_tl_domainllm_optimizer_amd import models
     from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
     from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
     from rag_tl_domainllm_optimizer_amd.train.sft import SFTConfig, SFTTrainer
 
-    world = 2
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), bucket_bytes), nprocs=world,
                        start_method="spawn", join=True)
     dp = torch.load(tmp_path / "dp.pt")
-    # single process on the full batch, grad_accum=2 over the same two shards == mean of shard means
+    # single process on the full batch, accumulated over the same shards == mean of shard means
     torch.manual_seed(0)
     cfg = PRESETS["tiny-llama"]
     tok = Tokenizer.synthetic(cfg.vocab_size, "llama")
@@ -79,10 +78,11 @@ def test_dp_allreduce_equals_single_process(tmp_path, bucket_bytes):
     m.refresh_lora()
     ex = _examples(tok)
     tr.opt.zero_grad()
-    for shard in (ex[0::2], ex[1::2]):
+    for r in range(world):
+        shard = ex[r::world]
         ids, start, tgt = tr.encode([e["prompt"] for e in shard], [e["answer"] for e in shard])
         loss, _ = tr.loss(ids, start, tgt)
-        (loss / 2).backward()
+        (loss / world).backward()
     tr.flat.relink_grads()
     torch.testing.assert_close(dp, tr.flat.grad, rtol=1e-4, atol=1e-7)
     assert dp.abs().sum() > 0

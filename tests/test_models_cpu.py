@@ -36,7 +36,6 @@ def test_decoder_logits_match_hf(preset):
     cfg = PRESETS[preset]
     ours = models.CausalLM(cfg, dtype=torch.float32, seed=1)
     hf = _hf_causal(cfg)
-    io.load_hf_state_dict(hf, {}, strict=False) if False else None
     # ours -> HF
     sd = io.to_hf_state_dict(ours)
     missing, unexpected = hf.load_state_dict(sd, strict=False)
@@ -49,6 +48,28 @@ def test_decoder_logits_match_hf(preset):
         lg = ours.logits(h).view(2, 37, -1)
         ref = hf(input_ids=ids).logits
     torch.testing.assert_close(lg, ref, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("preset", ["tiny-llama", "tiny-opt"])
+def test_greedy_generation_matches_hf_generate(preset):
+    """KV-cache decode loop (prefill + per-token decode) == HF generate(do_sample=False)."""
+    from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
+
+    torch.manual_seed(0)
+    cfg = PRESETS[preset]
+    ours = models.CausalLM(cfg, dtype=torch.float32, seed=2)
+    hf = _hf_causal(cfg)
+    hf.load_state_dict(io.to_hf_state_dict(ours), strict=False)
+    if cfg.tie_embeddings:
+        hf.tie_weights()
+    prompt = torch.randint(3, cfg.vocab_size, (1, 19))
+    T = 10
+    with torch.no_grad():
+        ref = hf.generate(prompt, max_new_tokens=T, min_new_tokens=T, do_sample=False, eos_token_id=None,
+                          pad_token_id=0)[0, 19:]
+    out = Generator(ours, 1, 64).generate([prompt[0].tolist()], SamplingParams(max_new_tokens=T, do_sample=False),
+                                          pad_id=0, eos_ids=[-1])
+    assert out.tokens[0].tolist() == ref.tolist()
 
 
 def test_decoder_left_padding_matches_unpadded():

@@ -1,0 +1,59 @@
+"""Per-phase kernel breakdown from a rocprofv3 run with --kernel-trace --marker-trace -f csv.
+
+Usage: python tools/phase_breakdown.py <rocprof output dir> [--out summary.json] [--top 15]
+Kernels are attributed to the innermost roctx range (PhaseTimer phases: rollout,
+ref_logprobs+reward, update) whose time span contains the kernel's start timestamp.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("d")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--top", type=int, default=15)
+    a = ap.parse_args()
+    kf = glob.glob(os.path.join(a.d, "**", "*kernel_trace.csv"), recursive=True)
+    mf = glob.glob(os.path.join(a.d, "**", "*marker_api_trace.csv"), recursive=True)
+    assert kf and mf, (kf, mf)
+    ranges = []
+    for r in csv.DictReader(open(mf[0])):
+        try:
+            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        except (KeyError, ValueError):
+            continue
+        name = r.get("Function") or r.get("Message") or r.get("Name") or ""
+        if e > s:
+            ranges.append((s, e, name))
+    res = collections.defaultdict(lambda: collections.defaultdict(float))
+    span = collections.defaultdict(float)
+    for r in csv.DictReader(open(kf[0])):
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        best = None
+        for (rs, re_, n) in ranges:
+            if rs <= s <= re_ and (best is None or re_ - rs < best[1] - best[0]):
+                best = (rs, re_, n)
+        ph = best[2] if best else "(none)"
+        res[ph][r["Kernel_Name"][:90]] += (e - s) / 1e6
+    for (rs, re_, n) in ranges:
+        span[n] += (re_ - rs) / 1e6
+    out = {}
+    for ph, ks in res.items():
+        tot = sum(ks.values())
+        top = sorted(ks.items(), key=lambda x: -x[1])[: a.top]
+        out[ph] = {"kernel_ms": tot, "wall_ms": span.get(ph, 0.0), "top": [[k, round(v, 3)] for k, v in top]}
+        print(f"== {ph}: kernels {tot:.1f} ms / range {span.get(ph, 0.0):.1f} ms")
+        for k, v in top:
+            print(f"   {v:8.2f} ms  {k}")
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
