@@ -156,7 +156,18 @@ def cmd_ppo(cfg, args, policy=None):
                     max_batch=cfg.data.batch_size)
     loader = RecordLoader(recs, cfg.data.batch_size, seed=cfg.model.seed, rank=di.rank, world=di.world)
     best = -float("inf")
-    for ep in range(cfg.data.epochs):
+    first = 0
+    if getattr(args, "resume", False):
+        # resume from the latest completed epoch checkpoint of this run
+        done = [int(d[len("epoch_"):-len("_trainer_state")]) for d in (os.listdir(run_dir) if os.path.isdir(run_dir) else [])
+                if d.startswith("epoch_") and d.endswith("_trainer_state")]
+        if done:
+            st_ = tr.load_checkpoint(os.path.join(run_dir, f"epoch_{max(done)}"))
+            first = max(done)
+            best = float(st_.get("best_reward", best)) if isinstance(st_, dict) else best
+            if di.is_main:
+                print(f"Resumed from {os.path.join(run_dir, f'epoch_{first}')}")
+    for ep in range(first, cfg.data.epochs):
         loader.set_epoch(ep)
         rewards = []
         for batch in loader:
@@ -232,6 +243,7 @@ def main(argv: Optional[List[str]] = None):
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--nproc", type=int, default=1)
+    ap.add_argument("--resume", action="store_true", help="ppo: continue from the run's latest epoch checkpoint")
     if argv and argv[0] == "launch":
         a, rest = ap.parse_known_args(argv)
         return cmd_launch(a, [x for x in rest])

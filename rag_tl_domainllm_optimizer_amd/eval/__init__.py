@@ -62,7 +62,15 @@ class Evaluator:
         return out_txt
 
     def evaluate_model(self, model, tokenizer, test_data: Sequence[dict]) -> Dict[str, float]:
-        responses = self.generate(model, tokenizer, test_data)
+        """Under data parallelism each rank scores its shard (items rank::world); the per-item
+        scores are all-gathered (object all-gather) so every rank returns the same
+        means over the whole test set."""
+        from ..parallel import all_gather_object, info
+
+        di = info()
+        full = list(test_data)
+        test_data = full[di.rank::di.world] if di.world > 1 else full
+        responses = self.generate(model, tokenizer, test_data) if test_data else []
         res = {k: [] for k in METRIC_KEYS}
         for it, resp in zip(test_data, responses):
             gt = it.get("ground_truth")
@@ -72,13 +80,17 @@ class Evaluator:
                 res["rouge2"].append(r["rouge2"])
                 res["rougeL"].append(r["rougeL"])
                 res["bleu"].append(bleu([resp], [[gt]])["bleu"])
-        rewards, comps = self.reward_model.score(responses, [it["query"] for it in test_data],
-                                                 [it.get("retrieved_docs") or [] for it in test_data],
-                                                 [it.get("ground_truth") for it in test_data])
-        res["relevance"] = comps["relevance"].tolist()
-        res["factual_accuracy"] = comps["factual_accuracy"].tolist()
-        res["overall_score"] = rewards.tolist()
+        if test_data:
+            rewards, comps = self.reward_model.score(responses, [it["query"] for it in test_data],
+                                                     [it.get("retrieved_docs") or [] for it in test_data],
+                                                     [it.get("ground_truth") for it in test_data])
+            res["relevance"] = comps["relevance"].tolist()
+            res["factual_accuracy"] = comps["factual_accuracy"].tolist()
+            res["overall_score"] = rewards.tolist()
         self.last_responses = responses
+        if di.world > 1:
+            parts = all_gather_object(res)
+            res = {k: sum((p[k] for p in parts), []) for k in res}
         return {k: float(np.mean(v)) for k, v in res.items() if v}
 
     def compare_models(self, models: Dict[str, tuple], test_data: Sequence[dict]):

@@ -68,3 +68,12 @@ def test_serve_app():
     assert c.get("/health").json()["docs"] == 2
     r = c.post("/answer", json={"query": "q"}).json()
     assert r["answer"] == "ans" and r["doc_ids"] == [0]
+
+
+def test_cli_ppo_resume_from_latest(tmp_path, capsys):
+    args = _tiny(tmp_path) + ["--data.epochs=1"]
+    cli.main(["ppo", *args])
+    cli.main(["ppo", *[a for a in args if not a.startswith("--data.epochs")], "--data.epochs=2", "--resume"])
+    out = capsys.readouterr().out
+    assert "Resumed from" in out and "Epoch 2/2" in out and "Epoch 1/2" not in out
+    assert (tmp_path / "run" / "epoch_2_trainer_state").is_dir()
