@@ -1001,8 +1001,6 @@ static int decode_split(int N, int K) {
 
 using namespace rt;
 
-extern "C" int rt_gemm_decode_split(int N, int K) { return decode_split(N, K); }
-
 // never let a split-K launch write past the workspace (slabs: groups x split x slab floats;
 // tickets: one per column group)
 static int fit_split(int split, int groups, long slab_floats) {

@@ -357,6 +357,227 @@ __global__ __launch_bounds__(256) void sample_bf16_lds_kernel(const bf16_t* __re
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// top-k (+ top-p) sampler for bf16 logits, one 1024-thread workgroup per row
+// ---------------------------------------------------------------------------------------------
+// The radix-histogram select above serialises on LDS atomics: bf16 logits share a handful of
+// exponent values, so most lanes of a wave hit the same few high-byte bins (~100 us per row at
+// V = 32000). Here the k-th largest key is found by a 16-step bitwise binary search over the
+// LDS-resident keys (count >= candidate: a block reduction, no atomics), the <= CAP survivors are
+// compacted, and top-p / the Gumbel draw run on the survivors only. Same kept set and the same
+// Philox stream (seed, row, offset * V + token) as sample_bf16_lds_kernel, so the same token wins.
+constexpr int TK_CAP = 2048;
+
+__device__ __forceinline__ int block_sum_int1024(int v, int* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) t += red[w];
+  return t;
+}
+
+__global__ __launch_bounds__(1024) void sample_topk_search_kernel(
+    const bf16_t* __restrict__ logits, long ld, int V, float inv_temp, int top_k, float top_p, uint64_t seed,
+    const int64_t* __restrict__ offset_ptr, const uint8_t* __restrict__ row_active, long* __restrict__ out_tok,
+    float* __restrict__ out_logp) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t keys[];  // [V]
+  __shared__ int lidx[TK_CAP];
+  __shared__ float lval[TK_CAP];   // tempered logit of each survivor
+  __shared__ int redi[16];
+  __shared__ float redf[16];
+  __shared__ int cnt;
+  const long row = blockIdx.x;
+  const bf16_t* x = logits + row * ld;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nv = V / 8;
+
+  // pass 1: stage keys, max + argmax
+  uint32_t kmax = 0;
+  int amx = 0;
+  for (int c = tid; c < nv; c += 1024) {
+    const uint4 v = *(const uint4*)(x + (long)c * 8);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint16_t k8[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      k8[2 * q] = (uint16_t)key16((uint16_t)(w[q] & 0xFFFF));
+      k8[2 * q + 1] = (uint16_t)key16((uint16_t)(w[q] >> 16));
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (k8[e] > kmax) { kmax = k8[e]; amx = c * 8 + e; }
+    *(uint4*)(keys + c * 8) = *(const uint4*)k8;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t ok = __shfl_xor(kmax, off, 64);
+    const int oi = __shfl_xor(amx, off, 64);
+    if (ok > kmax || (ok == kmax && oi < amx)) { kmax = ok; amx = oi; }
+  }
+  if (tid == 0) cnt = 0;
+  if (lane == 0) { redi[wid] = amx; redf[wid] = __uint_as_float(kmax); }
+  __syncthreads();
+  uint32_t KM = __float_as_uint(redf[0]);
+  int AM = redi[0];
+  for (int w2 = 1; w2 < 16; ++w2) {
+    const uint32_t k = __float_as_uint(redf[w2]);
+    if (k > KM || (k == KM && redi[w2] < AM)) { KM = k; AM = redi[w2]; }
+  }
+  const float M = key16_to_f(KM) * inv_temp;
+  // pass 2: normaliser of the full tempered distribution (behaviour log-prob)
+  float s = 0.f;
+  for (int c = tid; c < nv; c += 1024) {
+    const uint4 kv = *(const uint4*)(keys + c * 8);
+    const uint16_t* k8 = (const uint16_t*)&kv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += __expf(key16_to_f(k8[e]) * inv_temp - M);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  __syncthreads();
+  if (lane == 0) redf[wid] = s;
+  __syncthreads();
+  float S = 0.f;
+#pragma unroll
+  for (int w2 = 0; w2 < 16; ++w2) S += redf[w2];
+  const float lse = M + __logf(S);
+
+  int tok = AM;
+  const bool active = row_active ? row_active[row] != 0 : true;
+  if (active) {
+    // k-th largest key: largest t with count(keys >= t) >= K, bit by bit from the top
+    const int K = min(top_k, V);
+    uint32_t prefix = 0;
+    for (int b = 15; b >= 0; --b) {
+      const uint32_t cand = prefix | (1u << b);
+      int c = 0;
+      for (int cc = tid; cc < nv; cc += 1024) {
+        const uint4 kv = *(const uint4*)(keys + cc * 8);
+        const uint16_t* k8 = (const uint16_t*)&kv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c += k8[e] >= cand;
+      }
+      if (block_sum_int1024(c, redi) >= K) prefix = cand;
+    }
+    const uint32_t kth = prefix;
+    // compact the survivors (ties at the threshold kept)
+    for (int cc = tid; cc < nv; cc += 1024) {
+      const uint4 kv = *(const uint4*)(keys + cc * 8);
+      const uint16_t* k8 = (const uint16_t*)&kv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (k8[e] >= kth) {
+          const int pos = atomicAdd(&cnt, 1);
+          if (pos < TK_CAP) { lidx[pos] = cc * 8 + e; lval[pos] = key16_to_f(k8[e]) * inv_temp; }
+        }
+    }
+    __syncthreads();
+    const bool overflow = cnt > TK_CAP;  // > TK_CAP - top_k ties at the k-th value: draw from the keys
+    const int n = min(cnt, TK_CAP);
+    float vthr = -INFINITY;  // kept: lval >= vthr
+    if (top_p < 1.f && n > 1 && !overflow) {
+      // sort survivors by value, descending (bitonic over the next power of two)
+      int P = 1;
+      while (P < n) P <<= 1;
+      for (int i = n + tid; i < P; i += 1024) { lval[i] = -INFINITY; lidx[i] = 0x7fffffff; }
+      __syncthreads();
+      for (int size = 2; size <= P; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int i = tid; i < P / 2; i += 1024) {
+            const int lo = 2 * i - (i & (stride - 1));
+            const int hi = lo + stride;
+            const bool desc = ((lo & size) == 0);
+            const float a = lval[lo], bv = lval[hi];
+            const int ia = lidx[lo], ib = lidx[hi];
+            const bool a_first = a > bv || (a == bv && ia < ib);
+            if (a_first != desc) { lval[lo] = bv; lval[hi] = a; lidx[lo] = ib; lidx[hi] = ia; }
+          }
+          __syncthreads();
+        }
+      // smallest prefix whose mass reaches top_p of the survivors' mass (one wave, serial chunks)
+      if (wid == 0) {
+        const int per = (n + 63) / 64;
+        float part = 0.f;
+        for (int j = lane * per; j < min(n, (lane + 1) * per); ++j) part += __expf(lval[j] - M);
+        float incl = part;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const float t = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += t;
+        }
+        const float total = __shfl(incl, 63, 64);
+        const float target = top_p * total;
+        float run = incl - part;  // exclusive prefix of this lane's chunk
+        int jcut = n - 1;
+        bool found = false;
+        for (int j = lane * per; j < min(n, (lane + 1) * per); ++j) {
+          run += __expf(lval[j] - M);
+          if (run >= target) { jcut = j; found = true; break; }
+        }
+        // first lane (lowest index) that reached the target
+        const unsigned long long m = __ballot(found);
+        const int src = m ? __ffsll((long long)m) - 1 : 63;
+        jcut = __shfl(jcut, src, 64);
+        if (lane == 0) redf[0] = lval[jcut];
+      }
+      __syncthreads();
+      vthr = redf[0];
+      __syncthreads();
+    }
+    // Gumbel-max over the kept survivors
+    const uint64_t off = offset_ptr ? (uint64_t)offset_ptr[0] : 0ull;
+    float best = -INFINITY;
+    int bi = AM;
+    if (!overflow) {
+      for (int j = tid; j < n; j += 1024) {
+        const float v = lval[j];
+        if (v >= vthr) {
+          const int i = lidx[j];
+          const uint4 r = Philox::gen(seed, (uint64_t)row, off * (uint64_t)V + (uint64_t)i);
+          const float sc = v - __logf(-__logf(u32_to_unit(r.x)));
+          if (sc > best || (sc == best && i < bi)) { best = sc; bi = i; }
+        }
+      }
+    } else {  // degenerate tie plateau: top-k set only (top-p not applied), straight from the keys
+      for (int i = tid; i < V; i += 1024) {
+        const uint32_t k = keys[i];
+        if (k >= kth) {
+          const uint4 r = Philox::gen(seed, (uint64_t)row, off * (uint64_t)V + (uint64_t)i);
+          const float sc = key16_to_f(k) * inv_temp - __logf(-__logf(u32_to_unit(r.x)));
+          if (sc > best || (sc == best && i < bi)) { best = sc; bi = i; }
+        }
+      }
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+      const float ob = __shfl_xor(best, o2, 64);
+      const int oi = __shfl_xor(bi, o2, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    __syncthreads();
+    if (lane == 0) { redf[wid] = best; redi[wid] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      float Bv = redf[0];
+      int BI = redi[0];
+      for (int w2 = 1; w2 < 16; ++w2)
+        if (redf[w2] > Bv || (redf[w2] == Bv && redi[w2] < BI)) { Bv = redf[w2]; BI = redi[w2]; }
+      redi[0] = BI;
+    }
+    __syncthreads();
+    tok = redi[0];
+  }
+  if (tid == 0) {
+    out_tok[row] = tok;
+    if (out_logp) out_logp[row] = key16_to_f(keys[tok]) * inv_temp - lse;
+  }
+}
+
 }  // namespace rt
 
 using namespace rt;
@@ -365,6 +586,13 @@ extern "C" int rt_sample(const void* logits, int is_f32, long ld, long B, int V,
                          int greedy, uint64_t seed, const int64_t* offset_ptr, const uint8_t* row_active, long* out_tok,
                          float* out_logp, hipStream_t stream) {
   if (B == 0) return 0;
+  if (!is_f32 && !greedy && top_k > 0 && top_k <= 1024 && V % 8 == 0 && ld % 8 == 0 && (size_t)V * 2 <= 96 * 1024) {
+    const size_t shm = ((size_t)V * 2 + 15) / 16 * 16;
+    hipLaunchKernelGGL(sample_topk_search_kernel, dim3(B), dim3(1024), shm, stream, (const bf16_t*)logits, ld, V,
+                       inv_temp, top_k, top_p, seed, offset_ptr, row_active, out_tok, out_logp);
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
   if (!is_f32 && V % 8 == 0 && ld % 8 == 0 && (size_t)V * 2 <= 96 * 1024) {
     const size_t shm = ((size_t)V * 2 + 15) / 16 * 16;
     hipLaunchKernelGGL(sample_bf16_lds_kernel, dim3(B), dim3(256), shm, stream, (const bf16_t*)logits, ld, V, inv_temp,

@@ -301,6 +301,33 @@ def test_sampler_bf16_topk_topp_vocab():
     _close(lp, lpr, rtol=2e-3, atol=2e-3)
 
 
+@pytest.mark.parametrize("top_k,top_p", [(50, 1.0), (50, 0.9), (1000, 0.95), (7, 0.5)])
+def test_sampler_search_path_matches_f32_kernel(top_k, top_p):
+    """The bf16 binary-search top-k sampler keeps the same set and uses the same Philox stream as the
+    fp32 radix kernel, so both draw the same tokens (top-p boundary rounding may flip a rare row)."""
+    B, V = 64, 32000
+    logits = (torch.randn(B, V, device=DEV) * 2).to(torch.bfloat16)
+    off = torch.full((1,), 3, dtype=torch.long, device=DEV)
+    tb, lb = ops.sample(logits, 1 / 0.7, top_k=top_k, top_p=top_p, seed=21, offset=off)
+    tf, lf = ops.sample(logits.float(), 1 / 0.7, top_k=top_k, top_p=top_p, seed=21, offset=off)
+    assert (tb == tf).float().mean().item() >= 0.95
+    keep = ref.filter_logits(logits.float(), 1 / 0.7, top_k, top_p)
+    assert keep.gather(1, tb[:, None]).float().mean().item() >= 0.98
+    _close(lb, ref.logprob(logits, tb, 1 / 0.7)[0], rtol=2e-3, atol=2e-3)
+
+
+def test_sampler_search_path_tie_plateau():
+    # > 2048 tokens tied at the k-th value: survivors overflow the list, the draw falls back to the keys
+    V = 32000
+    logits = torch.zeros(4, V, device=DEV, dtype=torch.bfloat16)
+    logits[:, :3] = 5.0
+    off = torch.zeros(1, dtype=torch.long, device=DEV)
+    tok, _ = ops.sample(logits, 1.0, top_k=10, seed=2, offset=off)
+    assert bool((tok >= 0).all()) and bool((tok < V).all())
+    tok, _ = ops.sample(logits, 1.0, top_k=3, seed=2, offset=off)
+    assert bool((tok < 3).all())
+
+
 def test_adamw_matches_torch():
     n = 10007
     p0 = torch.randn(n, device=DEV)

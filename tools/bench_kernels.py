@@ -119,6 +119,24 @@ def main():
             print(json.dumps(r), flush=True)
             del wqs
         torch.cuda.empty_cache()
+    # fused decode attention at batch 1: partition size sweep (NP = ceil(Smax / PS))
+    for L in ((456, 2048) if want("attnps") else ()):
+        Hq, Hkv, D = 32, 8, 128
+        q1 = torch.randn(1, (Hq + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
+        kc1 = torch.randn(1, Hkv, L + 8, D, device=dev, dtype=torch.bfloat16)
+        vc1 = torch.randn_like(kc1)
+        slot = torch.full((1,), L - 1, device=dev, dtype=torch.int32)
+        cos, sin = ops.reference.rope_tables(D, 8192, 10000.0, dev)
+        o1 = torch.empty(1, Hq * D, device=dev, dtype=torch.bfloat16)
+        for PS in (64, 128, 256, 512, 1024, 2048, 4096):
+            if PS > 4 * (L + 8) + 64:
+                continue
+            ws1 = ops.decode_workspace(1, Hq, Hkv, D, L + 8, dev, PS=PS)
+            t = timeit(lambda: ops.decode_step_attention(q1, kc1, vc1, slot, slot + 1, Hq, slot, cos, sin, workspace=ws1,
+                                                         out=o1))
+            r = dict(kind="attn_decode_fused_ps", B=1, L=L, PS=PS, NP=(L + 8 + PS - 1) // PS, us=t)
+            res.append(r)
+            print(json.dumps(r), flush=True)
     # one decode layer: fused (norm folded, residual epilogues, SwiGLU epilogue) vs unfused
     for M in ((1, 16, 32, 64) if want("layer") else ()):
         Hs, Fs = H, F
@@ -256,10 +274,11 @@ def main():
     print(json.dumps(r), flush=True)
     lg = torch.randn(64, V, device=dev, dtype=torch.bfloat16)
     off = torch.zeros(1, dtype=torch.long, device=dev)
-    t = timeit(lambda: ops.sample(lg, 1 / 0.7, top_k=50, top_p=0.9, seed=1, offset=off))
-    r = dict(kind="sample_topk_topp", B=64, us=t)
-    res.append(r)
-    print(json.dumps(r), flush=True)
+    for B_, k_, p_ in ((64, 50, 0.9), (1, 50, 0.9), (1, 50, 1.0), (64, 50, 1.0), (1, 0, 1.0), (64, 0, 1.0)):
+        t = timeit(lambda: ops.sample(lg[:B_], 1 / 0.7, top_k=k_, top_p=p_, seed=1, offset=off))
+        r = dict(kind="sample", B=B_, top_k=k_, top_p=p_, us=t)
+        res.append(r)
+        print(json.dumps(r), flush=True)
     if args.json:
         with open(args.json, "w") as f:
             json.dump(res, f, indent=1)
