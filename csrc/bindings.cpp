@@ -21,6 +21,7 @@ int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const vo
                long, int, int, int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
 void rt_gemm_set_variant(int);
 void rt_gemm_set_m64_split(int);
+void rt_gemm_set_decode_split(int);
 int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
                 int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
 int rt_quant_fp8_rows(const void*, long, void*, long, float*, long, int, hipStream_t);
@@ -551,6 +552,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_f32") = false, py::arg("out") = py::none(), py::arg("residual") = py::none(),
         py::arg("norm_eps") = 0.0);
   m.def("gemm_set_m64_split", &rt_gemm_set_m64_split, "tuning: fixed split-K of the M<=64 ring kernel (0 = auto)");
+  m.def("gemm_set_decode_split", &rt_gemm_set_decode_split, "tuning: fixed split-K of the M<=16 decode kernel (0 = auto)");
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
   m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");

@@ -508,9 +508,11 @@ __global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
 // 64 columns x (K / (4*split)), so every X fragment feeds 4 MFMAs (X:W traffic 1:1 at M = 64
 // instead of 4:1 with 16-column waves). Its W rows stream straight to VGPRs (read once: no LDS,
 // cdna_hip_programming.md §5 'GEMV / M <= 16'), one 64-deep k-chunk ahead in two named register
-// sets (no runtime-indexed register arrays). Per 64-chunk, lane group g = lane>>4 owns
-// k in [16g, 16g+16): MFMA step s uses k = 16g + 8s + j for BOTH operands (exact reordering of the
-// sum), so each W row is read as one full 128-B line per chunk.
+// sets (no runtime-indexed register arrays). Per 64-chunk the fragments follow the MFMA's own k
+// layout (lane group g = lane>>4 holds k [8g, 8g+8) of each 32-deep half), so each 16-B load
+// instruction reads 64 contiguous bytes of 16 weight rows. (A layout where a lane group owned one
+// 32-B run per row measured the same; an HBM pattern probe, tools/microbench/hbm_pattern.hip, puts
+// this 16-rows x 128-B step at 5.9 TB/s vs 6.3-6.7 for 512-B..1-KiB row spans.)
 // Reduction: the 4 waves of a block sum through LDS; the `split` blocks of a column group publish
 // fp32 slabs and the LAST arriver (agent-scope release -> relaxed ticket -> agent-scope acquire,
 // §6 Guideline 16 / §5 'In-launch split-K reduction') sums them and runs the epilogue (LoRA U*UB^T,
@@ -535,13 +537,13 @@ __device__ __forceinline__ void dg_load(DGRegs<MT>& r, const char* const* wrow, 
       r.w[j][0] = load_nt16(wrow[j] + c * 64);
     } else {
       r.w[j][0] = load_nt16(wrow[j] + c * 128);
-      r.w[j][1] = load_nt16(wrow[j] + c * 128 + 16);
+      r.w[j][1] = load_nt16(wrow[j] + c * 128 + 64);
     }
   }
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     r.x[m][0] = *(const uint4*)(xrow[m] + c * 64);
-    r.x[m][1] = *(const uint4*)(xrow[m] + c * 64 + 8);
+    r.x[m][1] = *(const uint4*)(xrow[m] + c * 64 + (W8 ? 8 : 32));
   }
 }
 
@@ -600,10 +602,12 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
   for (int j = 0; j < 4; ++j) {
     const int wr_ = pair ? (j < 2 ? cg * 32 + j * 16 + frow : F + cg * 32 + (j - 2) * 16 + frow)
                          : min(n0 + j * 16 + frow, p.N - 1);
-    wrow[j] = (const char*)p.B + ((long)wr_ * p.ldb + g * 16) * WSZ;
+    // bf16: lane group g holds k [8g, 8g+8) and [32+8g, 32+8g+8) of each 64-deep chunk (the MFMA's
+    // own layout: each load instruction reads 64 contiguous bytes per row); fp8: [16g, 16g+16)
+    wrow[j] = (const char*)p.B + ((long)wr_ * p.ldb + g * (W8 ? 16 : 8)) * WSZ;
   }
 #pragma unroll
-  for (int m = 0; m < MT; ++m) xrow[m] = p.A + (long)min(m * 16 + frow, p.M - 1) * p.lda + g * 16;
+  for (int m = 0; m < MT; ++m) xrow[m] = p.A + (long)min(m * 16 + frow, p.M - 1) * p.lda + g * (W8 ? 16 : 8);
 
   f32x4 acc[MT][4];
 #pragma unroll
@@ -779,102 +783,19 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// M in (16, 64]: LDS-DMA ring GEMM (rollout decode at batch 64)
-// ---------------------------------------------------------------------------------------------
-// Block = 4 waves, 64 output columns x all (<= 64) rows x a K range (split-K over workgroups).
-// Each 64-deep K-step stages X[64 x 64] and W[64 x 64] (8 KiB each, 2 x 16-B global_load_lds
-// per lane per operand) into one slot of a 4-slot ring; three steps stay in flight (counted
-// vmcnt, raw s_barrier — never __syncthreads inside the loop, which would drain the DMA queue),
-// so ~96 KiB per CU of loads are outstanding at 2 blocks/CU without costing VGPRs. Wave w owns
-// rows [16w, 16w+16) x 64 columns (4 MFMA fragments). Split-K partials use the write-through
-// ticket hand-off of gemm_decode_kernel.
-constexpr int R64_SLOTS = 4;
-constexpr int R64_SLOT = 2 * 64 * 128;  // X + W, 64 rows x 128 B each
-
+// Shared tail of the M <= 64 kernels: split-K hand-off (write-through slabs + ticket, last arriver
+// reduces), in-GEMM RMS-norm scaling, SwiGLU pair / bias + activation + residual epilogues.
+// acc[j][r] = C[16 wid + 4 fq + r][16 j + frow] of the block's 64 columns; sq = sum of squares of
+// X row (16 wid + frow) over this block's K range (norm only).
 template <bool OUT_F32>
-__global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __restrict__ slabs,
-                                                          unsigned* __restrict__ tickets, int split) {
-  __shared__ __attribute__((aligned(16))) char smem[R64_SLOTS * R64_SLOT];  // the only __shared__ object
+__device__ __forceinline__ void m64_finish(const GemmArgs& p, f32x4 (&acc)[4], float sq, float* __restrict__ slabs,
+                                           unsigned* __restrict__ tickets, int split, int cg, int sp, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int cg = blockIdx.x / split, sp = blockIdx.x % split;
-  const int n0 = cg * 64;
   const int frow = lane & 15, fq = lane >> 4;
-  const int nk = p.K / 64;
-  const int t0 = (int)((long)sp * nk / split), t1 = (int)((long)(sp + 1) * nk / split);
-  const int nt = t1 - t0;
+  const int n0 = cg * 64;
+  const bool normed = p.norm_eps > 0.f;
   const bool pair = p.act == ACT_SWIGLU;
   const int F = p.N / 2;
-
-  // staging: lane -> (row within an 8-row piece, 16-B slot); 2 pieces per operand per wave
-  const int srow = lane >> 3;
-  auto stage = [&](int t) {  // K-step t (absolute) -> slot (t - t0) % R64_SLOTS
-    char* slot = smem + ((t - t0) % R64_SLOTS) * R64_SLOT;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int lr = (wid * 2 + j) * 8 + srow;  // 0..63
-      const int ck = (lane & 7) ^ lds_swz(lr);
-      const bf16_t* xa = p.A + (long)min(lr, p.M - 1) * p.lda + (long)t * 64 + ck * 8;
-      const int wrow_ = pair ? (lr < 32 ? cg * 32 + lr : F + cg * 32 + lr - 32) : min(n0 + lr, p.N - 1);
-      const bf16_t* wb = p.B + (long)wrow_ * p.ldb + (long)t * 64 + ck * 8;
-      __builtin_amdgcn_global_load_lds((const void*)xa, (lds_void*)(slot + (wid * 2 + j) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)wb, (lds_void*)(slot + 8192 + (wid * 2 + j) * 1024), 16, 0, 0);
-    }
-  };
-
-  f32x4 acc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool normed = p.norm_eps > 0.f;
-  float sq = 0.f;
-
-  // prologue: steps t0 .. t0+2 in flight
-#pragma unroll
-  for (int i = 0; i < R64_SLOTS - 1; ++i)
-    if (i < nt) stage(t0 + i);
-
-  for (int i = 0; i < nt; ++i) {
-    // retire step i (each step = 4 DMAs per lane); later steps stay in flight
-    const int ahead = min(R64_SLOTS - 2, nt - 1 - i);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_barrier" ::: "memory");
-    // refill the slot read in the previous iteration (every wave is past it: barrier above)
-    if (i + R64_SLOTS - 1 < nt) stage(t0 + i + R64_SLOTS - 1);
-    const char* slot = smem + (i % R64_SLOTS) * R64_SLOT;
-    bf16x8 a[2], b[4][2];
-    const int ar = wid * 16 + frow;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = kk * 4 + fq;
-      a[kk] = *(const bf16x8*)(slot + ar * 128 + ((c ^ lds_swz(ar)) << 4));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int br = j * 16 + frow;
-        b[j][kk] = *(const bf16x8*)(slot + 8192 + br * 128 + ((c ^ lds_swz(br)) << 4));
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk], b[j][kk], acc[j], 0, 0, 0);
-    if (normed) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float f = (float)a[kk][e];
-          sq += f * f;
-        }
-    }
-  }
-  // lanes of row (16 wid + frow) differ in fq: the row's sum of squares over this block's K range
-  if (normed) {
-    sq += __shfl_xor(sq, 16, 64);
-    sq += __shfl_xor(sq, 32, 64);
-  }
-
   // lane holds C[16 wid + 4 fq + r][16 j + frow]
   if (split > 1) {
     constexpr int SLAB = 64 * 64 + 64;
@@ -971,6 +892,104 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// M in (16, 64]: LDS-DMA ring GEMM (rollout decode at batch 64)
+// ---------------------------------------------------------------------------------------------
+// Block = 4 waves, 64 output columns x all (<= 64) rows x a K range (split-K over workgroups).
+// Each 64-deep K-step stages X[64 x 64] and W[64 x 64] (8 KiB each, 2 x 16-B global_load_lds
+// per lane per operand) into one slot of a 4-slot ring; three steps stay in flight (counted
+// vmcnt, raw s_barrier — never __syncthreads inside the loop, which would drain the DMA queue),
+// so ~96 KiB per CU of loads are outstanding at 2 blocks/CU without costing VGPRs. Wave w owns
+// rows [16w, 16w+16) x 64 columns (4 MFMA fragments). Split-K partials use the write-through
+// ticket hand-off of gemm_decode_kernel.
+constexpr int R64_SLOTS = 4;
+constexpr int R64_SLOT = 2 * 64 * 128;  // X + W, 64 rows x 128 B each
+
+template <bool OUT_F32>
+__global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __restrict__ slabs,
+                                                          unsigned* __restrict__ tickets, int split) {
+  __shared__ __attribute__((aligned(16))) char smem[R64_SLOTS * R64_SLOT];  // the only __shared__ object
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int cg = blockIdx.x / split, sp = blockIdx.x % split;
+  const int n0 = cg * 64;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int nk = p.K / 64;
+  const int t0 = (int)((long)sp * nk / split), t1 = (int)((long)(sp + 1) * nk / split);
+  const int nt = t1 - t0;
+  const bool pair = p.act == ACT_SWIGLU;
+  const int F = p.N / 2;
+
+  // staging: lane -> (row within an 8-row piece, 16-B slot); 2 pieces per operand per wave
+  const int srow = lane >> 3;
+  auto stage = [&](int t) {  // K-step t (absolute) -> slot (t - t0) % R64_SLOTS
+    char* slot = smem + ((t - t0) % R64_SLOTS) * R64_SLOT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lr = (wid * 2 + j) * 8 + srow;  // 0..63
+      const int ck = (lane & 7) ^ lds_swz(lr);
+      const bf16_t* xa = p.A + (long)min(lr, p.M - 1) * p.lda + (long)t * 64 + ck * 8;
+      const int wrow_ = pair ? (lr < 32 ? cg * 32 + lr : F + cg * 32 + lr - 32) : min(n0 + lr, p.N - 1);
+      const bf16_t* wb = p.B + (long)wrow_ * p.ldb + (long)t * 64 + ck * 8;
+      __builtin_amdgcn_global_load_lds((const void*)xa, (lds_void*)(slot + (wid * 2 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)wb, (lds_void*)(slot + 8192 + (wid * 2 + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool normed = p.norm_eps > 0.f;
+  float sq = 0.f;
+
+  // prologue: steps t0 .. t0+2 in flight
+#pragma unroll
+  for (int i = 0; i < R64_SLOTS - 1; ++i)
+    if (i < nt) stage(t0 + i);
+
+  for (int i = 0; i < nt; ++i) {
+    // retire step i (each step = 4 DMAs per lane); later steps stay in flight
+    const int ahead = min(R64_SLOTS - 2, nt - 1 - i);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    // refill the slot read in the previous iteration (every wave is past it: barrier above)
+    if (i + R64_SLOTS - 1 < nt) stage(t0 + i + R64_SLOTS - 1);
+    const char* slot = smem + (i % R64_SLOTS) * R64_SLOT;
+    bf16x8 a[2], b[4][2];
+    const int ar = wid * 16 + frow;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fq;
+      a[kk] = *(const bf16x8*)(slot + ar * 128 + ((c ^ lds_swz(ar)) << 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int br = j * 16 + frow;
+        b[j][kk] = *(const bf16x8*)(slot + 8192 + br * 128 + ((c ^ lds_swz(br)) << 4));
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk], b[j][kk], acc[j], 0, 0, 0);
+    if (normed) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = (float)a[kk][e];
+          sq += f * f;
+        }
+    }
+  }
+  // lanes of row (16 wid + frow) differ in fq: the row's sum of squares over this block's K range
+  if (normed) {
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+  }
+  m64_finish<OUT_F32>(p, acc, sq, slabs, tickets, split, cg, sp, smem);
+}
+
 // split-K for the ring kernel, from a cold-weight sweep on MI355X (profiles/kernels_m64_split.log,
 // M = 64): wide outputs (>= 256 column groups) stream best unsplit, long K / narrow N want 8-way
 // split, mid shapes 2-way.
@@ -987,13 +1006,20 @@ static int m64_split(int N, int K) {
   return split;
 }
 
-// split-K so the grid reaches ~256 workgroups (one per CU) while every wave keeps >= 4 k-chunks of
-// 64 in flight-able work (short waves pay the reduction without amortising it)
+// split-K of the M <= 16 kernel, from a hipGraph-replayed sweep over distinct (cold) weights
+// (tools/sweep_decode.py, profiles/kernels_decode_split_sweep.log): wide outputs (>= 256 column
+// groups: gate_up, lm_head) stream best unsplit — a second round of workgroups costs more than it
+// hides; narrower ones split until ~2 workgroups per CU are resident, keeping >= 2 k-chunks per wave
+// (M = 1: qkv 16.5 -> 13.7 us, o 11.8 -> 10.9, down 29.4 -> 28.4 at split 8 vs 4).
+static int g_decode_split = 0;  // 0 = heuristic below; tuning override (rt_gemm_set_decode_split)
+
 static int decode_split(int N, int K) {
+  if (g_decode_split > 0) return g_decode_split;
   const int groups = (N + DG_COLS - 1) / DG_COLS;
   const int nc = K / 64;
+  if (groups >= 256) return 1;
   int split = 1;
-  while (groups * split < 256 && nc / (4 * split * 2) >= 4 && split < 16) split *= 2;
+  while (groups * split < 512 && nc / (4 * split * 2) >= 2 && split < 16) split *= 2;
   return split;
 }
 
@@ -1013,6 +1039,8 @@ static int fit_split(int split, int groups, long slab_floats) {
 static int g_gemm_variant = 0;
 extern "C" void rt_gemm_set_variant(int v) { g_gemm_variant = v; }
 extern "C" void rt_gemm_set_m64_split(int s) { g_m64_split = s; }
+extern "C" void rt_gemm_set_decode_split(int s) { g_decode_split = s; }
+
 
 // Wave quantisation decides between the kernels: the 256-tile kernel runs one workgroup per CU
 // (256 slots), the 128-tile kernel two (512 slots); the 256 kernel is ~10 % faster per FLOP

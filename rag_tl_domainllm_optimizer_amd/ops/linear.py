@@ -28,9 +28,10 @@ ACT_SWIGLU = 5  # w = [gate; up] (2F rows) -> silu(x gate^T) * (x up^T), [.., F]
 #                faster than hipBLASLt on cold (HBM-streamed) decode weights at batch 1-8
 #                (profiles/kernels_skinny_cold.log: qkv 16.5 vs 19.5 us, o 11.4 vs 19.0 us,
 #                gate_up 46.9 vs 56.0 us, lm_head 47.8 vs 57.4 us)
-#   16 < M <= 64 MID_BACKEND, default "auto": the LDS-DMA ring kernel for wide or deep weights
-#                (N >= 16384 or K >= 8192: gate_up 52 vs 55 us, down 36 vs 41 us, lm_head 54 vs
-#                60 us cold at M = 64), hipBLASLt for the rest (qkv / o: 20 vs 25 / 20 us)
+#   16 < M <= 64 MID_BACKEND, default "auto": the LDS-DMA ring kernel for deep weights (K >= 8192:
+#                down 36.6 vs 39.8 us), hipBLASLt for the rest (qkv 18 vs 26, o 15 vs 21, gate_up
+#                49-52 vs 58, lm_head 54-58 vs 58 us) — hipGraph replay over distinct weights at
+#                M = 64, profiles/kernels_decode_split_sweep.log
 #   M > 64       PLAIN_BACKEND, default "lib" (hipBLASLt ~1.5 PF/s vs ~1.2 PF/s for the 256x256
 #                8-phase kernel on plain GEMMs)
 # Everything with a fused epilogue or a LoRA term always runs on the hand-written kernels.
@@ -58,7 +59,7 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
             M = x.shape[0]
             backend = SKINNY_BACKEND if M <= 16 else (MID_BACKEND if M <= 64 else PLAIN_BACKEND)
             if backend == "auto":
-                backend = "native" if (w.shape[0] >= 16384 or w.shape[1] >= 8192) else "lib"
+                backend = "native" if w.shape[1] >= 8192 else "lib"
             if backend == "lib":
                 return torch.matmul(x, w.t(), out=out)
         return native().gemm(x, w, u, ub, bias, act, out_f32, out)

@@ -552,3 +552,29 @@ def test_gemm_decode_norm_residual(M, N, K):
     wd = ops.dequantize_fp8(q, s)
     yr8 = (x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)) @ wd.t() + res.float()
     _close(ops.gemm_decode(x, wf, residual=res, norm_eps=1e-5, fp8=c8), yr8)
+
+
+@pytest.mark.parametrize("M,N,K,split", [(64, 6144, 4096, 0), (64, 4096, 14336, 8), (33, 28672, 4096, 1),
+                                         (64, 4096, 4096, 4), (17, 1152, 384, 0), (64, 32000, 4096, 2),
+                                         (48, 4096, 512, 3)])
+def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split):
+    """16 < M <= 64 ring kernel with every split-K and epilogue (plain, in-GEMM RMS norm, residual,
+    SwiGLU pair) against fp32 references; tickets re-arm across launches."""
+    C = ops.native()
+    C.gemm_set_m64_split(split)
+    try:
+        torch.manual_seed(M + N + K)
+        x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2
+        w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+        res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+        yr = x.float() @ w.float().t()
+        for _ in range(2):
+            _close(ops.gemm(x, w), yr)
+        rstd = torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+        _close(ops.gemm_decode(x, w, residual=res, norm_eps=1e-5), yr * rstd + res.float())
+        if N % 64 == 0:
+            F = N // 2
+            g, u = (x.float() * rstd) @ w[:F].float().t(), (x.float() * rstd) @ w[F:].float().t()
+            _close(ops.gemm_decode(x, w, act=ops.ACT_SWIGLU, norm_eps=1e-5), torch.nn.functional.silu(g) * u)
+    finally:
+        C.gemm_set_m64_split(0)

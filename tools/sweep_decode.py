@@ -1,0 +1,87 @@
+"""Decode-GEMM sweep under hipGraph replay (no host launch overhead in the numbers).
+
+For each Mistral-7B decode shape, captures `reps` back-to-back GEMMs over distinct weight copies
+(> 256 MB total, so every launch streams its weights from HBM like a real decode step) and reports
+kernel time per GEMM and effective weight bandwidth, for each split-K setting and for hipBLASLt.
+
+    python tools/sweep_decode.py [--M 1] [--splits 0,2,4,8,16]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rag_tl_domainllm_optimizer_amd import ops  # noqa: E402
+
+SHAPES = [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
+          ("lm_head", 32000, 4096)]
+
+
+def graph_time(fn, replays=10):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(replays):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / replays * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", default="1")
+    ap.add_argument("--splits", default="0,1,2,4,8,16")
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    C = ops.native()
+    dev = "cuda"
+    ops.set_gemm_backend("native", "native", "native")
+    for M in [int(m) for m in args.M.split(",")]:
+        for name, N, K in SHAPES:
+            if args.only and name not in args.only.split(","):
+                continue
+            reps = max(4, int(1.2e9 // (N * K * 2)))
+            ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) for _ in range(reps)]
+            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(reps)]
+            byts = N * K * 2
+            for sp in [int(v) for v in args.splits.split(",")]:
+                (C.gemm_set_m64_split if M > 16 else C.gemm_set_decode_split)(sp)
+
+                def run():
+                    for w, o in zip(ws, outs):
+                        ops.gemm(x, w, out=o)
+                t = graph_time(run) / reps
+                r = dict(kind="decode_gemm", name=name, M=M, N=N, K=K, split=sp, us=round(t, 2),
+                         tbs=round(byts / t / 1e6, 2))
+                print(json.dumps(r), flush=True)
+            C.gemm_set_decode_split(0)
+            C.gemm_set_m64_split(0)
+            prev = ops.set_gemm_backend("lib", "lib", "lib")
+
+            def run_lib():
+                for w, o in zip(ws, outs):
+                    ops.gemm(x, w, out=o)
+            t = graph_time(run_lib) / reps
+            ops.set_gemm_backend(*prev)
+            print(json.dumps(dict(kind="decode_gemm", name=name, M=M, N=N, K=K, split="lib", us=round(t, 2),
+                                  tbs=round(byts / t / 1e6, 2))), flush=True)
+            del ws, outs
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
