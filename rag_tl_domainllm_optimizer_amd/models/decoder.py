@@ -230,10 +230,9 @@ class CausalLM(nn.Module):
     def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks):
         cfg = self.cfg
         qkv, residual = layer.attn_in(x, residual)
-        if cos is not None:
-            qkv = ops.rope_qkv(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim)
         o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
-                                    cfg.sliding_window, kv_start=ks)
+                                    cfg.sliding_window, kv_start=ks,
+                                    rope=(pos, cos, sin) if cos is not None else None)
         return layer.mlp(o, residual)
 
     # ------------------------------------------------------------------ generation

@@ -63,8 +63,19 @@ def rope_qkv(qkv, pos, cos, sin, Hq, Hkv, D, rope_q=True):
 
 # ----------------------------------------------------------------------------- flash attention
 class _FlashFn(torch.autograd.Function):
+    """Flash attention over fused qkv rows, optionally with RoPE applied in place first.
+
+    With ``rope`` = (pos, cos, sin) the rotation runs inside this Function: forward rotates q/k in
+    the (otherwise unused) projection output and attends; backward inverse-rotates dq/dk in the
+    gradient buffer the attention kernel just wrote. Versus a separate in-place RoPE autograd node
+    this saves the CopySlices copy and the gradient clone of the whole qkv tensor per layer."""
+
     @staticmethod
-    def forward(ctx, qkv, B, S, Hq, Hkv, D, causal, window, scale, kv_start):
+    def forward(ctx, qkv, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope=None):
+        if rope is not None:
+            # in place on the projection output: nothing else holds it (the linear saved its input)
+            rope_qkv_(qkv, rope[0], rope[1], rope[2], Hq, Hkv, D)
+        ctx.rope = rope
         q = qkv[:, : Hq * D]
         k = qkv[:, Hq * D:(Hq + Hkv) * D]
         v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D]
@@ -85,19 +96,26 @@ class _FlashFn(torch.autograd.Function):
         native().attn_bwd(q, k, v, o, do, lse, dqkv[:, : Hq * D], dqkv[:, Hq * D:(Hq + Hkv) * D],
                           dqkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D], B, S, Hq, Hkv, D, causal, window, scale,
                           kv_start if has_start else None)
-        return dqkv, None, None, None, None, None, None, None, None, None
+        if ctx.rope is not None:
+            pos, cos, sin = ctx.rope
+            rope_qkv_(dqkv, pos, cos, sin, Hq, Hkv, D, sign=-1.0)
+        return dqkv, None, None, None, None, None, None, None, None, None, None
 
 
-def flash_attention_qkv(qkv, B, S, Hq, Hkv, D, causal=True, window=0, scale=None, kv_start=None):
-    """Self-attention over fused qkv rows [B*S, (Hq+2Hkv)*D] -> o [B*S, Hq*D]."""
+def flash_attention_qkv(qkv, B, S, Hq, Hkv, D, causal=True, window=0, scale=None, kv_start=None, rope=None):
+    """Self-attention over fused qkv rows [B*S, (Hq+2Hkv)*D] -> o [B*S, Hq*D]. ``rope`` =
+    (pos, cos, sin) rotates q/k first (in place on ``qkv``, which must not be needed elsewhere)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if rope is not None and not (on_gpu(qkv) and torch.is_grad_enabled() and qkv.requires_grad):
+        qkv = rope_qkv(qkv, rope[0], rope[1], rope[2], Hq, Hkv, D)
+        rope = None
     if not on_gpu(qkv):
         q = qkv[:, : Hq * D]
         k = qkv[:, Hq * D:(Hq + Hkv) * D]
         v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D]
         return ref.attention(q, k, v, B, S, S, Hq, Hkv, D, causal, window, scale, kv_start)[0]
     if torch.is_grad_enabled() and qkv.requires_grad:
-        return _FlashFn.apply(qkv, B, S, Hq, Hkv, D, causal, window, scale, kv_start)
+        return _FlashFn.apply(qkv, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope)
     q = qkv[:, : Hq * D]
     k = qkv[:, Hq * D:(Hq + Hkv) * D]
     v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D]

@@ -137,12 +137,43 @@ class LoRAGroup:
         return self.merged
 
 
-def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a @ b with an fp32 result; on the GPU bf16 operands go straight to hipBLASLt with fp32
-    output (no fp32 copies of the operands)."""
-    if a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype:
-        return torch.mm(a, b, out_dtype=torch.float32)
-    return a.float() @ b.float()
+def _mm_tn_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a^T @ b in fp32 for the LoRA weight gradients: a [M, P], b [M, Q] with M = tokens (thousands)
+    and a small output (P or Q = the padded rank). As one GEMM the library tiles only the small
+    output (64-128 workgroups for [64, 4096]: a quarter of the chip); split over M into a batched
+    GEMM of ~512 tiles and summed (the [c, P, Q] partials are a few MB)."""
+    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype):
+        return a.float().t() @ b.float()
+    M, P = a.shape
+    Q = b.shape[1]
+    tiles = max(1, ((P + 63) // 64) * ((Q + 63) // 64))
+    c = 1
+    while c * tiles < 512 and M % (2 * c) == 0 and M // (2 * c) >= 256:
+        c *= 2
+    if c == 1:
+        return torch.mm(a.t(), b, out_dtype=torch.float32)
+    part = torch.bmm(a.view(c, M // c, P).transpose(1, 2), b.view(c, M // c, Q), out_dtype=torch.float32)
+    return part.sum(0)
+
+
+def _mm_splitk(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b for the LoRA rank-sized products (a [M, K] tokens x features, b [K, Rp], a view is fine):
+    a deep reduction (K up to 28672) into a narrow [M, Rp] output, which one library GEMM tiles into
+    only M/64 workgroups. Split K into a batched GEMM of ~512 tiles (fp32 partials [c, M, Rp], a
+    few MB, summed). Used for U = X A^T (forward) and dU = dY UB (backward)."""
+    M, K = a.shape
+    N = b.shape[1]
+    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype):
+        return a @ b
+    tiles = max(1, ((M + 63) // 64) * ((N + 63) // 64))
+    c = 1
+    while c * tiles < 512 and K % (2 * c) == 0 and K // (2 * c) >= 512:
+        c *= 2
+    if c == 1:
+        return a @ b
+    Kc = K // c
+    part = torch.bmm(a.unflatten(1, (c, Kc)).transpose(0, 1), b.unflatten(0, (c, Kc)), out_dtype=torch.float32)
+    return part.sum(0).to(a.dtype)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -150,7 +181,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], *lora_params):
         u = ub = None
         if lora is not None:
-            u = gemm(x2, lora.a_pad)  # [M, Rp] = X (s*A)^T
+            u = _mm_splitk(x2, lora.a_pad.t()) if x2.shape[0] > 64 else gemm(x2, lora.a_pad)  # [M, Rp] = X (sA)^T
             ub = lora.ub
         y = gemm(x2, w, u, ub, bias, act)
         ctx.act = act
@@ -177,21 +208,23 @@ class _LinearFn(torch.autograd.Function):
             dy = g.to(dy.dtype)
         needs = ctx.needs_input_grad
         dx = dw = db = None
+        du = _mm_splitk(dy, lora.ub) if lora is not None else None  # [M, Rp] (= dL/dU)
         if needs[0]:
             dx = dy @ w
+            if lora is not None:
+                # dX += dU A_pad as a separate K = Rp pass: measured cheaper than seeding dX with it and
+                # letting the big GEMM accumulate (beta = 1 slowed the big GEMM by more)
+                dx.addmm_(du, lora.a_pad)
         if needs[1]:
             dw = (dy.t() @ x2).to(w.dtype)
         if ctx.has_bias and needs[2]:
             db = dy.float().sum(0).to(bias.dtype)
         lora_grads = []
         if lora is not None:
-            du = dy @ lora.ub  # [M, Rp]  (= dL/dU)
-            if needs[0]:
-                dx.addmm_(du, lora.a_pad)  # dX += dU A_pad in the GEMM epilogue (no temporary)
             # all adapters of the projection in two GEMMs with fp32 output (bf16 in, fp32 accumulate):
             # dA_all = dU^T X [Rp, K]; dB_all = dY^T U [N, Rp] (adapter i uses its diagonal block)
-            ga_all = _mm_f32(du.t(), x2)
-            gb_all = _mm_f32(dy.t(), u)
+            ga_all = _mm_tn_f32(du, x2)
+            gb_all = _mm_tn_f32(dy, u)
             for a, b, r0, c0, s in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
                 ri, ni = a.shape[0], b.shape[0]
                 lora_grads.append((ga_all[r0:r0 + ri] * s).to(a.dtype))
@@ -243,7 +276,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
         x2.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)
         or (use_lora and any(p.requires_grad for p in lora.a + lora.b)))
     if not grad_needed:
-        u = gemm(x2, lora.a_pad) if use_lora else None
+        u = None
+        if use_lora:
+            u = _mm_splitk(x2, lora.a_pad.t()) if x2.shape[0] > 64 else gemm(x2, lora.a_pad)
         y = gemm(x2, w, u, lora.ub if use_lora else None, bias, act_id)
     else:
         params = []
