@@ -116,6 +116,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int s = 0; s < DS; ++s) qf[u][s] = *(const bf16x8*)(qp + 32 * s);
   }
+  // retire the Q loads here, once: otherwise hipcc's wait tracking loses them at the loop header
+  // and drains vmcnt(0) before the first S MFMA of EVERY tile — which also waits out the next
+  // tile's prefetch and serialises load latency with compute
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int s = 0; s < DS; ++s) asm volatile("" : "+v"(qf[u][s]));
 
   f32x4 o[2][DT];
 #pragma unroll
@@ -124,26 +131,28 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
     for (int c = 0; c < DT; ++c) o[u][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
 
-  // register prefetch of one K/V tile: 64 rows x NCH chunks each, spread over 256 threads
+  // register prefetch of one K/V tile: 64 rows x NCH chunks each, spread over 256 threads. Thread
+  // tid always owns chunk c = tid % NCH of keys tid / NCH + (256 / NCH) r. Native vector registers
+  // (an array of the HIP uint4 struct went to scratch, serialising every prefetch load)
   constexpr int CPT = 64 * NCH / 256;  // chunks per thread per tensor (4 for D=128)
-  uint4 kreg[CPT], vreg[CPT];
+  constexpr int KSTEP = 256 / NCH;     // key stride between a thread's chunks
+  const int lc = tid % NCH, lkey = tid / NCH;
+  const bf16_t* kb = a.k + (long)b * a.Sk * a.ldk + (long)hk * D + lc * 8;
+  const bf16_t* vb = a.v + (long)b * a.Sk * a.ldv + (long)hk * D + lc * 8;
+  u32x4 kreg[CPT], vreg[CPT];
   auto load_tile = [&](int kv0) {
 #pragma unroll
     for (int r = 0; r < CPT; ++r) {
-      const int e = tid + 256 * r;
-      const int key = e / NCH, c = e % NCH;
-      const int kk = min(kv0 + key, a.Sk - 1);
-      kreg[r] = *(const uint4*)(a.k + ((long)b * a.Sk + kk) * a.ldk + (long)hk * D + c * 8);
-      vreg[r] = *(const uint4*)(a.v + ((long)b * a.Sk + kk) * a.ldv + (long)hk * D + c * 8);
+      const long kk = min(kv0 + lkey + KSTEP * r, a.Sk - 1);
+      kreg[r] = *(const u32x4*)(kb + kk * a.ldk);
+      vreg[r] = *(const u32x4*)(vb + kk * a.ldv);
     }
   };
   auto store_tile = [&]() {
 #pragma unroll
     for (int r = 0; r < CPT; ++r) {
-      const int e = tid + 256 * r;
-      const int key = e / NCH, c = e % NCH;
-      *(uint4*)(Ks + k_off<D>(key, c)) = kreg[r];
-      *(uint4*)(Vs + v_off<D>(key, c)) = vreg[r];
+      *(u32x4*)(Ks + k_off<D>(lkey + KSTEP * r, lc)) = kreg[r];
+      *(u32x4*)(Vs + v_off<D>(lkey + KSTEP * r, lc)) = vreg[r];
     }
   };
 
@@ -752,21 +761,29 @@ struct AttnBwdArgs {
 
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
-  // delta[b,h,q] = sum_d dO*O ; one wave per (b,q,h) row
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // delta[b,h,q] = sum_d dO*O: LPR = D/8 lanes per (token, head) row, one 16-B load per operand
+  // per lane (a wave covers 64 / LPR rows; the former one-row-per-wave, 4-B-per-lane version ran
+  // at a third of the copy bandwidth)
+  constexpr int LPR = D / 8, RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
   const long total = (long)a.B * a.S * a.Hq;
-  if (row >= total) return;
-  const int h = row % a.Hq;
-  const long t = row / a.Hq;  // b*S + q
+  const int c = lane % LPR;
   float s = 0.f;
-  for (int d = lane * 2; d < D; d += 128) {
-    const float o0 = bf2f(a.o[t * a.ldo + (long)h * D + d]), o1 = bf2f(a.o[t * a.ldo + (long)h * D + d + 1]);
-    const float g0 = bf2f(a.dout[t * a.lddo + (long)h * D + d]), g1 = bf2f(a.dout[t * a.lddo + (long)h * D + d + 1]);
-    s += o0 * g0 + o1 * g1;
+  if (row < total) {
+    const int h = row % a.Hq;
+    const long t = row / a.Hq;  // b*S + q
+    float o8[8], g8[8];
+    unpack8(*(const uint4*)(a.o + t * a.ldo + (long)h * D + c * 8), o8);
+    unpack8(*(const uint4*)(a.dout + t * a.lddo + (long)h * D + c * 8), g8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += o8[e] * g8[e];
   }
-  s = wave_sum(s);
-  if (lane == 0) {
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (row < total && c == 0) {
+    const int h = row % a.Hq;
+    const long t = row / a.Hq;
     const long b = t / a.S, q = t % a.S;
     a.delta[(b * a.Hq + h) * a.S + q] = s;
   }
@@ -811,6 +828,10 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnBwdArgs a) {
       vf[s] = *(const bf16x8*)(a.v + ((long)b * a.S + kk) * a.ldv + (long)hk * D + 32 * s + 8 * g);
     }
   }
+  // retire these loads once, here (else hipcc re-waits vmcnt(0) for them inside the loop, which
+  // also drains the Q/dO prefetch and the dQ atomics every iteration)
+#pragma unroll
+  for (int s = 0; s < DS; ++s) asm volatile("" : "+v"(kf[s]), "+v"(vf[s]));
   f32x4 dk[DT], dvv[DT];
 #pragma unroll
   for (int c = 0; c < DT; ++c) { dk[c] = f32x4{0.f, 0.f, 0.f, 0.f}; dvv[c] = f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -821,27 +842,50 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnBwdArgs a) {
   if (a.window > 0) qend = min(qend, kb0 + 63 + a.window);
   const bool key_valid = mykey >= start && mykey < a.S;
 
-  for (int hh = 0; hh < G; ++hh) {
-    const int h = hk * G + hh;
-    for (int qt = qbeg; qt < qend; qt += 64) {
+  // (head, q-tile) iterations, flattened; the next one's Q / dO tile, lse and delta are prefetched
+  // into registers while the current one computes (staged to LDS after the loop-top barrier)
+  const int nqt = qend > qbeg ? (qend - qbeg + 63) / 64 : 0;
+  const int nit = G * nqt;
+  const int lc = tid % NCH, lrow = tid / NCH;
+  constexpr int RSTEP = 256 / NCH;
+  u32x4 qreg[CPT], oreg[CPT];
+  float lse_r = 0.f, del_r = 0.f;  // raw loads: scaled / masked only when staged (no early wait)
+  bool row_ok = false;
+  auto load_qdo = [&](int it) {
+    const int h = hk * G + it / nqt, qt = qbeg + (it % nqt) * 64;
+    const bf16_t* qb = a.q + (long)b * a.S * a.ldq + (long)h * D + lc * 8;
+    const bf16_t* ob = a.dout + (long)b * a.S * a.lddo + (long)h * D + lc * 8;
+#pragma unroll
+    for (int r = 0; r < CPT; ++r) {
+      const long qq = min(qt + lrow + RSTEP * r, a.S - 1);
+      qreg[r] = *(const u32x4*)(qb + qq * a.ldq);
+      oreg[r] = *(const u32x4*)(ob + qq * a.lddo);
+    }
+    if (tid < 64) {
+      const int qq = qt + tid;
+      row_ok = qq < a.S;
+      const long li = ((long)b * a.Hq + h) * a.S + min(qq, a.S - 1);
+      lse_r = a.lse[li];
+      del_r = a.delta[li];
+    }
+  };
+  if (nit > 0) load_qdo(0);
+
+  for (int it = 0; it < nit; ++it) {
+    const int h = hk * G + it / nqt, qt = qbeg + (it % nqt) * 64;
+    {
       __syncthreads();  // previous users of Q/dO/dS tiles are done
-      // stage Q and dO tile (64 rows) + lse/delta
 #pragma unroll
       for (int r = 0; r < CPT; ++r) {
-        const int e = tid + 256 * r;
-        const int row = e / NCH, c = e % NCH;
-        const int qq = min(qt + row, a.S - 1);
-        *(uint4*)(Qs + k_off<D>(row, c)) = *(const uint4*)(a.q + ((long)b * a.S + qq) * a.ldq + (long)h * D + c * 8);
-        *(uint4*)(Os + k_off<D>(row, c)) =
-            *(const uint4*)(a.dout + ((long)b * a.S + qq) * a.lddo + (long)h * D + c * 8);
+        *(u32x4*)(Qs + k_off<D>(lrow + RSTEP * r, lc)) = qreg[r];
+        *(u32x4*)(Os + k_off<D>(lrow + RSTEP * r, lc)) = oreg[r];
       }
       if (tid < 64) {
-        const int qq = qt + tid;
-        const bool ok = qq < a.S;
-        lse_s[tid] = ok ? a.lse[((long)b * a.Hq + h) * a.S + qq] * 1.4426950408889634f : INFINITY;
-        del_s[tid] = ok ? a.delta[((long)b * a.Hq + h) * a.S + qq] : 0.f;
+        lse_s[tid] = row_ok ? lse_r * 1.4426950408889634f : INFINITY;
+        del_s[tid] = row_ok ? del_r : 0.f;
       }
       __syncthreads();
+      if (it + 1 < nit) load_qdo(it + 1);
 
       // S[q][key] and dP[q][key] for 4 q-subtiles (key on lane)
       f32x4 sp[4], dp[4];
@@ -1049,7 +1093,8 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
   if (B == 0 || S == 0) return 0;
   RT_HIP_CHECK(hipMemsetAsync(dq_f32, 0, (size_t)B * S * Hq * D * sizeof(float), stream));
   const long rows = (long)B * S * Hq;
-  dim3 pgrid((unsigned)((rows + 3) / 4)), grid((S + 63) / 64, Hkv, B);
+  const long rows_per_block = 4L * (64 / (D / 8));
+  dim3 pgrid((unsigned)((rows + rows_per_block - 1) / rows_per_block)), grid((S + 63) / 64, Hkv, B);
   switch (D) {
     case 64:
       hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, pgrid, dim3(256), 0, stream, a);
