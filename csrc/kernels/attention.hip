@@ -530,9 +530,12 @@ __device__ __forceinline__ void consume_chunk(KVChunk<D, NK>& c, int c0, int p1,
                                               float scale_log2) {
   constexpr int LPK = D / 8, KPW = 64 / LPK;
   if (has_new) {
+    // compare the CLAMPED index load_chunk read: lanes past p1 re-read slot p1 - 1, which in a
+    // decode step is s_new itself — a slot this very launch is still writing (stale or
+    // uninitialised cache memory; masked, but 0 * NaN would poison the PV sum)
 #pragma unroll
     for (int i = 0; i < NK; ++i)
-      if (c0 + (i * 4 + wid) * KPW + sub == s_new) { c.k[i] = kp; c.v[i] = vp; }
+      if (min(c0 + (i * 4 + wid) * KPW + sub, p1 - 1) == s_new) { c.k[i] = kp; c.v[i] = vp; }
   }
   float sc[G][NK];
 #pragma unroll

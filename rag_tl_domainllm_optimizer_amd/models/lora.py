@@ -81,7 +81,7 @@ def _group_out(cfg, group: str) -> int:
             "down": cfg.hidden_size, "fc1": cfg.intermediate_size, "fc2": cfg.hidden_size}[group]
 
 
-def attach_lora(model, r=16, alpha=32.0, targets=None, dropout=0.0, seed=0):
+def attach_lora(model, r=16, alpha=32.0, targets=None, dropout=0.0, seed=0, ext_layout=None):
     cfg = model.cfg
     gm = group_map(cfg)
     if targets is None or targets == "all":
@@ -91,6 +91,8 @@ def attach_lora(model, r=16, alpha=32.0, targets=None, dropout=0.0, seed=0):
         raise NotImplementedError("lora_dropout > 0 is not supported by the fused LoRA GEMM path")
     lcfg = LoraConfig(r=r, lora_alpha=alpha, lora_dropout=dropout, target_modules=list(targets),
                       base_model_name_or_path=cfg.name)
+    if ext_layout is None:
+        ext_layout = os.environ.get("RAGTL_LORA_EXT", "1") == "1"
     g = torch.Generator(device="cpu").manual_seed(seed)
     dev = model.embed.device
     for layer in model.layers:
@@ -117,6 +119,10 @@ def attach_lora(model, r=16, alpha=32.0, targets=None, dropout=0.0, seed=0):
                 c0s.append(row0)
                 scales.append(lcfg.scaling)
             layer.lora[grp] = ops.LoRAGroup(projs, a_list, b_list, c0s, scales, _group_out(cfg, grp))
+            # GPU: store the frozen base weight as [W | UB] so the token-parallel LoRA forward is
+            # one plain library GEMM (ops.linear, "Extended-weight layout")
+            if ext_layout:
+                layer.lora[grp].attach_ext(_group_weight(layer, cfg, grp))
     model.lora_config = lcfg
     model.refresh_lora()
     return lcfg

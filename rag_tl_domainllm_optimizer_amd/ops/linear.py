@@ -1,9 +1,16 @@
 """Linear projections: frozen/trainable base weight + fused LoRA adapters + bias/activation.
 
-GPU forward is one MFMA GEMM (``_C.gemm``) in which the LoRA term rides on the same accumulators
-as extra K-steps:  ``Y = act(X W^T + U UB^T + b)`` with ``U = X A_pad^T`` (A_pad = scaling * A,
-zero-padded to a multiple of 64 rows) computed by a small GEMM first. Several adapters on one
-fused projection (q|k|v, gate|up) share one padded rank dimension, with UB block-diagonal.
+GPU forward is one MFMA GEMM in which the LoRA term rides on the same accumulators as extra
+K-steps:  ``Y = act(X W^T + U UB^T + b)`` with ``U = X A_pad^T`` (A_pad = scaling * A, zero-padded
+to a multiple of 64 rows) computed by a small GEMM first. Several adapters on one fused projection
+(q|k|v, gate|up) share one padded rank dimension, with UB block-diagonal.
+
+Extended-weight layout (``LoRAGroup.attach_ext``): a frozen base weight that carries adapters is
+stored ONCE as ``ext = [W | UB]`` ([N, K + Rp], the parameter becomes the strided view
+``ext[:, :K]`` and ``UB`` the view ``ext[:, K:]``), so the token-parallel (M > 64) LoRA forward is
+ONE plain GEMM ``[X | U] @ ext^T`` on hipBLASLt — measured 1.2-1.5 PF/s on the PPO-update shapes
+against 0.7-1.05 PF/s for the hand-written fused kernel (tools/update_gemm_probe.py,
+profiles/update_gemm_probe.log). Decode / skinny shapes keep the hand-written kernels.
 
 Backward (training): dX = dY W + dU A_pad, dA = s dU^T X, dB = dY^T U, dW = dY^T X (full FT) are
 plain library GEMMs (torch.matmul -> hipBLASLt); only the forward carries fused epilogues.
@@ -94,6 +101,8 @@ class LoRAGroup:
     use_merged: bool = False
     merged: Optional[torch.Tensor] = None
     merged_dirty: bool = True
+    # [W | UB] storage of the base weight (attach_ext); None = W stored on its own
+    ext: Optional[torch.Tensor] = None
 
     @property
     def rank_total(self) -> int:
@@ -104,6 +113,31 @@ class LoRAGroup:
         return max(64, (self.rank_total + 63) // 64 * 64)
 
     @torch.no_grad()
+    def attach_ext(self, w: torch.nn.Parameter) -> bool:
+        """Re-home the base weight ``w`` [N, K] into ``ext = [W | UB]`` (one copy, then W's old
+        storage is released); ``w.data`` becomes the strided view ``ext[:, :K]``. GPU bf16 only."""
+        if not (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.shape[0] == self.n_out):
+            return False
+        N, K = w.shape
+        rp = self.rp
+        if self.ext is not None and self.ext.shape == (N, K + rp) and self.ext_linked(w):
+            return True
+        ext = torch.empty(N, K + rp, dtype=w.dtype, device=w.device)
+        ext[:, :K].copy_(w.data)
+        ext[:, K:].zero_()
+        w.data = ext[:, :K]
+        self.ext = ext
+        self.a_pad = None  # rebuilt by refresh() with ub as a view of ext
+        self.refresh(dtype=w.dtype)
+        return True
+
+    def ext_linked(self, w: torch.Tensor) -> bool:
+        """True if ``w`` still is the W-view of ``ext`` (something may have replaced w.data)."""
+        e = self.ext
+        return (e is not None and w.data_ptr() == e.data_ptr() and w.shape[0] == e.shape[0]
+                and w.stride(0) == e.stride(0) and w.device == e.device)
+
+    @torch.no_grad()
     def refresh(self, dtype=torch.bfloat16):
         """Rebuild the padded bf16 images from the fp32 parameters (after each optimizer step)."""
         K = self.a[0].shape[1]
@@ -111,7 +145,11 @@ class LoRAGroup:
         rp = self.rp
         if self.a_pad is None or self.a_pad.shape != (rp, K) or self.a_pad.device != dev:
             self.a_pad = torch.zeros(rp, K, dtype=dtype, device=dev)
-            self.ub = torch.zeros(self.n_out, rp, dtype=dtype, device=dev)
+            if self.ext is not None and self.ext.device == dev and self.ext.shape[1] - rp > 0:
+                self.ub = self.ext[:, self.ext.shape[1] - rp:]
+                self.ub.zero_()
+            else:
+                self.ub = torch.zeros(self.n_out, rp, dtype=dtype, device=dev)
         self.r0 = []
         r = 0
         for a, b, c0, s in zip(self.a, self.b, self.col0, self.scale):
@@ -124,15 +162,21 @@ class LoRAGroup:
 
     @torch.no_grad()
     def merged_weight(self, w: torch.Tensor, rows_per_chunk: int = 4096) -> torch.Tensor:
-        """W + UB A_pad (fp32 accumulate, bf16 result), updated IN PLACE so captured graphs that
-        read it stay valid across adapter updates."""
+        """W + UB A_pad (fp32 accumulate, one bf16 rounding), updated IN PLACE so captured graphs
+        that read it stay valid across adapter updates. On the GPU: copy W, then one bf16 GEMM with
+        beta = 1 (4 B of traffic per weight element instead of the 20 B of an fp32 round trip)."""
         if self.merged is None or self.merged.shape != w.shape or self.merged.device != w.device:
-            self.merged = torch.empty_like(w)
+            self.merged = torch.empty(w.shape, dtype=w.dtype, device=w.device)
             self.merged_dirty = True
         if self.merged_dirty:
-            for r0 in range(0, w.shape[0], rows_per_chunk):
-                r1 = min(w.shape[0], r0 + rows_per_chunk)
-                self.merged[r0:r1].copy_(torch.addmm(w[r0:r1].float(), self.ub[r0:r1].float(), self.a_pad.float()))
+            if on_gpu(w) and w.dtype == torch.bfloat16:
+                self.merged.copy_(w)
+                self.merged.addmm_(self.ub, self.a_pad)
+            else:
+                for r0 in range(0, w.shape[0], rows_per_chunk):
+                    r1 = min(w.shape[0], r0 + rows_per_chunk)
+                    self.merged[r0:r1].copy_(torch.addmm(w[r0:r1].float(), self.ub[r0:r1].float(),
+                                                         self.a_pad.float()))
             self.merged_dirty = False
         return self.merged
 
@@ -176,14 +220,36 @@ def _mm_splitk(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return part.sum(0).to(a.dtype)
 
 
+EXT_MIN_M = 65  # token-parallel shapes take the [X | U] @ [W | UB]^T library GEMM
+
+
+def _use_ext(x2, w, bias, act, lora) -> bool:
+    return (lora is not None and lora.ext is not None and bias is None and act == 0 and on_gpu(x2)
+            and x2.shape[0] >= EXT_MIN_M and lora.ext_linked(w))
+
+
+def _ext_forward(x2: torch.Tensor, lora: LoRAGroup):
+    """y = [X | U] @ ext^T with U = X A_pad^T written next to X: returns (y, x view, u view)."""
+    M, K = x2.shape
+    rp = lora.ext.shape[1] - K
+    xe = torch.empty(M, K + rp, dtype=x2.dtype, device=x2.device)
+    xv, uv = xe[:, :K], xe[:, K:]
+    xv.copy_(x2)
+    uv.copy_(_mm_splitk(x2, lora.a_pad.t()))
+    return torch.matmul(xe, lora.ext.t()), xv, uv
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], *lora_params):
         u = ub = None
-        if lora is not None:
-            u = _mm_splitk(x2, lora.a_pad.t()) if x2.shape[0] > 64 else gemm(x2, lora.a_pad)  # [M, Rp] = X (sA)^T
-            ub = lora.ub
-        y = gemm(x2, w, u, ub, bias, act)
+        if _use_ext(x2, w, bias, act, lora):
+            y, x2, u = _ext_forward(x2, lora)
+        else:
+            if lora is not None:
+                u = _mm_splitk(x2, lora.a_pad.t()) if x2.shape[0] > 64 else gemm(x2, lora.a_pad)  # [M, Rp] = X (sA)^T
+                ub = lora.ub
+            y = gemm(x2, w, u, ub, bias, act)
         ctx.act = act
         ctx.lora = lora
         ctx.has_bias = bias is not None
@@ -276,6 +342,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
         x2.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)
         or (use_lora and any(p.requires_grad for p in lora.a + lora.b)))
     if not grad_needed:
+        if use_lora and _use_ext(x2, w, bias, act_id, lora):
+            y = _ext_forward(x2, lora)[0]
+            return y.reshape(*shp[:-1], w.shape[0])
         u = None
         if use_lora:
             u = _mm_splitk(x2, lora.a_pad.t()) if x2.shape[0] > 64 else gemm(x2, lora.a_pad)

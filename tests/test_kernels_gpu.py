@@ -62,17 +62,30 @@ def test_gemm_asymmetric_identity():
     assert torch.equal(out.float(), w.t().float())
 
 
-def test_linear_lora_autograd():
+@pytest.mark.parametrize("ext", [False, True])
+@pytest.mark.parametrize("M", [96, 40])
+def test_linear_lora_autograd(ext, M):
+    """Fused K-extension kernel and the [X | U] @ [W | UB]^T extended-weight library path."""
     torch.manual_seed(1)
-    M, K, N, r = 96, 256, 192, 8
+    K, N, r = 256, 192, 8
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    w = (torch.randn(N, K, device=DEV) / 16).to(torch.bfloat16)
+    w = torch.nn.Parameter((torch.randn(N, K, device=DEV) / 16).to(torch.bfloat16), requires_grad=False)
     a1 = torch.nn.Parameter(torch.randn(r, K, device=DEV) * 0.05)
     b1 = torch.nn.Parameter(torch.randn(N // 2, r, device=DEV) * 0.05)
     a2 = torch.nn.Parameter(torch.randn(r, K, device=DEV) * 0.05)
     b2 = torch.nn.Parameter(torch.randn(N // 2, r, device=DEV) * 0.05)
     grp = ops.LoRAGroup(["q", "v"], [a1, a2], [b1, b2], [0, N // 2], [2.0, 2.0], N)
+    if ext:
+        w0 = w.detach().clone()
+        assert grp.attach_ext(w)
+        assert grp.ext_linked(w) and w.stride(0) == K + grp.rp and torch.equal(w, w0)
+        grp.refresh()
+        assert grp.ub.data_ptr() == grp.ext[:, K:].data_ptr()
     y = ops.linear(x, w, lora=grp)
+    with torch.no_grad():  # merged inference weight (W + UB A_pad, bf16 GEMM with beta = 1)
+        wm = grp.merged_weight(w).float()
+        wr = w.float() + torch.cat([2.0 * b1 @ a1, 2.0 * b2 @ a2], 0)
+        _close(wm, wr, rtol=1e-2, atol=1e-2)
     g = torch.randn_like(y)
     (y.float() * g.float()).sum().backward()
     # reference
@@ -430,8 +443,11 @@ def test_gemm_256_identity():
 @pytest.mark.parametrize("B,Hq,Hkv,D,Smax,rot,window", [(1, 32, 8, 128, 456, True, 0), (64, 32, 8, 128, 456, True, 0),
                                                         (3, 8, 8, 64, 200, False, 0), (5, 8, 2, 32, 300, True, 64),
                                                         (2, 16, 2, 128, 64, True, 0)])
-def test_decode_step_fused(B, Hq, Hkv, D, Smax, rot, window):
-    """Fused RoPE + append + attention + in-launch combine == rope_qkv_ + decode_attention."""
+@pytest.mark.parametrize("poison", [False, True])
+def test_decode_step_fused(B, Hq, Hkv, D, Smax, rot, window, poison):
+    """Fused RoPE + append + attention + in-launch combine == rope_qkv_ + decode_attention.
+    ``poison``: the slot being appended and every slot after it hold NaN before the launch (a
+    fresh torch.empty cache): masked lanes that re-read the last slot must not see them (0 * NaN)."""
     torch.manual_seed(B + D)
     W = (Hq + 2 * Hkv) * D
     kc = torch.randn(B, Hkv, Smax, D, device=DEV, dtype=torch.bfloat16)
@@ -439,6 +455,10 @@ def test_decode_step_fused(B, Hq, Hkv, D, Smax, rot, window):
     kv_start = torch.randint(0, 8, (B,), device=DEV, dtype=torch.int32)
     slot = torch.randint(20, Smax - 1, (B,), device=DEV, dtype=torch.int32)
     attn_len = slot + 1
+    if poison:
+        tail = torch.arange(Smax, device=DEV)[None, None, :, None] >= slot.long()[:, None, None, None]
+        kc.masked_fill_(tail, float("nan"))
+        vc.masked_fill_(tail, float("nan"))
     pos = (slot - kv_start).to(torch.int32)
     cos, sin = ref.rope_tables(D, 4096, 10000.0, DEV) if rot else (None, None)
     ws = ops.decode_workspace(B, Hq, Hkv, D, Smax, DEV)
@@ -449,7 +469,9 @@ def test_decode_step_fused(B, Hq, Hkv, D, Smax, rot, window):
                                         workspace=ws)
         q_ref = ops.rope_qkv_(qkv.clone(), pos, cos, sin, Hq, Hkv, D, S=1, k_cache=kc2, v_cache=vc2, slot_base=slot)
         o_ref = ref.decode_attention(q_ref, kc2, vc2, attn_len, Hq, kv_start, window, 1.0 / math.sqrt(D))
-        assert torch.equal(kc, kc2) and torch.equal(vc, vc2), "cache append differs"
+        assert torch.equal(kc.nan_to_num(), kc2.nan_to_num()) and torch.equal(vc.nan_to_num(), vc2.nan_to_num()), \
+            "cache append differs"
+        assert torch.isfinite(out).all()
         _close(out, o_ref)
     assert int(ws.tickets.abs().sum()) == 0
 
