@@ -120,9 +120,13 @@ class LoRAGroup:
             return False
         N, K = w.shape
         rp = self.rp
-        if self.ext is not None and self.ext.shape == (N, K + rp) and self.ext_linked(w):
+        # deep K (down_proj, K = 14336): pad so K + Rp is a multiple of 256 — hipBLASLt runs K = 14400
+        # 1.65x slower than K = 14336 or 14592 (profiles/lora_fwd_probe.log); shallow K keeps Rp = 64
+        # (K = 4160 is within 0-6 % of the adapter-free GEMM)
+        rp_ext = rp if K < 8192 or K % 256 else (rp + 255) // 256 * 256
+        if self.ext is not None and self.ext.shape == (N, K + rp_ext) and self.ext_linked(w):
             return True
-        ext = torch.empty(N, K + rp, dtype=w.dtype, device=w.device)
+        ext = torch.empty(N, K + rp_ext, dtype=w.dtype, device=w.device)
         ext[:, :K].copy_(w.data)
         ext[:, K:].zero_()
         w.data = ext[:, :K]
@@ -145,9 +149,9 @@ class LoRAGroup:
         rp = self.rp
         if self.a_pad is None or self.a_pad.shape != (rp, K) or self.a_pad.device != dev:
             self.a_pad = torch.zeros(rp, K, dtype=dtype, device=dev)
-            if self.ext is not None and self.ext.device == dev and self.ext.shape[1] - rp > 0:
-                self.ub = self.ext[:, self.ext.shape[1] - rp:]
-                self.ub.zero_()
+            if self.ext is not None and self.ext.device == dev and self.ext.shape[1] - K >= rp:
+                self.ub = self.ext[:, K:K + rp]
+                self.ext[:, K:].zero_()
             else:
                 self.ub = torch.zeros(self.n_out, rp, dtype=dtype, device=dev)
         self.r0 = []
@@ -231,12 +235,32 @@ def _use_ext(x2, w, bias, act, lora) -> bool:
 def _ext_forward(x2: torch.Tensor, lora: LoRAGroup):
     """y = [X | U] @ ext^T with U = X A_pad^T written next to X: returns (y, x view, u view)."""
     M, K = x2.shape
-    rp = lora.ext.shape[1] - K
-    xe = torch.empty(M, K + rp, dtype=x2.dtype, device=x2.device)
-    xv, uv = xe[:, :K], xe[:, K:]
+    rp = lora.a_pad.shape[0]
+    xe = torch.empty(M, lora.ext.shape[1], dtype=x2.dtype, device=x2.device)
+    xv, uv = xe[:, :K], xe[:, K:K + rp]
+    if xe.shape[1] > K + rp:
+        xe[:, K + rp:].zero_()
     xv.copy_(x2)
     uv.copy_(_mm_splitk(x2, lora.a_pad.t()))
     return torch.matmul(xe, lora.ext.t()), xv, uv
+
+
+def _mm_nn_deep(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a [M, K] @ b [K, N] for a deep reduction into a narrow output (dX of gate_up: K = 28672 into
+    N = 4096): one GEMM tiles only ceil(M/256) x 16 = 304 tiles at M = 4800 (1.2 waves on 256 CUs);
+    split K four ways into a batched GEMM with fp32 partials, summed: 1448 -> 1116 us at M = 4800,
+    1758 -> 1432 us at M = 7168 (profiles/splitk_probe.log). Shallow reductions lose with the split
+    (dX of qkv / o), so only K >= 16384 takes it."""
+    M, K = a.shape
+    N = b.shape[1]
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and K >= 16384 and K % 4 == 0 and tiles < 1024
+            and b.stride(1) == 1):
+        return a @ b
+    c = 4
+    kc = K // c
+    part = torch.bmm(a.unflatten(1, (c, kc)).transpose(0, 1), b.unflatten(0, (c, kc)), out_dtype=torch.float32)
+    return part.sum(0).to(a.dtype)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -276,7 +300,7 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         du = _mm_splitk(dy, lora.ub) if lora is not None else None  # [M, Rp] (= dL/dU)
         if needs[0]:
-            dx = dy @ w
+            dx = _mm_nn_deep(dy, w) if on_gpu(dy) else dy @ w
             if lora is not None:
                 # dX += dU A_pad as a separate K = Rp pass: measured cheaper than seeding dX with it and
                 # letting the big GEMM accumulate (beta = 1 slowed the big GEMM by more)

@@ -100,6 +100,36 @@ def test_linear_lora_autograd(ext, M):
         _close(p.grad, pr.grad, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(96, 16384, 256), (300, 512, 8192)])
+def test_linear_lora_ext_deep(M, N, K):
+    """Deep shapes of the extended-weight path: K >= 8192 pads [W | UB] to a multiple of 256
+    columns; a >= 16384-deep dX reduction takes the 4-way split-K batched GEMM."""
+    from rag_tl_domainllm_optimizer_amd.ops.linear import _mm_nn_deep
+
+    torch.manual_seed(2)
+    r = 16
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = torch.nn.Parameter((torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16), requires_grad=False)
+    a = torch.nn.Parameter(torch.randn(r, K, device=DEV) / math.sqrt(K))
+    b = torch.nn.Parameter(torch.randn(N, r, device=DEV) * 0.05)
+    grp = ops.LoRAGroup(["x"], [a], [b], [0], [2.0], N)
+    assert grp.attach_ext(w)
+    assert (w.stride(0) - K) >= grp.rp and (K < 8192 or w.stride(0) % 256 == 0)
+    y = ops.linear(x, w, lora=grp)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    ar, br = a.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    yr = xr @ w.float().t() + 2.0 * (xr @ ar.t()) @ br.t()
+    (yr * g.float()).sum().backward()
+    _close(y, yr)
+    _close(x.grad, xr.grad)
+    _close(a.grad, ar.grad, rtol=3e-2, atol=3e-2)
+    _close(b.grad, br.grad, rtol=3e-2, atol=3e-2)
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    _close(_mm_nn_deep(dy, w), dy.float() @ w.float())
+
+
 @pytest.mark.parametrize("H", [384, 768, 4096, 5120])
 @pytest.mark.parametrize("layernorm", [False, True])
 def test_norm(H, layernorm):
