@@ -58,6 +58,8 @@ int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*
 int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const void*, const long*, int, float*, long*,
                 hipStream_t);
 int rt_gae(const float*, const float*, const float*, int, int, float, float, float*, float*, hipStream_t);
+int rt_ppo_loss(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
+                const float*, long, float, float, float, float, float*, float*, float*, float*, hipStream_t);
 int rt_decode_update(const long*, long*, int, float*, const float*, float*, const float*, uint8_t*, int*, int*, long*,
                      int*, int64_t*, int64_t*, int, const long*, int, long, hipStream_t);
 }
@@ -527,6 +529,29 @@ std::vector<Tensor> gae(const Tensor& rewards, const Tensor& values, const Tenso
   return {adv, ret};
 }
 
+// fused token-level PPO objective: returns {stats[6], dlp, dv, dent} (see rl.hip)
+std::vector<Tensor> ppo_loss(const Tensor& lp, const Tensor& old, const Tensor& adv, const Tensor& v,
+                             const Tensor& ret, const optional<Tensor>& vold, const Tensor& ent, const Tensor& mask,
+                             double eps, double c_v, double c_e, double vclip) {
+  for (const Tensor* t : {&lp, &old, &adv, &v, &ret, &ent, &mask}) {
+    CHECK_CUDA(*t); CHECK_F32(*t);
+    TORCH_CHECK(t->is_contiguous() && t->numel() == lp.numel(), "ppo_loss: operands must be contiguous, same size");
+  }
+  if (vclip > 0) {
+    TORCH_CHECK(vold.has_value() && vold->defined() && vold->numel() == lp.numel() && vold->is_contiguous());
+    CHECK_F32(*vold);
+  }
+  auto stats = at::empty({6}, lp.options());
+  auto dlp = at::empty_like(lp), dv = at::empty_like(lp), dent = at::empty_like(lp);
+  check_rc(rt_ppo_loss(lp.data_ptr<float>(), old.data_ptr<float>(), adv.data_ptr<float>(), v.data_ptr<float>(),
+                       ret.data_ptr<float>(), vclip > 0 ? vold->data_ptr<float>() : nullptr, ent.data_ptr<float>(),
+                       mask.data_ptr<float>(), lp.numel(), (float)eps, (float)c_v, (float)c_e, (float)vclip,
+                       stats.data_ptr<float>(), dlp.data_ptr<float>(), dv.data_ptr<float>(), dent.data_ptr<float>(),
+                       cur_stream()),
+           "ppo_loss");
+  return {stats, dlp, dv, dent};
+}
+
 void decode_update(const Tensor& tok, Tensor out_tokens, const optional<Tensor>& out_logp,
                    const optional<Tensor>& logp, const optional<Tensor>& out_values, const optional<Tensor>& values,
                    Tensor active, Tensor kv_len, Tensor pos, Tensor next_input, Tensor gen_len, Tensor step,
@@ -578,6 +603,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk", &topk);
   m.def("ivf_scan", &ivf_scan);
   m.def("gae", &gae);
+  m.def("ppo_loss", &ppo_loss, "fused token-level PPO loss: {stats[6], dlp, dv, dent}");
   m.def("decode_update", &decode_update);
   ragtl::bind_tokenizer(m);
   ragtl::bind_ivf_host(m);

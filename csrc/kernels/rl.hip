@@ -67,9 +67,113 @@ __global__ void decode_update_kernel(const long* __restrict__ tok, long* __restr
   }
 }
 
+// Token-level PPO objective over [B, T] (masked mean over the n response tokens), forward AND its
+// closed-form gradient in one single-workgroup launch (a minibatch holds a few thousand tokens):
+//   pg   = mean(-min(r A, clip(r, 1 +- eps) A)),  r = exp(lp - old)
+//   vl   = 0.5 mean((v - R)^2)   [value_clip > 0: 0.5 mean(max((v - R)^2, (vc - R)^2)),
+//                                 vc = v_old + clamp(v - v_old, +-value_clip)]
+//   ent  = mean(entropy);  loss = pg + c_v vl - c_e ent
+//   stats[0..5] = loss, pg, vl, ent, approx_kl = mean(old - lp), clipfrac = mean(|r - 1| > eps)
+//   dlp = d loss / d lp, dv = d loss / d v, dent = d loss / d entropy (per token, 0 off the mask)
+// Formulas: reference PPOTrainer.ppo_update (reinforcement_learning_optimization_after_rag.py:212-225)
+// at token level, with the SURVEY B5 true-entropy fix. Replaces ~25 tiny elementwise/reduction
+// launches (and as many in the backward) per minibatch with one.
+__global__ __launch_bounds__(1024) void ppo_loss_kernel(
+    const float* __restrict__ lp, const float* __restrict__ old, const float* __restrict__ adv,
+    const float* __restrict__ v, const float* __restrict__ ret, const float* __restrict__ vold,
+    const float* __restrict__ ent, const float* __restrict__ mask, long n_el, float eps, float c_v, float c_e,
+    float vclip, float* __restrict__ stats, float* __restrict__ dlp, float* __restrict__ dv,
+    float* __restrict__ dent) {
+  __shared__ float red[16][6];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // n, pg, vl, ent, kl, clipfrac (sums)
+  for (long i = tid; i < n_el; i += 1024) {
+    const float m = mask[i];
+    if (m == 0.f) continue;
+    const float r = __expf(lp[i] - old[i]);
+    const float A = adv[i];
+    const float rc = fminf(fmaxf(r, 1.f - eps), 1.f + eps);
+    acc[0] += m;
+    acc[1] += m * fmaxf(-r * A, -rc * A);
+    const float dvv = v[i] - ret[i];
+    float vterm = dvv * dvv;
+    if (vclip > 0.f) {
+      const float vc = vold[i] + fminf(fmaxf(v[i] - vold[i], -vclip), vclip);
+      vterm = fmaxf(vterm, (vc - ret[i]) * (vc - ret[i]));
+    }
+    acc[2] += m * vterm;
+    acc[3] += m * ent[i];
+    acc[4] += m * (old[i] - lp[i]);
+    acc[5] += m * (fabsf(r - 1.f) > eps ? 1.f : 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) red[wid][k] = acc[k];
+  __syncthreads();
+  float tot[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][k];
+    tot[k] = t;
+  }
+  const float inv_n = 1.f / fmaxf(tot[0], 1.f);
+  if (tid == 0) {
+    const float pg = tot[1] * inv_n, vl = 0.5f * tot[2] * inv_n, em = tot[3] * inv_n;
+    stats[0] = pg + c_v * vl - c_e * em;
+    stats[1] = pg;
+    stats[2] = vl;
+    stats[3] = em;
+    stats[4] = tot[4] * inv_n;
+    stats[5] = tot[5] * inv_n;
+  }
+  for (long i = tid; i < n_el; i += 1024) {
+    const float m = mask[i];
+    float g_lp = 0.f, g_v = 0.f, g_e = 0.f;
+    if (m != 0.f) {
+      const float r = __expf(lp[i] - old[i]);
+      const float A = adv[i];
+      const float rc = fminf(fmaxf(r, 1.f - eps), 1.f + eps);
+      // -min(rA, rc A): the unclipped branch is active (or tied) -> d/dlp = -A r; the clipped branch
+      // only differs when r is outside the range, where clamp has no gradient
+      g_lp = (r * A <= rc * A) ? -A * r : 0.f;
+      const float dvv = v[i] - ret[i];
+      float gv = dvv;
+      if (vclip > 0.f) {
+        const float d0 = v[i] - vold[i];
+        const float vc = vold[i] + fminf(fmaxf(d0, -vclip), vclip);
+        if ((vc - ret[i]) * (vc - ret[i]) > dvv * dvv) gv = (fabsf(d0) < vclip) ? (vc - ret[i]) : 0.f;
+      }
+      g_v = c_v * gv;  // d(0.5 x^2)/dx = x
+      g_e = -c_e;
+      g_lp *= m * inv_n;
+      g_v *= m * inv_n;
+      g_e *= m * inv_n;
+    }
+    dlp[i] = g_lp;
+    dv[i] = g_v;
+    dent[i] = g_e;
+  }
+}
+
 }  // namespace rt
 
 using namespace rt;
+
+extern "C" int rt_ppo_loss(const float* lp, const float* old, const float* adv, const float* v, const float* ret,
+                           const float* vold, const float* ent, const float* mask, long n_el, float eps, float c_v,
+                           float c_e, float vclip, float* stats, float* dlp, float* dv, float* dent,
+                           hipStream_t stream) {
+  hipLaunchKernelGGL(ppo_loss_kernel, dim3(1), dim3(1024), 0, stream, lp, old, adv, v, ret, vold, ent, mask, n_el,
+                     eps, c_v, c_e, vclip, stats, dlp, dv, dent);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int rt_gae(const float* rewards, const float* values, const float* mask, int B, int T, float gamma, float lam,
                       float* adv, float* ret, hipStream_t stream) {

@@ -227,8 +227,15 @@ def cmd_bench(cfg, args, rest):
 def cmd_launch(args, rest):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.nproc}",
            "--master-addr", "127.0.0.1", f"--master-port={args.port}", "-m", "rag_tl_domainllm_optimizer_amd", *rest]
+    # the caller's environment (NCCL_* / RCCL_* / HSA_* tuning) passes through to every rank;
+    # --env KEY=VALUE adds or overrides entries (e.g. --env NCCL_MIN_NCHANNELS=32)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for kv in args.env or []:
+        k, sep, v = kv.partition("=")
+        if not sep or not k:
+            raise SystemExit(f"launch: --env expects KEY=VALUE, got {kv!r}")
+        env[k] = v
     sys.exit(subprocess.run(cmd, env=env).returncode)
 
 
@@ -243,6 +250,7 @@ def main(argv: Optional[List[str]] = None):
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--nproc", type=int, default=1)
+    ap.add_argument("--env", action="append", default=[], help="launch: KEY=VALUE set for every rank (repeatable)")
     ap.add_argument("--resume", action="store_true", help="ppo: continue from the run's latest epoch checkpoint")
     if argv and argv[0] == "launch":
         a, rest = ap.parse_known_args(argv)

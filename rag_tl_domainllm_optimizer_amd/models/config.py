@@ -76,6 +76,11 @@ PRESETS = {
     "mistral-7b": ModelConfig(arch="mistral", vocab_size=32000, hidden_size=4096, num_layers=32, num_heads=32,
                               num_kv_heads=8, head_dim=128, intermediate_size=14336, max_position=32768,
                               norm_eps=1e-5, rope_theta=10000.0, sliding_window=4096, name="mistral-7b"),
+    # OpenChat-3.5 (README.md:25 lists OpenChat): the Mistral-7B architecture with two added
+    # chat tokens (vocab 32002), rope theta 1e4, 8k context
+    "openchat-3.5": ModelConfig(arch="mistral", vocab_size=32002, hidden_size=4096, num_layers=32, num_heads=32,
+                                num_kv_heads=8, head_dim=128, intermediate_size=14336, max_position=8192,
+                                norm_eps=1e-5, rope_theta=10000.0, sliding_window=4096, name="openchat-3.5"),
     "llama2-7b": ModelConfig(arch="llama", vocab_size=32000, hidden_size=4096, num_layers=32, num_heads=32,
                              num_kv_heads=32, head_dim=128, intermediate_size=11008, max_position=4096,
                              norm_eps=1e-5, name="llama2-7b"),
@@ -118,6 +123,8 @@ PRESETS = {
 ALIASES = {
     "mistralai/mistral-7b-v0.1": "mistral-7b",
     "mistral": "mistral-7b",
+    "openchat/openchat_3.5": "openchat-3.5",
+    "openchat": "openchat-3.5",
     "meta-llama/llama-2-7b-hf": "llama2-7b",
     "meta-llama/llama-2-13b-hf": "llama2-13b",
     "facebook/opt-125m": "opt-125m",

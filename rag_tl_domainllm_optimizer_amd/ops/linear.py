@@ -67,7 +67,9 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
             backend = SKINNY_BACKEND if M <= 16 else (MID_BACKEND if M <= 64 else PLAIN_BACKEND)
             if backend == "auto":
                 backend = "native" if w.shape[1] >= 8192 else "lib"
-            if backend == "lib":
+            # the hand-written kernels store 8-column vectors: an output width that is not a multiple
+            # of 8 (e.g. OpenChat's 32002-token vocabulary) takes the library GEMM
+            if backend == "lib" or w.shape[0] % 8:
                 return torch.matmul(x, w.t(), out=out)
         return native().gemm(x, w, u, ub, bias, act, out_f32, out)
     y = ref.gemm(x, w, u, ub, bias, act, out_f32)

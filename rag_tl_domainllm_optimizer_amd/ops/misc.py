@@ -146,6 +146,33 @@ def ivf_scan(q, probes, offsets, vecs, ids, maxlen):
 
 
 # ---------------------------------------------------------------------------------------- RL
+class _PPOLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lp, vals, ent, old, adv, ret, mask, vold, eps, c_v, c_e, vclip):
+        f = lambda t: t.detach().float().contiguous()  # noqa: E731
+        stats, dlp, dv, dent = native().ppo_loss(f(lp), f(old), f(adv), f(vals), f(ret),
+                                                 f(vold) if vold is not None else None, f(ent), f(mask),
+                                                 eps, c_v, c_e, vclip if vclip else 0.0)
+        ctx.save_for_backward(dlp, dv, dent)
+        ctx.mark_non_differentiable(stats)
+        return stats[0], stats
+
+    @staticmethod
+    def backward(ctx, g, _gstats):
+        dlp, dv, dent = ctx.saved_tensors
+        return dlp * g, dv * g, dent * g, None, None, None, None, None, None, None, None, None
+
+
+def ppo_loss(lp, vals, ent, old, adv, ret, mask, eps: float, c_v: float, c_e: float, vclip=None, vold=None):
+    """Token-level clipped PPO objective: ``(loss, stats)`` with stats = [loss,
+    policy_loss, value_loss, entropy, approx_kl, clipfrac]; one fused HIP kernel computes the loss
+    and its gradient (w.r.t. lp, vals, ent) together on the GPU."""
+    if on_gpu(lp):
+        return _PPOLossFn.apply(lp, vals, ent, old, adv, ret, mask.float(), vold, float(eps), float(c_v),
+                                float(c_e), float(vclip) if vclip else 0.0)
+    return ref.ppo_loss(lp, old, adv, vals, ret, ent, mask.float(), eps, c_v, c_e, vclip, vold)
+
+
 def gae(rewards, values, mask, gamma: float, lam: float):
     if on_gpu(rewards):
         return native().gae(rewards.float().contiguous(), values.float().contiguous(), mask.float().contiguous(),

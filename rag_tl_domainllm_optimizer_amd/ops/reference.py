@@ -238,6 +238,27 @@ def gae(rewards, values, mask, gamma, lam):
     return adv, ret
 
 
+def ppo_loss(lp, old, adv, vals, ret, ent, mask, eps, c_v, c_e, vclip=None, vold=None):
+    """Token-level PPO objective (eager oracle of the fused kernel): returns (loss, stats[6]) with
+    stats = loss, policy_loss, value_loss, entropy, approx_kl, clipfrac."""
+    m = mask.to(lp.dtype)
+    n = m.sum().clamp(min=1.0)
+    ratio = torch.exp(lp - old)
+    pg = (-torch.min(ratio * adv, torch.clamp(ratio, 1 - eps, 1 + eps) * adv) * m).sum() / n
+    if vclip is not None and vclip > 0:
+        vc = vold + torch.clamp(vals - vold, -vclip, vclip)
+        vl = 0.5 * (torch.max((vals - ret) ** 2, (vc - ret) ** 2) * m).sum() / n
+    else:
+        vl = 0.5 * (((vals - ret) ** 2) * m).sum() / n
+    em = (ent * m).sum() / n
+    loss = pg + c_v * vl - c_e * em
+    with torch.no_grad():
+        kl = ((old - lp) * m).sum() / n
+        cf = ((((ratio - 1).abs() > eps).to(lp.dtype)) * m).sum() / n
+        stats = torch.stack([loss.detach(), pg.detach(), vl.detach(), em.detach(), kl, cf])
+    return loss, stats
+
+
 def adamw_(p, g, m, v, lr, b1, b2, eps, wd, step, max_norm=0.0):
     """In-place torch.optim.AdamW semantics with global-norm clipping; returns (norm, skipped)."""
     norm = g.float().norm()

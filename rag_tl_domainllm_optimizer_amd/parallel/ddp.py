@@ -55,6 +55,7 @@ class GradSync:
         self._handles: List[Optional[object]] = [None] * len(bounds)
         self._hooks = []
         self.sync_enabled = True
+        self.wait_s = 0.0  # host time blocked in finish() (exposed all-reduce tail), reset by the caller
         if self.overlap:
             for p, bi in zip(flat.params, self.param_bucket):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
@@ -94,6 +95,9 @@ class GradSync:
         """Complete all buckets (launch the ones whose hooks did not fire) and average."""
         if not self.enabled:
             return
+        import time
+
+        t0 = time.perf_counter()
         self.flat.relink_grads()
         for bi in range(len(self.buckets)):
             if self._handles[bi] is None:
@@ -101,6 +105,7 @@ class GradSync:
         for h in self._handles:
             h.wait()
         self.flat.grad.div_(self.world)
+        self.wait_s += time.perf_counter() - t0
         self._handles = [None] * len(self.buckets)
         self._ready = [0] * len(self.buckets)
 

@@ -285,8 +285,7 @@ class PPOTrainer:
     def update(self, ro: Rollout) -> dict:
         c = self.cfg
         B = ro.resp.shape[0]
-        stats = {"policy_loss": [], "value_loss": [], "entropy_loss": [], "total_loss": [], "approx_kl": [],
-                 "clipfrac": [], "entropy": []}
+        stats = []
         inv_t = 1.0 / c.temperature
         g = torch.Generator(device="cpu").manual_seed(c.seed + self.global_step)
         with self.timer.phase("update"):
@@ -297,22 +296,11 @@ class PPOTrainer:
                     lp, ent, vals, mask = score_sequences(self.policy, ro.prompt_ids[idx], ro.start[idx],
                                                           ro.resp[idx], ro.resp_len[idx], inv_t, self.value_head,
                                                           c.gradient_checkpointing)
-                    old = ro.old_logp[idx]
-                    adv = ro.adv[idx]
-                    ratio = torch.exp(lp - old)
-                    s1 = ratio * adv
-                    s2 = torch.clamp(ratio, 1 - c.clip_range, 1 + c.clip_range) * adv
-                    pg = masked_mean(-torch.min(s1, s2), mask)
-                    ret = ro.returns[idx]
-                    if c.value_clip is not None:
-                        ov = ro.old_values[idx]
-                        vc = ov + torch.clamp(vals - ov, -c.value_clip, c.value_clip)
-                        vl = 0.5 * masked_mean(torch.max((vals - ret) ** 2, (vc - ret) ** 2), mask)
-                    else:
-                        vl = 0.5 * masked_mean((vals - ret) ** 2, mask)
-                    ent_m = masked_mean(ent, mask)
-                    ent_loss = -c.entropy_coef * ent_m
-                    loss = pg + c.value_coef * vl + ent_loss
+                    # fused token-level objective (clipped surrogate + value + entropy) and its
+                    # gradient in one kernel on the GPU (ops.ppo_loss; eager oracle on CPU)
+                    loss, st = ops.ppo_loss(lp, vals, ent, ro.old_logp[idx], ro.adv[idx], ro.returns[idx], mask,
+                                            c.clip_range, c.value_coef, c.entropy_coef, c.value_clip,
+                                            ro.old_values[idx] if c.value_clip is not None else None)
                     self.opt.zero_grad()
                     self.sync.start()
                     loss.backward()
@@ -320,16 +308,15 @@ class PPOTrainer:
                     lr = lr_at(self.opt.step_count, c.lr, c.lr_schedule, c.warmup_steps, c.total_steps)
                     self.opt.step(lr)
                     self.policy.refresh_lora()
-                    with torch.no_grad():
-                        stats["policy_loss"].append(pg.detach())
-                        stats["value_loss"].append(vl.detach())
-                        stats["entropy_loss"].append(ent_loss.detach())
-                        stats["total_loss"].append(loss.detach())
-                        stats["approx_kl"].append(masked_mean(old - lp.detach(), mask))
-                        stats["clipfrac"].append(masked_mean(((ratio.detach() - 1).abs() > c.clip_range).float(), mask))
-                        stats["entropy"].append(ent_m.detach())
-        out = {k: float(torch.stack(v).mean()) for k, v in stats.items()}
+                    stats.append(st)
+        # stats rows: [loss, policy_loss, value_loss, entropy, approx_kl, clipfrac] (one D2H copy)
+        sm = torch.stack(stats).mean(0).tolist()
+        out = {"total_loss": sm[0], "policy_loss": sm[1], "value_loss": sm[2], "entropy": sm[3],
+               "entropy_loss": -c.entropy_coef * sm[3], "approx_kl": sm[4], "clipfrac": sm[5]}
         out["grad_norm"] = float(self.opt.last_norm)
+        out["skipped_steps"] = float(self.opt.skipped)
+        out["time/allreduce_wait"] = self.sync.wait_s
+        self.sync.wait_s = 0.0
         out["lr"] = lr
         return out
 

@@ -130,3 +130,22 @@ def test_ppo_step_gpu():
     for m in (m1, m2):
         assert all(math.isfinite(v) for v in m.values() if isinstance(v, float))
     assert 8 <= m1["rollout_tokens"] <= 8 * 8  # rows stop early when the random policy samples EOS
+
+
+def test_odd_vocab_generation_gpu():
+    """A vocabulary that is not a multiple of 8 (OpenChat-3.5: 32002) generates and scores on the
+    GPU: the LM head falls back to the library GEMM, the sampler to its generic kernel."""
+    import dataclasses
+
+    from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
+    from rag_tl_domainllm_optimizer_amd.train.common import score_sequences
+
+    cfg = dataclasses.replace(PRESETS["tiny-mistral"], vocab_size=514, name="tiny-openchat")
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=4)
+    prompts = [[5, 9, 33, 41, 7, 8, 9, 513], [12, 300, 4]]
+    p = SamplingParams(max_new_tokens=6, temperature=0.7, top_k=20, seed=5)
+    out = Generator(m, 2, 64, DEV).generate(prompts, p, pad_id=0, eos_ids=[-1])
+    assert out.tokens.shape == (2, 6) and int(out.tokens.max()) < 514 and torch.isfinite(out.logprobs).all()
+    with torch.no_grad():
+        lp, _, _, _ = score_sequences(m, out.prompt_ids, out.prompt_start, out.tokens, out.lengths, 1 / 0.7)
+    torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=0.08)
