@@ -1,0 +1,66 @@
+"""Fused decode attention (RoPE + append + split-K + combine) time vs keys-per-partition PS at
+rollout shapes (Mistral-7B GQA 32/8, D = 128). hipGraph-free, back-to-back launches over 8
+distinct caches (cold-ish KV like the 32 layers of a decode step).
+
+    python tools/attn_ps_sweep.py [--B 64] [--L 330]
+"""
+import argparse
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from rag_tl_domainllm_optimizer_amd import ops  # noqa: E402
+from rag_tl_domainllm_optimizer_amd.ops import reference as ref  # noqa: E402
+from rag_tl_domainllm_optimizer_amd.ops.attention import decode_partition  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, nargs="+", default=[64, 16, 1])
+    ap.add_argument("--L", type=int, nargs="+", default=[330, 1024])
+    a = ap.parse_args()
+    dev = "cuda"
+    Hq, Hkv, D = 32, 8, 128
+    Smax = 2048
+    cos, sin = ref.rope_tables(D, 4096, 10000.0, dev)
+    for B in a.B:
+        for L in a.L:
+            nl = 8
+            kc = [torch.randn(B, Hkv, Smax, D, device=dev, dtype=torch.bfloat16) for _ in range(nl)]
+            vc = [torch.randn_like(k) for k in kc]
+            qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
+            kv_start = torch.zeros(B, device=dev, dtype=torch.int32)
+            slot = torch.full((B,), L - 1, device=dev, dtype=torch.int32)
+            attn_len = slot + 1
+            pos = slot.clone()
+            out = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
+            res = []
+            default_ps = decode_partition(B * Hkv, D, Smax)
+            for ps in (64, 128, 256, 512, 1024, 2048):
+                ws = ops.decode_workspace(B, Hq, Hkv, D, Smax, dev, PS=ps)
+
+                def run():
+                    for i in range(nl):
+                        ops.decode_step_attention(qkv, kc[i], vc[i], slot, attn_len, Hq, pos, cos, sin, kv_start,
+                                                  0, workspace=ws, out=out)
+                for _ in range(3):
+                    run()
+                torch.cuda.synchronize()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(10):
+                    run()
+                e.record()
+                torch.cuda.synchronize()
+                us = s.elapsed_time(e) / (10 * nl) * 1e3
+                gbs = B * Hkv * L * D * 2 * 2 / us / 1e3
+                res.append(f"PS{ps}={us:6.1f}us({gbs:5.0f}GB/s)")
+            print(f"B={B} L={L} default_PS={default_ps}: " + " ".join(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,45 @@
+"""One rollout-shaped generation (Mistral-7B, random init, LoRA r=16 merged) for kernel profiling:
+    rocprofv3 --kernel-trace --stats -- python tools/decode_profile.py --batch 64 --new 64
+Prints the per-step wall time; the rocprof stats give the per-kernel split of a decode step."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--prompt", type=int, default=300)
+    ap.add_argument("--new", type=int, default=64)
+    ap.add_argument("--model", default="mistral-7b")
+    ap.add_argument("--no-lora", action="store_true")
+    a = ap.parse_args()
+    from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
+    from rag_tl_domainllm_optimizer_amd.models import build_model
+
+    dev = torch.device("cuda")
+    m = build_model(a.model, device=dev, dtype=torch.bfloat16, seed=0, fast_init=True)
+    if not a.no_lora:
+        m.add_lora(16, 32.0, "all")
+    g = torch.Generator().manual_seed(0)
+    prompts = [torch.randint(5, m.cfg.vocab_size, (a.prompt - (i % 7) * 3,), generator=g).tolist()
+               for i in range(a.batch)]
+    gen = Generator(m, a.batch, a.prompt + a.new + 8, dev)
+    sp = SamplingParams(max_new_tokens=a.new, temperature=0.7, top_k=50)
+    for it in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = gen.generate_async(prompts, sp, pad_id=0, eos_ids=[-1]).result()
+        dt = time.perf_counter() - t0
+        print(f"iter {it}: total {dt * 1e3:.1f} ms prefill {out.timings['prefill_s'] * 1e3:.1f} ms decode "
+              f"{out.timings['decode_s'] * 1e3:.1f} ms = {out.timings['decode_s'] / (a.new - 1) * 1e3:.3f} ms/step",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
