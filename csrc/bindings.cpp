@@ -58,6 +58,7 @@ int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*
 int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const void*, const long*, int, float*, long*,
                 hipStream_t);
 int rt_gae(const float*, const float*, const float*, int, int, float, float, float*, float*, hipStream_t);
+void rt_attn_decode_set_nk(int nk);
 int rt_ppo_loss(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
                 const float*, long, float, float, float, float, float*, float*, float*, float*, hipStream_t);
 int rt_decode_update(const long*, long*, int, float*, const float*, float*, const float*, uint8_t*, int*, int*, long*,
@@ -602,6 +603,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_norm", &pool_norm);
   m.def("topk", &topk);
   m.def("ivf_scan", &ivf_scan);
+  m.def("attn_decode_set_nk", &rt_attn_decode_set_nk, "fused decode attention: keys per lane per chunk (0 = default 4)");
   m.def("gae", &gae);
   m.def("ppo_loss", &ppo_loss, "fused token-level PPO loss: {stats[6], dlp, dv, dent}");
   m.def("decode_update", &decode_update);

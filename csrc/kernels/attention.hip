@@ -1054,6 +1054,10 @@ extern "C" int rt_attn_decode(const void* q, long ldq, const void* kc, const voi
 // keys per chunk of the fused kernel: 4 waves x (64 / (D/8)) keys per step x NK (= 4)
 extern "C" int rt_attn_decode_fused_ps(int D, int nk) { return 4 * (64 / (D / 8)) * nk; }
 
+// keys per lane per chunk (bytes in flight per block); 0 = default 4. Tuning hook.
+static int g_dec_nk = 0;
+extern "C" void rt_attn_decode_set_nk(int nk) { g_dec_nk = nk; }
+
 extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* vc, int Smax, const int* slot,
                                     const int* attn_len, const int* kv_start, const int* pos, const float* cosT,
                                     const float* sinT, float sign, int window, float* part, unsigned* tickets, int NP,
@@ -1067,7 +1071,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -1;
-  const int nk = 4;  // keys per lane per chunk; PS must be a multiple of the chunk
+  const int nk = g_dec_nk > 0 ? g_dec_nk : 4;  // keys per lane per chunk; PS must be a multiple of the chunk
   if (PS % (4 * (64 / (D / 8)) * nk) != 0) return -1;
   dim3 grid(NP, Hkv, B), block(256);
 #define DF_CASE(DD, GG, NN)                                                                   \
@@ -1077,7 +1081,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     return 0;                                                                                 \
   }
 #define DF_G(DD, NN) DF_CASE(DD, 1, NN) DF_CASE(DD, 2, NN) DF_CASE(DD, 4, NN) DF_CASE(DD, 8, NN)
-  DF_G(128, 4) DF_G(64, 4) DF_G(32, 4)
+  DF_G(128, 4) DF_G(64, 4) DF_G(32, 4) DF_CASE(128, 4, 8) DF_CASE(128, 4, 2)
 #undef DF_G
 #undef DF_CASE
   return -1;

@@ -139,14 +139,17 @@ def decode_partition(batch_heads: int, D: int = 128, Smax: int = 4096) -> int:
     """Keys per split-K partition of the fused decode kernel. A partition is a whole number of
     key chunks (4 waves x 64/(D/8) keys x 4 keys per lane). With >= 256 (batch, kv-head) pairs the
     grid already fills the chip: one partition per pair (no cross-block combine); with fewer pairs
-    the keys are split so that ~256 workgroups run, merged in-launch by the last arriver."""
+    the keys are split so that ~256 workgroups run (at most 8 partitions of at least 2 chunks each:
+    the in-launch combine costs more than a third partition of a short cache saves), merged
+    in-launch by the last arriver. Batch 1 (MI355X, profiles/kernels_attn_fused_b1_partition_sweep.log):
+    456 keys -> 2-chunk partitions (15.4 vs 16.5 us at 1 chunk), 2048 keys -> 4 chunks (22.2 vs 34.7)."""
     chunk = 4 * (64 // (D // 8)) * 4
     nchunks = (Smax + chunk - 1) // chunk
     if batch_heads >= 256:
         return nchunks * chunk
-    want_np = max(1, -(-256 // batch_heads))
-    per = max(1, -(-nchunks // want_np))
-    return per * chunk
+    want_np = min(8, max(1, -(-256 // batch_heads)))
+    per = max(2, -(-nchunks // want_np))
+    return min(per, nchunks) * chunk
 
 
 class DecodeWorkspace(tuple):

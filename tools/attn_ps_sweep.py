@@ -22,6 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, nargs="+", default=[64, 16, 1])
     ap.add_argument("--L", type=int, nargs="+", default=[330, 1024])
+    ap.add_argument("--nk", type=int, nargs="+", default=[4], help="keys per lane per chunk (tuning hook)")
+    ap.add_argument("--ps", type=int, nargs="+", default=[64, 128, 256, 512, 1024, 2048])
     a = ap.parse_args()
     dev = "cuda"
     Hq, Hkv, D = 32, 8, 128
@@ -40,7 +42,10 @@ def main():
             out = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
             res = []
             default_ps = decode_partition(B * Hkv, D, Smax)
-            for ps in (64, 128, 256, 512, 1024, 2048):
+            for nk, ps in [(nk, ps) for nk in a.nk for ps in a.ps]:
+                if ps % (16 * nk):
+                    continue
+                ops.native().attn_decode_set_nk(nk)
                 ws = ops.decode_workspace(B, Hq, Hkv, D, Smax, dev, PS=ps)
 
                 def run():
@@ -58,7 +63,8 @@ def main():
                 torch.cuda.synchronize()
                 us = s.elapsed_time(e) / (10 * nl) * 1e3
                 gbs = B * Hkv * L * D * 2 * 2 / us / 1e3
-                res.append(f"PS{ps}={us:6.1f}us({gbs:5.0f}GB/s)")
+                res.append(f"nk{nk}/PS{ps}={us:6.1f}us({gbs:5.0f}GB/s)")
+            ops.native().attn_decode_set_nk(0)
             print(f"B={B} L={L} default_PS={default_ps}: " + " ".join(res), flush=True)
 
 
