@@ -42,6 +42,9 @@ int rt_attn_decode_fused(const void*, long, void*, void*, int, const int*, const
                          const float*, const float*, float, int, float*, unsigned*, int, int, void*, long, int, int, int,
                          int, float, hipStream_t);
 int rt_attn_decode_fused_ps(int, int);
+int rt_attn_o_fused(const void*, void*, void*, int, const int*, const int*, const int*, const int*, const float*,
+                    const float*, float, int, float*, int, int, int, int, int, float, const void*, long, const void*,
+                    void*, int, unsigned*, int*, hipStream_t);
 int rt_attn_bwd(const void*, long, const void*, long, const void*, long, const void*, long, const void*, long,
                 const float*, float*, float*, void*, long, void*, long, void*, long, const int*, int, int, int, int,
                 int, int, int, float, hipStream_t);
@@ -59,6 +62,7 @@ int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const void*,
                 hipStream_t);
 int rt_gae(const float*, const float*, const float*, int, int, float, float, float*, float*, hipStream_t);
 void rt_attn_decode_set_nk(int nk);
+void rt_attn_o_set_stamps(long long* p);
 int rt_ppo_loss(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
                 const float*, long, float, float, float, float, float*, float*, float*, float*, hipStream_t);
 int rt_decode_update(const long*, long*, int, float*, const float*, float*, const float*, uint8_t*, int*, int*, long*,
@@ -394,6 +398,42 @@ void attn_decode_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& sl
            "attn_decode_fused");
 }
 
+// batch-1 decode step of one layer: attention (RoPE + append + split-K) and o_proj + residual in
+// one launch. Returns false (nothing launched) when the shape is not supported.
+bool attn_o_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& slot, const Tensor& attn_len,
+                  const optional<Tensor>& kv_start, const optional<Tensor>& pos, const optional<Tensor>& cos,
+                  const optional<Tensor>& sin, double sign, int64_t window, double scale, int64_t Hq, Tensor part,
+                  int64_t PS, const Tensor& w, const Tensor& residual, Tensor out, Tensor sync, Tensor err) {
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_BF16(kc); CHECK_BF16(vc); CHECK_I32(slot); CHECK_I32(attn_len);
+  CHECK_F32(part); CHECK_BF16(w); CHECK_ROWS(w); CHECK_ALIGN16(w); CHECK_BF16(residual); CHECK_BF16(out);
+  CHECK_I32(sync); CHECK_I32(err);
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes(),
+              "attn_o_fused: cache layout");
+  const int64_t B = kc.size(0), Hkv = kc.size(1), Smax = kc.size(2), D = kc.size(3);
+  if (B != 1 || qkv.size(0) != 1) return false;
+  const int64_t NP = (Smax + PS - 1) / PS, G = Hq / Hkv, H = w.size(0);
+  TORCH_CHECK(G * Hkv == Hq && w.size(1) == Hq * D, "attn_o_fused: o_proj weight must be [H, Hq*D]");
+  TORCH_CHECK(qkv.is_contiguous() && qkv.size(1) >= (Hq + 2 * Hkv) * D, "attn_o_fused: qkv row");
+  TORCH_CHECK(residual.is_contiguous() && residual.numel() == H && out.is_contiguous() && out.numel() == H,
+              "attn_o_fused: residual / out must be contiguous [1, H]");
+  TORCH_CHECK(D == 128 && part.numel() >= Hkv * NP * G * 132, "attn_o_fused: partial workspace too small");
+  TORCH_CHECK(sync.numel() >= 2 && err.numel() >= 1, "attn_o_fused: sync workspace");
+  const bool rot = cos.has_value() && cos->defined();
+  if (rot) {
+    CHECK_F32(*cos); CHECK_F32(*sin); CHECK_I32(*pos);
+    TORCH_CHECK(cos->size(-1) == D / 2 && cos->is_contiguous() && sin->is_contiguous(), "attn_o_fused: tables");
+  }
+  if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
+  const int rc = rt_attn_o_fused(qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), (int)Smax, slot.data_ptr<int>(),
+                                 attn_len.data_ptr<int>(), (const int*)opt_ptr(kv_start),
+                                 rot ? pos->data_ptr<int>() : nullptr, rot ? cos->data_ptr<float>() : nullptr,
+                                 rot ? sin->data_ptr<float>() : nullptr, (float)sign, (int)window,
+                                 part.data_ptr<float>(), (int)NP, (int)PS, (int)Hq, (int)Hkv, (int)D, (float)scale,
+                                 w.data_ptr(), w.stride(0), residual.data_ptr(), out.data_ptr(), (int)H,
+                                 (unsigned*)sync.data_ptr<int>(), err.data_ptr<int>(), cur_stream());
+  return rc == 0;
+}
+
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout, const Tensor& lse,
               Tensor dq, Tensor dk, Tensor dv, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D, bool causal,
               int64_t window, double scale, const optional<Tensor>& kv_start) {
@@ -604,6 +644,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk", &topk);
   m.def("ivf_scan", &ivf_scan);
   m.def("attn_decode_set_nk", &rt_attn_decode_set_nk, "fused decode attention: keys per lane per chunk (0 = default 4)");
+  m.def("attn_o_set_stamps", [](optional<Tensor> t) {
+    rt_attn_o_set_stamps(t.has_value() && t->defined() ? (long long*)t->data_ptr() : nullptr);
+  }, "debug: int64 [NB, 8] buffer receiving per-block s_memrealtime phase stamps of attn_o_fused (None = off)");
+  m.def("attn_o_fused", &attn_o_fused, "batch-1 decode: attention + o_proj + residual in one launch (false = unsupported)");
   m.def("gae", &gae);
   m.def("ppo_loss", &ppo_loss, "fused token-level PPO loss: {stats[6], dlp, dv, dent}");
   m.def("decode_update", &decode_update);

@@ -28,6 +28,8 @@
 
 namespace rt {
 
+typedef __attribute__((address_space(3))) void lds_void;  // global_load_lds destination
+
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -742,6 +744,277 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Batch-1 decode: attention + o_proj + residual in ONE launch (RAG answer latency path)
+// ---------------------------------------------------------------------------------------------
+// At batch 1 the attention of a layer is latency-bound (~1.8 MB of K/V over 8 kv-heads) and the
+// o_proj GEMV that follows is a 33.5 MB weight stream whose own launch ramp and split-K hand-off
+// cost about as much as its bytes. Here the two share a launch and overlap:
+//   * every block owns AO_ROWS output rows of o_proj and DMAs its [AO_ROWS x Hq*D] weight slice
+//     into LDS (global_load_lds, 128 KiB) while the attention runs;
+//   * blocks 0 .. Hkv*NP-1 (the first dispatched) are also attention producers: each computes the
+//     (m, l, sum p*v) partial of one key partition of one kv-head (RoPE + cache append as in
+//     attn_decode_fused_kernel), publishes it with write-through stores and bumps sync[0];
+//   * every block waits for sync[0] == Hkv*NP (bounded spin; a give-up sets *err), merges the
+//     partials of its 16 elements of the attention vector per thread, and dots them with its LDS
+//     weight rows; row sums + residual -> the new residual stream (bf16).
+// Producers are the lowest block ids and wait on nothing before publishing, so the grid cannot
+// deadlock even when not every block is resident. The last block to finish re-arms sync[].
+constexpr int AO_ROWS = 16;  // o_proj rows per block: 16 x 4096 bf16 = 128 KiB of LDS
+constexpr int AO_K = 4096;   // Hq * D of the supported models (Llama-2-7B / Mistral-7B shapes)
+constexpr int AO_PSTR = 128 + 4;  // floats per (partition, q-head) partial record: o[D] | m | l | pad
+
+struct AttnOArgs {
+  DecodeFusedArgs at;          // attention of the single sequence; at.part = [Hkv, NP, G, D + 2]
+  const bf16_t* w; long ldw;   // o_proj weight [H, Hq * D] (row stride ldw)
+  const bf16_t* res;           // residual row [H]
+  bf16_t* out;                 // new residual row [H] = o_proj(attn) + res
+  int H;
+  unsigned* sync;              // [2] producers published / blocks done; zero between launches
+  int* err;                    // set to 1 if a block gave up waiting
+  long long* stamps;           // debug: [NB][8] s_memrealtime stamps per phase, or null
+};
+
+template <int D, int G, int NK>
+__global__ __launch_bounds__(256) void attn_o_fused_kernel(AttnOArgs args) {
+  __shared__ __attribute__((aligned(16))) char wsl[AO_ROWS * AO_K * 2];  // o_proj weight slice
+  __shared__ float red[4 * G * D];
+  __shared__ float wst[4][G][2];
+  __shared__ float rsum[4][AO_ROWS];
+  constexpr int LPK = D / 8, KPW = 64 / LPK, CH = 4 * KPW * NK;
+  constexpr int EPT = AO_K / 256;  // attention-vector elements per thread in the GEMV (16)
+  const DecodeFusedArgs& a = args.at;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int bid = blockIdx.x, NB = gridDim.x;
+  const int P = a.Hkv * a.NP;
+  const int r0 = bid * AO_ROWS;
+
+  auto issue_w = [&]() {  // each wave instruction moves 1 KiB (64 lanes x 16 B) of one weight row
+    constexpr int PER_ROW = AO_K / 512;
+    for (int i = wid; i < AO_ROWS * PER_ROW; i += 4) {
+      const int r = i / PER_ROW, c = i % PER_ROW;
+      const bf16_t* src = args.w + (long)(r0 + r) * args.ldw + c * 512 + lane * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(wsl + ((long)r * AO_K + c * 512) * 2), 16, 0,
+                                       0);
+    }
+  };
+#define AO_STAMP(k) \
+  if (args.stamps && tid == 0) args.stamps[(long)bid * 8 + (k)] = (long long)__builtin_amdgcn_s_memrealtime()
+  AO_STAMP(0);
+  // consumers start their weight stream at once; producers only after publishing (hipcc drains
+  // an outstanding LDS-DMA at the first use of a plain load, which would put the 128 KiB ahead of
+  // the attention everyone waits for)
+  if (bid >= P) issue_w();
+
+  if (bid < P) {
+    const int hk = bid % a.Hkv, part = bid / a.Hkv;
+    const int len = a.attn_len[0];
+    const int s_new = a.slot[0];
+    RT_ASSERT(len <= a.Smax && s_new >= 0 && s_new < a.Smax);
+    int kbeg = a.kv_start ? a.kv_start[0] : 0;
+    if (a.window > 0) kbeg = max(kbeg, len - a.window);
+    const int p0 = max(part * a.PS, kbeg), p1 = min((part + 1) * a.PS, len);
+    const int sub = lane / LPK, dl = lane % LPK;
+    const bool active = p0 < p1;
+    float mrow[G], lrow[G];
+    if (active) {
+      const int p = a.pos ? a.pos[0] : 0;
+      const bf16_t* kbase = a.kc + (long)hk * a.Smax * D;
+      const bf16_t* vbase = a.vc + (long)hk * a.Smax * D;
+      KVChunk<D, NK> ca, cb;
+      load_chunk<D, NK>(ca, kbase, vbase, p0, p1, wid, sub, dl);
+      float qv[G][8];
+#pragma unroll
+      for (int gg = 0; gg < G; ++gg) rope_chunk<D>(a.qkv + (long)(hk * G + gg) * D, dl, a, p, qv[gg]);
+      const bool has_new = s_new >= p0 && s_new < p1;
+      uint4 kp = make_uint4(0, 0, 0, 0), vp = kp;
+      if (has_new) {
+        float kn[8], vn[8];
+        rope_chunk<D>(a.qkv + (long)(a.Hq + hk) * D, dl, a, p, kn);
+        unpack8(*(const uint4*)(a.qkv + (long)(a.Hq + a.Hkv + hk) * D + dl * 8), vn);
+        kp = pack8(kn);
+        vp = pack8(vn);
+        if (wid == 0 && sub == 0) {
+          *(uint4*)(a.kc + ((long)hk * a.Smax + s_new) * D + dl * 8) = kp;
+          *(uint4*)(a.vc + ((long)hk * a.Smax + s_new) * D + dl * 8) = vp;
+        }
+      }
+      float m[G], l[G], acc[G][8];
+#pragma unroll
+      for (int gg = 0; gg < G; ++gg) {
+        m[gg] = -INFINITY;
+        l[gg] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[gg][e] = 0.f;
+      }
+      for (int c0 = p0; c0 < p1; c0 += 2 * CH) {
+        if (c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl);
+        consume_chunk<D, G, NK>(ca, c0, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
+        if (c0 + CH < p1) {
+          if (c0 + 2 * CH < p1) load_chunk<D, NK>(ca, kbase, vbase, c0 + 2 * CH, p1, wid, sub, dl);
+          consume_chunk<D, G, NK>(cb, c0 + CH, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
+        }
+      }
+#pragma unroll
+      for (int gg = 0; gg < G; ++gg) {
+        float mw = m[gg];
+#pragma unroll
+        for (int off = LPK; off < 64; off <<= 1) mw = fmaxf(mw, __shfl_xor(mw, off, 64));
+        const float r = (m[gg] == -INFINITY) ? 0.f : exp2f(m[gg] - mw);
+        l[gg] *= r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[gg][e] *= r;
+        m[gg] = mw;
+        if (lane == 0) wst[wid][gg][0] = mw;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int gg = 0; gg < G; ++gg) {
+        mrow[gg] = fmaxf(fmaxf(wst[0][gg][0], wst[1][gg][0]), fmaxf(wst[2][gg][0], wst[3][gg][0]));
+        const float r = (m[gg] == -INFINITY) ? 0.f : exp2f(m[gg] - mrow[gg]);
+        float lsum = l[gg] * r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[gg][e] *= r;
+#pragma unroll
+        for (int off = LPK; off < 64; off <<= 1) {
+          lsum += __shfl_xor(lsum, off, 64);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[gg][e] += __shfl_xor(acc[gg][e], off, 64);
+        }
+        if (sub == 0) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) red[(wid * G + gg) * D + dl * 8 + e] = acc[gg][e];
+        }
+        if (lane == 0) wst[wid][gg][1] = lsum;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int gg = 0; gg < G; ++gg) lrow[gg] = wst[0][gg][1] + wst[1][gg][1] + wst[2][gg][1] + wst[3][gg][1];
+    }
+    // publish this partition's partial with write-through stores, then count it. Record stride
+    // AO_PSTR (16-B aligned) so consumers read it with vector loads.
+    float* outp = a.part + ((long)hk * a.NP + part) * G * AO_PSTR;
+    for (int e = tid; e < G * D; e += 256) {
+      const int gg = e / D, d = e % D;
+      if (active)
+        __hip_atomic_store(outp + gg * AO_PSTR + d,
+                           red[(0 * G + gg) * D + d] + red[(1 * G + gg) * D + d] + red[(2 * G + gg) * D + d] +
+                               red[(3 * G + gg) * D + d],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid < G) {
+      __hip_atomic_store(outp + tid * AO_PSTR + D, active ? mrow[tid] : -INFINITY, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(outp + tid * AO_PSTR + D + 1, active ? lrow[tid] : 0.f, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(args.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    AO_STAMP(1);
+    issue_w();
+  }
+
+  // ---- wait for every partial (bounded: a stuck grid reports instead of hanging the GPU) ----
+  if (tid == 0) {
+    unsigned n = 0;
+    while (__hip_atomic_load(args.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)P) {
+      if (++n > (1u << 22)) {
+        __hip_atomic_store(args.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    // acquire once for the block, then plain vector loads of the partials (the guide's counter
+    // hand-off: stale lines of the previous replay's partials must not be read from this XCD's L2)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  AO_STAMP(2);
+
+  // ---- merge: thread t owns attention-vector elements [t*EPT, t*EPT + EPT) (one head's slice) ----
+  float ov[EPT];
+  {
+    const int e0 = tid * EPT;
+    const int h = e0 / D, d0 = e0 % D, hk = h / G, gg = h % G;
+    const float* base = a.part + (long)hk * a.NP * G * AO_PSTR;
+    float M = -INFINITY, L = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) ov[i] = 0.f;
+    // partitions in groups of 4 with every load of a group issued before any is used (clamped
+    // index, no per-load branch): one round trip per group instead of one per partition
+    for (int q0 = 0; q0 < a.NP; q0 += 4) {
+      float mq[4], lq[4], oq[4][EPT];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float* r = base + (min(q0 + j, a.NP - 1) * G + gg) * AO_PSTR;
+        const float2 ml = *(const float2*)(r + D);
+        mq[j] = ml.x;
+        lq[j] = ml.y;
+#pragma unroll
+        for (int i = 0; i < EPT; i += 4) {
+          const float4 v4 = *(const float4*)(r + d0 + i);
+          oq[j][i] = v4.x; oq[j][i + 1] = v4.y; oq[j][i + 2] = v4.z; oq[j][i + 3] = v4.w;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // empty partition (o[] never written) or clamped duplicate: skip
+        if (q0 + j >= a.NP || mq[j] == -INFINITY) continue;
+        const float Mn = fmaxf(M, mq[j]);
+        const float s0 = exp2f(M - Mn), s1 = exp2f(mq[j] - Mn);
+        L = L * s0 + lq[j] * s1;
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) ov[i] = ov[i] * s0 + oq[j][i] * s1;
+        M = Mn;
+      }
+    }
+    // the unfused path hands o_proj a bf16 attention vector: round identically
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) ov[i] = bf2f(f2bf(L > 0.f ? ov[i] / L : 0.f));
+  }
+
+  AO_STAMP(3);
+  // ---- o_proj rows of this block from the LDS weight slice ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  AO_STAMP(4);
+  float ps[AO_ROWS];
+#pragma unroll
+  for (int r = 0; r < AO_ROWS; ++r) {
+    const char* wr = wsl + ((long)r * AO_K + tid * EPT) * 2;
+    float w8[8], w8b[8];
+    unpack8(*(const uint4*)wr, w8);
+    unpack8(*(const uint4*)(wr + 16), w8b);
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s2 += w8[i] * ov[i] + w8b[i] * ov[8 + i];
+    ps[r] = s2;
+  }
+#pragma unroll
+  for (int r = 0; r < AO_ROWS; ++r)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ps[r] += __shfl_xor(ps[r], off, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int r = 0; r < AO_ROWS; ++r) rsum[wid][r] = ps[r];
+  __syncthreads();
+  if (tid < AO_ROWS) {
+    const int row = r0 + tid;
+    const float y = rsum[0][tid] + rsum[1][tid] + rsum[2][tid] + rsum[3][tid] + bf2f(args.res[row]);
+    args.out[row] = f2bf(y);
+  }
+  AO_STAMP(5);
+  // ---- re-arm: the last block out resets both counters (every block is past its wait) ----
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(args.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned)(NB - 1)) {
+      __hip_atomic_store(args.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(args.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------------------
 struct AttnBwdArgs {
@@ -1119,3 +1392,39 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
   RT_LAUNCH_CHECK();
   return 0;
 }
+
+static long long* g_ao_stamps = nullptr;  // debug hook: per-block phase stamps
+extern "C" void rt_attn_o_set_stamps(long long* p) { g_ao_stamps = p; }
+
+// batch-1 attention + o_proj (+ residual); returns -1 when the shape is not supported (caller
+// falls back to the two-kernel path)
+extern "C" int rt_attn_o_fused(const void* qkv, void* kc, void* vc, int Smax, const int* slot, const int* attn_len,
+                               const int* kv_start, const int* pos, const float* cosT, const float* sinT, float sign,
+                               int window, float* part, int NP, int PS, int Hq, int Hkv, int D, float scale,
+                               const void* w, long ldw, const void* res, void* out, int H, unsigned* sync, int* err,
+                               hipStream_t stream) {
+  AttnOArgs g;
+  DecodeFusedArgs& a = g.at;
+  a.qkv = (const bf16_t*)qkv; a.ldq = 0; a.kc = (bf16_t*)kc; a.vc = (bf16_t*)vc; a.Smax = Smax;
+  a.slot = slot; a.attn_len = attn_len; a.kv_start = kv_start; a.pos = pos; a.cosT = cosT; a.sinT = sinT;
+  a.sign = sign; a.window = window; a.part = part; a.tickets = nullptr; a.o = nullptr; a.ldo = 0;
+  a.B = 1; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
+  g.w = (const bf16_t*)w; g.ldw = ldw; g.res = (const bf16_t*)res; g.out = (bf16_t*)out; g.H = H;
+  g.sync = sync; g.err = err; g.stamps = g_ao_stamps;
+  const int G = Hq / Hkv;
+  const int nk = 4;
+  if (G * Hkv != Hq || Hq * D != AO_K || H % AO_ROWS != 0 || (ldw % 8) != 0) return -1;
+  if (PS % (4 * (64 / (D / 8)) * nk) != 0) return -1;
+  const int NB = H / AO_ROWS;
+  if (NB < Hkv * NP) return -1;
+#define AO_CASE(DD, GG)                                                                        \
+  if (D == DD && G == GG) {                                                                    \
+    hipLaunchKernelGGL((attn_o_fused_kernel<DD, GG, 4>), dim3(NB), dim3(256), 0, stream, g);   \
+    RT_LAUNCH_CHECK();                                                                         \
+    return 0;                                                                                  \
+  }
+  AO_CASE(128, 1) AO_CASE(128, 2) AO_CASE(128, 4) AO_CASE(128, 8)
+#undef AO_CASE
+  return -1;
+}
+#undef AO_STAMP

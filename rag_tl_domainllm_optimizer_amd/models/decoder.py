@@ -14,6 +14,7 @@ the same architectures through ``AutoModelForCausalLM`` (reinforcement_learning_
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -96,16 +97,20 @@ class DecoderLayer(nn.Module):
             if c is not None:
                 c.get(w)
 
-    def decode_fused(self, h, attend):
+    def decode_fused(self, h, attend, attend_o=None):
         """One Llama/Mistral layer of a decode step in four kernels: [RMSNorm folded into the qkv
         GEMM] -> attention (RoPE + append + split-K) -> [o GEMM + residual] -> [RMSNorm folded into
-        the gate/up GEMM + SwiGLU] -> [down GEMM + residual]. ``h`` is the bf16 residual stream."""
+        the gate/up GEMM + SwiGLU] -> [down GEMM + residual]. ``h`` is the bf16 residual stream.
+        ``attend_o`` (batch 1): attention and o GEMM + residual in one launch — three kernels."""
         cfg = self.cfg
         eps = cfg.norm_eps
         wq = self._fold.setdefault("qkv", ops.FoldCache()).get(self._w_eff("qkv_w", "qkv"), self.ln1_w)
         qkv = ops.gemm_decode(h, wq, norm_eps=eps, fp8=self._f8("qkv_folded"))
-        o = attend(qkv)
-        h = ops.gemm_decode(o, self._w_eff("o_w", "o"), residual=h, fp8=self._f8("o"))
+        wo = self._w_eff("o_w", "o")
+        h_new = attend_o(qkv, wo, h) if (attend_o is not None and self._f8("o") is None) else None
+        if h_new is None:
+            h_new = ops.gemm_decode(attend(qkv), wo, residual=h, fp8=self._f8("o"))
+        h = h_new
         wgu = self._fold.setdefault("gate_up", ops.FoldCache()).get(self._w_eff("gate_up_w", "gate_up"), self.ln2_w)
         f = ops.gemm_decode(h, wgu, act=ops.ACT_SWIGLU, norm_eps=eps, fp8=self._f8("gate_up_folded"))
         return ops.gemm_decode(f, self._w_eff("down_w", "down"), residual=h, fp8=self._f8("down"))
@@ -155,6 +160,10 @@ class CausalLM(nn.Module):
         # (MI355X, Mistral-7B: batch 1 4.15 -> 4.0 ms/token fused; batch 64 5.1 -> 5.5 ms/step)
         self.fused_decode = True
         self.fused_decode_max_batch = 16
+        # batch 1: attention + o_proj + residual in one launch (ops.decode_step_attention_o). Off by
+        # default: measured 26.4 vs 25.0 us per layer for the two-kernel path (docs/DESIGN.md,
+        # profiles/kernels_attn_o_fused_rejected.log); RAGTL_ATTN_O=1 turns it on
+        self.fused_attn_o = os.environ.get("RAGTL_ATTN_O", "0") == "1"
         if init:
             self.reset_parameters(seed)
 
@@ -273,7 +282,12 @@ class CausalLM(nn.Module):
                     return ops.decode_step_attention(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads,
                                                      pos, cos, sin, kv_start, cfg.sliding_window,
                                                      workspace=workspace)
-                h = layer.decode_fused(h, attend)
+
+                def attend_o(qkv, w_o, res, li=li):
+                    return ops.decode_step_attention_o(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads,
+                                                       w_o, res, pos, cos, sin, kv_start, cfg.sliding_window,
+                                                       workspace=workspace)
+                h = layer.decode_fused(h, attend, attend_o if self.fused_attn_o else None)
             y, _ = ops.rms_norm(h, self.norm_w, cfg.norm_eps)
             return y
         residual = None

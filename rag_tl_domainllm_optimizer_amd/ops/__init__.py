@@ -4,7 +4,8 @@ from ._ext import native, native_available, on_gpu  # noqa: F401
 from .linear import ACT_IDS, ACT_SWIGLU, FoldCache, LoRAGroup, gemm, gemm_decode, linear, set_gemm_backend  # noqa: F401
 from .norm import layer_norm, rms_norm  # noqa: F401
 from .attention import (  # noqa: F401
-    attention, decode_attention, decode_step_attention, decode_workspace, flash_attention_qkv, rope_qkv, rope_qkv_,
+    attention, decode_attention, decode_step_attention, decode_step_attention_o, decode_workspace, flash_attention_qkv,
+    rope_qkv, rope_qkv_,
 )
 from .misc import embedding, gae, ivf_scan, pool_normalize, ppo_loss, sample, swiglu, token_logprobs, topk  # noqa: F401
 from .optim import FlatParams, FusedAdamW  # noqa: F401

@@ -172,9 +172,13 @@ class DecodeWorkspace(tuple):
 def decode_workspace(B, Hq, Hkv, D, Smax, device, PS=None):
     PS = PS or decode_partition(B * Hkv, D, Smax)
     NP = (Smax + PS - 1) // PS
-    part = torch.empty(B * Hkv * NP * (Hq // Hkv) * (D + 2), dtype=torch.float32, device=device)
+    # records of D + 2 floats (o | m | l); the batch-1 attention + o_proj kernel uses 16-B aligned
+    # records of 132 floats
+    part = torch.empty(max(B * (D + 2), 132) * Hkv * NP * (Hq // Hkv), dtype=torch.float32, device=device)
     tickets = torch.zeros(B * Hkv, dtype=torch.int32, device=device)
-    return DecodeWorkspace((part, PS, tickets))
+    # batch-1 attention + o_proj launch: [producers published, blocks done] counters + give-up flag
+    sync = torch.zeros(3, dtype=torch.int32, device=device)
+    return DecodeWorkspace((part, PS, tickets, sync))
 
 
 def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, cos=None, sin=None, kv_start=None,
@@ -196,6 +200,26 @@ def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, c
     native().attn_decode_fused(qkv, k_cache, v_cache, slot, attn_len, kv_start, pos, cos, sin, sign, window, scale,
                                Hq, part, tickets, PS, out)
     return out
+
+
+def decode_step_attention_o(qkv, k_cache, v_cache, slot, attn_len, Hq, w_o, residual, pos=None, cos=None, sin=None,
+                            kv_start=None, window=0, scale=None, workspace=None):
+    """Batch-1 decode step of a layer in ONE launch: fused attention (as ``decode_step_attention``)
+    followed by ``o_proj`` and the residual add: returns ``residual + attn @ w_o^T`` [1, H], or
+    None when the shape is not covered (batch != 1, Hq*D != 4096, CPU, ...) — the caller then runs
+    the two-kernel path. The o_proj weight slice of every workgroup streams into LDS while the
+    attention partials are computed (csrc/kernels/attention.hip, attn_o_fused_kernel)."""
+    if not on_gpu(qkv) or qkv.shape[0] != 1 or workspace is None or len(workspace) < 4:
+        return None
+    B, Hkv, Smax, D = k_cache.shape
+    if Hq * D != 4096 or w_o.shape[0] % 16 or w_o.stride(1) != 1:
+        return None
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    part, PS, sync = workspace[0], workspace[1], workspace[3]
+    out = torch.empty_like(residual)
+    ok = native().attn_o_fused(qkv.contiguous(), k_cache, v_cache, slot, attn_len, kv_start, pos, cos, sin, 1.0,
+                               window, scale, Hq, part, PS, w_o, residual.contiguous(), out, sync[:2], sync[2:])
+    return out if ok else None
 
 
 def decode_attention(q, k_cache, v_cache, kv_len, Hq, kv_start=None, window=0, scale=None, workspace=None, out=None):
