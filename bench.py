@@ -2,7 +2,7 @@
 """Headline benchmark: PPO rollout tokens/sec (node) + p50 RAG answer latency, Mistral-7B.
 
 Metric and config from BASELINE.json: Mistral-7B-shaped bf16 policy (random init, LoRA r=16 on all
-linear projections, value head), all-MiniLM-L6-shaped reward/retrieval encoder, 100k-doc synthetic
+linear projections — or every weight with --full-ft — value head), 256 rollouts per GPU, all-MiniLM-L6-shaped reward/retrieval encoder, 100k-doc synthetic
 corpus in an HBM-resident IVF index. One process per GPU (torchrun env, RCCL over xGMI), data
 parallel; per-GPU work is fixed (weak scaling).
 
@@ -49,10 +49,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--encoder", default="minilm-l6")
-    ap.add_argument("--rollout-batch", type=int, default=64, help="sequences per GPU per PPO step")
+    ap.add_argument("--rollout-batch", type=int, default=None,
+                    help="sequences per GPU per PPO step (default 256; 64 for --mode pipeline)")
     ap.add_argument("--new-tokens", type=int, default=128)
     ap.add_argument("--max-prompt", type=int, default=320)
-    ap.add_argument("--minibatch", type=int, default=16)
+    ap.add_argument("--minibatch", type=int, default=None, help="PPO minibatch (default 32; 16 for pipeline)")
     ap.add_argument("--top-k-docs", type=int, default=3)
     ap.add_argument("--ndocs", type=int, default=100_000)
     ap.add_argument("--doc-words", type=int, default=48)
@@ -64,10 +65,20 @@ def main():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--mode", default="ppo", choices=["ppo", "sft", "pipeline"])
     ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3fn) weights for no-grad forwards (config 5)")
-    ap.add_argument("--sft-batch", type=int, default=16, help="SFT sequences per GPU per step")
+    ap.add_argument("--sft-batch", type=int, default=64, help="SFT sequences per GPU per step")
+    ap.add_argument("--full-ft", action="store_true",
+                    help="PPO over every policy weight (the reference's full-parameter mode: bf16 compute copies "
+                         "+ fp32 master, frozen reference copy) instead of LoRA r=16")
     args = ap.parse_args()
     if args.mode == "pipeline" and args.model == "mistral-7b" and "--model" not in sys.argv:
         args.model = "llama2-13b"
+    # 256 rollouts per GPU: a decode step streams the 14.5 GB of weights once whatever the batch, so
+    # a larger rollout batch amortises it (64 -> 128 -> 256: 4660 -> 5108 -> 6101 tokens/s on one
+    # MI355X, profiles/bench_r1_rollout*.log); 288 GB of HBM hold its 15 GB KV cache
+    if args.rollout_batch is None:
+        args.rollout_batch = 64 if args.mode == "pipeline" else 256
+    if args.minibatch is None:
+        args.minibatch = 16 if args.mode == "pipeline" else 32
 
     from rag_tl_domainllm_optimizer_amd import models, parallel
     from rag_tl_domainllm_optimizer_amd.data import SyntheticCorpus
@@ -109,7 +120,8 @@ def main():
 
     # ---- PPO trainer ----
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
-                   lora_r=16, lora_alpha=32.0, seed=0, rollout_chunks=1, overlap_reward=True)
+                   lora_r=16, lora_alpha=32.0, seed=0, rollout_chunks=1, overlap_reward=True,
+                   full_finetune=args.full_ft)
     trainer = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
     if args.no_graph:
         trainer.gen.use_graph = False
@@ -181,7 +193,8 @@ def main():
         "data": f"synthetic (random-init weights, synthetic {args.ndocs}-doc corpus)",
         "config": {"model": args.model, "global_batch": args.rollout_batch * di.world,
                    "seq_len": args.max_prompt + args.new_tokens, "parallelism": f"dp{di.world}",
-                   "new_tokens": args.new_tokens, "lora_r": 16, "encoder": args.encoder, "ndocs": args.ndocs,
+                   "new_tokens": args.new_tokens, "lora_r": None if args.full_ft else 16,
+                   "full_finetune": bool(args.full_ft), "encoder": args.encoder, "ndocs": args.ndocs,
                    "index": f"ivf{index.nlist}/nprobe{args.nprobe}", "minibatch": args.minibatch},
         "p50_rag_latency_s": lat["p50_s"] if lat else None,
         "p90_rag_latency_s": lat["p90_s"] if lat else None,

@@ -56,6 +56,9 @@ int rt_sample(const void*, int, long, long, int, float, int, float, int, uint64_
 int rt_grad_sumsq(const float*, long, float*, int, hipStream_t);
 int rt_adamw(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, float, float,
              const float*, int, float*, int*, hipStream_t);
+int rt_grad_sumsq_mixed(const void*, long, const float*, long, float*, int, hipStream_t);
+int rt_adamw_mixed(float*, const void*, long, const float*, float*, float*, void*, long, float, float, float, float,
+                   float, float, float, float, const float*, int, float*, int*, hipStream_t);
 int rt_pool_norm(const void*, const int*, int, int, int, int, float*, hipStream_t);
 int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*, hipStream_t);
 int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const void*, const long*, int, float*, long*,
@@ -512,6 +515,33 @@ void adamw(Tensor p, const Tensor& g, Tensor m, Tensor v, const optional<Tensor>
            "adamw");
 }
 
+// Full-parameter training of a bf16 model (ops.MixedFlatParams): bf16 gradients g16 of the first
+// n16 elements + fp32 gradients g32 of the fp32 tail; fp32 master p and moments over all n; the bf16
+// compute copy p16 of the first n16 elements is rewritten in the same pass.
+void adamw_mixed(Tensor p, const Tensor& g16, const Tensor& g32, Tensor m, Tensor v, Tensor p16, double lr,
+                 double b1, double b2, double eps, double wd, int64_t step, double max_norm, Tensor partials,
+                 Tensor norm_out, Tensor skipped) {
+  CHECK_CUDA(p); CHECK_F32(p); CHECK_BF16(g16); CHECK_F32(g32); CHECK_F32(m); CHECK_F32(v); CHECK_BF16(p16);
+  CHECK_F32(partials);
+  TORCH_CHECK(p.is_contiguous() && g16.is_contiguous() && g32.is_contiguous() && m.is_contiguous() &&
+              v.is_contiguous() && p16.is_contiguous(), "adamw_mixed: buffers must be contiguous");
+  const int64_t n = p.numel(), n16 = g16.numel();
+  TORCH_CHECK(p16.numel() == n16 && n16 + g32.numel() == n && m.numel() == n && v.numel() == n,
+              "adamw_mixed: sizes");
+  TORCH_CHECK(n16 % 16 == 0 && (n - n16) % 4 == 0, "adamw_mixed: segments must be 16 / 4-element aligned");
+  CHECK_ALIGN16(p); CHECK_ALIGN16(g16); CHECK_ALIGN16(m); CHECK_ALIGN16(v); CHECK_ALIGN16(p16);
+  const int nparts = (int)partials.numel();
+  const float bc1 = 1.f - (float)std::pow(b1, (double)step), bc2 = 1.f - (float)std::pow(b2, (double)step);
+  const float* g32p = g32.numel() ? g32.data_ptr<float>() : nullptr;
+  check_rc(rt_grad_sumsq_mixed(g16.data_ptr(), n16, g32p, n - n16, partials.data_ptr<float>(), nparts, cur_stream()),
+           "grad_sumsq_mixed");
+  check_rc(rt_adamw_mixed(p.data_ptr<float>(), g16.data_ptr(), n16, g32p, m.data_ptr<float>(), v.data_ptr<float>(),
+                          p16.data_ptr(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, bc1, bc2,
+                          (float)max_norm, partials.data_ptr<float>(), nparts, norm_out.data_ptr<float>(),
+                          skipped.data_ptr<int>(), cur_stream()),
+           "adamw_mixed");
+}
+
 Tensor grad_norm(const Tensor& g, Tensor partials) {
   CHECK_CUDA(g); CHECK_F32(g);
   check_rc(rt_grad_sumsq(g.data_ptr<float>(), g.numel(), partials.data_ptr<float>(), (int)partials.numel(),
@@ -639,6 +669,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("logprob_bwd", &logprob_bwd);
   m.def("sample", &sample);
   m.def("adamw", &adamw);
+  m.def("adamw_mixed", &adamw_mixed);
   m.def("grad_norm", &grad_norm);
   m.def("pool_norm", &pool_norm);
   m.def("topk", &topk);

@@ -9,6 +9,11 @@
 //                      capped at 1) and a skip flag when the norm is non-finite, then applies
 //                      torch.optim.AdamW semantics (decoupled weight decay, bias correction) and
 //                      optionally refreshes a bf16 shadow copy used by the MFMA kernels.
+// Mixed form (rt_grad_sumsq_mixed / rt_adamw_mixed, full-parameter training of a bf16 model,
+// ops.MixedFlatParams): elements [0, n16) read bf16 gradients and rewrite the bf16 compute copy
+// in the same pass; elements [n16, n) (fp32 parameters: the value head) read fp32 gradients.
+// 4 elements per lane (16-B master / moment accesses); every segment boundary is a multiple of 16
+// elements, so a group of 4 never straddles the bf16 / fp32 seam.
 // Replaces clip_grad_norm_ + AdamW.step of reinforcement_learning_optimization_after_rag.py:230-232.
 #include "rt_common.h"
 
@@ -34,7 +39,35 @@ struct AdamArgs {
   float lr, b1, b2, eps, wd, bc1, bc2, max_norm;
   const float* partials; int nparts;
   float* norm_out; int* skipped;
+  // mixed form: g16 = bf16 gradients of elements [0, n16), g = fp32 gradients of [n16, n) indexed
+  // from n16; pbf (if given) covers [0, npbf). Plain form: g16 = nullptr, n16 = 0, npbf = n.
+  const bf16_t* g16; long n16; long npbf;
 };
+
+__global__ __launch_bounds__(256) void grad_sumsq_mixed_kernel(const bf16_t* __restrict__ g16, long n16,
+                                                               const float* __restrict__ g32, long n32,
+                                                               float* __restrict__ partials) {
+  __shared__ float sb[4];
+  float s = 0.f;
+  const long stride = (long)gridDim.x * 256, t = (long)blockIdx.x * 256 + threadIdx.x;
+  for (long i = t; i < n16 / 8; i += stride) {  // n16 % 8 == 0 (checked by the binding)
+    float f[8];
+    unpack8(((const uint4*)g16)[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += f[k] * f[k];
+  }
+  for (long i = t; i < n32; i += stride) s += g32[i] * g32[i];
+  s = block_sum(s, sb);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__device__ __forceinline__ void adam_elem(const AdamArgs& a, float gr, float& pp, float& mm, float& vv, float decay,
+                                          float step_scale, float inv_bc2_sqrt) {
+  mm = a.b1 * mm + (1.f - a.b1) * gr;
+  vv = a.b2 * vv + (1.f - a.b2) * gr * gr;
+  pp = pp * decay;
+  pp -= step_scale * mm / (sqrtf(vv) * inv_bc2_sqrt + a.eps);
+}
 
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   __shared__ float sb[4];
@@ -54,17 +87,36 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   const float decay = 1.f - a.lr * a.wd;
   const float step_scale = a.lr / a.bc1;
   const float inv_bc2_sqrt = rsqrtf(a.bc2);
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (long)gridDim.x * 256) {
-    const float gr = a.g[i] * clip;
-    float mm = a.m[i], vv = a.v[i], pp = a.p[i];
-    mm = a.b1 * mm + (1.f - a.b1) * gr;
-    vv = a.b2 * vv + (1.f - a.b2) * gr * gr;
-    pp = pp * decay;
-    pp -= step_scale * mm / (sqrtf(vv) * inv_bc2_sqrt + a.eps);
+  const long stride = (long)gridDim.x * 256, t = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n4 = a.n / 4;
+  for (long q = t; q < n4; q += stride) {
+    const long i = q * 4;
+    float g[4];
+    if (i < a.n16) {
+      const uint2 w = ((const uint2*)a.g16)[q];
+      g[0] = __uint_as_float(w.x << 16); g[1] = __uint_as_float(w.x & 0xffff0000u);
+      g[2] = __uint_as_float(w.y << 16); g[3] = __uint_as_float(w.y & 0xffff0000u);
+    } else {
+      const float4 w = *(const float4*)(a.g + (i - a.n16));
+      g[0] = w.x; g[1] = w.y; g[2] = w.z; g[3] = w.w;
+    }
+    const float4 p4 = ((const float4*)a.p)[q], m4 = ((const float4*)a.m)[q], v4 = ((const float4*)a.v)[q];
+    float P[4] = {p4.x, p4.y, p4.z, p4.w}, M[4] = {m4.x, m4.y, m4.z, m4.w}, V[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) adam_elem(a, g[k] * clip, P[k], M[k], V[k], decay, step_scale, inv_bc2_sqrt);
+    ((float4*)a.p)[q] = make_float4(P[0], P[1], P[2], P[3]);
+    ((float4*)a.m)[q] = make_float4(M[0], M[1], M[2], M[3]);
+    ((float4*)a.v)[q] = make_float4(V[0], V[1], V[2], V[3]);
+    if (i < a.npbf) ((uint2*)a.pbf)[q] = make_uint2(pack2bf(P[0], P[1]), pack2bf(P[2], P[3]));
+  }
+  for (long i = n4 * 4 + t; i < a.n; i += stride) {  // tail (n % 4 != 0)
+    const float gr = (i < a.n16 ? bf2f(a.g16[i]) : a.g[i - a.n16]) * clip;
+    float pp = a.p[i], mm = a.m[i], vv = a.v[i];
+    adam_elem(a, gr, pp, mm, vv, decay, step_scale, inv_bc2_sqrt);
+    a.p[i] = pp;
     a.m[i] = mm;
     a.v[i] = vv;
-    a.p[i] = pp;
-    if (a.pbf) a.pbf[i] = f2bf(pp);
+    if (i < a.npbf) a.pbf[i] = f2bf(pp);
   }
 }
 
@@ -82,8 +134,33 @@ extern "C" int rt_grad_sumsq(const float* g, long n, float* partials, int nparts
 extern "C" int rt_adamw(float* p, const float* g, float* m, float* v, void* pbf, long n, float lr, float b1, float b2,
                         float eps, float wd, float bc1, float bc2, float max_norm, const float* partials, int nparts,
                         float* norm_out, int* skipped, hipStream_t stream) {
-  AdamArgs a{p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd, bc1, bc2, max_norm, partials, nparts, norm_out, skipped};
+  AdamArgs a{p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd, bc1, bc2, max_norm, partials, nparts, norm_out, skipped,
+             nullptr, 0, pbf ? n : 0};
   long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int rt_grad_sumsq_mixed(const void* g16, long n16, const float* g32, long n32, float* partials, int nparts,
+                                   hipStream_t stream) {
+  if (nparts > OPT_NBLK || nparts <= 0 || n16 % 8) return -1;
+  hipLaunchKernelGGL(grad_sumsq_mixed_kernel, dim3(nparts), dim3(256), 0, stream, (const bf16_t*)g16, n16, g32, n32,
+                     partials);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int rt_adamw_mixed(float* p, const void* g16, long n16, const float* g32, float* m, float* v, void* p16,
+                              long n, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
+                              float max_norm, const float* partials, int nparts, float* norm_out, int* skipped,
+                              hipStream_t stream) {
+  if (n16 % 4 || n16 > n) return -1;
+  AdamArgs a{p, g32, m, v, (bf16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, max_norm, partials, nparts, norm_out, skipped,
+             (const bf16_t*)g16, n16, n16};
+  long blocks = (n / 4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);

@@ -86,7 +86,7 @@ class PPOTrainer:
     reference scores response token t+1 at query position t and raises on length mismatch, B1);
     the value is read at the last real query token (B6); "entropy" is the mean token entropy (B5).
     Parameters trained: LoRA adapters + value head (fused AdamW; the reference fine-tunes all
-    weights — pass ``full_finetune=True`` on CPU models for that)."""
+    weights — pass ``full_finetune=True`` for that: bf16 compute copies + fp32 master on the GPU)."""
 
     def __init__(self, model_path, tokenizer_path, lr=5e-5, gamma=0.99, clip_range=0.2, value_coef=0.5,
                  entropy_coef=0.01, max_grad_norm=0.5, lora_r: int = 16, full_finetune: bool = False):
@@ -95,13 +95,19 @@ class PPOTrainer:
         if self.tokenizer.pad_token_id is None:  # rl.py:143-146
             self.policy.cfg.pad_token_id = self.policy.cfg.eos_token_id
         self.value_head = ValueHead(self.policy.cfg.hidden_size, device=self.device)
+        self._ref_copy = None
         if full_finetune:
+            # the reference's mode (rl.py:153-156): every weight trains; the frozen reference is a
+            # copy of the starting weights (rl.py:171-174)
+            import copy
+
+            self._ref_copy = copy.deepcopy(self.policy).requires_grad_(False)
             params = list(self.policy.parameters())
         else:
             self.policy.add_lora(lora_r, 2.0 * lora_r, "all")
             self.policy.freeze_base()
             params = self.policy.lora_parameters()
-        self.flat = ops.FlatParams(list(params) + list(self.value_head.parameters()))
+        self.flat = ops.flat_params(list(params) + list(self.value_head.parameters()))
         self.policy.refresh_lora()
         self.optimizer = ops.FusedAdamW(self.flat, lr=lr, weight_decay=0.01, max_grad_norm=max_grad_norm)
         self.gamma, self.clip_range = gamma, clip_range
@@ -110,8 +116,9 @@ class PPOTrainer:
 
     @property
     def ref_model(self):
-        """The frozen reference = base weights with LoRA disabled (no third model copy)."""
-        return _RefView(self.policy)
+        """The frozen reference: base weights with LoRA disabled (no third model copy), or the
+        starting-weight copy under full fine-tuning."""
+        return _RefView(self._ref_copy if self._ref_copy is not None else self.policy)
 
     def compute_advantages(self, rewards, values, dones, next_value=0):
         """Exactly rl.py:176-191 (GAE over the batch, lambda 0.95)."""

@@ -193,6 +193,25 @@ def merge_lora(model, sign: float = 1.0):
                 w[c0:c0 + b.shape[0]] += delta.to(w.dtype)
 
 
+@torch.no_grad()
+def merge_and_drop_lora(model):
+    """Fold every adapter into its base weight (W += s B A) and remove the adapters, leaving a plain
+    model (full fine-tuning after a LoRA stage, merged export). Base weights kept in the extended
+    [W | UB] layout move back to storage of their own."""
+    if getattr(model, "lora_config", None) is None:
+        return
+    merge_lora(model)
+    cfg = model.cfg
+    for layer in model.layers:
+        for grp_name, grp in layer.lora.items():
+            if grp.ext is not None:
+                w = _group_weight(layer, cfg, grp_name)
+                w.data = w.data.contiguous()
+        layer.lora = {}
+        layer.lora_params = nn.ParameterDict()
+    del model.lora_config
+
+
 def _group_weight(layer, cfg, grp):
     return {"qkv": layer.qkv_w, "o": layer.o_w, "gate_up": getattr(layer, "gate_up_w", None),
             "down": getattr(layer, "down_w", None), "fc1": getattr(layer, "fc1_w", None),

@@ -1,6 +1,7 @@
 """Data-parallel gradient synchronisation over a flat gradient buffer.
 
-Trainable parameters live in one flat fp32 buffer (:class:`ops.FlatParams`), ordered as the model
+Trainable parameters live in one flat fp32 buffer (:class:`ops.FlatParams`; bf16 + fp32 buffers
+for full-parameter training, :class:`ops.MixedFlatParams`), ordered as the model
 runs forward, so backward produces gradients from the END of the buffer towards its start. The
 buffer is cut into contiguous buckets; a post-accumulate-grad hook counts ready parameters and, as
 soon as a bucket is complete, launches an asynchronous all-reduce (RCCL over xGMI on GPU) of that
@@ -71,7 +72,17 @@ class GradSync:
 
     def _launch(self, bi):
         s, e = self.buckets[bi]
-        self._handles[bi] = dist.all_reduce(self.flat.grad[s:e], async_op=True)
+        hs = []
+        # one slice per gradient buffer the bucket touches (fp32, or bf16 + fp32 under full-parameter
+        # training: ops.MixedFlatParams); RCCL reduces bf16 in place, 2 B per weight over xGMI
+        for t in self.flat.grad_slices(s, e):
+            if t.dtype == torch.bfloat16 and not t.is_cuda:
+                f = t.float()  # CPU (gloo) runs: reduce an fp32 copy of a bf16 slice
+                dist.all_reduce(f)
+                t.copy_(f)
+            else:
+                hs.append(dist.all_reduce(t, async_op=True))
+        self._handles[bi] = hs
 
     def no_sync(self):
         """Context manager: accumulate gradients locally (micro-batches before the last one)."""
@@ -102,9 +113,10 @@ class GradSync:
         for bi in range(len(self.buckets)):
             if self._handles[bi] is None:
                 self._launch(bi)
-        for h in self._handles:
-            h.wait()
-        self.flat.grad.div_(self.world)
+        for hs in self._handles:
+            for h in hs:
+                h.wait()
+        self.flat.div_grads(self.world)
         self.wait_s += time.perf_counter() - t0
         self._handles = [None] * len(self.buckets)
         self._ready = [0] * len(self.buckets)

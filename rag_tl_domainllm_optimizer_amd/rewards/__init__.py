@@ -86,8 +86,9 @@ class RewardModel:
             gsim = torch.where(has_gt, (R * G).sum(-1), torch.zeros_like(rel))
             a, b = self.cfg.gt_mix
             reward = torch.where(has_gt, a * reward + b * gsim, reward)
+        gl = gsim.tolist()  # one device->host copy, not one per row
         comps = {"factual_accuracy": fact, "relevance": rel, "conciseness": conc,
-                 "ground_truth_similarity": [float(gsim[i]) if g_i[i] >= 0 else None for i in range(B)],
+                 "ground_truth_similarity": [gl[i] if g_i[i] >= 0 else None for i in range(B)],
                  "total_reward": reward}
         return reward, comps
 

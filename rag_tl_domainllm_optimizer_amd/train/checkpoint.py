@@ -119,8 +119,13 @@ def save_checkpoint(prefix: str, model, tokenizer, value_head=None, optimizer=No
             st["optimizer"] = {k: v for k, v in osd.items() if k not in ("exp_avg", "exp_avg_sq", "skipped")}
             st["optimizer"]["skipped"] = int(osd["skipped"])
         rng = st.pop("rng", None)
-        if rng is not None:
-            torch.save(rng, os.path.join(tmp, "rng.pt"))
+        if rng is not None:  # safetensors + JSON: nothing in a checkpoint needs unpickling
+            from ..utils.seed import rng_state_pack
+
+            rt, rm = rng_state_pack(rng)
+            save_file(rt, os.path.join(tmp, "rng.safetensors"))
+            with open(os.path.join(tmp, "rng.json"), "w") as f:
+                json.dump(rm, f)
         with open(os.path.join(tmp, "state.json"), "w") as f:
             json.dump(st, f, indent=2, default=float)
         _commit(tmp, f"{prefix}_trainer_state")
@@ -153,8 +158,15 @@ def load_checkpoint(prefix: str, model, value_head=None, optimizer=None, load_po
             optimizer.load_state_dict(osd)
             with torch.no_grad():
                 optimizer.flat.data.copy_(t["params"].to(optimizer.flat.data.device))
-        if os.path.exists(os.path.join(tsd, "rng.pt")):
-            st["rng"] = torch.load(os.path.join(tsd, "rng.pt"), weights_only=False)
+            if hasattr(optimizer.flat, "refresh_shadow"):  # full fine-tuning: bf16 copies <- master
+                optimizer.flat.refresh_shadow()
+        if os.path.exists(os.path.join(tsd, "rng.safetensors")):
+            from safetensors.torch import load_file
+
+            from ..utils.seed import rng_state_unpack
+
+            with open(os.path.join(tsd, "rng.json")) as f:
+                st["rng"] = rng_state_unpack(load_file(os.path.join(tsd, "rng.safetensors")), json.load(f))
     if hasattr(model, "refresh_lora"):
         model.refresh_lora()
     print(f"Checkpoint loaded from {prefix}")

@@ -8,6 +8,8 @@ with the same RAG prompt that is trained on (B3); log-probs are per response tok
 frozen reference enters as a per-token KL penalty (B4; the reference is the base weights with LoRA
 disabled, no third model copy); "entropy" is the true token entropy (B5); values are read at the
 last real position (B6) from the same forward as the log-probs (B7); GAE runs over tokens (B8).
+Trainables: LoRA adapters + value head (default), or every policy weight (``full_finetune``, the
+reference's mode: bf16 compute copies + fp32 master, ops.MixedFlatParams, frozen reference copy).
 
 Device flow per step (one process per GPU, DP over RCCL):
   generate (hipGraph decode, behaviour log-probs + values emitted by the sampler step)
@@ -17,6 +19,7 @@ Device flow per step (one process per GPU, DP over RCCL):
 """
 from __future__ import annotations
 
+import copy
 import math
 import time
 from dataclasses import asdict, dataclass, field
@@ -54,6 +57,7 @@ class PPOConfig:
     kl_horizon: int = 10000
     ppo_epochs: int = 1                  # reference: one update per batch (rl.py:328)
     minibatch_size: int = 16
+    ref_minibatch_size: int = 64        # reference log-prob scoring (no grad)
     whiten_advantages: bool = True
     # generation (rl.py:38-44)
     max_new_tokens: int = 128
@@ -65,7 +69,7 @@ class PPOConfig:
     lora_r: int = 16
     lora_alpha: float = 32.0
     lora_targets: Sequence[str] = ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj")
-    full_finetune: bool = False
+    full_finetune: bool = False         # True: every weight (the reference's mode, rl.py:153)
     gradient_checkpointing: bool = False
     overlap_reward: bool = True
     rollout_chunks: int = 1          # >1: score chunk i while chunk i+1 decodes
@@ -119,14 +123,25 @@ class PPOTrainer:
         self.device = policy.embed.device
         self.sink = sink or MetricsSink(enabled=False)
         if c.full_finetune:
-            raise NotImplementedError("PPO trains LoRA adapters + value head; full-parameter fine-tuning is "
-                                      "provided by train.sft.SFTTrainer(full_finetune=True)")
-        if getattr(policy, "lora_config", None) is None:
-            policy.add_lora(c.lora_r, c.lora_alpha, list(c.lora_targets), seed=c.seed)
-        policy.freeze_base()
+            # the reference's mode (rl.py:140-174): AdamW over EVERY policy weight and the value
+            # head; the frozen reference is then a copy of the starting weights (the LoRA mode needs
+            # no copy: reference = adapters off)
+            from ..models.lora import merge_and_drop_lora
+
+            merge_and_drop_lora(policy)
+            self.ref_policy = copy.deepcopy(policy).requires_grad_(False)
+            policy.requires_grad_(True)
+            trainable = list(policy.parameters())
+        else:
+            self.ref_policy = None
+            if getattr(policy, "lora_config", None) is None:
+                policy.add_lora(c.lora_r, c.lora_alpha, list(c.lora_targets), seed=c.seed)
+            policy.freeze_base()
+            trainable = list(policy.lora_parameters())
         self.value_head = value_head or ValueHead(policy.cfg.hidden_size, device=self.device, seed=c.seed + 17)
-        # LoRA A/B + value head re-homed into one flat fp32 buffer (fused AdamW, bucketed all-reduce)
-        self.flat = ops.FlatParams(list(policy.lora_parameters()) + list(self.value_head.parameters()))
+        # trainables + value head re-homed into one flat buffer (fused AdamW, bucketed all-reduce):
+        # fp32 LoRA adapters, or bf16 compute copies + fp32 master under full fine-tuning
+        self.flat = ops.flat_params(trainable + list(self.value_head.parameters()))
         policy.refresh_lora()
         self.opt = ops.FusedAdamW(self.flat, lr=c.lr, betas=c.betas, eps=c.eps, weight_decay=c.weight_decay,
                                   max_grad_norm=c.max_grad_norm)
@@ -254,18 +269,20 @@ class PPOTrainer:
         then token rewards (score at the last token, -beta*KL per token) and GAE."""
         c = self.cfg
         with self.timer.phase("ref_logprobs+reward"):
-            self.policy.set_lora_enabled(False)
+            # the frozen reference: adapters off (LoRA) or the starting-weight copy (full FT)
+            ref_model = self.ref_policy if self.ref_policy is not None else self.policy
+            ref_model.set_lora_enabled(False)
             try:
                 ref_lp = []
-                mb = c.minibatch_size
+                mb = max(c.minibatch_size, c.ref_minibatch_size)  # no-grad: larger GEMMs, no saved activations
                 for s in range(0, ro.resp.shape[0], mb):
-                    lp, _, _, _ = score_sequences(self.policy, ro.prompt_ids[s:s + mb], ro.start[s:s + mb],
+                    lp, _, _, _ = score_sequences(ref_model, ro.prompt_ids[s:s + mb], ro.start[s:s + mb],
                                                   ro.resp[s:s + mb], ro.resp_len[s:s + mb],
                                                   1.0 / c.temperature)
                     ref_lp.append(lp)
                 ro.ref_logp = torch.cat(ref_lp, 0)
             finally:
-                self.policy.set_lora_enabled(True)
+                ref_model.set_lora_enabled(True)
             # host-side detokenisation + reward encoder run while the reference forward executes
             self._collect_rewards(ro)
         mask = response_mask(ro.resp_len, ro.resp.shape[1])

@@ -51,15 +51,15 @@ class SFTTrainer:
         self.device = model.embed.device
         self.sink = sink or MetricsSink(enabled=False)
         if c.full_finetune:
-            if self.device.type == "cuda":
-                raise NotImplementedError("full fine-tuning runs on fp32 CPU models; GPU path trains LoRA")
-            params = [p for p in model.parameters() if p.requires_grad]
+            # every weight trains: bf16 compute copies + fp32 master on the GPU (ops.MixedFlatParams)
+            model.requires_grad_(True)
+            params = list(model.parameters())
         else:
             if getattr(model, "lora_config", None) is None:
                 model.add_lora(c.lora_r, c.lora_alpha, list(c.lora_targets), seed=c.seed)
             model.freeze_base()
             params = model.lora_parameters()
-        self.flat = ops.FlatParams(params)
+        self.flat = ops.flat_params(params)
         if not c.full_finetune:
             model.refresh_lora()
         self.opt = ops.FusedAdamW(self.flat, lr=c.lr, betas=c.betas, eps=c.eps, weight_decay=c.weight_decay,

@@ -28,3 +28,27 @@ def set_rng_state(st: dict):
     torch.set_rng_state(st["torch"])
     if "cuda" in st and torch.cuda.is_available():
         torch.cuda.set_rng_state(st["cuda"])
+
+
+def rng_state_pack(st: dict):
+    """(tensors, meta) form of an ``rng_state()`` dict for safetensors + JSON (no pickle)."""
+    tensors = {"torch": st["torch"].clone().contiguous()}
+    if "cuda" in st:
+        tensors["cuda"] = st["cuda"].clone().contiguous()
+    name, keys, pos, has_gauss, cached = st["numpy"]
+    tensors["numpy_keys"] = torch.from_numpy(np.asarray(keys, dtype=np.int64))
+    ver, internal, gauss = st["python"]
+    meta = {"python": {"version": ver, "state": list(internal), "gauss": gauss},
+            "numpy": {"name": name, "pos": int(pos), "has_gauss": int(has_gauss), "cached_gaussian": float(cached)}}
+    return tensors, meta
+
+
+def rng_state_unpack(tensors: dict, meta: dict) -> dict:
+    py, npm = meta["python"], meta["numpy"]
+    st = {"python": (py["version"], tuple(py["state"]), py["gauss"]),
+          "numpy": (npm["name"], tensors["numpy_keys"].numpy().astype(np.uint32), npm["pos"], npm["has_gauss"],
+                    npm["cached_gaussian"]),
+          "torch": tensors["torch"]}
+    if "cuda" in tensors:
+        st["cuda"] = tensors["cuda"]
+    return st
