@@ -22,6 +22,10 @@ int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const vo
 void rt_gemm_set_variant(int);
 void rt_gemm_set_m64_split(int);
 void rt_gemm_set_decode_split(int);
+int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, long, const void*, long, int,
+                const void*, void*, long, void*, long, const void*, long, int, int, int, int, int, int, const void*,
+                hipStream_t);
+int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
 int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
                 int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
 int rt_quant_fp8_rows(const void*, long, void*, long, float*, long, int, hipStream_t);
@@ -54,11 +58,11 @@ int rt_logprob_bwd(const void*, int, long, const long*, float, long, int, const 
 int rt_sample(const void*, int, long, long, int, float, int, float, int, uint64_t, const int64_t*, const uint8_t*, long*,
               float*, hipStream_t);
 int rt_grad_sumsq(const float*, long, float*, int, hipStream_t);
-int rt_adamw(float*, const float*, float*, float*, void*, long, float, float, float, float, float, float, float, float,
+int rt_adamw(float*, const float*, float*, float*, void*, long, float, float, float, float, float, int, float,
              const float*, int, float*, int*, hipStream_t);
 int rt_grad_sumsq_mixed(const void*, long, const float*, long, float*, int, hipStream_t);
 int rt_adamw_mixed(float*, const void*, long, const float*, float*, float*, void*, long, float, float, float, float,
-                   float, float, float, float, const float*, int, float*, int*, hipStream_t);
+                   float, int, float, const float*, int, float*, int*, hipStream_t);
 int rt_pool_norm(const void*, const int*, int, int, int, int, float*, hipStream_t);
 int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*, hipStream_t);
 int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const void*, const long*, int, float*, long*,
@@ -172,6 +176,135 @@ Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const o
                       (int)N, (int)K, (int)act, out_f32 ? 1 : 0, slabs, tickets,
                       has_res ? residual->data_ptr() : nullptr, has_res ? residual->stride(0) : 0, (float)norm_eps, st),
            "gemm");
+  return c;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Token-parallel GEMM family (csrc/kernels/gemm_big.hip). 2-D operands with unit column stride:
+//   layout_a 0: a = [M, K]   1: a = [K, M]        layout_b 0: b = [N, K]   1: b = [K, N]
+// a2 / b2: K-extension (LoRA) in the same layouts with their own reduction length K2.
+// out_mode 0: bf16 (bias + act epilogue; act 5 = SwiGLU: b = [gate; up] (2F rows), C = [M, F],
+// out2 = optional [M, 2F] pre-activation), 1: fp32, 2: fp32 atomic accumulate into `out`
+// (split-K `nsplit`; `out` must be given and initialised).
+const Tensor& zero_page(const Tensor& like) {
+  static std::mutex mu;
+  static auto* map = new std::unordered_map<int, Tensor>();
+  std::lock_guard<std::mutex> g(mu);
+  auto it = map->find(like.get_device());
+  if (it != map->end()) return it->second;
+  (*map)[like.get_device()] = at::zeros({2048}, like.options().dtype(at::kBFloat16));
+  return (*map)[like.get_device()];
+}
+
+Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layout_b, const optional<Tensor>& a2,
+                const optional<Tensor>& b2, const optional<Tensor>& bias, int64_t act, int64_t out_mode,
+                int64_t nsplit, optional<Tensor> out, const optional<Tensor>& out2, const optional<Tensor>& residual) {
+  CHECK_CUDA(a); CHECK_CUDA(b); CHECK_BF16(a); CHECK_BF16(b); CHECK_ROWS(a); CHECK_ROWS(b);
+  CHECK_ALIGN16(a); CHECK_ALIGN16(b);
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_big: row strides must be multiples of 8");
+  const int64_t M = layout_a ? a.size(1) : a.size(0), K = layout_a ? a.size(0) : a.size(1);
+  const int64_t N = layout_b ? b.size(1) : b.size(0), Kb = layout_b ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm_big: K mismatch ", K, " vs ", Kb);
+  TORCH_CHECK((layout_a && layout_b) || K % 8 == 0, "gemm_big: K must be a multiple of 8 (a K-contiguous operand)");
+  TORCH_CHECK(!layout_a || M % 8 == 0, "gemm_big: [K, M] operand needs M % 8 == 0");
+  TORCH_CHECK(!layout_b || N % 8 == 0, "gemm_big: [K, N] operand needs N % 8 == 0");
+  int64_t K2 = 0;
+  const bool ext = a2.has_value() && a2->defined();
+  if (ext) {
+    TORCH_CHECK(b2.has_value() && b2->defined(), "gemm_big: a2 without b2");
+    CHECK_BF16(*a2); CHECK_BF16(*b2); CHECK_ROWS(*a2); CHECK_ROWS(*b2); CHECK_ALIGN16(*a2); CHECK_ALIGN16(*b2);
+    TORCH_CHECK(a2->stride(0) % 8 == 0 && b2->stride(0) % 8 == 0, "gemm_big: extension row strides % 8");
+    K2 = layout_a ? a2->size(0) : a2->size(1);
+    const int64_t M2 = layout_a ? a2->size(1) : a2->size(0);
+    const int64_t N2 = layout_b ? b2->size(1) : b2->size(0), K2b = layout_b ? b2->size(0) : b2->size(1);
+    TORCH_CHECK(M2 == M && N2 == N && K2b == K2, "gemm_big: extension shape mismatch");
+    TORCH_CHECK((layout_a && layout_b) || K2 % 8 == 0, "gemm_big: K2 must be a multiple of 8");
+  }
+  const bool swiglu = act == 5;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && !swiglu, "gemm_big: bias");
+  }
+  const int64_t Nout = swiglu ? N / 2 : N;
+  const auto odt = out_mode == 0 ? at::kBFloat16 : at::kFloat;
+  Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == Nout && c.stride(1) == 1, "gemm_big: bad out shape");
+    TORCH_CHECK(c.scalar_type() == odt, "gemm_big: bad out dtype");
+    TORCH_CHECK(out_mode != 0 || c.stride(0) % 8 == 0, "gemm_big: bf16 out row stride % 8");
+    CHECK_ALIGN16(c);
+  } else {
+    TORCH_CHECK(out_mode != 2, "gemm_big: atomic accumulation needs an initialised out");
+    c = at::empty({M, Nout}, a.options().dtype(odt));
+  }
+  void* c2 = nullptr;
+  int64_t ldc2 = 0;
+  if (out2.has_value() && out2->defined()) {
+    TORCH_CHECK(swiglu, "gemm_big: out2 is the SwiGLU pre-activation");
+    CHECK_BF16(*out2);
+    TORCH_CHECK(out2->size(0) == M && out2->size(1) == N && out2->stride(1) == 1 && out2->stride(0) % 8 == 0,
+                "gemm_big: bad out2");
+    CHECK_ALIGN16(*out2);
+    c2 = out2->data_ptr();
+    ldc2 = out2->stride(0);
+  }
+  const bool has_r = residual.has_value() && residual->defined();
+  if (has_r) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(out_mode == 0 && !swiglu && residual->dim() == 2 && residual->size(0) == M && residual->size(1) == N &&
+                    residual->stride(1) == 1 && residual->stride(0) % 8 == 0,
+                "gemm_big: residual must be bf16 [M, N] (bf16 output, no SwiGLU)");
+    CHECK_ALIGN16(*residual);
+  }
+  if (M == 0 || N == 0) return c;
+  check_rc(rt_gemm_big((int)layout_a, (int)layout_b, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                       ext ? a2->data_ptr() : nullptr, ext ? a2->stride(0) : 0, ext ? b2->data_ptr() : nullptr,
+                       ext ? b2->stride(0) : 0, (int)K2, opt_ptr(bias), c.data_ptr(), c.stride(0), c2, ldc2,
+                       has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, (int)M,
+                       (int)N, (int)K, (int)act, (int)out_mode, (int)nsplit, zero_page(a).data_ptr(), cur_stream()),
+           "gemm_big");
+  return c;
+}
+
+// Small-M GEMM (decode at batch 65..256, any NT GEMM whose 256x256 tiles cannot fill the chip):
+// K split over `nsplit` workgroup rows into fp32 slabs (workspace `slabs`, >= nsplit*M*N floats),
+// then one reduce kernel with the epilogue (bias, act / SwiGLU pairing, residual).
+Tensor gemm_splitk(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor slabs, const optional<Tensor>& bias,
+                   int64_t act, optional<Tensor> out, const optional<Tensor>& residual) {
+  CHECK_CUDA(a); CHECK_BF16(a); CHECK_BF16(w); CHECK_ROWS(a); CHECK_ROWS(w); CHECK_F32(slabs);
+  CHECK_ALIGN16(a); CHECK_ALIGN16(w);
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 8 == 0 && N % 8 == 0, "gemm_splitk: shapes");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_splitk: row strides % 8");
+  TORCH_CHECK(slabs.is_contiguous() && slabs.numel() >= nsplit * M * N, "gemm_splitk: workspace too small");
+  const bool swiglu = act == 5;
+  TORCH_CHECK(!swiglu || N % 16 == 0, "gemm_splitk: SwiGLU needs N % 16 == 0");
+  const int64_t Nout = swiglu ? N / 2 : N;
+  if (bias.has_value() && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(!swiglu && bias->numel() == N); }
+  const bool has_r = residual.has_value() && residual->defined();
+  if (has_r) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(!swiglu && residual->size(0) == M && residual->size(1) == N && residual->stride(1) == 1 &&
+                    residual->stride(0) % 8 == 0, "gemm_splitk: residual");
+  }
+  Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    CHECK_BF16(c);
+    TORCH_CHECK(c.size(0) == M && c.size(1) == Nout && c.stride(1) == 1 && c.stride(0) % 8 == 0, "gemm_splitk: out");
+  } else {
+    c = at::empty({M, Nout}, a.options());
+  }
+  if (M == 0) return c;
+  check_rc(rt_gemm_big(0, 0, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), nullptr, 0, nullptr, 0, 0,
+                       nullptr, slabs.data_ptr(), N, nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, 0, 3,
+                       (int)nsplit, zero_page(a).data_ptr(), cur_stream()),
+           "gemm_splitk");
+  check_rc(rt_gemm_splitk_reduce(slabs.data_ptr<float>(), (int)nsplit, (int)M, (int)N, opt_ptr(bias), (int)act,
+                                 has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, c.data_ptr(),
+                                 c.stride(0), cur_stream()),
+           "gemm_splitk_reduce");
   return c;
 }
 
@@ -506,10 +639,9 @@ void adamw(Tensor p, const Tensor& g, Tensor m, Tensor v, const optional<Tensor>
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adamw: sizes");
   if (pbf.has_value() && pbf->defined()) { CHECK_BF16(*pbf); TORCH_CHECK(pbf->numel() == n); }
   const int nparts = (int)partials.numel();
-  const float bc1 = 1.f - (float)std::pow(b1, (double)step), bc2 = 1.f - (float)std::pow(b2, (double)step);
   check_rc(rt_grad_sumsq(g.data_ptr<float>(), n, partials.data_ptr<float>(), nparts, cur_stream()), "grad_sumsq");
   check_rc(rt_adamw(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-                    (void*)opt_ptr(pbf), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, bc1, bc2,
+                    (void*)opt_ptr(pbf), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step,
                     (float)max_norm, partials.data_ptr<float>(), nparts, norm_out.data_ptr<float>(),
                     skipped.data_ptr<int>(), cur_stream()),
            "adamw");
@@ -531,12 +663,11 @@ void adamw_mixed(Tensor p, const Tensor& g16, const Tensor& g32, Tensor m, Tenso
   TORCH_CHECK(n16 % 16 == 0 && (n - n16) % 4 == 0, "adamw_mixed: segments must be 16 / 4-element aligned");
   CHECK_ALIGN16(p); CHECK_ALIGN16(g16); CHECK_ALIGN16(m); CHECK_ALIGN16(v); CHECK_ALIGN16(p16);
   const int nparts = (int)partials.numel();
-  const float bc1 = 1.f - (float)std::pow(b1, (double)step), bc2 = 1.f - (float)std::pow(b2, (double)step);
   const float* g32p = g32.numel() ? g32.data_ptr<float>() : nullptr;
   check_rc(rt_grad_sumsq_mixed(g16.data_ptr(), n16, g32p, n - n16, partials.data_ptr<float>(), nparts, cur_stream()),
            "grad_sumsq_mixed");
   check_rc(rt_adamw_mixed(p.data_ptr<float>(), g16.data_ptr(), n16, g32p, m.data_ptr<float>(), v.data_ptr<float>(),
-                          p16.data_ptr(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, bc1, bc2,
+                          p16.data_ptr(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step,
                           (float)max_norm, partials.data_ptr<float>(), nparts, norm_out.data_ptr<float>(),
                           skipped.data_ptr<int>(), cur_stream()),
            "adamw_mixed");
@@ -653,6 +784,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
   m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");
   m.def("quant_fp8", &quant_fp8, "per-row absmax e4m3fn quantisation -> (uint8 [R,C], scale fp32 [R])");
+  m.def("gemm_big", &gemm_big, "token-parallel GEMM family (NT / NN / TN, LoRA K-extension, split-K, SwiGLU)",
+        py::arg("a"), py::arg("b"), py::arg("layout_a"), py::arg("layout_b"), py::arg("a2") = py::none(),
+        py::arg("b2") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("out_mode") = 0,
+        py::arg("nsplit") = 1, py::arg("out") = py::none(), py::arg("out2") = py::none(),
+        py::arg("residual") = py::none());
+  m.def("gemm_splitk", &gemm_splitk, "small-M NT GEMM: split-K fp32 slabs + fused reduce epilogue", py::arg("a"),
+        py::arg("w"), py::arg("nsplit"), py::arg("slabs"), py::arg("bias") = py::none(), py::arg("act") = 0,
+        py::arg("out") = py::none(), py::arg("residual") = py::none());
   m.def("gemm_fp8", &gemm_fp8, "fp8 GEMM: W8A8 (MX MFMA 256x256) or W8A16 (skinny, M <= 64)", py::arg("a"),
         py::arg("sa") = py::none(), py::arg("wq"), py::arg("sw"), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("norm_eps") = 0.0);

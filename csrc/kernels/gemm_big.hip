@@ -1,0 +1,604 @@
+// Token-parallel bf16 GEMM family for gfx950 (M > 64): prefill, reference scoring, and the
+// forward / backward GEMMs of LoRA SFT, PPO and full fine-tuning.
+//
+//   C[M,N] = epi( A·B  +  A2·B2 )          (A2·B2 = LoRA K-extension, optional)
+//
+// Operand layouts (per operand, template parameters):
+//   ROW  : the operand's K index is contiguous — A stored [M][K], B stored [N][K] (nn.Linear
+//          weight [out, in]). LDS image [256 rows][128 B], 16-B slot = k-chunk ^ ((row>>1)&7),
+//          read with ds_read_b128 (conflict-free over every 16-lane group).
+//   KMAJ : the operand's M/N index is contiguous — A stored [K][M], B stored [K][N]. LDS image
+//          8 blocks of [64 k][32 mn] (64-B rows), 16-B chunk ^ (((k>>3)&1)<<1), read with
+//          ds_read_b64_tr_b16 (hardware transpose; conflict-free over each 32-lane half).
+// so NT (forward: X·Wᵀ) = ROW/ROW, NN (dX = dY·W) = ROW/KMAJ, TN (dW = dYᵀ·X) = KMAJ/KMAJ.
+// The reference's forward and backward passes (reinforcement_learning_optimization_after_rag.py
+// :200-209 policy/value forwards, :229 backward) are these GEMMs.
+//
+// Block: 256x256 output tile, 8 waves (2 x 4), each wave 128 x 64 = 8 x 4 fragments of
+// mfma_f32_16x16x32_bf16, K-step 64, two K-step buffers (128 KiB LDS, 1 block per CU).
+// The K-step is computed in four phases of 16 MFMAs per wave (quadrants a0b0, a0b1, a1b1,
+// a1b0). LDS-DMA (global_load_lds, 16 B / lane) moves one 16-KiB GRANULE per phase:
+//   a0 / a1 = A rows with bit 6 = 0 / 1 (A sub-block 0 / 1 of every wave),
+//   b0 / b1 = B rows with bit 5 = 0 / 1 (B sub-block 0 / 1 of every wave).
+// Issue schedule (global phase P = 4t + p, p = 1..4):  a0(u) at P = 4u-5, b0(u) 4u-4,
+// b1(u) 4u-3, a1(u) 4u-2  — i.e. granules of step u+2 are written into the buffer of step u
+// two or more phases after their last ds_read there (WAR), and every granule has ~4 phases
+// (≈ 2 µs) to land; counted `s_waitcnt vmcnt(2n)` (never 0 in the loop) retire a granule in
+// the phase BEFORE the one that reads it, behind a raw s_barrier (cdna_hip_programming.md §5
+// 'Pipelining across barriers', 'Read a staged buffer one phase AFTER the wait').
+// Waves 4-7 run one barrier behind waves 0-3, so each SIMD pairs one wave's MFMA cluster with
+// its partner's LDS reads / DMA issue (guide §5 T3-T5). All LDS is one __shared__ array.
+// Tiles: XCD-aware bijective remap + grouped (GROUP_M) order; split-K over blockIdx.y with fp32
+// atomic accumulation (narrow outputs with a deep reduction, e.g. LoRA dA / dB).
+// Reduction tails (K % 64 != 0) and the K-extension read a zero page for out-of-range k.
+#include "rt_common.h"
+
+namespace rt {
+
+namespace gb {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int GRAN = 16384;         // one granule
+constexpr int OPB = 2 * GRAN;       // one operand's K-step image (256 x 64 bf16)
+constexpr int BUF = 2 * OPB;        // A + B of one K-step
+constexpr int GROUP_M = 4;
+
+enum Layout { ROW = 0, KMAJ = 1 };
+enum Out { O_BF16 = 0, O_F32 = 1, O_F32_ATOMIC = 2, O_F32_SLAB = 3 };
+enum Epi { E_NONE = 0, E_RELU = 1, E_GELU = 2, E_GELU_TANH = 3, E_SILU = 4, E_SWIGLU = 5 };
+
+struct Args {
+  const bf16_t* A; long lda;
+  const bf16_t* B; long ldb;
+  const bf16_t* A2; long lda2;    // K-extension operands (same layouts), K2 reduction length
+  const bf16_t* B2; long ldb2;
+  int K2;
+  const bf16_t* bias;             // [N] (bf16) or null
+  void* C; long ldc;
+  bf16_t* C2; long ldc2;          // E_SWIGLU: optional pre-activation [M, 2F] ([gate | up])
+  const bf16_t* R; long ldr;      // bf16 out: C = act(acc + bias) + R (residual / beta = 1 input), or null
+  int M, N, K;                    // E_SWIGLU: N = 2F rows of the [gate; up] weight
+  int act;
+  int nsplit;                     // split-K factor (gridDim.y)
+  const bf16_t* zpage;            // >= 128 zero bytes
+};
+
+__device__ __forceinline__ int row_swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int kmaj_swz(int k) { return ((k >> 3) & 1) << 1; }
+
+__device__ __forceinline__ float act_fn(float x, int act) {
+  switch (act) {
+    case E_RELU: return fmaxf(x, 0.f);
+    case E_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case E_GELU_TANH: {
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+    }
+    case E_SILU: return x / (1.f + __expf(-x));
+    default: return x;
+  }
+}
+
+// counted wait: leave n (wave-uniform, 0..4) granules = 2n LDS-DMA instructions per lane in flight
+__device__ __forceinline__ void wait_granules(int n) {
+  if (n >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+#define GB_BARRIER() asm volatile("s_barrier" ::: "memory")
+
+template <int LA, int LB, int OUT, int EPI>
+__global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];  // the only __shared__ object
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS bases
+  const int wr = wid >> 2, wc = wid & 3;
+  const int frow = lane & 15, fq = lane >> 4;
+
+  // ---- tile assignment: XCD remap, then GROUP_M-row groups (L2 reuse of B panels) ----
+  const int tiles_m = (p.M + 255) / 256;
+  const int tiles_n = EPI == E_SWIGLU ? p.N / 256 : (p.N + 255) / 256;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % gsz);
+  const int tn = (bid % (GROUP_M * tiles_n)) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int Fh = p.N / 2;  // E_SWIGLU: gate rows [0, F), up rows [F, 2F)
+
+  // ---- K-steps of this split ----
+  const int nk1 = (p.K + 63) / 64;
+  const int nk2 = p.A2 ? (p.K2 + 63) / 64 : 0;
+  const int nk = nk1 + nk2;
+  const int t_begin = (int)((long)blockIdx.y * nk / p.nsplit);
+  const int t_end = (int)((long)(blockIdx.y + 1) * nk / p.nsplit);
+
+  // ---- LDS-DMA geometry of instruction j (0, 1) of this wave in granule g (0 a0, 1 a1, 2 b0, 3 b1) ----
+  // ROW : 8 rows x 128 B per instruction; lane -> row rb + lane/8, 16-B slot lane%8 holding k-chunk
+  //       slot ^ row_swz(row) (source-side swizzle, guide rule 21)
+  // KMAJ: 16 k-rows x 64 B of one 32-wide block; lane -> k-row kr0 + lane/4, chunk lane%4 holding
+  //       mn-chunk (lane%4) ^ kmaj_swz(kr)
+  auto lds_dst = [&](int g, int j) -> int {  // byte offset of the instruction's 1 KiB in the K-step image
+    const int op = g >> 1, s = g & 1, o = wid * 2 + j;
+    if ((op ? LB : LA) == ROW) {
+      const int rb = op == 0 ? (o >> 3) * 128 + s * 64 + (o & 7) * 8 : (o >> 2) * 64 + s * 32 + (o & 3) * 8;
+      return op * OPB + rb * 128;
+    }
+    const int blk = op == 0 ? (o >> 3) * 4 + s * 2 + ((o >> 2) & 1) : (o >> 2) * 2 + s;
+    return op * OPB + blk * 4096 + (o & 3) * 16 * 64;
+  };
+  // per-lane element offset of the source (relative to the operand base + K-step advance) and the
+  // lane's reduction index within the K-step (for ragged tails)
+  auto src_off = [&](int g, int j, long ld, bool main_w, int& kin) -> uint32_t {
+    const int op = g >> 1, s = g & 1, o = wid * 2 + j;
+    if ((op ? LB : LA) == ROW) {
+      const int rb = op == 0 ? (o >> 3) * 128 + s * 64 + (o & 7) * 8 : (o >> 2) * 64 + s * 32 + (o & 3) * 8;
+      const int row = rb + (lane >> 3);
+      const int kc = (lane & 7) ^ row_swz(row);
+      int grow;
+      if (op == 0) grow = min(m0 + row, p.M - 1);
+      else if (EPI == E_SWIGLU && main_w) grow = row < 128 ? tn * 128 + row : Fh + tn * 128 + row - 128;
+      else grow = min(n0 + row, p.N - 1);
+      kin = kc * 8;
+      return (uint32_t)grow * (uint32_t)ld + (uint32_t)(kc * 8);
+    }
+    const int blk = op == 0 ? (o >> 3) * 4 + s * 2 + ((o >> 2) & 1) : (o >> 2) * 2 + s;
+    const int kr = (o & 3) * 16 + (lane >> 2);
+    const int ch = (lane & 3) ^ kmaj_swz(kr);
+    const int col = min((op == 0 ? m0 : n0) + blk * 32 + ch * 8, (op == 0 ? p.M : p.N) - 8);
+    kin = kr;
+    return (uint32_t)kr * (uint32_t)ld + (uint32_t)col;
+  };
+  uint32_t off[4][2];
+  int kin[2][2];  // reduction index of the lane within a K-step: A granules (ROW: k-chunk; KMAJ: k-row)
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int ki;
+      off[g][j] = src_off(g, j, (g >> 1) ? p.ldb : p.lda, true, ki);
+      if (g < 2) kin[g][j] = ki;
+    }
+  // one granule g of K-step t into buffer t & 1 (g is a literal at every call site)
+  auto stage = [&](int g, int t) {
+    const int op = g >> 1;
+    char* img = smem + (t & 1) * BUF;
+    if (t < nk1) {
+      const int k0 = t * 64;
+      const long adv = ((op ? LB : LA) == ROW) ? (long)k0 : (long)k0 * (op ? p.ldb : p.lda);
+      const bf16_t* base = (op ? p.B : p.A) + adv;
+      if (k0 + 64 <= p.K) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+      } else {  // ragged reduction tail: out-of-range k reads the zero page
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          int ki;
+          src_off(g, j, 1, true, ki);
+          const bf16_t* src = k0 + ki < p.K ? base + off[g][j] : p.zpage + (lane & 7) * 8;
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+        }
+      }
+    } else {  // K-extension (LoRA): a few steps, offsets recomputed with the extension strides
+      const int k0 = (t - nk1) * 64;
+      const long ld2 = op ? p.ldb2 : p.lda2;
+      const long adv = ((op ? LB : LA) == ROW) ? (long)k0 : (long)k0 * ld2;
+      const bf16_t* base = (op ? p.B2 : p.A2) + adv;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        int ki;
+        const uint32_t o2 = src_off(g, j, ld2, false, ki);
+        const bf16_t* src = k0 + ki < p.K2 ? base + o2 : p.zpage + (lane & 7) * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+      }
+    }
+  };
+  (void)kin;
+
+  // ---- fragment reads ----
+  i32x8 fa[4], fb0[2], fb1[2];
+  auto rd_row = [&](const char* img, int row) -> i32x8 {
+    const i32x4 lo = *(const i32x4*)(img + row * 128 + ((fq ^ row_swz(row)) << 4));
+    const i32x4 hi = *(const i32x4*)(img + row * 128 + (((4 + fq) ^ row_swz(row)) << 4));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  // KMAJ: fragment of 16 mn starting at mn (multiple of 16) — both 32-deep k halves
+  auto rd_kmaj = [&](const char* img, int mn) -> i32x8 {
+    const int blk = mn >> 5, c0 = mn & 31;
+    const int q = frow >> 2, pp = frow & 3;
+    const int col = c0 + 4 * pp;
+    const char* b = img + blk * 4096;
+    s16x4 v[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {  // h = 2 kk + half
+      const int kr = (h >> 1) * 32 + fq * 8 + (h & 1) * 4 + q;
+      const int ch = (col >> 3) ^ kmaj_swz(kr);
+      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + kr * 64 + ch * 16 + (col & 7) * 2));
+    }
+    typedef __attribute__((ext_vector_type(16))) short s16x16;
+    const s16x16 w = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3],
+                      v[2][0], v[2][1], v[2][2], v[2][3], v[3][0], v[3][1], v[3][2], v[3][3]};
+    return __builtin_bit_cast(i32x8, w);
+  };
+  auto read_a = [&](int buf, int s) {
+    const char* img = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 128 + s * 64 + i * 16;
+      fa[i] = LA == ROW ? rd_row(img, row + frow) : rd_kmaj(img, row);
+    }
+  };
+  auto read_b = [&](int buf, int s, i32x8 (&fb)[2]) {
+    const char* img = smem + buf * BUF + OPB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (wc >> 1) * 128 + (wc & 1) * 64 + s * 32 + j * 16;
+      fb[j] = LB == ROW ? rd_row(img, row + frow) : rd_kmaj(img, row);
+    }
+  };
+  auto half = [](const i32x8& v, int h) -> bf16x8 {
+    return h == 0 ? __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 0, 1, 2, 3))
+                  : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // SWAP: B fragment as the MFMA's A operand -> the accumulator holds C^T, i.e. every lane owns
+  // 4 CONSECUTIVE output columns of one row (16-B fp32 / 8-B bf16 epilogue stores instead of
+  // 2-4-B scattered ones). The atomic form keeps C (16 consecutive columns per 16 lanes per row).
+  constexpr bool SWAP = OUT != O_F32_ATOMIC;
+#define GB_MMA(SA, SB, FB)                                                                   \
+  do {                                                                                      \
+    GB_BARRIER();                                                                           \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    __builtin_amdgcn_s_setprio(1);                                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                           \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                         \
+        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                    \
+          acc[(SA) * 4 + i][(SB) * 2 + j] = SWAP                                            \
+              ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(half(FB[j], kk), half(fa[i], kk),   \
+                                                        acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0) \
+              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(half(fa[i], kk), half(FB[j], kk),   \
+                                                        acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                          \
+    GB_BARRIER();                                                                           \
+  } while (0)
+
+  if (t_begin < t_end) {
+    // prologue: step t_begin complete (a0, b0, b1, a1) + a0, b0 of step t_begin + 1; granules are
+    // always issued in key order a0(u) b0(u) b1(u) a1(u) a0(u+1) b0(u+1) ... (see header)
+    const bool two = t_begin + 1 < t_end;
+    stage(0, t_begin); stage(2, t_begin); stage(3, t_begin); stage(1, t_begin);
+    if (two) { stage(0, t_begin + 1); stage(2, t_begin + 1); }
+    wait_granules(two ? 4 : 2);  // retire a0, b0 of t_begin
+    GB_BARRIER();  // raw: a __syncthreads() would drain the granules still in flight
+    if (wr == 1) GB_BARRIER();
+
+    // steady state: every granule staged by steps t < t_fast is a full main-K step (no tail, no
+    // extension, no end-of-range checks): straight-line phases with fixed counted waits
+    const int nk1f = p.K / 64;
+    const int t_fast = min(t_end, nk1f) - 2;
+    auto stage_fast = [&](int g, int u) {
+      const int op = g >> 1;
+      const long adv = ((op ? LB : LA) == ROW) ? (long)u * 64 : (long)u * 64 * (op ? p.ldb : p.lda);
+      const bf16_t* base = (op ? p.B : p.A) + adv;
+      char* img = smem + (u & 1) * BUF;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+    };
+    int t = t_begin;
+    for (; t < t_fast; ++t) {
+      const int buf = t & 1;
+      read_a(buf, 0);
+      read_b(buf, 0, fb0);
+      stage_fast(3, t + 1);
+      wait_granules(4);
+      GB_MMA(0, 0, fb0);
+      read_b(buf, 1, fb1);
+      stage_fast(1, t + 1);
+      wait_granules(4);
+      GB_MMA(0, 1, fb1);
+      read_a(buf, 1);
+      stage_fast(0, t + 2);
+      GB_MMA(1, 1, fb1);
+      stage_fast(2, t + 2);
+      wait_granules(4);
+      GB_MMA(1, 0, fb0);
+    }
+    for (; t < t_end; ++t) {
+      const int buf = t & 1;
+      const bool n1 = t + 1 < t_end, n2 = t + 2 < t_end;
+      // p1: quadrant a0 x b0; stage b1(t+1); retire b1(t) (issued after it: a1(t), a0 / b0 / b1 (t+1))
+      read_a(buf, 0);
+      read_b(buf, 0, fb0);
+      if (n1) stage(3, t + 1);
+      wait_granules(n1 ? 4 : 1);
+      GB_MMA(0, 0, fb0);
+      // p2: a0 x b1; stage a1(t+1); retire a1(t)
+      read_b(buf, 1, fb1);
+      if (n1) stage(1, t + 1);
+      wait_granules(n1 ? 4 : 0);
+      GB_MMA(0, 1, fb1);
+      // p3: a1 x b1; stage a0(t+2)
+      read_a(buf, 1);
+      if (n2) stage(0, t + 2);
+      GB_MMA(1, 1, fb1);
+      // p4: a1 x b0; stage b0(t+2); retire a0 / b0 of t+1 (after them: b1 / a1 (t+1), a0 / b0 (t+2))
+      if (n2) stage(2, t + 2);
+      if (n1) wait_granules(n2 ? 4 : 2);
+      GB_MMA(1, 0, fb0);
+    }
+    if (wr == 0) GB_BARRIER();
+  }
+#undef GB_MMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue ----
+  // SWAP: acc[i][j][r] = C[m0 + 128 wr + 16 i + frow][n0 + 64 wc + 16 j + 4 fq + r]
+  // else: acc[i][j][r] = C[m0 + 128 wr + 16 i + 4 fq + r][n0 + 64 wc + 16 j + frow]
+  if constexpr (OUT == O_F32_ATOMIC) {
+    float* C = (float*)p.C;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + frow;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
+          if (row < p.M && col < p.N)
+            __hip_atomic_fetch_add(C + (long)row * p.ldc + col, acc[i][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+  } else if constexpr (OUT == O_F32 || OUT == O_F32_SLAB) {
+    // O_F32_SLAB: split ks writes its partial tile to slab ks ([nsplit][M][ldc], plain stores);
+    // splitk_reduce_kernel sums the slabs and runs the epilogue. N % 4 == 0 (launcher).
+    float* C = (float*)p.C + (OUT == O_F32_SLAB ? (long)blockIdx.y * p.M * p.ldc : 0L);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + fq * 4;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (OUT == O_F32 && p.bias && col < p.N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[col + r]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = m0 + wr * 128 + i * 16 + frow;
+        if (row < p.M && col < p.N) {
+          float4 v;
+          v.x = act_fn(acc[i][j][0] + bv[0], EPI);
+          v.y = act_fn(acc[i][j][1] + bv[1], EPI);
+          v.z = act_fn(acc[i][j][2] + bv[2], EPI);
+          v.w = act_fn(acc[i][j][3] + bv[3], EPI);
+          *(float4*)(C + (long)row * p.ldc + col) = v;
+        }
+      }
+    }
+  } else {
+    // bf16 through LDS (two 128-row halves; row stride 260 elements = 520 B: the 8-B ds_write of
+    // 16 lanes in 16 rows hit 16 distinct bank pairs) for 16-B coalesced global stores
+    constexpr int LDT = 256 + 4;
+    bf16_t* tile = (bf16_t*)smem;
+    float bcol[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + fq * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bcol[j][r] = (EPI != E_SWIGLU && p.bias && col < p.N) ? bf2f(p.bias[col + r]) : 0.f;
+    }
+    auto ld16 = [&](int row, int c8) -> uint4 {  // 8 bf16 at tile[row][8 c8], 8-B aligned
+      const uint2 lo = *(const uint2*)(tile + row * LDT + c8 * 8);
+      const uint2 hi = *(const uint2*)(tile + row * LDT + c8 * 8 + 4);
+      return make_uint4(lo.x, lo.y, hi.x, hi.y);
+    };
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      if (wr == hh) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = i * 16 + frow, col = wc * 64 + j * 16 + fq * 4;
+            float y[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = EPI == E_SWIGLU ? acc[i][j][r] : act_fn(acc[i][j][r] + bcol[j][r], EPI);
+            *(uint2*)(tile + row * LDT + col) = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+          }
+      }
+      __syncthreads();
+      if constexpr (EPI == E_SWIGLU) {
+        // tile columns [0,128) = gate F-cols tn*128.., [128,256) = up; f = silu(g) * u from the
+        // bf16-rounded pre-activations (bitwise what a separate SwiGLU kernel would read)
+        bf16_t* Cf = (bf16_t*)p.C;
+        const int cc = tid & 15;
+#pragma unroll
+        for (int pass = 0; pass < 4; ++pass) {
+          const int row = pass * 32 + (tid >> 4);
+          const int grow = m0 + hh * 128 + row;
+          if (grow < p.M) {
+            const uint4 g4 = ld16(row, cc), u4 = ld16(row, 16 + cc);
+            float g[8], u[8], f[8];
+            unpack8(g4, g);
+            unpack8(u4, u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = g[e] / (1.f + __expf(-g[e])) * u[e];
+            const int fcol = tn * 128 + cc * 8;
+            *(uint4*)(Cf + (long)grow * p.ldc + fcol) = pack8(f);
+            if (p.C2) {
+              *(uint4*)(p.C2 + (long)grow * p.ldc2 + fcol) = g4;
+              *(uint4*)(p.C2 + (long)grow * p.ldc2 + Fh + fcol) = u4;
+            }
+          }
+        }
+      } else {
+        bf16_t* C = (bf16_t*)p.C;
+        const int cc = tid & 31;
+#pragma unroll
+        for (int pass = 0; pass < 8; ++pass) {
+          const int row = pass * 16 + (tid >> 5);
+          const int grow = m0 + hh * 128 + row, gcol = n0 + cc * 8;
+          if (grow < p.M && gcol < p.N) {
+            uint4 v = ld16(row, cc);
+            if (p.R) {  // residual in fp32 on the bf16-rounded GEMM result (= a separate add kernel)
+              float y[8], r[8];
+              unpack8(v, y);
+              unpack8(*(const uint4*)(p.R + (long)grow * p.ldr + gcol), r);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[e] += r[e];
+              v = pack8(y);
+            }
+            *(uint4*)(C + (long)grow * p.ldc + gcol) = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Split-K reduction + epilogue of the O_F32_SLAB form (decode / small-M GEMMs, M <= 256):
+//   C[m, c] = act( sum_s slab[s][m][c] + bias[c] ) + R[m, c]            (Nout = N)
+//   C[m, c] = silu(bf16(g)) * bf16(u),  g / u = sum_s slab[s][m][c] / [F + c]   (SwiGLU, Nout = F)
+// 8 output columns per thread, 16-B slab loads, all nsplit partial loads of a thread in flight.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slabs, int nsplit, int M, int N,
+                                                            const bf16_t* __restrict__ bias, int act,
+                                                            const bf16_t* __restrict__ R, long ldr,
+                                                            bf16_t* __restrict__ C, long ldc) {
+  const bool swiglu = act == E_SWIGLU;
+  const int Nout = swiglu ? N / 2 : N;
+  const int cpr = Nout / 8;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)M * cpr) return;
+  const int m = (int)(e / cpr), c0 = (int)(e % cpr) * 8;
+  const long sstride = (long)M * N;
+  float a[8], b[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) a[q] = b[q] = 0.f;
+  const float* base = slabs + (long)m * N + c0;
+  for (int s = 0; s < nsplit; ++s) {
+    const float4 x0 = *(const float4*)(base + s * sstride), x1 = *(const float4*)(base + s * sstride + 4);
+    a[0] += x0.x; a[1] += x0.y; a[2] += x0.z; a[3] += x0.w; a[4] += x1.x; a[5] += x1.y; a[6] += x1.z; a[7] += x1.w;
+    if (swiglu) {
+      const float4 y0 = *(const float4*)(base + s * sstride + Nout), y1 = *(const float4*)(base + s * sstride + Nout + 4);
+      b[0] += y0.x; b[1] += y0.y; b[2] += y0.z; b[3] += y0.w; b[4] += y1.x; b[5] += y1.y; b[6] += y1.z; b[7] += y1.w;
+    }
+  }
+  float y[8];
+  if (swiglu) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float g = bf2f(f2bf(a[q])), u = bf2f(f2bf(b[q]));
+      y[q] = g / (1.f + __expf(-g)) * u;
+    }
+  } else {
+    float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (bias) unpack8(*(const uint4*)(bias + c0), bb);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) y[q] = act_fn(a[q] + bb[q], act);
+    if (R) {
+      // the residual adds to the bf16-rounded GEMM result (= a separate add kernel)
+      unpack8(*(const uint4*)(R + (long)m * ldr + c0), rr);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) y[q] = bf2f(f2bf(y[q])) + rr[q];
+    }
+  }
+  *(uint4*)(C + (long)m * ldc + c0) = pack8(y);
+}
+
+}  // namespace gb
+}  // namespace rt
+
+using namespace rt;
+using namespace rt::gb;
+
+// layout_a / layout_b: 0 = ROW (K contiguous), 1 = KMAJ (M / N contiguous).
+// out: 0 bf16 (epilogue bias + act, or SwiGLU), 1 fp32 store (bias + act), 2 fp32 atomic add
+// (split-K; C must be initialised by the caller). Requirements (checked): KMAJ operands have
+// M / N % 8 == 0 and 16-B aligned rows; ROW operands 16-B aligned rows; K, K2 % 8 == 0;
+// E_SWIGLU: ROW/ROW, bf16 out, N % 256 == 0, no K-extension of B beyond the weight rows.
+extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb,
+                           const void* A2, long lda2, const void* B2, long ldb2, int K2, const void* bias,
+                           void* C, long ldc, void* C2, long ldc2, const void* R, long ldr, int M, int N, int K,
+                           int act, int out, int nsplit, const void* zpage, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  // a ROW operand reads 8-element k-chunks: its reduction length must be a multiple of 8
+  const bool any_row = layout_a == ROW || layout_b == ROW;
+  if ((any_row && (K % 8 || (A2 && K2 % 8))) || !zpage) return -1;
+  if (R && (out != O_BF16 || act == E_SWIGLU)) return -6;
+  if ((out == O_F32 || out == O_F32_SLAB) && (N % 4 || ldc % 4)) return -7;  // 16-B fp32 row stores
+  if ((layout_a == KMAJ && M % 8) || (layout_b == KMAJ && N % 8)) return -1;
+  if (nsplit < 1) nsplit = 1;
+  if (nsplit > 1 && out != O_F32_ATOMIC && out != O_F32_SLAB) return -2;
+  if (act == E_SWIGLU && (layout_a != ROW || layout_b != ROW || out != O_BF16 || N % 256)) return -3;
+  if (act != E_NONE && (layout_a != ROW || layout_b != ROW || out != O_BF16)) return -5;
+  Args p;
+  p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
+  p.A2 = (A2 && B2) ? (const bf16_t*)A2 : nullptr; p.lda2 = lda2;
+  p.B2 = (const bf16_t*)B2; p.ldb2 = ldb2; p.K2 = K2;
+  p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = (bf16_t*)C2; p.ldc2 = ldc2;
+  p.R = (const bf16_t*)R; p.ldr = ldr;
+  p.M = M; p.N = N; p.K = K; p.act = act; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
+  const int tiles_n = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
+  dim3 grid(((M + 255) / 256) * tiles_n, nsplit), block(512);
+  const int key = layout_a * 100 + layout_b * 10 + out;
+#define GB_LAUNCH(LA, LB, O, E) hipLaunchKernelGGL((gemm_big_kernel<LA, LB, O, E>), grid, block, 0, stream, p)
+  if (key == 0) {  // NT, bf16 out: the activation is a template parameter (no runtime switch in the epilogue)
+    switch (act) {
+      case E_NONE: GB_LAUNCH(ROW, ROW, O_BF16, E_NONE); break;
+      case E_RELU: GB_LAUNCH(ROW, ROW, O_BF16, E_RELU); break;
+      case E_GELU: GB_LAUNCH(ROW, ROW, O_BF16, E_GELU); break;
+      case E_GELU_TANH: GB_LAUNCH(ROW, ROW, O_BF16, E_GELU_TANH); break;
+      case E_SILU: GB_LAUNCH(ROW, ROW, O_BF16, E_SILU); break;
+      case E_SWIGLU: GB_LAUNCH(ROW, ROW, O_BF16, E_SWIGLU); break;
+      default: return -4;
+    }
+  } else {
+    if (act != E_NONE) return -5;  // fp32 outputs and the NN / TN forms carry no activation
+    switch (key) {
+      case 1: GB_LAUNCH(ROW, ROW, O_F32, E_NONE); break;
+      case 2: GB_LAUNCH(ROW, ROW, O_F32_ATOMIC, E_NONE); break;
+      case 3: GB_LAUNCH(ROW, ROW, O_F32_SLAB, E_NONE); break;
+      case 10: GB_LAUNCH(ROW, KMAJ, O_BF16, E_NONE); break;
+      case 11: GB_LAUNCH(ROW, KMAJ, O_F32, E_NONE); break;
+      case 12: GB_LAUNCH(ROW, KMAJ, O_F32_ATOMIC, E_NONE); break;
+      case 110: GB_LAUNCH(KMAJ, KMAJ, O_BF16, E_NONE); break;
+      case 111: GB_LAUNCH(KMAJ, KMAJ, O_F32, E_NONE); break;
+      case 112: GB_LAUNCH(KMAJ, KMAJ, O_F32_ATOMIC, E_NONE); break;
+      default: return -4;
+    }
+  }
+#undef GB_LAUNCH
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int rt_gemm_splitk_reduce(const float* slabs, int nsplit, int M, int N, const void* bias, int act,
+                                     const void* R, long ldr, void* C, long ldc, hipStream_t stream) {
+  const int Nout = act == E_SWIGLU ? N / 2 : N;
+  if (Nout % 8 || M <= 0) return M <= 0 ? 0 : -1;
+  const long work = (long)M * (Nout / 8);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, slabs, nsplit,
+                     M, N, (const bf16_t*)bias, act, (const bf16_t*)R, ldr, (bf16_t*)C, ldc);
+  RT_LAUNCH_CHECK();
+  return 0;
+}

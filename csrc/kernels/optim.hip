@@ -36,7 +36,9 @@ __global__ __launch_bounds__(256) void grad_sumsq_kernel(const float* __restrict
 
 struct AdamArgs {
   float* p; const float* g; float* m; float* v; bf16_t* pbf; long n;
-  float lr, b1, b2, eps, wd, bc1, bc2, max_norm;
+  float lr, b1, b2, eps, wd;
+  int step;  // optimizer calls so far (this one included); bias correction uses step - *skipped
+  float max_norm;
   const float* partials; int nparts;
   float* norm_out; int* skipped;
   // mixed form: g16 = bf16 gradients of elements [0, n16), g = fp32 gradients of [n16, n) indexed
@@ -85,8 +87,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.norm_out) *a.norm_out = norm;
   const float clip = a.max_norm > 0.f ? fminf(1.f, a.max_norm / (norm + 1e-6f)) : 1.f;
   const float decay = 1.f - a.lr * a.wd;
-  const float step_scale = a.lr / a.bc1;
-  const float inv_bc2_sqrt = rsqrtf(a.bc2);
+  // applied steps = calls - skipped (non-finite) calls, read on the device so a skip decided by an
+  // earlier launch never desynchronises the bias correction from the host's call counter
+  const float tstep = (float)(a.step - (a.skipped ? *a.skipped : 0));
+  const float bc1 = 1.f - powf(a.b1, tstep), bc2 = 1.f - powf(a.b2, tstep);
+  const float step_scale = a.lr / bc1;
+  const float inv_bc2_sqrt = rsqrtf(bc2);
   const long stride = (long)gridDim.x * 256, t = (long)blockIdx.x * 256 + threadIdx.x;
   const long n4 = a.n / 4;
   for (long q = t; q < n4; q += stride) {
@@ -132,9 +138,9 @@ extern "C" int rt_grad_sumsq(const float* g, long n, float* partials, int nparts
 }
 
 extern "C" int rt_adamw(float* p, const float* g, float* m, float* v, void* pbf, long n, float lr, float b1, float b2,
-                        float eps, float wd, float bc1, float bc2, float max_norm, const float* partials, int nparts,
+                        float eps, float wd, int step, float max_norm, const float* partials, int nparts,
                         float* norm_out, int* skipped, hipStream_t stream) {
-  AdamArgs a{p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd, bc1, bc2, max_norm, partials, nparts, norm_out, skipped,
+  AdamArgs a{p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd, step, max_norm, partials, nparts, norm_out, skipped,
              nullptr, 0, pbf ? n : 0};
   long blocks = (n + 255) / 256;
   if (blocks > 2048) blocks = 2048;
@@ -154,11 +160,11 @@ extern "C" int rt_grad_sumsq_mixed(const void* g16, long n16, const float* g32, 
 }
 
 extern "C" int rt_adamw_mixed(float* p, const void* g16, long n16, const float* g32, float* m, float* v, void* p16,
-                              long n, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
+                              long n, float lr, float b1, float b2, float eps, float wd, int step,
                               float max_norm, const float* partials, int nparts, float* norm_out, int* skipped,
                               hipStream_t stream) {
   if (n16 % 4 || n16 > n) return -1;
-  AdamArgs a{p, g32, m, v, (bf16_t*)p16, n, lr, b1, b2, eps, wd, bc1, bc2, max_norm, partials, nparts, norm_out, skipped,
+  AdamArgs a{p, g32, m, v, (bf16_t*)p16, n, lr, b1, b2, eps, wd, (int)step, max_norm, partials, nparts, norm_out, skipped,
              (const bf16_t*)g16, n16, n16};
   long blocks = (n / 4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;

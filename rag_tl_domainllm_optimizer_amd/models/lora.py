@@ -81,18 +81,16 @@ def _group_out(cfg, group: str) -> int:
             "down": cfg.hidden_size, "fc1": cfg.intermediate_size, "fc2": cfg.hidden_size}[group]
 
 
-def attach_lora(model, r=16, alpha=32.0, targets=None, dropout=0.0, seed=0, ext_layout=None):
+def attach_lora(model, r=16, alpha=32.0, targets=None, dropout=0.0, seed=0):
     cfg = model.cfg
     gm = group_map(cfg)
     if targets is None or targets == "all":
         targets = list(gm.keys())
     targets = [t for t in targets if t in gm]
-    if dropout:
-        raise NotImplementedError("lora_dropout > 0 is not supported by the fused LoRA GEMM path")
+    if not 0.0 <= dropout < 1.0:
+        raise ValueError(f"lora_dropout must be in [0, 1), got {dropout}")
     lcfg = LoraConfig(r=r, lora_alpha=alpha, lora_dropout=dropout, target_modules=list(targets),
                       base_model_name_or_path=cfg.name)
-    if ext_layout is None:
-        ext_layout = os.environ.get("RAGTL_LORA_EXT", "1") == "1"
     g = torch.Generator(device="cpu").manual_seed(seed)
     dev = model.embed.device
     for layer in model.layers:
@@ -118,11 +116,8 @@ def attach_lora(model, r=16, alpha=32.0, targets=None, dropout=0.0, seed=0, ext_
                 b_list.append(pb)
                 c0s.append(row0)
                 scales.append(lcfg.scaling)
-            layer.lora[grp] = ops.LoRAGroup(projs, a_list, b_list, c0s, scales, _group_out(cfg, grp))
-            # GPU: store the frozen base weight as [W | UB] so the token-parallel LoRA forward is
-            # one plain library GEMM (ops.linear, "Extended-weight layout")
-            if ext_layout:
-                layer.lora[grp].attach_ext(_group_weight(layer, cfg, grp))
+            layer.lora[grp] = ops.LoRAGroup(projs, a_list, b_list, c0s, scales, _group_out(cfg, grp),
+                                            dropout=float(dropout))
     model.lora_config = lcfg
     model.refresh_lora()
     return lcfg
@@ -196,17 +191,11 @@ def merge_lora(model, sign: float = 1.0):
 @torch.no_grad()
 def merge_and_drop_lora(model):
     """Fold every adapter into its base weight (W += s B A) and remove the adapters, leaving a plain
-    model (full fine-tuning after a LoRA stage, merged export). Base weights kept in the extended
-    [W | UB] layout move back to storage of their own."""
+    model (full fine-tuning after a LoRA stage, merged export)."""
     if getattr(model, "lora_config", None) is None:
         return
     merge_lora(model)
-    cfg = model.cfg
     for layer in model.layers:
-        for grp_name, grp in layer.lora.items():
-            if grp.ext is not None:
-                w = _group_weight(layer, cfg, grp_name)
-                w.data = w.data.contiguous()
         layer.lora = {}
         layer.lora_params = nn.ParameterDict()
     del model.lora_config

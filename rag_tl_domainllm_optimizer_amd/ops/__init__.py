@@ -1,7 +1,8 @@
 """Public op API. One entry per native kernel; GPU tensors run the gfx950 HIP kernels, CPU tensors
 the eager reference implementations (:mod:`.reference`, also the test oracles)."""
 from ._ext import native, native_available, on_gpu  # noqa: F401
-from .linear import ACT_IDS, ACT_SWIGLU, FoldCache, LoRAGroup, gemm, gemm_decode, linear, set_gemm_backend  # noqa: F401
+from .linear import (  # noqa: F401
+    ACT_IDS, ACT_SWIGLU, KMAJ, ROW, FoldCache, LoRAGroup, gemm, gemm_big, gemm_decode, gemm_nn, gemm_tn, linear)
 from .norm import layer_norm, rms_norm  # noqa: F401
 from .attention import (  # noqa: F401
     attention, decode_attention, decode_step_attention, decode_step_attention_o, decode_workspace, flash_attention_qkv,

@@ -1,23 +1,24 @@
 """Linear projections: frozen/trainable base weight + fused LoRA adapters + bias/activation.
 
-GPU forward is one MFMA GEMM in which the LoRA term rides on the same accumulators as extra
-K-steps:  ``Y = act(X W^T + U UB^T + b)`` with ``U = X A_pad^T`` (A_pad = scaling * A, zero-padded
-to a multiple of 64 rows) computed by a small GEMM first. Several adapters on one fused projection
+Every GPU GEMM is a hand-written MFMA kernel; dispatch is by shape only (no library backend):
+  * M <= 64 (decode, small batch): the weight-streaming kernels of gemm_bf16.hip (split-K,
+    in-GEMM RMS-norm, SwiGLU / residual epilogues);
+  * M > 64 (prefill, reference scoring, training): the 256x256 MFMA family of gemm_big.hip in
+    three operand layouts — NT forward, NN input gradient (W read transposed in-kernel), TN weight
+    / LoRA gradients (split-K, fp32).
+
+LoRA: ``Y = act(X W^T + U UB^T + b)`` with ``U = X A_pad^T`` (A_pad = scaling x A,
+zero-padded to a multiple of 64 rows). U is a narrow split-K pass; ``U UB^T`` then rides on the
+base GEMM's accumulators as extra K-steps (the K-extension operands of gemm_big), so the adapter
+product needs no output pass and no concatenated copy. Several adapters on one fused projection
 (q|k|v, gate|up) share one padded rank dimension, with UB block-diagonal.
-
-Extended-weight layout (``LoRAGroup.attach_ext``): a frozen base weight that carries adapters is
-stored ONCE as ``ext = [W | UB]`` ([N, K + Rp], the parameter becomes the strided view
-``ext[:, :K]`` and ``UB`` the view ``ext[:, K:]``), so the token-parallel (M > 64) LoRA forward is
-ONE plain GEMM ``[X | U] @ ext^T`` on hipBLASLt — measured 1.2-1.5 PF/s on the PPO-update shapes
-against 0.7-1.05 PF/s for the hand-written fused kernel (tools/update_gemm_probe.py,
-profiles/update_gemm_probe.log). Decode / skinny shapes keep the hand-written kernels.
-
-Backward (training): dX = dY W + dU A_pad, dA = s dU^T X, dB = dY^T U, dW = dY^T X (full FT) are
-plain library GEMMs (torch.matmul -> hipBLASLt); only the forward carries fused epilogues.
+Backward: dX = dY W + dU A_pad (one NN GEMM with the same K-extension), dU = dY UB,
+dA = s dU^T X, dB = dY^T U (TN, fp32), dW = dY^T X (full fine-tuning).
+The reference runs these products through HF/PyTorch (reinforcement_learning_optimization_after_rag
+.py:200-209 forward, :229 backward).
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -30,53 +31,101 @@ ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new":
 ACT_SWIGLU = 5  # w = [gate; up] (2F rows) -> silu(x gate^T) * (x up^T), [.., F]
 
 
-# Plain GEMMs (no LoRA K-extension, bias or activation epilogue, bf16 out) pick a backend by M:
-#   M <= 16      SKINNY_BACKEND, default "native": split-K MFMA weight-streaming kernel, measured
-#                faster than hipBLASLt on cold (HBM-streamed) decode weights at batch 1-8
-#                (profiles/kernels_skinny_cold.log: qkv 16.5 vs 19.5 us, o 11.4 vs 19.0 us,
-#                gate_up 46.9 vs 56.0 us, lm_head 47.8 vs 57.4 us)
-#   16 < M <= 64 MID_BACKEND, default "auto": the LDS-DMA ring kernel for deep weights (K >= 8192:
-#                down 36.6 vs 39.8 us), hipBLASLt for the rest (qkv 18 vs 26, o 15 vs 21, gate_up
-#                49-52 vs 58, lm_head 54-58 vs 58 us) — hipGraph replay over distinct weights at
-#                M = 64, profiles/kernels_decode_split_sweep.log
-#   M > 64       PLAIN_BACKEND, default "lib" (hipBLASLt ~1.5 PF/s vs ~1.2 PF/s for the 256x256
-#                8-phase kernel on plain GEMMs)
-# Everything with a fused epilogue or a LoRA term always runs on the hand-written kernels.
-PLAIN_BACKEND = os.environ.get("RAGTL_PLAIN_GEMM", "lib")
-MID_BACKEND = os.environ.get("RAGTL_MID_GEMM", "auto")
-SKINNY_BACKEND = os.environ.get("RAGTL_SKINNY", "native")
+def splitk_plan(M: int, N: int, K: int, act: int = 0) -> int:
+    """Split-K factor for an NT GEMM whose 256x256 tiles cannot fill the 256 CUs (decode at batch
+    65..256, narrow outputs): ~256 workgroups, >= 4 K-steps each; 1 = the plain tiled kernel."""
+    tiles = ((M + 255) // 256) * (N // 256 if act == ACT_SWIGLU else (N + 255) // 256)
+    if tiles >= 128 or M > 1024:
+        return 1
+    nk = (K + 63) // 64
+    return max(1, min(nk // 4, (256 + tiles // 2) // tiles))
 
 
-def set_gemm_backend(plain: Optional[str] = None, skinny: Optional[str] = None, mid: Optional[str] = None):
-    """Select "lib" (hipBLASLt) or "native" (hand-written kernels) for plain GEMMs by M range;
-    returns the previous (plain, skinny, mid) triple."""
-    global PLAIN_BACKEND, SKINNY_BACKEND, MID_BACKEND
-    prev = (PLAIN_BACKEND, SKINNY_BACKEND, MID_BACKEND)
-    for name, val in (("PLAIN_BACKEND", plain), ("SKINNY_BACKEND", skinny), ("MID_BACKEND", mid)):
-        if val is not None:
-            assert val in ("lib", "native", "auto")
-            globals()[name] = val
-    return prev
-
-
-def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None):
-    """Raw (non-autograd) fused GEMM on 2-D row-major operands."""
+def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None,
+         residual=None, nsplit: int = 0):
+    """Raw (non-autograd) fused GEMM on 2-D row-major operands: act(x w^T + u ub^T + bias) (+ residual).
+    M <= 64: weight-streaming kernels; small M with few output tiles: split-K fp32 slabs + fused
+    reduce epilogue (``nsplit`` overrides the plan); otherwise the 256x256 MFMA kernel."""
     if on_gpu(x):
-        if u is None and bias is None and act == 0 and not out_f32:
-            M = x.shape[0]
-            backend = SKINNY_BACKEND if M <= 16 else (MID_BACKEND if M <= 64 else PLAIN_BACKEND)
-            if backend == "auto":
-                backend = "native" if w.shape[1] >= 8192 else "lib"
-            # the hand-written kernels store 8-column vectors: an output width that is not a multiple
-            # of 8 (e.g. OpenChat's 32002-token vocabulary) takes the library GEMM
-            if backend == "lib" or w.shape[0] % 8:
-                return torch.matmul(x, w.t(), out=out)
-        return native().gemm(x, w, u, ub, bias, act, out_f32, out)
+        M, K = x.shape
+        N = w.shape[0]
+        if M <= 64 and residual is None:
+            return native().gemm(x, w, u, ub, bias, act, out_f32, out)
+        s = nsplit or (splitk_plan(M, N, K, act) if (u is None and not out_f32 and N % 16 == 0) else 1)
+        if s > 1:
+            slabs = torch.empty(s * M * N, dtype=torch.float32, device=x.device)
+            return native().gemm_splitk(x, w, s, slabs, bias, act, out, residual)
+        return native().gemm_big(x, w, ROW, ROW, u, ub, bias, act, 1 if out_f32 else 0, 1, out, None, residual)
     y = ref.gemm(x, w, u, ub, bias, act, out_f32)
+    if residual is not None:
+        y = (y.float() + residual.float()).to(y.dtype)
     if out is not None:
         out.copy_(y)
         return out
     return y
+
+
+ROW, KMAJ = 0, 1  # operand layouts of the token-parallel GEMM family (csrc/kernels/gemm_big.hip)
+
+
+def _op(t: torch.Tensor, layout: int, trans_for_a: bool) -> torch.Tensor:
+    """Logical operand of the CPU oracle: A as [M, K] / B as [K, N]."""
+    if trans_for_a:
+        return t if layout == ROW else t.t()
+    return t.t() if layout == ROW else t
+
+
+def gemm_big(a, b, la: int, lb: int, a2=None, b2=None, bias=None, act: int = 0, out_mode: int = 0,
+             nsplit: int = 1, out=None, out2=None):
+    """C = epi(A·B + A2·B2) with per-operand layouts (ROW: K contiguous, KMAJ: M / N contiguous).
+    GPU: one hand-written MFMA kernel (gemm_big_kernel); CPU: fp32 oracle (tests, plumbing).
+    out_mode 0 bf16 / 1 fp32 / 2 fp32 accumulate into ``out``; act 5 = SwiGLU over [gate; up]."""
+    if on_gpu(a):
+        return native().gemm_big(a, b, la, lb, a2, b2, bias, act, out_mode, nsplit, out, out2)
+    A = _op(a, la, True).float()
+    B = _op(b, lb, False).float()
+    y = A @ B
+    if a2 is not None:
+        y = y + _op(a2, la, True).float() @ _op(b2, lb, False).float()
+    if act == ACT_SWIGLU:
+        F = y.shape[1] // 2
+        pre = y.to(a.dtype)
+        if out2 is not None:
+            out2.copy_(pre)
+        g, u = pre[:, :F].float(), pre[:, F:].float()
+        y = torch.nn.functional.silu(g) * u
+    else:
+        if bias is not None:
+            y = y + bias.float()
+        y = ref.apply_act(y, act)
+    if out_mode == 2:
+        out.add_(y)
+        return out
+    y = y.to(a.dtype if out_mode == 0 else torch.float32)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def gemm_nn(dy: torch.Tensor, w: torch.Tensor, du=None, a_pad=None) -> torch.Tensor:
+    """dX = dY W (+ dU A_pad): W [N, K] is read K-contiguous-transposed in-kernel (no W^T copy)."""
+    return gemm_big(dy, w, ROW, KMAJ, du, a_pad)
+
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, nsplit: int = 0, out=None) -> torch.Tensor:
+    """a^T b in fp32 (weight / LoRA gradients): a [T, P], b [T, Q] -> [P, Q]; the token reduction
+    is split over ``nsplit`` workgroup rows (0 = fill the chip) with fp32 atomic accumulation."""
+    T, P = a.shape
+    Q = b.shape[1]
+    if nsplit <= 0:
+        tiles = ((P + 255) // 256) * ((Q + 255) // 256)
+        nsplit = max(1, min(64, 256 // max(tiles, 1), T // 512))
+    if out is None:
+        out = torch.zeros(P, Q, dtype=torch.float32, device=a.device)
+    else:
+        out.zero_()
+    return gemm_big(a, b, KMAJ, KMAJ, out_mode=2, nsplit=nsplit, out=out)
 
 
 @dataclass
@@ -103,8 +152,8 @@ class LoRAGroup:
     use_merged: bool = False
     merged: Optional[torch.Tensor] = None
     merged_dirty: bool = True
-    # [W | UB] storage of the base weight (attach_ext); None = W stored on its own
-    ext: Optional[torch.Tensor] = None
+    # PEFT lora_dropout on the adapter input (training forwards only)
+    dropout: float = 0.0
 
     @property
     def rank_total(self) -> int:
@@ -115,35 +164,6 @@ class LoRAGroup:
         return max(64, (self.rank_total + 63) // 64 * 64)
 
     @torch.no_grad()
-    def attach_ext(self, w: torch.nn.Parameter) -> bool:
-        """Re-home the base weight ``w`` [N, K] into ``ext = [W | UB]`` (one copy, then W's old
-        storage is released); ``w.data`` becomes the strided view ``ext[:, :K]``. GPU bf16 only."""
-        if not (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.shape[0] == self.n_out):
-            return False
-        N, K = w.shape
-        rp = self.rp
-        # deep K (down_proj, K = 14336): pad so K + Rp is a multiple of 256 — hipBLASLt runs K = 14400
-        # 1.65x slower than K = 14336 or 14592 (profiles/lora_fwd_probe.log); shallow K keeps Rp = 64
-        # (K = 4160 is within 0-6 % of the adapter-free GEMM)
-        rp_ext = rp if K < 8192 or K % 256 else (rp + 255) // 256 * 256
-        if self.ext is not None and self.ext.shape == (N, K + rp_ext) and self.ext_linked(w):
-            return True
-        ext = torch.empty(N, K + rp_ext, dtype=w.dtype, device=w.device)
-        ext[:, :K].copy_(w.data)
-        ext[:, K:].zero_()
-        w.data = ext[:, :K]
-        self.ext = ext
-        self.a_pad = None  # rebuilt by refresh() with ub as a view of ext
-        self.refresh(dtype=w.dtype)
-        return True
-
-    def ext_linked(self, w: torch.Tensor) -> bool:
-        """True if ``w`` still is the W-view of ``ext`` (something may have replaced w.data)."""
-        e = self.ext
-        return (e is not None and w.data_ptr() == e.data_ptr() and w.shape[0] == e.shape[0]
-                and w.stride(0) == e.stride(0) and w.device == e.device)
-
-    @torch.no_grad()
     def refresh(self, dtype=torch.bfloat16):
         """Rebuild the padded bf16 images from the fp32 parameters (after each optimizer step)."""
         K = self.a[0].shape[1]
@@ -151,11 +171,7 @@ class LoRAGroup:
         rp = self.rp
         if self.a_pad is None or self.a_pad.shape != (rp, K) or self.a_pad.device != dev:
             self.a_pad = torch.zeros(rp, K, dtype=dtype, device=dev)
-            if self.ext is not None and self.ext.device == dev and self.ext.shape[1] - K >= rp:
-                self.ub = self.ext[:, K:K + rp]
-                self.ext[:, K:].zero_()
-            else:
-                self.ub = torch.zeros(self.n_out, rp, dtype=dtype, device=dev)
+            self.ub = torch.zeros(self.n_out, rp, dtype=dtype, device=dev)
         self.r0 = []
         r = 0
         for a, b, c0, s in zip(self.a, self.b, self.col0, self.scale):
@@ -169,15 +185,14 @@ class LoRAGroup:
     @torch.no_grad()
     def merged_weight(self, w: torch.Tensor, rows_per_chunk: int = 4096) -> torch.Tensor:
         """W + UB A_pad (fp32 accumulate, one bf16 rounding), updated IN PLACE so captured graphs
-        that read it stay valid across adapter updates. On the GPU: copy W, then one bf16 GEMM with
-        beta = 1 (4 B of traffic per weight element instead of the 20 B of an fp32 round trip)."""
+        that read it stay valid across adapter updates. On the GPU one NN GEMM (K = Rp) with W as
+        the residual input of its epilogue: 4 B of traffic per weight element."""
         if self.merged is None or self.merged.shape != w.shape or self.merged.device != w.device:
             self.merged = torch.empty(w.shape, dtype=w.dtype, device=w.device)
             self.merged_dirty = True
         if self.merged_dirty:
             if on_gpu(w) and w.dtype == torch.bfloat16:
-                self.merged.copy_(w)
-                self.merged.addmm_(self.ub, self.a_pad)
+                native().gemm_big(self.ub, self.a_pad, ROW, KMAJ, None, None, None, 0, 0, 1, self.merged, None, w)
             else:
                 for r0 in range(0, w.shape[0], rows_per_chunk):
                     r1 = min(w.shape[0], r0 + rows_per_chunk)
@@ -187,95 +202,40 @@ class LoRAGroup:
         return self.merged
 
 
-def _mm_tn_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a^T @ b in fp32 for the LoRA weight gradients: a [M, P], b [M, Q] with M = tokens (thousands)
-    and a small output (P or Q = the padded rank). As one GEMM the library tiles only the small
-    output (64-128 workgroups for [64, 4096]: a quarter of the chip); split over M into a batched
-    GEMM of ~512 tiles and summed (the [c, P, Q] partials are a few MB)."""
-    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype):
-        return a.float().t() @ b.float()
-    M, P = a.shape
-    Q = b.shape[1]
-    tiles = max(1, ((P + 63) // 64) * ((Q + 63) // 64))
-    c = 1
-    while c * tiles < 512 and M % (2 * c) == 0 and M // (2 * c) >= 256:
-        c *= 2
-    if c == 1:
-        return torch.mm(a.t(), b, out_dtype=torch.float32)
-    part = torch.bmm(a.view(c, M // c, P).transpose(1, 2), b.view(c, M // c, Q), out_dtype=torch.float32)
-    return part.sum(0)
-
-
-def _mm_splitk(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a @ b for the LoRA rank-sized products (a [M, K] tokens x features, b [K, Rp], a view is fine):
-    a deep reduction (K up to 28672) into a narrow [M, Rp] output, which one library GEMM tiles into
-    only M/64 workgroups. Split K into a batched GEMM of ~512 tiles (fp32 partials [c, M, Rp], a
-    few MB, summed). Used for U = X A^T (forward) and dU = dY UB (backward)."""
+def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int) -> torch.Tensor:
+    """a [M, K] (ROW) times a narrow operand b (ROW [R, K] or KMAJ [K, R]; R = padded LoRA rank) ->
+    [M, R] bf16. One 256-row tile per 256 tokens cannot fill the chip, so the reduction is split
+    over workgroup rows with fp32 atomic accumulation (U = X A_pad^T forward, dU = dY UB backward)."""
     M, K = a.shape
-    N = b.shape[1]
-    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype):
-        return a @ b
-    tiles = max(1, ((M + 63) // 64) * ((N + 63) // 64))
-    c = 1
-    while c * tiles < 512 and K % (2 * c) == 0 and K // (2 * c) >= 512:
-        c *= 2
-    if c == 1:
-        return a @ b
-    Kc = K // c
-    part = torch.bmm(a.unflatten(1, (c, Kc)).transpose(0, 1), b.unflatten(0, (c, Kc)), out_dtype=torch.float32)
-    return part.sum(0).to(a.dtype)
+    R = b.shape[0] if lb == ROW else b.shape[1]
+    if not on_gpu(a):
+        B = b.float().t() if lb == ROW else b.float()
+        return (a.float() @ B).to(a.dtype)
+    tiles = (M + 255) // 256
+    nsplit = max(1, min(K // 256, (512 + tiles - 1) // tiles))
+    acc = torch.zeros(M, R, dtype=torch.float32, device=a.device)
+    native().gemm_big(a, b, ROW, lb, None, None, None, 0, 2, nsplit, acc)
+    return acc.to(a.dtype)
 
 
-EXT_MIN_M = 65  # token-parallel shapes take the [X | U] @ [W | UB]^T library GEMM
-
-
-def _use_ext(x2, w, bias, act, lora) -> bool:
-    return (lora is not None and lora.ext is not None and bias is None and act == 0 and on_gpu(x2)
-            and x2.shape[0] >= EXT_MIN_M and lora.ext_linked(w))
-
-
-def _ext_forward(x2: torch.Tensor, lora: LoRAGroup):
-    """y = [X | U] @ ext^T with U = X A_pad^T written next to X: returns (y, x view, u view)."""
-    M, K = x2.shape
-    rp = lora.a_pad.shape[0]
-    xe = torch.empty(M, lora.ext.shape[1], dtype=x2.dtype, device=x2.device)
-    xv, uv = xe[:, :K], xe[:, K:K + rp]
-    if xe.shape[1] > K + rp:
-        xe[:, K + rp:].zero_()
-    xv.copy_(x2)
-    uv.copy_(_mm_splitk(x2, lora.a_pad.t()))
-    return torch.matmul(xe, lora.ext.t()), xv, uv
-
-
-def _mm_nn_deep(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a [M, K] @ b [K, N] for a deep reduction into a narrow output (dX of gate_up: K = 28672 into
-    N = 4096): one GEMM tiles only ceil(M/256) x 16 = 304 tiles at M = 4800 (1.2 waves on 256 CUs);
-    split K four ways into a batched GEMM with fp32 partials, summed: 1448 -> 1116 us at M = 4800,
-    1758 -> 1432 us at M = 7168 (profiles/splitk_probe.log). Shallow reductions lose with the split
-    (dX of qkv / o), so only K >= 16384 takes it."""
-    M, K = a.shape
-    N = b.shape[1]
-    tiles = ((M + 255) // 256) * ((N + 255) // 256)
-    if not (a.is_cuda and a.dtype == torch.bfloat16 and K >= 16384 and K % 4 == 0 and tiles < 1024
-            and b.stride(1) == 1):
-        return a @ b
-    c = 4
-    kc = K // c
-    part = torch.bmm(a.unflatten(1, (c, kc)).transpose(0, 1), b.unflatten(0, (c, kc)), out_dtype=torch.float32)
-    return part.sum(0).to(a.dtype)
+def _dropout_mask(x: torch.Tensor, p: float) -> torch.Tensor:
+    """Inverted-dropout multiplier (0 or 1/(1-p)) of the adapter input."""
+    keep = torch.empty_like(x, dtype=torch.float32).bernoulli_(1.0 - p)
+    return (keep / (1.0 - p)).to(x.dtype)
 
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], *lora_params):
-        u = ub = None
-        if _use_ext(x2, w, bias, act, lora):
-            y, x2, u = _ext_forward(x2, lora)
-        else:
-            if lora is not None:
-                u = _mm_splitk(x2, lora.a_pad.t()) if x2.shape[0] > 64 else gemm(x2, lora.a_pad)  # [M, Rp] = X (sA)^T
-                ub = lora.ub
-            y = gemm(x2, w, u, ub, bias, act)
+        u = ub = xd = None
+        if lora is not None:
+            xd = x2
+            if lora.dropout > 0:
+                ctx.mask = _dropout_mask(x2, lora.dropout)
+                xd = x2 * ctx.mask
+            u = _narrow(xd, lora.a_pad, ROW)  # [M, Rp] = drop(X) (s A)^T
+            ub = lora.ub
+        y = gemm(x2, w, u, ub, bias, act)
         ctx.act = act
         ctx.lora = lora
         ctx.has_bias = bias is not None
@@ -300,23 +260,31 @@ class _LinearFn(torch.autograd.Function):
             dy = g.to(dy.dtype)
         needs = ctx.needs_input_grad
         dx = dw = db = None
-        du = _mm_splitk(dy, lora.ub) if lora is not None else None  # [M, Rp] (= dL/dU)
+        gpu = on_gpu(dy)
+        du = _narrow(dy, lora.ub, KMAJ) if lora is not None else None  # [M, Rp] = dL/dU
+        mask = getattr(ctx, "mask", None)
         if needs[0]:
-            dx = _mm_nn_deep(dy, w) if on_gpu(dy) else dy @ w
-            if lora is not None:
-                # dX += dU A_pad as a separate K = Rp pass: measured cheaper than seeding dX with it and
-                # letting the big GEMM accumulate (beta = 1 slowed the big GEMM by more)
-                dx.addmm_(du, lora.a_pad)
+            if lora is not None and mask is None:
+                # dX = dY W + dU A_pad in ONE NN GEMM (the adapter term as K-extension steps)
+                dx = gemm_big(dy, w, ROW, KMAJ, du, lora.a_pad)
+            else:
+                dx = gemm_big(dy, w, ROW, KMAJ)
+                if lora is not None:  # dropout: the adapter gradient flows through the mask
+                    dx = dx + gemm_big(du, lora.a_pad, ROW, KMAJ) * mask
         if needs[1]:
-            dw = (dy.t() @ x2).to(w.dtype)
+            # full fine-tuning: dW = dY^T X [N, K] (TN; bf16 compute-copy gradient)
+            dw = gemm_big(dy, x2, KMAJ, KMAJ) if (gpu and w.dtype == torch.bfloat16) else \
+                (dy.float().t() @ x2.float()).to(w.dtype)
         if ctx.has_bias and needs[2]:
             db = dy.float().sum(0).to(bias.dtype)
         lora_grads = []
         if lora is not None:
-            # all adapters of the projection in two GEMMs with fp32 output (bf16 in, fp32 accumulate):
-            # dA_all = dU^T X [Rp, K]; dB_all = dY^T U [N, Rp] (adapter i uses its diagonal block)
-            ga_all = _mm_tn_f32(du, x2)
-            gb_all = _mm_tn_f32(dy, u)
+            # all adapters of the projection in two TN GEMMs with fp32 output (bf16 in, fp32
+            # accumulate): dA_all = dU^T drop(X) [Rp, K]; dB_all = dY^T U [N, Rp] (adapter i uses
+            # its diagonal block)
+            xd = x2 * mask if mask is not None else x2
+            ga_all = gemm_tn(du, xd)
+            gb_all = gemm_tn(dy, u)
             for a, b, r0, c0, s in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
                 ri, ni = a.shape[0], b.shape[0]
                 lora_grads.append((ga_all[r0:r0 + ri] * s).to(a.dtype))
@@ -336,19 +304,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
     use_lora = lora is not None and lora.enabled
     if use_lora and (lora.a_pad is None or lora.a_pad.device != x.device):
         lora.refresh(dtype=w.dtype)
+    grad_needed = torch.is_grad_enabled() and (
+        x2.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)
+        or (use_lora and any(p.requires_grad for p in lora.a + lora.b)))
     if act_id == ACT_SWIGLU:
-        # fused into the skinny gate/up GEMM when it can run there (no-grad decode on the GPU)
-        if (on_gpu(x2) and not torch.is_grad_enabled() and x2.shape[0] <= 64 and bias is None
-                and w.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0):
+        # no-grad: SwiGLU is the GEMM epilogue (skinny kernels for decode, gemm_big otherwise);
+        # training keeps the [gate | up] pre-activation for the SwiGLU backward
+        if on_gpu(x2) and not grad_needed and bias is None and w.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0 \
+                and (x2.shape[0] <= 64 or w.shape[0] % 256 == 0):
             w_eff = lora.merged_weight(w) if use_lora else w
-            if fp8 is not None:
+            if fp8 is not None and x2.shape[0] <= 64:
                 from .fp8 import fp8_supported
 
                 if fp8_supported(w_eff):
                     q, sc = fp8.get(w_eff)
                     y = native().gemm_fp8(x2, None, q, sc, None, ACT_SWIGLU, None)
                     return y.reshape(*shp[:-1], w.shape[0] // 2)
-            y = native().gemm(x2, w_eff, None, None, None, ACT_SWIGLU, False, None)
+            y = gemm(x2, w_eff, None, None, None, ACT_SWIGLU)
             return y.reshape(*shp[:-1], w.shape[0] // 2)
         from .misc import swiglu
 
@@ -364,16 +336,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
     if use_lora and lora.use_merged and not torch.is_grad_enabled():
         y = gemm(x2, lora.merged_weight(w), None, None, bias, act_id)
         return y.reshape(*shp[:-1], w.shape[0])
-    grad_needed = torch.is_grad_enabled() and (
-        x2.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)
-        or (use_lora and any(p.requires_grad for p in lora.a + lora.b)))
     if not grad_needed:
-        if use_lora and _use_ext(x2, w, bias, act_id, lora):
-            y = _ext_forward(x2, lora)[0]
-            return y.reshape(*shp[:-1], w.shape[0])
-        u = None
-        if use_lora:
-            u = _mm_splitk(x2, lora.a_pad.t()) if x2.shape[0] > 64 else gemm(x2, lora.a_pad)
+        u = _narrow(x2, lora.a_pad, ROW) if use_lora else None
         y = gemm(x2, w, u, lora.ub if use_lora else None, bias, act_id)
     else:
         params = []

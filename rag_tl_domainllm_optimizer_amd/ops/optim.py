@@ -222,12 +222,13 @@ class FusedAdamW:
                                self.last_norm, self.skipped)
         else:
             g = self.flat.full_grad() if mixed else self.flat.grad
+            # bias correction over APPLIED steps (calls - skipped), as the GPU kernel derives it
             norm, skipped = ref.adamw_(self.flat.data, g, self.exp_avg, self.exp_avg_sq, lr, self.b1,
-                                       self.b2, self.eps, self.wd, self.step_count, self.max_grad_norm)
+                                       self.b2, self.eps, self.wd, self.step_count - int(self.skipped),
+                                       self.max_grad_norm)
             self.last_norm.fill_(float(norm))
             if skipped:
                 self.skipped += 1
-                self.step_count -= 1
             elif mixed:
                 with torch.no_grad():
                     self.flat.data16.copy_(self.flat.data[:self.flat.n16])

@@ -24,13 +24,6 @@ def _close(a, b, rtol=2e-2, atol=2e-2):
     assert err <= atol + rtol * (b.abs().max().item() + 1e-6), err
 
 
-@pytest.fixture(autouse=True, scope="module")
-def _native_gemms():
-    prev = ops.set_gemm_backend("native", "native", "native")
-    yield
-    ops.set_gemm_backend(*prev)
-
-
 @SET
 @given(M=st.integers(1, 700), n8=st.integers(1, 150), k64=st.integers(1, 12), act=st.sampled_from([0, 1, 4]),
        lora=st.booleans(), seed=st.integers(0, 1 << 16))
