@@ -159,14 +159,15 @@ def main():
         m = trainer.step(make_batch())
         log(f"[bench] warmup {w}: {m['step_time_s']:.2f}s tokens={m['rollout_tokens']:.0f} "
             f"reward={m['reward_mean']:.3f}")
-    batches = [make_batch() for _ in range(args.steps)]
     parallel.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tokens = 0.0
     phase = {}
     for s in range(args.steps):
-        m = trainer.step(batches[s])
+        # inside the timed region: sample the rank's queries, encode them and search the IVF index
+        # (retrieval), then the full PPO iteration on the retrieved RAG prompts
+        m = trainer.step(make_batch())
         tokens += m["rollout_tokens"] * di.world  # reduce_metrics averaged over ranks
         for k, v in m.items():
             if k.startswith("time/"):
@@ -196,6 +197,8 @@ def main():
                    "new_tokens": args.new_tokens, "lora_r": None if args.full_ft else 16,
                    "full_finetune": bool(args.full_ft), "encoder": args.encoder, "ndocs": args.ndocs,
                    "index": f"ivf{index.nlist}/nprobe{args.nprobe}", "minibatch": args.minibatch},
+        "backend": di.backend or "none",
+        "world": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
         "p50_rag_latency_s": lat["p50_s"] if lat else None,
         "p90_rag_latency_s": lat["p90_s"] if lat else None,
         "rag_latency_vs_baseline": (REF_LATENCY_S / lat["p50_s"]) if lat else None,

@@ -232,11 +232,15 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
     c = *out;
     TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == Nout && c.stride(1) == 1, "gemm_big: bad out shape");
     TORCH_CHECK(c.scalar_type() == odt, "gemm_big: bad out dtype");
-    TORCH_CHECK(out_mode != 0 || c.stride(0) % 8 == 0, "gemm_big: bf16 out row stride % 8");
+    TORCH_CHECK(out_mode == 2 || c.stride(0) % 8 == 0, "gemm_big: out row stride must be a multiple of 8");
     CHECK_ALIGN16(c);
   } else {
     TORCH_CHECK(out_mode != 2, "gemm_big: atomic accumulation needs an initialised out");
-    c = at::empty({M, Nout}, a.options().dtype(odt));
+    // an output width that is not a multiple of 8 (e.g. OpenChat's 32002-token vocabulary) gets a
+    // row stride padded to 8 elements: the epilogue writes whole 16-B (bf16) / 4-float chunks
+    const int64_t Np = (Nout + 7) / 8 * 8;
+    c = at::empty({M, Np}, a.options().dtype(odt));
+    if (Np != Nout) c = c.narrow(1, 0, Nout);
   }
   void* c2 = nullptr;
   int64_t ldc2 = 0;

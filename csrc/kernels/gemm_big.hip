@@ -545,7 +545,10 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   const bool any_row = layout_a == ROW || layout_b == ROW;
   if ((any_row && (K % 8 || (A2 && K2 % 8))) || !zpage) return -1;
   if (R && (out != O_BF16 || act == E_SWIGLU)) return -6;
-  if ((out == O_F32 || out == O_F32_SLAB) && (N % 4 || ldc % 4)) return -7;  // 16-B fp32 row stores
+  // whole-chunk epilogue stores (8 bf16 / 4 fp32 from every valid column start): the row stride
+  // must cover the padded width
+  const int Nout = act == E_SWIGLU ? N / 2 : N;
+  if (out != O_F32_ATOMIC && (ldc % 8 || (M > 1 && ldc < (long)((Nout + 7) / 8 * 8)))) return -7;
   if ((layout_a == KMAJ && M % 8) || (layout_b == KMAJ && N % 8)) return -1;
   if (nsplit < 1) nsplit = 1;
   if (nsplit > 1 && out != O_F32_ATOMIC && out != O_F32_SLAB) return -2;

@@ -103,6 +103,19 @@ def cmd_index(cfg, args):
     print(json.dumps({"index": path, "ntotal": st["index"].ntotal, "kind": st["index"].kind}))
 
 
+def latest_checkpoint(run_dir: str):
+    """Prefix of the checkpoint with the highest global step in ``run_dir`` (or None)."""
+    if not os.path.isdir(run_dir):
+        return None
+    cands = []
+    for d in os.listdir(run_dir):
+        sf = os.path.join(run_dir, d, "state.json")
+        if d.endswith("_trainer_state") and os.path.exists(sf):
+            with open(sf) as f:
+                cands.append((int(json.load(f).get("global_step", 0)), os.path.join(run_dir, d[:-len("_trainer_state")])))
+    return max(cands)[1] if cands else None
+
+
 def cmd_rag(cfg, args):
     from .generation import SamplingParams
     from .rag import RagPipeline
@@ -133,7 +146,7 @@ def cmd_sft(cfg, args):
     sink = MetricsSink(run_dir if di.is_main else None, config=C.to_dict(cfg), use_wandb=cfg.use_wandb)
     tr = SFTTrainer(st["policy"], st["tokenizer"], cfg.sft, sink)
     hist = tr.fit(examples, epochs=cfg.data.epochs)
-    tr.save(os.path.join(run_dir, "sft"))
+    tr.save(os.path.join(run_dir, "sft"), full_policy=getattr(cfg.sft, "save_full_policy", True))
     if di.is_main:
         print(json.dumps({"final_loss": hist[-1]["loss"] if hist else None, "steps": len(hist)}))
     return tr
@@ -156,33 +169,40 @@ def cmd_ppo(cfg, args, policy=None):
                     max_batch=cfg.data.batch_size)
     loader = RecordLoader(recs, cfg.data.batch_size, seed=cfg.model.seed, rank=di.rank, world=di.world)
     best = -float("inf")
-    first = 0
+    first, start_batch, rewards = 0, 0, []
     if getattr(args, "resume", False):
-        # resume from the latest completed epoch checkpoint of this run
-        done = [int(d[len("epoch_"):-len("_trainer_state")]) for d in (os.listdir(run_dir) if os.path.isdir(run_dir) else [])
-                if d.startswith("epoch_") and d.endswith("_trainer_state")]
-        if done:
-            st_ = tr.load_checkpoint(os.path.join(run_dir, f"epoch_{max(done)}"))
-            first = max(done)
-            best = float(st_.get("best_reward", best)) if isinstance(st_, dict) else best
+        # resume from the run's most advanced checkpoint (epoch end or mid-epoch "latest"): model,
+        # optimizer, every rank's RNG, the sampler's device RNG counter and the loader position
+        prefix = latest_checkpoint(run_dir)
+        if prefix is not None:
+            st_ = tr.load_checkpoint(prefix)
+            first, start_batch = int(st_.get("epoch", 0)), int(st_.get("batch_in_epoch", 0))
+            best = float(st_.get("best_reward", best))
+            rewards = list(st_.get("epoch_rewards", []))
             if di.is_main:
-                print(f"Resumed from {os.path.join(run_dir, f'epoch_{first}')}")
+                print(f"Resumed from {prefix} (epoch {first}, batch {start_batch})")
     for ep in range(first, cfg.data.epochs):
-        loader.set_epoch(ep)
-        rewards = []
+        loader.set_epoch(ep, start_batch if ep == first else 0)
+        if ep != first:
+            rewards = []
+        b = start_batch if ep == first else 0
         for batch in loader:
             m = tr.step(batch)
             rewards.append(m["reward_mean"])
+            b += 1
             if di.is_main:
                 print(json.dumps({k: m[k] for k in ("reward_mean", "total_loss", "kl_ref", "rollout_tokens_per_s")}),
                       flush=True)
+            if cfg.ppo.save_every and tr.global_step % cfg.ppo.save_every == 0 and b < len(loader):
+                tr.save_checkpoint(os.path.join(run_dir, "latest"), ep, best, full_policy=False, batch_in_epoch=b,
+                                   extra_state={"epoch_rewards": rewards})
         avg = sum(rewards) / max(len(rewards), 1)
         if di.is_main:
             print(f"Epoch {ep + 1}/{cfg.data.epochs}: Average Reward = {avg:.4f}")
-        if avg > best:
+        if avg > best:  # rl.py:358-360
             best = avg
-            tr.save_checkpoint(os.path.join(run_dir, "best_model"), ep, best)
-        tr.save_checkpoint(os.path.join(run_dir, f"epoch_{ep + 1}"), ep, best)
+            tr.save_checkpoint(os.path.join(run_dir, "best_model"), ep + 1, best)
+        tr.save_checkpoint(os.path.join(run_dir, f"epoch_{ep + 1}"), ep + 1, best)
     return tr
 
 
@@ -207,9 +227,18 @@ def cmd_eval(cfg, args):
 
 
 def cmd_pipeline(cfg, args):
-    """Config 5: RAG index -> RAFT LoRA SFT -> PPO, chained through the SFT adapter checkpoint."""
+    """Config 5: RAG index -> RAFT LoRA SFT -> PPO, chained THROUGH CHECKPOINTS: the SFT stage
+    writes its PEFT adapter to disk, the PPO stage builds a fresh policy and loads that adapter
+    from the directory (as the reference hands stages over by path, rl.py:365-379,494-498)."""
+    from .models import load_adapter
+
     tr = cmd_sft(cfg, args)
-    cmd_ppo(cfg, args, policy=tr.model)
+    adapter_dir = os.path.join(cfg.out_dir, cfg.name, "sft_adapter")
+    del tr
+    di = _device()
+    st = build_stack(cfg, di.device)
+    load_adapter(st["policy"], adapter_dir)
+    return cmd_ppo(cfg, args, policy=st["policy"])
 
 
 def cmd_serve(cfg, args):

@@ -61,9 +61,14 @@ class RecordLoader:
         self.rank, self.world = rank, world
         self.drop_last = drop_last
         self.epoch = 0
+        self.start_batch = 0  # mid-epoch resume: batches of the current epoch already consumed
 
-    def set_epoch(self, e: int):
+    def set_epoch(self, e: int, start_batch: int = 0):
         self.epoch = e
+        self.start_batch = start_batch
+
+    def state_dict(self) -> dict:
+        return {"epoch": self.epoch, "start_batch": self.start_batch, "seed": self.seed}
 
     def _indices(self) -> List[int]:
         idx = list(range(len(self.records)))
@@ -77,7 +82,8 @@ class RecordLoader:
 
     def __iter__(self) -> Iterator[Dict[str, list]]:
         idx = self._indices()
-        for s in range(0, len(idx), self.batch_size):
+        skip, self.start_batch = self.start_batch, 0  # the resume offset applies to one epoch
+        for s in range(skip * self.batch_size, len(idx), self.batch_size):
             chunk = idx[s:s + self.batch_size]
             if self.drop_last and len(chunk) < self.batch_size:
                 break

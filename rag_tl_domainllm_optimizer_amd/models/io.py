@@ -126,11 +126,10 @@ def load_hf_state_dict(model, sd: Dict[str, torch.Tensor], strict: bool = True, 
 
 
 def save_pretrained(model, path: str, max_shard_bytes: int = 5 * 1024 ** 3, dtype=torch.bfloat16,
-                    generation_config: dict = None):
+                    generation_config: dict = None, write_weights: bool = True):
     from safetensors.torch import save_file
 
     os.makedirs(path, exist_ok=True)
-    sd = to_hf_state_dict(model, dtype)
     with open(os.path.join(path, "config.json"), "w") as f:
         d = config_to_hf(model.cfg)
         d["_ragtl_preset"] = model.cfg.name
@@ -141,6 +140,9 @@ def save_pretrained(model, path: str, max_shard_bytes: int = 5 * 1024 ** 3, dtyp
         gc.update(generation_config or {})
         with open(os.path.join(path, "generation_config.json"), "w") as f:
             json.dump(gc, f, indent=2)
+    if not write_weights:
+        return
+    sd = to_hf_state_dict(model, dtype)
     total = sum(t.numel() * t.element_size() for t in sd.values())
     if total <= max_shard_bytes:
         save_file(sd, os.path.join(path, "model.safetensors"), metadata={"format": "pt"})

@@ -33,12 +33,15 @@ ACT_SWIGLU = 5  # w = [gate; up] (2F rows) -> silu(x gate^T) * (x up^T), [.., F]
 
 def splitk_plan(M: int, N: int, K: int, act: int = 0) -> int:
     """Split-K factor for an NT GEMM whose 256x256 tiles cannot fill the 256 CUs (decode at batch
-    65..256, narrow outputs): ~256 workgroups, >= 4 K-steps each; 1 = the plain tiled kernel."""
+    65..256, narrow outputs): ~256 workgroups with >= 8 K-steps each (each split streams its weight
+    slice from HBM with ~1 K-step of prefetch; shorter splits pay the pipeline fill and the fp32
+    slab round trip more than they gain — M = 256 sweep, profiles/gemm_r2_m256_split_sweep.log:
+    qkv / o 8-way, gate_up 2-way, down 16-way); 1 = the plain tiled kernel."""
     tiles = ((M + 255) // 256) * (N // 256 if act == ACT_SWIGLU else (N + 255) // 256)
     if tiles >= 128 or M > 1024:
         return 1
     nk = (K + 63) // 64
-    return max(1, min(nk // 4, (256 + tiles // 2) // tiles))
+    return max(1, min(nk // 8, (256 + tiles // 2) // tiles))
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None,
@@ -49,7 +52,7 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
     if on_gpu(x):
         M, K = x.shape
         N = w.shape[0]
-        if M <= 64 and residual is None:
+        if M <= 64 and residual is None and N % 8 == 0:
             return native().gemm(x, w, u, ub, bias, act, out_f32, out)
         s = nsplit or (splitk_plan(M, N, K, act) if (u is None and not out_f32 and N % 16 == 0) else 1)
         if s > 1:

@@ -27,6 +27,7 @@ class GradSync:
         self.flat = flat
         self.world = info().world
         self.enabled = info().enabled
+        self.gloo = self.enabled and dist.get_backend() == "gloo"
         self.overlap = overlap and self.enabled
         n = flat.numel
         per = max(1, bucket_bytes // 4)
@@ -76,8 +77,11 @@ class GradSync:
         # one slice per gradient buffer the bucket touches (fp32, or bf16 + fp32 under full-parameter
         # training: ops.MixedFlatParams); RCCL reduces bf16 in place, 2 B per weight over xGMI
         for t in self.flat.grad_slices(s, e):
-            if t.dtype == torch.bfloat16 and not t.is_cuda:
-                f = t.float()  # CPU (gloo) runs: reduce an fp32 copy of a bf16 slice
+            if t.dtype == torch.bfloat16 and (not t.is_cuda or self.gloo):
+                # gloo (CPU runs, and the one-GPU multi-rank rehearsal): reduce an fp32 copy of a
+                # bf16 slice. RCCL reduces bf16 in place (2 B per weight over xGMI); its ring sums
+                # in bf16, which the full-fine-tuning DP tests bound (docs/DESIGN.md)
+                f = t.float()
                 dist.all_reduce(f)
                 t.copy_(f)
             else:

@@ -84,16 +84,33 @@ def all_reduce_(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     return t
 
 
-def reduce_metrics(values: dict, device=None) -> dict:
-    """Mean of scalar metrics over ranks in ONE packed all-reduce."""
+def _is_time_key(k: str) -> bool:
+    return k.startswith("time/") or k.endswith("time_s")
+
+
+def reduce_metrics(values: dict, device=None, max_keys=None) -> dict:
+    """Scalar metrics over ranks: the MEAN of every key, except durations (``time/*``, ``*time_s``
+    and ``max_keys``), which take the MAX over ranks — a data-parallel step lasts as long as its
+    slowest rank, and throughput derived from it must match the bench's max-over-ranks clock.
+    Two packed all-reduces (sum, max)."""
     if not _INFO.enabled or not values:
         return dict(values)
+    max_keys = set(max_keys or ())
     keys = sorted(values)
-    vec = torch.tensor([float(values[k]) for k in keys], dtype=torch.float64,
-                       device=device or _INFO.device)
-    dist.all_reduce(vec)
-    vec /= _INFO.world
-    return {k: float(v) for k, v in zip(keys, vec.tolist())}
+    mk = [k for k in keys if _is_time_key(k) or k in max_keys]
+    sk = [k for k in keys if k not in set(mk)]
+    dev = device or _INFO.device
+    out = {}
+    if sk:
+        vec = torch.tensor([float(values[k]) for k in sk], dtype=torch.float64, device=dev)
+        dist.all_reduce(vec)
+        vec /= _INFO.world
+        out.update(zip(sk, vec.tolist()))
+    if mk:
+        vec = torch.tensor([float(values[k]) for k in mk], dtype=torch.float64, device=dev)
+        dist.all_reduce(vec, op=dist.ReduceOp.MAX)
+        out.update(zip(mk, vec.tolist()))
+    return {k: float(out[k]) for k in keys}
 
 
 def broadcast_module_(module: torch.nn.Module, src: int = 0):

@@ -32,27 +32,50 @@ def range_(name: str):
 
 
 class PhaseTimer:
-    """Wall-clock phase timer (synchronises the device at phase boundaries when asked)."""
+    """Phase timer on HIP events: a phase is the device time between an event recorded on the
+    current stream when it opens and one recorded when it closes (work the phase waits for on other
+    streams, e.g. the reward encoder joined back, is included). Nothing synchronises at phase
+    boundaries, so phases overlap freely; ``as_dict`` resolves the pending events (host wall clock
+    on CPU-only runs). ``sync=True`` restores the old behaviour (device sync around each phase)."""
 
-    def __init__(self, sync: bool = True):
-        self.sync = sync and torch.cuda.is_available()
+    def __init__(self, sync: bool = False, device=None):
+        self.cuda = torch.cuda.is_available() and (device is None or torch.device(device).type == "cuda")
+        self.sync = sync and self.cuda
         self.totals = defaultdict(float)
+        self._pending = []
 
     @contextlib.contextmanager
     def phase(self, name: str):
         if self.sync:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
+        ev0 = None
+        if self.cuda:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         with range_(name):
             yield
-        if self.sync:
-            torch.cuda.synchronize()
-        self.totals[name] += time.perf_counter() - t0
+        if self.cuda:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            if self.sync:
+                torch.cuda.synchronize()
+            self._pending.append((name, ev0, ev1))
+        else:
+            self.totals[name] += time.perf_counter() - t0
+
+    def _resolve(self):
+        for name, e0, e1 in self._pending:
+            e1.synchronize()
+            self.totals[name] += e0.elapsed_time(e1) / 1e3
+        self._pending.clear()
 
     def reset(self):
+        self._pending.clear()
         self.totals.clear()
 
     def as_dict(self, prefix: str = "time/"):
+        self._resolve()
         return {prefix + k: v for k, v in self.totals.items()}
 
 

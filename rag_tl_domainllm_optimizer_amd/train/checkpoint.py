@@ -7,11 +7,17 @@ layout SURVEY App. D.3) plus what the reference lacks:
                            loader gets the fine-tuned policy)
   {prefix}_tokenizer/      tokenizer.json + tokenizer_config.json + special_tokens_map.json
   {prefix}_value_head.pt   {"weight": [1, H], "bias": [1]} (torch.nn.Linear(H, 1) state_dict)
+                           + the TRL AutoModelForCausalLMWithValueHead names (v_head.summary.*) in
+                           {prefix}_value_head.safetensors and inside the policy's weight files
   {prefix}_adapter/        PEFT adapter (adapter_config.json + adapter_model.safetensors)
-  {prefix}_trainer_state/  optimizer moments, step/epoch/best metric, RNG states (resume)
+  {prefix}_trainer_state/  optimizer moments, step / epoch / position in the epoch, best metric,
+                           RNG states of EVERY rank (rng_rank{r}.*), the sampler's device RNG counter
 
+The merged policy is produced tensor by tensor: each LoRA-adapted projection is folded on the
+device (W + s B A as one GEMM with W as the epilogue's residual input, bf16 out) and copied to the
+host, which holds one safetensors shard at a time — never an fp32 copy of the model.
 Every directory is written to a temporary name and renamed into place (atomic on one filesystem);
-only rank 0 writes.
+rank 0 writes the artifacts, every other rank only its RNG state.
 """
 from __future__ import annotations
 
@@ -40,60 +46,125 @@ def _commit(tmp: str, final: str):
     os.replace(tmp, final)
 
 
+def _lora_group_of(model, native_name: str):
+    """LoRAGroup of a fused decoder projection parameter ("layers.{i}.qkv_w" -> layer i, "qkv")."""
+    if getattr(model, "lora_config", None) is None or not native_name.startswith("layers."):
+        return None
+    _, i, pname = native_name.split(".", 2)
+    grp = {"qkv_w": "qkv", "o_w": "o", "gate_up_w": "gate_up", "down_w": "down", "fc1_w": "fc1",
+           "fc2_w": "fc2"}.get(pname)
+    layer = model.layers[int(i)]
+    return layer.lora.get(grp) if grp else None
+
+
+@torch.no_grad()
+def iter_merged_hf_tensors(model, dtype=torch.bfloat16):
+    """Yield (hf_name, host tensor) in mapping order with every LoRA adapter folded in. A fused
+    weight is merged once on its device and sliced into its HF tensors; only one merged projection
+    lives at a time."""
+    from .. import ops
+
+    params = dict(model.named_parameters())
+    cur_name, cur = None, None
+    for hf, nat, r0, rn in mio.mapping_for(model):
+        t = params[nat].detach()
+        grp = _lora_group_of(model, nat)
+        if grp is not None:
+            if cur_name != nat:
+                if grp.a_pad is None or grp.a_pad.device != t.device:
+                    grp.refresh(dtype=t.dtype)
+                if ops.on_gpu(t) and t.dtype == torch.bfloat16:
+                    cur = torch.empty_like(t)
+                    ops.native().gemm_big(grp.ub, grp.a_pad, ops.ROW, ops.KMAJ, None, None, None, 0, 0, 1, cur, None, t)
+                else:
+                    cur = t.float() + grp.ub.float() @ grp.a_pad.float()
+                cur_name = nat
+            t = cur
+        if rn is not None:
+            t = t[r0:r0 + rn]
+        yield hf, t.to("cpu").to(dtype).contiguous()
+
+
 def merged_hf_state_dict(model, dtype=torch.bfloat16):
-    """HF state dict with every LoRA adapter folded in (W + s B A), computed in fp32 on the host."""
-    sd = mio.to_hf_state_dict(model, dtype=torch.float32)
-    if getattr(model, "lora_config", None) is not None:
-        ad = adapter_state_dict(model)
-        s = model.lora_config.scaling
-        for k in list(ad):
-            if ".lora_A.weight" not in k:
-                continue
-            base = k.replace("base_model.model.", "").replace(".lora_A.weight", ".weight")
-            a = ad[k]
-            b = ad[k.replace("lora_A", "lora_B")]
-            sd[base] = sd[base] + s * (b @ a)
-    return {k: v.to(dtype).contiguous() for k, v in sd.items()}
+    """HF state dict with every LoRA adapter folded in (W + s B A) — tests / small models; large
+    policies stream through ``save_policy``."""
+    return dict(iter_merged_hf_tensors(model, dtype))
 
 
-def save_policy(model, path: str, dtype=torch.bfloat16, max_shard_bytes: int = 5 * 1024 ** 3):
+def save_policy(model, path: str, dtype=torch.bfloat16, max_shard_bytes: int = 5 * 1024 ** 3, extra=None):
+    """HF layout (config + generation config + safetensors shards + index). ``extra`` tensors
+    (e.g. the TRL value head) are stored with the last shard."""
     from safetensors.torch import save_file
 
     tmp = _atomic_dir(path)
-    sd = merged_hf_state_dict(model, dtype)
-    # reuse save_pretrained's config/generation config writing, then overwrite weights with merged
-    mio.save_pretrained(model, tmp, max_shard_bytes=max_shard_bytes, dtype=dtype)
-    for f in os.listdir(tmp):
-        if f.endswith(".safetensors") or f.endswith(".index.json"):
-            os.remove(os.path.join(tmp, f))
-    total = sum(t.numel() * t.element_size() for t in sd.values())
-    if total <= max_shard_bytes:
-        save_file(sd, os.path.join(tmp, "model.safetensors"), metadata={"format": "pt"})
+    mio.save_pretrained(model, tmp, max_shard_bytes=max_shard_bytes, dtype=dtype, write_weights=False)
+    shards, cur, cur_b, total = [], {}, 0, 0
+
+    def flush():
+        nonlocal cur, cur_b
+        name = f"shard-{len(shards):05d}.safetensors"
+        save_file(cur, os.path.join(tmp, name), metadata={"format": "pt"})
+        shards.append((name, list(cur)))
+        cur, cur_b = {}, 0
+
+    for k, t in iter_merged_hf_tensors(model, dtype):
+        b = t.numel() * t.element_size()
+        if cur and cur_b + b > max_shard_bytes:
+            flush()
+        cur[k] = t
+        cur_b += b
+        total += b
+    for k, t in (extra or {}).items():
+        cur[k] = t.detach().to("cpu").contiguous()
+        total += t.numel() * t.element_size()
+    flush()
+    if len(shards) == 1:
+        os.replace(os.path.join(tmp, shards[0][0]), os.path.join(tmp, "model.safetensors"))
     else:
-        shards, cur, cur_b = [], {}, 0
-        for k, t in sd.items():
-            b = t.numel() * t.element_size()
-            if cur and cur_b + b > max_shard_bytes:
-                shards.append(cur)
-                cur, cur_b = {}, 0
-            cur[k] = t
-            cur_b += b
-        shards.append(cur)
         wm = {}
-        for i, sh in enumerate(shards):
-            name = f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors"
-            save_file(sh, os.path.join(tmp, name), metadata={"format": "pt"})
-            wm.update({k: name for k in sh})
+        for i, (name, keys) in enumerate(shards):
+            final = f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors"
+            os.replace(os.path.join(tmp, name), os.path.join(tmp, final))
+            wm.update({k: final for k in keys})
         with open(os.path.join(tmp, "model.safetensors.index.json"), "w") as f:
             json.dump({"metadata": {"total_size": total}, "weight_map": wm}, f, indent=2)
     _commit(tmp, path)
+
+
+def save_rank_rng(prefix: str, rank: int, rng: dict):
+    """RNG state of one data-parallel rank into {prefix}_trainer_state/rng_rank{rank}.*"""
+    from safetensors.torch import save_file
+
+    from ..utils.seed import rng_state_pack
+
+    d = f"{prefix}_trainer_state"
+    os.makedirs(d, exist_ok=True)
+    rt, rm = rng_state_pack(rng)
+    save_file(rt, os.path.join(d, f"rng_rank{rank}.safetensors.tmp"))
+    os.replace(os.path.join(d, f"rng_rank{rank}.safetensors.tmp"), os.path.join(d, f"rng_rank{rank}.safetensors"))
+    with open(os.path.join(d, f"rng_rank{rank}.json"), "w") as f:
+        json.dump(rm, f)
+
+
+def load_rank_rng(prefix: str, rank: int):
+    from safetensors.torch import load_file
+
+    from ..utils.seed import rng_state_unpack
+
+    d = f"{prefix}_trainer_state"
+    for r in (rank, 0):
+        f = os.path.join(d, f"rng_rank{r}.safetensors")
+        if os.path.exists(f):
+            with open(os.path.join(d, f"rng_rank{r}.json")) as fh:
+                return rng_state_unpack(load_file(f), json.load(fh))
+    return None
 
 
 def save_checkpoint(prefix: str, model, tokenizer, value_head=None, optimizer=None, trainer_state: Optional[dict] = None,
                     save_full_policy: bool = True):
     os.makedirs(os.path.dirname(os.path.abspath(prefix)), exist_ok=True)
     if save_full_policy:
-        save_policy(model, f"{prefix}_policy")
+        save_policy(model, f"{prefix}_policy", extra=value_head.trl_state_dict() if value_head is not None else None)
     if tokenizer is not None:
         tmp = _atomic_dir(f"{prefix}_tokenizer")
         tokenizer.save_pretrained(tmp)
@@ -102,6 +173,10 @@ def save_checkpoint(prefix: str, model, tokenizer, value_head=None, optimizer=No
         tmpf = f"{prefix}_value_head.pt.tmp"
         torch.save(value_head.reference_state_dict(), tmpf)
         os.replace(tmpf, f"{prefix}_value_head.pt")
+        from safetensors.torch import save_file
+
+        save_file(value_head.trl_state_dict(), f"{prefix}_value_head.safetensors.tmp", metadata={"format": "pt"})
+        os.replace(f"{prefix}_value_head.safetensors.tmp", f"{prefix}_value_head.safetensors")
     if getattr(model, "lora_config", None) is not None:
         tmp = _atomic_dir(f"{prefix}_adapter")
         save_adapter(model, tmp)
@@ -123,8 +198,8 @@ def save_checkpoint(prefix: str, model, tokenizer, value_head=None, optimizer=No
             from ..utils.seed import rng_state_pack
 
             rt, rm = rng_state_pack(rng)
-            save_file(rt, os.path.join(tmp, "rng.safetensors"))
-            with open(os.path.join(tmp, "rng.json"), "w") as f:
+            save_file(rt, os.path.join(tmp, "rng_rank0.safetensors"))
+            with open(os.path.join(tmp, "rng_rank0.json"), "w") as f:
                 json.dump(rm, f)
         with open(os.path.join(tmp, "state.json"), "w") as f:
             json.dump(st, f, indent=2, default=float)
@@ -160,13 +235,11 @@ def load_checkpoint(prefix: str, model, value_head=None, optimizer=None, load_po
                 optimizer.flat.data.copy_(t["params"].to(optimizer.flat.data.device))
             if hasattr(optimizer.flat, "refresh_shadow"):  # full fine-tuning: bf16 copies <- master
                 optimizer.flat.refresh_shadow()
-        if os.path.exists(os.path.join(tsd, "rng.safetensors")):
-            from safetensors.torch import load_file
+        from ..parallel import info as dist_info
 
-            from ..utils.seed import rng_state_unpack
-
-            with open(os.path.join(tsd, "rng.json")) as f:
-                st["rng"] = rng_state_unpack(load_file(os.path.join(tsd, "rng.safetensors")), json.load(f))
+        rng = load_rank_rng(prefix, dist_info().rank)
+        if rng is not None:
+            st["rng"] = rng
     if hasattr(model, "refresh_lora"):
         model.refresh_lora()
     print(f"Checkpoint loaded from {prefix}")

@@ -13,8 +13,10 @@ reference's mode: bf16 compute copies + fp32 master, ops.MixedFlatParams, frozen
 
 Device flow per step (one process per GPU, DP over RCCL):
   generate (hipGraph decode, behaviour log-probs + values emitted by the sampler step)
-  || reward encoder on a side stream (overlapped with the next rollout chunk)
-  -> reference log-probs (LoRA off, no grad) -> token rewards / GAE kernel
+  -> reference log-probs (LoRA off, no grad) on the main stream
+     || reward: rollout tokens reach the host right after the rollout, the host detokenises while
+        the reference forward runs, the reward encoder runs on a side stream (``overlap_reward``)
+  -> token rewards / GAE kernel
   -> ppo_epochs x minibatches of (forward, backward with bucketed all-reduce, fused AdamW).
 """
 from __future__ import annotations
@@ -71,14 +73,29 @@ class PPOConfig:
     lora_targets: Sequence[str] = ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj")
     full_finetune: bool = False         # True: every weight (the reference's mode, rl.py:153)
     gradient_checkpointing: bool = False
-    overlap_reward: bool = True
+    overlap_reward: bool = True      # reward encoder on a side stream beside the reference forward
     rollout_chunks: int = 1          # >1: score chunk i while chunk i+1 decodes
     merged_lora_rollout: bool = True  # decode/prefill rollouts on W + sBA (refreshed per update)
     lr_schedule: str = "constant"
+    save_every: int = 0              # CLI: mid-epoch "latest" checkpoint every N steps (0 = epoch ends)
     bucket_mb: float = 64.0
     warmup_steps: int = 0
     total_steps: int = 0
     seed: int = 0
+
+
+def _event():
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+class _nullcontext:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 class AdaptiveKL:
@@ -153,8 +170,12 @@ class PPOTrainer:
         self.sampling = SamplingParams(max_new_tokens=c.max_new_tokens, temperature=c.temperature, top_k=c.top_k,
                                        top_p=c.top_p, do_sample=True, seed=c.seed + 1000 * dist_info().rank)
         self.streams = StreamPair(self.device)
-        self.timer = PhaseTimer(sync=self.device.type == "cuda")
+        self.timer = PhaseTimer(device=self.device)
         self.global_step = 0
+        # set record_overlap_events = True to get HIP events of the reference forward / reward
+        # encoder (tests and traces check that the two really overlap)
+        self.record_overlap_events = False
+        self.overlap_events: Dict[str, torch.cuda.Event] = {}
 
     @property
     def kl_coef(self):
@@ -235,20 +256,34 @@ class PPOTrainer:
                      cat_pad([o.values for o in outs], T, False, 0.0), None, {}, [], list(queries))
         ro.n_tokens = int(ro.resp_len.sum())
         ro._outs, ro._pending, ro._batch = outs, pending, (queries, docs, gts)
+        if not pending:
+            # generation is complete here (result() waited): one D2H copy per output while the GPU
+            # is idle; detokenisation happens later, beside the reference forward
+            ro._host = [(o.tokens.cpu(), o.lengths.cpu()) for o in outs]
         return ro
 
-    def _texts(self, out) -> List[str]:
-        toks = out.tokens.cpu()
-        lens = out.lengths.cpu()
-        return [extract_answer(self.tok.decode(toks[b, :int(lens[b])].tolist())) for b in range(toks.shape[0])]
+    def _texts(self, out, host=None) -> List[str]:
+        toks, lens = host if host is not None else (out.tokens.cpu(), out.lengths.cpu())
+        lens = lens.tolist()
+        return [extract_answer(self.tok.decode(toks[b, :lens[b]].tolist())) for b in range(toks.shape[0])]
+
+    def _score_now(self, ro: Rollout, side: bool):
+        """Detokenise the (host-resident) rollout and run the reward encoder — on the side stream
+        when ``side`` (it then runs beside whatever the main stream has queued)."""
+        queries, docs, gts = ro._batch
+        host = getattr(ro, "_host", None) or [None] * len(ro._outs)
+        texts = sum((self._texts(o, h) for o, h in zip(ro._outs, host)), [])
+        with self.streams.on_side() if side else _nullcontext():
+            if self.record_overlap_events and self.device.type == "cuda":
+                self.overlap_events["reward_start"] = _event()
+            r, comp = self.reward_model.score(texts, queries, docs, gts)
+            if self.record_overlap_events and self.device.type == "cuda":
+                self.overlap_events["reward_end"] = _event()
+        ro._pending = [(0, len(texts), texts, r, comp)]
 
     def _collect_rewards(self, ro: Rollout):
-        queries, docs, gts = ro._batch
-        if not ro._pending:  # single chunk: score now, on the side stream (caller overlaps it)
-            texts = sum((self._texts(o) for o in ro._outs), [])
-            with self.streams.on_side():
-                r, comp = self.reward_model.score(texts, queries, docs, gts)
-            ro._pending = [(0, len(texts), texts, r, comp)]
+        if not ro._pending:
+            self._score_now(ro, side=True)
         self.streams.join()
         B = ro.resp.shape[0]
         scores = torch.zeros(B, device=self.device)
@@ -269,6 +304,11 @@ class PPOTrainer:
         then token rewards (score at the last token, -beta*KL per token) and GAE."""
         c = self.cfg
         with self.timer.phase("ref_logprobs+reward"):
+            if not c.overlap_reward and not ro._pending:
+                self._score_now(ro, side=False)  # serial schedule: reward first, on the main stream
+            rec = self.record_overlap_events and self.device.type == "cuda"
+            if rec:
+                self.overlap_events["ref_start"] = _event()
             # the frozen reference: adapters off (LoRA) or the starting-weight copy (full FT)
             ref_model = self.ref_policy if self.ref_policy is not None else self.policy
             ref_model.set_lora_enabled(False)
@@ -283,7 +323,10 @@ class PPOTrainer:
                 ro.ref_logp = torch.cat(ref_lp, 0)
             finally:
                 ref_model.set_lora_enabled(True)
-            # host-side detokenisation + reward encoder run while the reference forward executes
+            if rec:
+                self.overlap_events["ref_end"] = _event()
+            # the whole reference forward is queued and nothing above waited for the device: the
+            # host detokenises now and the reward encoder runs on the side stream beside it
             self._collect_rewards(ro)
         mask = response_mask(ro.resp_len, ro.resp.shape[1])
         kl = (ro.old_logp - ro.ref_logp) * mask
@@ -355,6 +398,8 @@ class PPOTrainer:
             "response_len": float(ro.resp_len.float().mean()), "step_time_s": dt,
         }
         m.update(self.timer.as_dict())
+        # means over ranks, except durations (max over ranks): throughput = all ranks' tokens /
+        # the slowest rank's step, as the bench measures it
         m = reduce_metrics(m)
         m["rollout_tokens_per_s"] = m["rollout_tokens"] * dist_info().world / max(m["step_time_s"], 1e-9)
         if self.kl is not None:
@@ -366,18 +411,33 @@ class PPOTrainer:
         return m
 
     # ------------------------------------------------------------------ checkpoints
-    def trainer_state(self, epoch: int = 0, best: float = -math.inf):
+    def trainer_state(self, epoch: int = 0, best: float = -math.inf, batch_in_epoch: int = 0):
         from ..utils import rng_state
 
-        return {"global_step": self.global_step, "epoch": epoch, "best_reward": best, "config": asdict(self.cfg),
-                "kl_coef": self.kl_coef, "rng": rng_state()}
+        return {"global_step": self.global_step, "epoch": epoch, "batch_in_epoch": batch_in_epoch,
+                "best_reward": best, "config": asdict(self.cfg),
+                "kl_coef": self.kl_coef, "rng": rng_state(),
+                # the on-device Philox counter of the rollout sampler: a resumed run continues the
+                # random stream instead of replaying step 0's draws
+                "gen_rng_offset": int(self.gen.rng_offset.item())}
 
-    def save_checkpoint(self, prefix: str, epoch: int = 0, best: float = -math.inf, full_policy: bool = True):
-        from .checkpoint import save_checkpoint
+    def save_checkpoint(self, prefix: str, epoch: int = 0, best: float = -math.inf, full_policy: bool = True,
+                        batch_in_epoch: int = 0, extra_state: Optional[dict] = None):
+        """Rank 0 writes the artifacts; every other rank adds its own RNG state (rng_rank{r})."""
+        from ..parallel import barrier
+        from ..utils import rng_state
+        from .checkpoint import save_checkpoint, save_rank_rng
 
-        if dist_info().is_main:
-            save_checkpoint(prefix, self.policy, self.tok, self.value_head, self.opt,
-                            self.trainer_state(epoch, best), save_full_policy=full_policy)
+        di = dist_info()
+        st = self.trainer_state(epoch, best, batch_in_epoch)  # collective-free; every rank
+        st.update(extra_state or {})
+        if di.is_main:
+            save_checkpoint(prefix, self.policy, self.tok, self.value_head, self.opt, st,
+                            save_full_policy=full_policy)
+        barrier()
+        if not di.is_main:
+            save_rank_rng(prefix, di.rank, rng_state())
+        barrier()
 
     def load_checkpoint(self, prefix: str) -> dict:
         from ..utils import set_rng_state
@@ -389,4 +449,6 @@ class PPOTrainer:
             self.kl.value = st["kl_coef"]
         if "rng" in st:
             set_rng_state(st["rng"])
+        if "gen_rng_offset" in st:
+            self.gen.rng_offset.fill_(int(st["gen_rng_offset"]))
         return st

@@ -40,6 +40,7 @@ class SFTConfig:
     total_steps: int = 0
     gradient_checkpointing: bool = False
     bucket_mb: float = 64.0          # DP all-reduce bucket size
+    save_full_policy: bool = True    # also write the merged HF policy next to the PEFT adapter
     seed: int = 0
 
 
@@ -147,18 +148,28 @@ class SFTTrainer:
             idx = list(range(len(examples)))
             if shuffle:
                 rng.shuffle(idx)
+            # wrap-around padding to a multiple of the world size: every rank gets a shard of the
+            # SAME length, hence the same number of steps (an extra step on one rank would wait
+            # forever in the gradient all-reduce of the others)
+            if len(idx) % di.world:
+                idx += idx[: di.world - len(idx) % di.world]
             idx = idx[di.rank::di.world]
-            for s in range(0, len(idx) - bs + 1 if len(idx) >= bs else 1, bs):
-                m = self.step([examples[i] for i in idx[s:s + bs]])
+            n_steps = max(1, len(idx) // bs)
+            for k in range(n_steps):
+                m = self.step([examples[i] for i in idx[k * bs:(k + 1) * bs]])
                 hist.append(m)
                 if di.is_main and log_every and len(hist) % log_every == 0:
                     print(f"[sft] epoch {ep} step {self.global_step} loss {m['loss']:.4f}", flush=True)
         return hist
 
-    def save(self, prefix: str):
+    def save(self, prefix: str, full_policy: bool = True):
+        """PEFT adapter (LoRA) + trainer state, and the merged HF policy when ``full_policy``;
+        rank 0 writes, the other ranks wait (every rank then reads the same files)."""
+        from ..parallel import barrier
         from .checkpoint import save_checkpoint
 
         if dist_info().is_main:
             save_checkpoint(prefix, self.model, self.tok, None, self.opt,
                             {"global_step": self.global_step, "config": asdict(self.cfg)},
-                            save_full_policy=True)
+                            save_full_policy=full_policy or self.cfg.full_finetune)
+        barrier()

@@ -1,0 +1,148 @@
+"""Data-parallel PPO and SFT on CPU with gloo (SURVEY §4.2 distributed layer).
+
+PPO (world 2 and 8): the bucketed all-reduce of a real ``PPOTrainer.step`` averages the ranks'
+local gradients; after the step every rank holds bitwise-identical LoRA and value-head parameters;
+``reduce_metrics`` gives every rank the same dict (durations max-reduced); a rank-0 checkpoint
+(+ per-rank RNG files) resumed on all ranks reproduces the uninterrupted next step.
+SFT: an example count that is not a multiple of the world size runs the same number of steps on
+every rank (regression test for the shard-imbalance deadlock).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env(rank, world, port):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+
+
+def _ppo_setup(seed=0):
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.data import SyntheticCorpus
+    from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
+    from rag_tl_domainllm_optimizer_amd.retrieval import Encoder
+    from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
+    from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
+    from rag_tl_domainllm_optimizer_amd.train.ppo import PPOConfig, PPOTrainer
+
+    torch.manual_seed(seed)
+    cfg = PRESETS["tiny-llama"]
+    tok = Tokenizer.synthetic(cfg.vocab_size, "llama")
+    policy = models.CausalLM(cfg, dtype=torch.float32, seed=1)
+    enc_cfg = PRESETS["tiny-bert"]
+    enc = Encoder(models.SentenceEncoder(enc_cfg, dtype=torch.float32, seed=2).eval(),
+                  Tokenizer.synthetic(enc_cfg.vocab_size, "bert"), max_length=64)
+    corpus = SyntheticCorpus(tok.words(), n_docs=40, doc_words=20, seed=3)
+    items = corpus.sample_queries(64, seed=4)
+    recs = [{"query": it.query, "retrieved_docs": [corpus.docs[it.gold_doc]], "ground_truth": it.ground_truth}
+            for it in items]
+    pc = PPOConfig(max_new_tokens=6, max_prompt_tokens=64, minibatch_size=4, lora_r=4, lora_alpha=8.0, lr=1e-3,
+                   bucket_mb=1e-3)  # tiny buckets: several all-reduces per backward
+    return PPOTrainer(policy, tok, RewardModel(enc), pc, max_batch=8), recs
+
+
+def _ppo_worker(rank, world, port, out_dir):
+    _env(rank, world, port)
+    from rag_tl_domainllm_optimizer_amd import parallel
+    from rag_tl_domainllm_optimizer_amd.data import RecordLoader
+
+    parallel.init(device="cpu")
+    tr, recs = _ppo_setup()
+    assert len(tr.sync.buckets) >= 2
+    batches = list(RecordLoader(recs, 4, seed=0, rank=rank, world=world))
+    # step 1 with the gradient hand-off instrumented: hooks off -> local gradients only, then
+    # finish() all-reduces every bucket; keep both
+    tr.sync.sync_enabled = False
+    real_finish = tr.sync.finish
+    captured = []
+
+    def finish():
+        captured.append(tr.flat.grad.clone())
+        real_finish()
+        captured.append(tr.flat.grad.clone())
+    tr.sync.finish = finish
+    m1 = tr.step(batches[0])
+    tr.sync.finish = real_finish
+    tr.sync.sync_enabled = True
+    ck = os.path.join(out_dir, "ck", "s1")
+    tr.save_checkpoint(ck, 0, m1["reward_mean"], full_policy=False, batch_in_epoch=1)
+    m2 = tr.step(batches[1])  # normal overlapped hooks
+    params = torch.cat([p.detach().reshape(-1) for p in tr.flat.params])
+    # resume on every rank from the rank-0 checkpoint + this rank's RNG, replay step 2
+    tr2, _ = _ppo_setup()
+    st = tr2.load_checkpoint(ck)
+    m2b = tr2.step(batches[1])
+    params_b = torch.cat([p.detach().reshape(-1) for p in tr2.flat.params])
+    torch.save({"local": captured[0], "reduced": captured[1], "m1": m1, "m2": m2, "m2b": m2b, "params": params,
+                "params_b": params_b, "batch_in_epoch": st.get("batch_in_epoch")},
+               os.path.join(out_dir, f"ppo{rank}.pt"))
+    parallel.barrier()
+    parallel.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_ppo_step(tmp_path, world):
+    mp.start_processes(_ppo_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn",
+                       join=True)
+    r = [torch.load(tmp_path / f"ppo{i}.pt", weights_only=False) for i in range(world)]
+    # the all-reduce averages the ranks' local gradients, and every rank ends with the same average
+    mean_local = torch.stack([x["local"] for x in r]).mean(0)
+    assert mean_local.abs().sum() > 0
+    for x in r:
+        torch.testing.assert_close(x["reduced"], mean_local, rtol=1e-5, atol=1e-7)
+    # identical parameters on every rank after two optimizer steps
+    for x in r[1:]:
+        assert torch.equal(x["params"], r[0]["params"])
+    # reduced metrics are the same dict on every rank; throughput uses the slowest rank's time
+    for k in ("reward_mean", "total_loss", "kl_ref", "step_time_s", "rollout_tokens_per_s"):
+        assert all(x["m2"][k] == r[0]["m2"][k] for x in r), k
+    assert r[0]["m2"]["rollout_tokens_per_s"] == pytest.approx(
+        r[0]["m2"]["rollout_tokens"] * world / r[0]["m2"]["step_time_s"])
+    # rank-0 checkpoint resumed on all ranks reproduces the uninterrupted step 2 exactly
+    for x in r:
+        assert x["batch_in_epoch"] == 1
+        torch.testing.assert_close(x["params_b"], x["params"], rtol=1e-6, atol=1e-7)
+        assert abs(x["m2b"]["total_loss"] - x["m2"]["total_loss"]) < 1e-5
+
+
+def _sft_worker(rank, world, port, out_dir, n_examples):
+    _env(rank, world, port)
+    from rag_tl_domainllm_optimizer_amd import models, parallel
+    from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
+    from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
+    from rag_tl_domainllm_optimizer_amd.train.sft import SFTConfig, SFTTrainer
+
+    parallel.init(device="cpu", timeout_s=120)
+    cfg = PRESETS["tiny-llama"]
+    tok = Tokenizer.synthetic(cfg.vocab_size, "llama")
+    m = models.CausalLM(cfg, dtype=torch.float32, seed=1)
+    tr = SFTTrainer(m, tok, SFTConfig(lr=1e-2, lora_r=4, lr_schedule="constant", warmup_steps=0, batch_size=4))
+    words = tok.words()
+    ex = [{"prompt": " ".join(words[i:i + 6]), "answer": " ".join(words[50 + i:54 + i])} for i in range(n_examples)]
+    hist = tr.fit(ex, epochs=2, log_every=0)
+    params = torch.cat([p.detach().reshape(-1) for p in tr.flat.params])
+    torch.save({"steps": len(hist), "params": params}, os.path.join(out_dir, f"sft{rank}.pt"))
+    parallel.barrier()
+    parallel.shutdown()
+
+
+@pytest.mark.parametrize("world,n", [(2, 15), (8, 13)])
+def test_dp_sft_uneven_shards(tmp_path, world, n):
+    mp.start_processes(_sft_worker, args=(world, _free_port(), str(tmp_path), n), nprocs=world, start_method="spawn",
+                       join=True)
+    r = [torch.load(tmp_path / f"sft{i}.pt", weights_only=False) for i in range(world)]
+    assert len({x["steps"] for x in r}) == 1 and r[0]["steps"] >= 2
+    for x in r[1:]:
+        assert torch.equal(x["params"], r[0]["params"])
