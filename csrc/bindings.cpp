@@ -25,6 +25,8 @@ void rt_gemm_set_decode_split(int);
 int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, long, const void*, long, int,
                 const void*, void*, long, void*, long, const void*, long, int, int, int, int, int, int, const void*,
                 hipStream_t);
+int rt_gemm_small(int, int, const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
+                  hipStream_t);
 int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
 int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
                 int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
@@ -65,7 +67,9 @@ int rt_adamw_mixed(float*, const void*, long, const float*, float*, float*, void
                    float, int, float, const float*, int, float*, int*, hipStream_t);
 int rt_pool_norm(const void*, const int*, int, int, int, int, float*, hipStream_t);
 int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*, hipStream_t);
-int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const void*, const long*, int, float*, long*,
+int rt_segment_mean(const float*, int, const long*, const int*, int, int, float*, hipStream_t);
+int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const int*, const void*, const long*, const float*,
+                int, int, float*, long*,
                 hipStream_t);
 int rt_gae(const float*, const float*, const float*, int, int, float, float, float*, float*, hipStream_t);
 void rt_attn_decode_set_nk(int nk);
@@ -268,6 +272,33 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
                        has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, (int)M,
                        (int)N, (int)K, (int)act, (int)out_mode, (int)nsplit, zero_page(a).data_ptr(), cur_stream()),
            "gemm_big");
+  return c;
+}
+
+// 64x64-tile GEMM for narrow products (LoRA U / dU / dA / dB): same operand layouts as gemm_big;
+// out_mode 0 bf16 / 1 fp32 / 2 fp32 atomic accumulate into `out` (split-K over `nsplit`).
+Tensor gemm_small(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layout_b, int64_t out_mode,
+                  int64_t nsplit, optional<Tensor> out) {
+  CHECK_CUDA(a); CHECK_CUDA(b); CHECK_BF16(a); CHECK_BF16(b); CHECK_ROWS(a); CHECK_ROWS(b);
+  CHECK_ALIGN16(a); CHECK_ALIGN16(b);
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_small: row strides must be multiples of 8");
+  const int64_t M = layout_a ? a.size(1) : a.size(0), K = layout_a ? a.size(0) : a.size(1);
+  const int64_t N = layout_b ? b.size(1) : b.size(0), Kb = layout_b ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm_small: K mismatch");
+  const auto odt = out_mode == 0 ? at::kBFloat16 : at::kFloat;
+  Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.scalar_type() == odt, "gemm_small: out");
+  } else {
+    TORCH_CHECK(out_mode != 2, "gemm_small: atomic accumulation needs an initialised out");
+    c = at::empty({M, N}, a.options().dtype(odt));
+  }
+  if (M == 0 || N == 0) return c;
+  check_rc(rt_gemm_small((int)layout_a, (int)layout_b, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                         c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K, (int)out_mode, (int)nsplit,
+                         zero_page(a).data_ptr(), cur_stream()),
+           "gemm_small");
   return c;
 }
 
@@ -710,18 +741,33 @@ std::vector<Tensor> topk(const Tensor& scores, int64_t k, const optional<Tensor>
   return {vals, ids};
 }
 
-std::vector<Tensor> ivf_scan(const Tensor& q, const Tensor& probes, const Tensor& offsets, const Tensor& vecs,
-                             const Tensor& ids, int64_t maxlen) {
-  CHECK_CUDA(q); CHECK_BF16(q); CHECK_I32(probes); CHECK_I32(offsets); CHECK_BF16(vecs); CHECK_I64(ids);
-  TORCH_CHECK(q.is_contiguous() && probes.is_contiguous() && vecs.is_contiguous());
+std::vector<Tensor> ivf_scan(const Tensor& q, const Tensor& probes, const Tensor& lstart, const Tensor& lsize,
+                             const Tensor& vecs, const Tensor& ids, const optional<Tensor>& sqnorm, bool l2,
+                             int64_t maxlen) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_I32(probes); CHECK_I32(lstart); CHECK_I32(lsize); CHECK_BF16(vecs); CHECK_I64(ids);
+  TORCH_CHECK(q.is_contiguous() && probes.is_contiguous() && vecs.is_contiguous() && lstart.is_contiguous() &&
+              lsize.is_contiguous());
+  if (l2) { TORCH_CHECK(sqnorm.has_value() && sqnorm->defined(), "ivf_scan: l2 needs sqnorm"); CHECK_F32(*sqnorm); }
   const int64_t nq = q.size(0), d = q.size(1), nprobe = probes.size(1);
   auto cand = at::empty({nq, nprobe * maxlen}, q.options().dtype(at::kFloat));
   auto cid = at::empty({nq, nprobe * maxlen}, q.options().dtype(at::kLong));
-  check_rc(rt_ivf_scan(q.data_ptr(), (int)nq, (int)d, probes.data_ptr<int>(), (int)nprobe, offsets.data_ptr<int>(),
-                       vecs.data_ptr(), (const long*)ids.data_ptr(), (int)maxlen, cand.data_ptr<float>(),
+  check_rc(rt_ivf_scan(q.data_ptr(), (int)nq, (int)d, probes.data_ptr<int>(), (int)nprobe, lstart.data_ptr<int>(),
+                       lsize.data_ptr<int>(), vecs.data_ptr(), (const long*)ids.data_ptr(),
+                       l2 ? sqnorm->data_ptr<float>() : nullptr, l2 ? 1 : 0, (int)maxlen, cand.data_ptr<float>(),
                        (long*)cid.data_ptr(), cur_stream()),
            "ivf_scan");
   return {cand, cid};
+}
+
+Tensor segment_mean(const Tensor& x, const Tensor& order, const Tensor& seg, bool normalize, Tensor out) {
+  CHECK_CUDA(x); CHECK_F32(x); CHECK_I64(order); CHECK_I32(seg); CHECK_F32(out);
+  TORCH_CHECK(x.is_contiguous() && order.is_contiguous() && seg.is_contiguous() && out.is_contiguous());
+  const int64_t k = seg.numel() - 1, d = x.size(1);
+  TORCH_CHECK(out.size(0) == k && out.size(1) == d, "segment_mean: out shape");
+  check_rc(rt_segment_mean(x.data_ptr<float>(), (int)d, (const long*)order.data_ptr(), seg.data_ptr<int>(), (int)k,
+                           normalize ? 1 : 0, out.data_ptr<float>(), cur_stream()),
+           "segment_mean");
+  return out;
 }
 
 std::vector<Tensor> gae(const Tensor& rewards, const Tensor& values, const Tensor& mask, double gamma, double lam) {
@@ -796,6 +842,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_splitk", &gemm_splitk, "small-M NT GEMM: split-K fp32 slabs + fused reduce epilogue", py::arg("a"),
         py::arg("w"), py::arg("nsplit"), py::arg("slabs"), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out") = py::none(), py::arg("residual") = py::none());
+  m.def("gemm_small", &gemm_small, "64x64-tile GEMM for narrow (LoRA) products", py::arg("a"), py::arg("b"),
+        py::arg("layout_a"), py::arg("layout_b"), py::arg("out_mode") = 0, py::arg("nsplit") = 1,
+        py::arg("out") = py::none());
   m.def("gemm_fp8", &gemm_fp8, "fp8 GEMM: W8A8 (MX MFMA 256x256) or W8A16 (skinny, M <= 64)", py::arg("a"),
         py::arg("sa") = py::none(), py::arg("wq"), py::arg("sw"), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("norm_eps") = 0.0);
@@ -817,6 +866,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pool_norm", &pool_norm);
   m.def("topk", &topk);
   m.def("ivf_scan", &ivf_scan);
+  m.def("segment_mean", &segment_mean, "k-means update: per-segment mean of sorted rows (+ L2 normalise)");
   m.def("attn_decode_set_nk", &rt_attn_decode_set_nk, "fused decode attention: keys per lane per chunk (0 = default 4)");
   m.def("attn_o_set_stamps", [](optional<Tensor> t) {
     rt_attn_o_set_stamps(t.has_value() && t->defined() ? (long long*)t->data_ptr() : nullptr);

@@ -476,6 +476,145 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Small-tile GEMM for the narrow LoRA products (SURVEY K1 dA / dB / LoRA down-projection):
+//   U  = X A_pad^T   [M, Rp]   (ROW / ROW)        dU = dY UB   [M, Rp]  (ROW / KMAJ)
+//   dA = dU^T X      [Rp, K]   (KMAJ / KMAJ)      dB = dY^T U  [N, Rp]  (KMAJ / KMAJ)
+// A 256x256 tile wastes 3/4 of its MFMAs and loads on a 64-wide side, so these run on 64x64 tiles:
+// 4 waves (2 x 2, 32 x 32 each = 2 x 2 fragments), K-step 64 through a 3-slot LDS-DMA ring
+// (one slot issued, one landing, one read; counted vmcnt + raw s_barrier), several workgroups per
+// CU for latency hiding. Split-K over blockIdx.y with fp32 atomics for the token reductions.
+constexpr int SM_SLOT = 2 * 64 * 128;  // A + B images of one K-step (8 KiB each)
+constexpr int SM_SLOTS = 3;
+
+template <int LA, int LB, int OUT>
+__global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) char smem[SM_SLOTS * SM_SLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int tiles_n = (p.N + 63) / 64;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int m0 = tm * 64, n0 = tn * 64;
+  const int nk = (p.K + 63) / 64;
+  const int t_begin = (int)((long)blockIdx.y * nk / p.nsplit), t_end = (int)((long)(blockIdx.y + 1) * nk / p.nsplit);
+
+  // instruction j (0, 1) of this wave for operand op: ROW 8 rows x 128 B; KMAJ 16 k-rows x 64 B
+  auto stage = [&](int t) {
+    char* slot = smem + ((t - t_begin) % SM_SLOTS) * SM_SLOT;
+    const int k0 = t * 64;
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      const bf16_t* base = op ? p.B : p.A;
+      const long ld = op ? p.ldb : p.lda;
+      const int lim = op ? p.N : p.M;
+      const int mn0 = op ? n0 : m0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int o = wid * 2 + j;
+        if ((op ? LB : LA) == ROW) {
+          const int row = o * 8 + (lane >> 3);
+          const int kc = (lane & 7) ^ row_swz(row);
+          const int gr = min(mn0 + row, lim - 1);
+          const int kk = k0 + kc * 8;
+          const bf16_t* src = kk < p.K ? base + (long)gr * ld + kk : p.zpage + (lane & 7) * 8;
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(slot + op * 8192 + o * 1024), 16, 0, 0);
+        } else {
+          const int blk = o >> 2, kr0 = (o & 3) * 16;
+          const int kr = kr0 + (lane >> 2);
+          const int ch = (lane & 3) ^ kmaj_swz(kr);
+          const int col = min(mn0 + blk * 32 + ch * 8, lim - 8);
+          const bf16_t* src = (k0 + kr) < p.K ? base + (long)(k0 + kr) * ld + col : p.zpage + (lane & 3) * 8;
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(slot + op * 8192 + blk * 4096 + kr0 * 64),
+                                           16, 0, 0);
+        }
+      }
+    }
+  };
+  auto rd_row = [&](const char* img, int row) -> i32x8 {
+    const i32x4 lo = *(const i32x4*)(img + row * 128 + ((fq ^ row_swz(row)) << 4));
+    const i32x4 hi = *(const i32x4*)(img + row * 128 + (((4 + fq) ^ row_swz(row)) << 4));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto rd_kmaj = [&](const char* img, int mn) -> i32x8 {
+    const int blk = mn >> 5, c0 = mn & 31;
+    const int q = frow >> 2, pp = frow & 3;
+    const int col = c0 + 4 * pp;
+    const char* b = img + blk * 4096;
+    s16x4 v[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int kr = (h >> 1) * 32 + fq * 8 + (h & 1) * 4 + q;
+      const int ch = (col >> 3) ^ kmaj_swz(kr);
+      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + kr * 64 + ch * 16 + (col & 7) * 2));
+    }
+    typedef __attribute__((ext_vector_type(16))) short s16x16;
+    const s16x16 w = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3],
+                      v[2][0], v[2][1], v[2][2], v[2][3], v[3][0], v[3][1], v[3][2], v[3][3]};
+    return __builtin_bit_cast(i32x8, w);
+  };
+  auto half = [](const i32x8& v, int h) -> bf16x8 {
+    return h == 0 ? __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 0, 1, 2, 3))
+                  : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (t_begin < t_end) {
+    stage(t_begin);
+    if (t_begin + 1 < t_end) stage(t_begin + 1);
+    for (int t = t_begin; t < t_end; ++t) {
+      // retire step t (4 DMA instructions per lane per step); step t+1 may stay in flight
+      if (t + 1 < t_end) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_barrier" ::: "memory");
+      // refill the slot read in iteration t-1 (every wave passed the barrier above after reading it)
+      if (t + 2 < t_end) stage(t + 2);
+      const char* slot = smem + ((t - t_begin) % SM_SLOTS) * SM_SLOT;
+      i32x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = LA == ROW ? rd_row(slot, wr * 32 + i * 16 + frow) : rd_kmaj(slot, wr * 32 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[j] = LB == ROW ? rd_row(slot + 8192, wc * 32 + j * 16 + frow) : rd_kmaj(slot + 8192, wc * 32 + j * 16);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(half(fa[i], kk), half(fb[j], kk), acc[i][j], 0, 0, 0);
+    }
+  }
+  // lane holds C[m0 + 32 wr + 16 i + 4 fq + r][n0 + 32 wc + 16 j + frow]
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wc * 32 + j * 16 + frow;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 32 + i * 16 + fq * 4 + r;
+        if (row < p.M && col < p.N) {
+          if constexpr (OUT == O_F32_ATOMIC)
+            __hip_atomic_fetch_add((float*)p.C + (long)row * p.ldc + col, acc[i][j][r], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          else if constexpr (OUT == O_F32)
+            ((float*)p.C)[(long)row * p.ldc + col] = acc[i][j][r];
+          else
+            ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(acc[i][j][r]);
+        }
+      }
+  }
+}
+
 // Split-K reduction + epilogue of the O_F32_SLAB form (decode / small-M GEMMs, M <= 256):
 //   C[m, c] = act( sum_s slab[s][m][c] + bias[c] ) + R[m, c]            (Nout = N)
 //   C[m, c] = silu(bf16(g)) * bf16(u),  g / u = sum_s slab[s][m][c] / [F + c]   (SwiGLU, Nout = F)
@@ -602,6 +741,37 @@ extern "C" int rt_gemm_splitk_reduce(const float* slabs, int nsplit, int M, int 
   const long work = (long)M * (Nout / 8);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, slabs, nsplit,
                      M, N, (const bf16_t*)bias, act, (const bf16_t*)R, ldr, (bf16_t*)C, ldc);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+// 64x64-tile GEMM (narrow LoRA products). out: 0 bf16, 1 fp32 store, 2 fp32 atomic add (split-K).
+extern "C" int rt_gemm_small(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb, void* C,
+                             long ldc, int M, int N, int K, int out, int nsplit, const void* zpage,
+                             hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (!zpage || ((layout_a == ROW || layout_b == ROW) && K % 8)) return -1;
+  if ((layout_a == KMAJ && M % 8) || (layout_b == KMAJ && N % 8)) return -1;
+  if (nsplit < 1) nsplit = 1;
+  if (nsplit > 1 && out != O_F32_ATOMIC) return -2;
+  Args p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
+  p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
+  dim3 grid(((M + 63) / 64) * ((N + 63) / 64), nsplit), block(256);
+  const int key = layout_a * 100 + layout_b * 10 + out;
+#define GS_LAUNCH(LA, LB, O) hipLaunchKernelGGL((gemm_small_kernel<LA, LB, O>), grid, block, 0, stream, p)
+  switch (key) {
+    case 0: GS_LAUNCH(ROW, ROW, O_BF16); break;
+    case 1: GS_LAUNCH(ROW, ROW, O_F32); break;
+    case 2: GS_LAUNCH(ROW, ROW, O_F32_ATOMIC); break;
+    case 10: GS_LAUNCH(ROW, KMAJ, O_BF16); break;
+    case 11: GS_LAUNCH(ROW, KMAJ, O_F32); break;
+    case 12: GS_LAUNCH(ROW, KMAJ, O_F32_ATOMIC); break;
+    case 112: GS_LAUNCH(KMAJ, KMAJ, O_F32_ATOMIC); break;
+    case 111: GS_LAUNCH(KMAJ, KMAJ, O_F32); break;
+    default: return -4;
+  }
+#undef GS_LAUNCH
   RT_LAUNCH_CHECK();
   return 0;
 }

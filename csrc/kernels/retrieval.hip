@@ -113,19 +113,31 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ sco
 }
 
 // IVF list scan: for query qi and its probe p (list L = probes[qi, p]), score every vector of the
-// list (vectors stored contiguously per list) and write into cand[qi, p*maxlen + j] (+ ids).
-// Unused slots get -inf. One workgroup per (probe, query); one thread per vector, query in LDS.
+// list (vectors stored contiguously per list from lstart[L], lsize[L] of them; lists may carry
+// spare capacity for incremental adds) and write into cand[qi, p*maxlen + j] (+ ids).
+// Metric: inner product, or (l2) the negated squared distance 2 q.x - |x|^2 - |q|^2 with |x|^2
+// stored per slot — both "higher is better" for the shared top-k. Unused slots get -inf.
+// One workgroup per (probe, query); one thread per vector, query in LDS.
 __global__ __launch_bounds__(256) void ivf_scan_kernel(const bf16_t* __restrict__ q, int d, const int* __restrict__ probes,
-                                                       int nprobe, const int* __restrict__ offsets,
-                                                       const bf16_t* __restrict__ vecs, const long* __restrict__ ids,
-                                                       int maxlen, float* __restrict__ cand, long* __restrict__ cand_ids) {
+                                                       int nprobe, const int* __restrict__ lstart,
+                                                       const int* __restrict__ lsize, const bf16_t* __restrict__ vecs,
+                                                       const long* __restrict__ ids, const float* __restrict__ sqnorm,
+                                                       int l2, int maxlen, float* __restrict__ cand,
+                                                       long* __restrict__ cand_ids) {
   extern __shared__ float qs[];
+  __shared__ float sb[4];
   const int p = blockIdx.x, qi = blockIdx.y;
-  for (int i = threadIdx.x; i < d; i += 256) qs[i] = bf2f(q[(long)qi * d + i]);
+  float qq = 0.f;
+  for (int i = threadIdx.x; i < d; i += 256) {
+    const float v = bf2f(q[(long)qi * d + i]);
+    qs[i] = v;
+    qq += v * v;
+  }
+  const float qn = l2 ? block_sum(qq, sb) : 0.f;  // block_sum synchronises
   __syncthreads();
   const int L = probes[(long)qi * nprobe + p];
-  const int b0 = L >= 0 ? offsets[L] : 0, b1 = L >= 0 ? offsets[L + 1] : 0;
-  const int len = min(b1 - b0, maxlen);
+  const int b0 = L >= 0 ? lstart[L] : 0;
+  const int len = L >= 0 ? min(lsize[L], maxlen) : 0;
   float* out = cand + ((long)qi * nprobe + p) * maxlen;
   long* oid = cand_ids + ((long)qi * nprobe + p) * maxlen;
   for (int j = threadIdx.x; j < maxlen; j += 256) {
@@ -138,13 +150,40 @@ __global__ __launch_bounds__(256) void ivf_scan_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int e = 0; e < 8; ++e) s += f[e] * qs[c + e];
       }
-      out[j] = s;
+      out[j] = l2 ? 2.f * s - sqnorm[b0 + j] - qn : s;
       oid[j] = ids[b0 + j];
     } else {
       out[j] = -INFINITY;
       oid[j] = -1;
     }
   }
+}
+
+// k-means update: centroid c = mean of the rows order[seg[c] .. seg[c+1]) of x (rows sorted by
+// assigned centroid), L2-normalised for the inner-product metric. One workgroup per centroid, a
+// column per thread, rows summed in a fixed order (deterministic, no atomics). Empty clusters are
+// left untouched (the caller reseeds them).
+__global__ __launch_bounds__(256) void segment_mean_kernel(const float* __restrict__ x, int d,
+                                                           const long* __restrict__ order, const int* __restrict__ seg,
+                                                           int normalize, float* __restrict__ out) {
+  extern __shared__ float col[];  // [d]
+  __shared__ float sb[4];
+  const int c = blockIdx.x;
+  const int r0 = seg[c], r1 = seg[c + 1];
+  if (r1 <= r0) return;  // uniform over the block
+  const float inv = 1.f / (float)(r1 - r0);
+  float ss = 0.f;
+  for (int j = threadIdx.x; j < d; j += 256) {
+    float a = 0.f;
+    for (int r = r0; r < r1; ++r) a += x[order[r] * (long)d + j];
+    a *= inv;
+    col[j] = a;
+    ss += a * a;
+  }
+  const float tot = normalize ? block_sum(ss, sb) : 1.f;
+  const float scale = normalize ? 1.f / fmaxf(sqrtf(tot), 1e-12f) : 1.f;
+  __syncthreads();
+  for (int j = threadIdx.x; j < d; j += 256) out[(long)c * d + j] = col[j] * scale;
 }
 
 }  // namespace rt
@@ -169,13 +208,22 @@ extern "C" int rt_topk(const float* scores, long ld, long nq, int N, int k, cons
   return 0;
 }
 
-extern "C" int rt_ivf_scan(const void* q, int nq, int d, const int* probes, int nprobe, const int* offsets,
-                           const void* vecs, const long* ids, int maxlen, float* cand, long* cand_ids,
-                           hipStream_t stream) {
-  if (d % 8 != 0) return -1;
+extern "C" int rt_ivf_scan(const void* q, int nq, int d, const int* probes, int nprobe, const int* lstart,
+                           const int* lsize, const void* vecs, const long* ids, const float* sqnorm, int l2,
+                           int maxlen, float* cand, long* cand_ids, hipStream_t stream) {
+  if (d % 8 != 0 || (l2 && !sqnorm)) return -1;
   if (nq == 0) return 0;
   hipLaunchKernelGGL(ivf_scan_kernel, dim3(nprobe, nq), dim3(256), d * sizeof(float), stream, (const bf16_t*)q, d,
-                     probes, nprobe, offsets, (const bf16_t*)vecs, ids, maxlen, cand, cand_ids);
+                     probes, nprobe, lstart, lsize, (const bf16_t*)vecs, ids, sqnorm, l2, maxlen, cand, cand_ids);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int rt_segment_mean(const float* x, int d, const long* order, const int* seg, int k, int normalize,
+                               float* out, hipStream_t stream) {
+  if (k == 0) return 0;
+  hipLaunchKernelGGL(segment_mean_kernel, dim3(k), dim3(256), d * sizeof(float), stream, x, d, order, seg, normalize,
+                     out);
   RT_LAUNCH_CHECK();
   return 0;
 }

@@ -21,7 +21,8 @@ class ValueHead(nn.Module):
             self.linear.bias.zero_()
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:
-        return (h.float() @ self.linear.weight.t()).squeeze(-1) + self.linear.bias
+        # a row dot product (memory-bound, one pass over h), not a library GEMV
+        return (h.float() * self.linear.weight[0]).sum(-1) + self.linear.bias
 
     def reference_state_dict(self):
         """{"weight": [1, H], "bias": [1]} exactly as torch.nn.Linear(H, 1).state_dict()."""

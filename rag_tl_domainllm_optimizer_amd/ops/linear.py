@@ -118,17 +118,24 @@ def gemm_nn(dy: torch.Tensor, w: torch.Tensor, du=None, a_pad=None) -> torch.Ten
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, nsplit: int = 0, out=None) -> torch.Tensor:
     """a^T b in fp32 (weight / LoRA gradients): a [T, P], b [T, Q] -> [P, Q]; the token reduction
-    is split over ``nsplit`` workgroup rows (0 = fill the chip) with fp32 atomic accumulation."""
+    is split over ``nsplit`` workgroup rows (0 = fill the chip) with fp32 atomic accumulation.
+    Narrow outputs (a LoRA rank side of 64) run on the 64x64-tile kernel, wide ones on gemm_big."""
     T, P = a.shape
     Q = b.shape[1]
-    if nsplit <= 0:
-        tiles = ((P + 255) // 256) * ((Q + 255) // 256)
-        nsplit = max(1, min(64, 256 // max(tiles, 1), T // 512))
     if out is None:
         out = torch.zeros(P, Q, dtype=torch.float32, device=a.device)
     else:
         out.zero_()
-    return gemm_big(a, b, KMAJ, KMAJ, out_mode=2, nsplit=nsplit, out=out)
+    if not on_gpu(a):
+        out.add_(a.float().t() @ b.float())
+        return out
+    if min(P, Q) <= 128:
+        tiles = ((P + 63) // 64) * ((Q + 63) // 64)
+        ns = nsplit or max(1, min(T // 256, (1024 + tiles - 1) // tiles))
+        return native().gemm_small(a, b, KMAJ, KMAJ, 2, ns, out)
+    tiles = ((P + 255) // 256) * ((Q + 255) // 256)
+    ns = nsplit or max(1, min(64, 256 // max(tiles, 1), T // 512))
+    return gemm_big(a, b, KMAJ, KMAJ, out_mode=2, nsplit=ns, out=out)
 
 
 @dataclass
@@ -207,18 +214,12 @@ class LoRAGroup:
 
 def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int) -> torch.Tensor:
     """a [M, K] (ROW) times a narrow operand b (ROW [R, K] or KMAJ [K, R]; R = padded LoRA rank) ->
-    [M, R] bf16. One 256-row tile per 256 tokens cannot fill the chip, so the reduction is split
-    over workgroup rows with fp32 atomic accumulation (U = X A_pad^T forward, dU = dY UB backward)."""
-    M, K = a.shape
-    R = b.shape[0] if lb == ROW else b.shape[1]
+    [M, R] bf16 on the 64x64-tile kernel, one workgroup per 64 tokens over the full reduction
+    (U = X A_pad^T forward, dU = dY UB backward)."""
     if not on_gpu(a):
         B = b.float().t() if lb == ROW else b.float()
         return (a.float() @ B).to(a.dtype)
-    tiles = (M + 255) // 256
-    nsplit = max(1, min(K // 256, (512 + tiles - 1) // tiles))
-    acc = torch.zeros(M, R, dtype=torch.float32, device=a.device)
-    native().gemm_big(a, b, ROW, lb, None, None, None, 0, 2, nsplit, acc)
-    return acc.to(a.dtype)
+    return native().gemm_small(a, b, ROW, lb, 0, 1)
 
 
 def _dropout_mask(x: torch.Tensor, p: float) -> torch.Tensor:

@@ -141,8 +141,18 @@ def topk(scores: torch.Tensor, k: int, idmap=None):
     return ref.topk(scores, k, idmap)
 
 
-def ivf_scan(q, probes, offsets, vecs, ids, maxlen):
-    return native().ivf_scan(q.contiguous(), probes.int().contiguous(), offsets, vecs, ids, maxlen)
+def ivf_scan(q, probes, lstart, lsize, vecs, ids, maxlen, sqnorm=None, l2: bool = False):
+    """IVF list scan (GPU): scores of every vector of each probed list -> (cand [nq, nprobe*maxlen],
+    ids); inner product, or the negated squared L2 distance."""
+    return native().ivf_scan(q.contiguous(), probes.int().contiguous(), lstart, lsize, vecs, ids, sqnorm, l2, maxlen)
+
+
+def segment_mean(x, order, seg, normalize: bool, out):
+    """out[c] = mean(x[order[seg[c]:seg[c+1]]]) (L2-normalised if asked); empty segments untouched."""
+    if on_gpu(x):
+        return native().segment_mean(x.float().contiguous(), order.long().contiguous(), seg.int().contiguous(),
+                                     normalize, out)
+    return ref.segment_mean(x, order, seg, normalize, out)
 
 
 # ---------------------------------------------------------------------------------------- RL

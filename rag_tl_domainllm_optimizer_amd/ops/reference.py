@@ -274,3 +274,18 @@ def adamw_(p, g, m, v, lr, b1, b2, eps, wd, step, max_norm=0.0):
     denom = (v / bc2).sqrt().add_(eps)
     p.addcdiv_(m, denom, value=-lr / bc1)
     return norm, False
+
+
+def segment_mean(x, order, seg, normalize: bool, out):
+    """fp32 oracle of the segment_mean kernel: out[c] = mean(x[order[seg[c]:seg[c+1]]]) (+ L2 norm);
+    rows of empty segments are left as they are."""
+    k = seg.numel() - 1
+    cnt = (seg[1:] - seg[:-1]).long()
+    lab = torch.repeat_interleave(torch.arange(k, device=x.device), cnt)
+    sums = torch.zeros(k, x.shape[1], device=x.device).index_add_(0, lab, x[order.long()].float())
+    m = sums / cnt.clamp(min=1)[:, None]
+    if normalize:
+        m = torch.nn.functional.normalize(m, dim=-1)
+    nz = cnt > 0
+    out[nz] = m[nz].to(out.dtype)
+    return out

@@ -1,9 +1,10 @@
 """Vector indexes resident in device memory (HBM on MI355X).
 
 * FlatIndex — exact search: one MFMA GEMM (queries x database, fp32 scores) + radix-select top-k.
-* IVFIndex  — inverted file: spherical k-means coarse quantiser (GEMM assignment on device,
-  k-means++ seeding and the list build in native host code), vectors stored contiguously per list,
-  search = coarse GEMM -> top-nprobe lists -> list-scan kernel -> top-k with id remap.
+* IVFIndex  — inverted file: k-means coarse quantiser trained on device (GEMM + top-1 assignment,
+  segmented-mean update kernel; k-means++ seeding in native host code), capacity-padded inverted
+  lists with incremental on-device add, search = coarse GEMM -> top-nprobe lists -> list-scan
+  kernel (ip or l2) -> top-k with id remap.
 
 A 100k x 384 bf16 database is 77 MB: the whole index lives in HBM next to the models.
 Metrics: "ip" (inner product; cosine for normalised vectors) and "l2".
@@ -48,9 +49,11 @@ class FlatIndex:
         x = x.to(self.device)
         if ids is None:
             ids = torch.arange(self.ntotal, self.ntotal + x.shape[0], device=self.device)
-        self.vecs = torch.cat([self.vecs, x.to(self.vecs.dtype)], 0)
+        xs = x.to(self.vecs.dtype)
+        self.vecs = torch.cat([self.vecs, xs], 0)
         self.ids = torch.cat([self.ids, ids.to(self.device).long()], 0)
-        self.sqnorm = torch.cat([self.sqnorm, x.float().pow(2).sum(-1)], 0)
+        # |x|^2 of the stored (bf16 on GPU) vector: distances are exact w.r.t. what is stored
+        self.sqnorm = torch.cat([self.sqnorm, xs.float().pow(2).sum(-1)], 0)
         self._padded = None
 
     def _db(self):
@@ -101,6 +104,24 @@ class FlatIndex:
 
 
 class IVFIndex:
+    """Inverted-file index, entirely device-resident on GPU.
+
+    Storage: one bf16 slab ``vecs`` holding every inverted list contiguously with spare capacity
+    (``lstart``/``lsize``/``lcap`` per list, int32), the external ``ids`` and the per-slot squared
+    norm ``sqnorm`` (for the L2 metric) beside it. ``add`` is incremental: new vectors are assigned
+    on device and scattered to the tail of their lists; only when a list overflows are the lists
+    re-laid out with 1.5x headroom (amortised O(1) per vector, all on device).
+
+    Training (spherical k-means for "ip", plain k-means for "l2"): k-means++ seeding in native host
+    code on a <=16k sample, then per iteration a coarse-quantiser GEMM + fused top-1
+    (``ops.gemm`` / ``ops.topk``), a device sort by assignment and the ``segment_mean`` kernel
+    (deterministic per-centroid mean, L2-normalised for "ip").
+
+    Search: coarse GEMM -> top-nprobe lists (``ops.topk``) -> ``ivf_scan`` list-scan kernel (ip or
+    -||q-x||^2) -> top-k over the candidates. CPU tensors run the same algorithm with torch ops.
+    The reference has no vector index at all (README.md:28 declares FAISS/ChromaDB).
+    """
+
     kind = "ivf"
 
     def __init__(self, dim: int, nlist: int = 256, metric: str = "ip", device="cpu", nprobe: int = 16):
@@ -110,144 +131,205 @@ class IVFIndex:
         self.gpu = self.device.type == "cuda"
         self.dtype = torch.bfloat16 if self.gpu else torch.float32
         self.centroids = None
-        self.vecs = torch.empty(0, dim, dtype=self.dtype, device=self.device)
+        self._reset_lists(nlist)
+
+    def _reset_lists(self, nlist):
+        z = lambda: torch.zeros(nlist, dtype=torch.int32, device=self.device)  # noqa: E731
+        self.lstart, self.lsize, self.lcap = z(), z(), z()
+        self.vecs = torch.empty(0, self.dim, dtype=self.dtype, device=self.device)
         self.ids = torch.empty(0, dtype=torch.long, device=self.device)
-        self.offsets = torch.zeros(nlist + 1, dtype=torch.int32, device=self.device)
+        self.sqnorm = torch.empty(0, dtype=torch.float32, device=self.device)
         self.maxlen = 0
+        self._ntotal = 0
 
     @property
     def ntotal(self) -> int:
-        return self.ids.numel()
+        return self._ntotal
 
     @property
     def is_trained(self) -> bool:
         return self.centroids is not None
 
-    # ------------------------------------------------------------------ training
+    @property
+    def offsets(self) -> torch.Tensor:
+        """Exclusive prefix sum of the list sizes (the compacted layout), int32 [nlist + 1]."""
+        z = torch.zeros(1, dtype=torch.int32, device=self.device)
+        return torch.cat([z, torch.cumsum(self.lsize, 0).int()])
+
+    # ------------------------------------------------------------------ coarse quantiser
+    def _set_centroids(self, cen: torch.Tensor):
+        self.centroids = cen.float().contiguous()
+        n = self.centroids.shape[0]
+        # score(x, c) = x.c - pen[c]: pen = |c|^2 / 2 for l2 (argmax == nearest), 0 for ip;
+        # padding rows of the GEMM operand get +inf so they never win
+        pen = self.centroids.pow(2).sum(-1) * 0.5 if self.metric == "l2" else torch.zeros(n, device=self.device)
+        if self.gpu:
+            self._cen_op = _pad_rows(self.centroids.to(self.dtype), 128).contiguous()
+            self._pen = torch.full((self._cen_op.shape[0],), float("inf"), device=self.device)
+            self._pen[:n] = pen
+        else:
+            self._cen_op, self._pen = self.centroids, pen
+
+    def _coarse(self, x: torch.Tensor, k: int) -> torch.Tensor:
+        """indices [n, k] of the k best centroids per row (x already on device)."""
+        if self.gpu:
+            s = ops.gemm(x.to(self.dtype).contiguous(), self._cen_op, out_f32=True)
+            s.sub_(self._pen)
+            return ops.topk(s, k)[1]
+        s = x.float() @ self._cen_op.t() - self._pen
+        return torch.topk(s, k, dim=-1).indices
+
     def _assign(self, x: torch.Tensor, bs: int = 65536) -> torch.Tensor:
-        """nearest centroid per row (by the index metric)."""
+        """nearest centroid per row (by the index metric), int64 [n]."""
         out = torch.empty(x.shape[0], dtype=torch.long, device=self.device)
-        cen = _pad_rows(self.centroids.to(self.dtype), 128).contiguous() if self.gpu else self.centroids
-        cn = self.centroids.float().pow(2).sum(-1)
         for s in range(0, x.shape[0], bs):
-            xb = x[s:s + bs].to(self.device)
-            if self.gpu:
-                sc = ops.gemm(xb.to(self.dtype).contiguous(), cen, out_f32=True)[:, :self.nlist]
-            else:
-                sc = xb.float() @ self.centroids.float().t()
-            if self.metric == "l2":
-                sc = 2 * sc - cn[None]
-            out[s:s + bs] = sc.argmax(-1)
+            out[s:s + bs] = self._coarse(x[s:s + bs].to(self.device), 1)[:, 0]
         return out
 
+    # ------------------------------------------------------------------ training
     @torch.no_grad()
     def train(self, x: torch.Tensor, niter: int = 20, seed: int = 0, sample: int = 65536):
         from ..ops._ext import native
 
-        x = x.float()
         n = x.shape[0]
         g = torch.Generator(device="cpu").manual_seed(seed)
         if n > sample:
             x = x[torch.randperm(n, generator=g)[:sample].to(x.device)]
         nlist = min(self.nlist, x.shape[0])
         self.nlist = nlist
-        self.offsets = torch.zeros(nlist + 1, dtype=torch.int32, device=self.device)
-        xs = x.cpu()
-        seed_rows = native().kmeanspp_init(xs[: min(len(xs), 16384)], nlist, seed)
+        self._reset_lists(nlist)
+        xs = x[: min(len(x), 16384)].float().cpu()
+        seed_rows = native().kmeanspp_init(xs, nlist, seed)
+        xd = x.to(self.device).float().contiguous()
+        xq = xd.to(self.dtype) if self.gpu else xd
         cen = xs[seed_rows].to(self.device)
-        xd = x.to(self.device)
+        if self.metric == "ip":
+            cen = torch.nn.functional.normalize(cen, dim=-1)
+        grid = torch.arange(nlist + 1, device=self.device)
         for _ in range(niter):
-            self.centroids = cen
-            a = self._assign(xd)
-            sums = torch.zeros(nlist, self.dim, device=self.device)
-            sums.index_add_(0, a, xd)
-            cnt = torch.bincount(a, minlength=nlist).float()
-            empty = cnt == 0
-            cen = sums / cnt.clamp(min=1)[:, None]
-            if empty.any():
-                ridx = torch.randint(0, xd.shape[0], (int(empty.sum()),), generator=g).to(self.device)
-                cen[empty] = xd[ridx]
-            if self.metric == "ip":
-                cen = torch.nn.functional.normalize(cen, dim=-1)
-        self.centroids = cen.float()
+            self._set_centroids(cen)
+            a = self._assign(xq)
+            srt, order = torch.sort(a, stable=True)
+            seg = torch.searchsorted(srt, grid).int()
+            new = cen.clone()
+            ops.segment_mean(xd, order, seg, self.metric == "ip", new)
+            empty = seg[1:] == seg[:-1]
+            ne = int(empty.sum())
+            if ne:  # reseed empty clusters with random training rows
+                ridx = torch.randint(0, xd.shape[0], (ne,), generator=g).to(self.device)
+                r = xd[ridx]
+                new[empty] = torch.nn.functional.normalize(r, dim=-1) if self.metric == "ip" else r
+            cen = new
+        self._set_centroids(cen)
 
     # ------------------------------------------------------------------ add / search
+    def _grow(self, need: torch.Tensor):
+        """Re-lay the lists out with capacity >= need (1.5x headroom, multiples of 16)."""
+        cap = torch.maximum(need, self.lcap + self.lcap // 2)
+        cap = ((cap + 15) // 16 * 16).int()
+        start = (torch.cumsum(cap, 0) - cap).int()
+        total = int(cap.sum())
+        vecs = torch.empty(total, self.dim, dtype=self.dtype, device=self.device)
+        ids = torch.full((total,), -1, dtype=torch.long, device=self.device)
+        sq = torch.zeros(total, dtype=torch.float32, device=self.device)
+        if self._ntotal:
+            lists = torch.repeat_interleave(torch.arange(self.nlist, device=self.device), self.lsize.long())
+            first = (torch.cumsum(self.lsize, 0) - self.lsize).long()
+            within = torch.arange(lists.numel(), device=self.device) - first[lists]
+            src = self.lstart.long()[lists] + within
+            dst = start.long()[lists] + within
+            vecs[dst] = self.vecs[src]
+            ids[dst] = self.ids[src]
+            sq[dst] = self.sqnorm[src]
+        self.vecs, self.ids, self.sqnorm = vecs, ids, sq
+        self.lstart, self.lcap = start, cap
+
     @torch.no_grad()
     def add(self, x: torch.Tensor, ids: Optional[torch.Tensor] = None):
-        from ..ops._ext import native
-
         assert self.is_trained, "IVFIndex.add before train"
-        x = x.to(self.device)
-        if ids is None:
-            ids = torch.arange(self.ntotal, self.ntotal + x.shape[0], device=self.device)
-        # merge with existing content and rebuild lists (counting sort in native host code)
-        allx = torch.cat([self.vecs.float(), x.float()], 0) if self.ntotal else x.float()
-        allid = torch.cat([self.ids, ids.to(self.device).long()], 0) if self.ntotal else ids.to(self.device).long()
-        a = self._assign(allx)
-        offsets, order = native().ivf_build_lists(a.cpu(), self.nlist)
-        order = order.to(self.device)
-        self.vecs = allx[order].to(self.dtype).contiguous()
-        self.ids = allid[order].contiguous()
-        self.offsets = offsets.to(self.device)
-        sizes = offsets[1:] - offsets[:-1]
-        self.maxlen = int(sizes.max()) if sizes.numel() else 0
+        n = x.shape[0]
+        if n == 0:
+            return
+        xq = x.to(self.device).to(self.dtype).contiguous()
+        ids = (torch.arange(self._ntotal, self._ntotal + n, device=self.device) if ids is None
+               else ids.to(self.device).long())
+        a = self._assign(xq)
+        cnt = torch.bincount(a, minlength=self.nlist).int()
+        need = self.lsize + cnt
+        if bool((need > self.lcap).any()):
+            self._grow(need)
+        srt, order = torch.sort(a, stable=True)
+        first = (torch.cumsum(cnt, 0) - cnt).long()
+        rank = torch.arange(n, device=self.device) - first[srt]
+        pos = self.lstart.long()[srt] + self.lsize.long()[srt] + rank
+        xs = xq[order]
+        self.vecs[pos] = xs
+        self.ids[pos] = ids[order]
+        self.sqnorm[pos] = xs.float().pow(2).sum(-1)
+        self.lsize = need.int()
+        self._ntotal += n
+        self.maxlen = int(self.lsize.max())
 
     def search(self, q: torch.Tensor, k: int, nprobe: Optional[int] = None):
+        """-> (scores [nq, k] descending (l2: squared distances ascending), ids [nq, k]; -1 pads)."""
         if q.dim() == 1:
             q = q[None]
         nprobe = min(nprobe or self.nprobe, self.nlist)
         q = q.to(self.device)
-        nq = q.shape[0]
-        # coarse quantiser
+        l2 = self.metric == "l2"
+        probes = self._coarse(q, nprobe)
+        maxlen = max(self.maxlen, 1)
+        kk = min(k, nprobe * maxlen)
         if self.gpu:
-            cen = _pad_rows(self.centroids.to(self.dtype), 128).contiguous()
-            cs = ops.gemm(q.to(self.dtype).contiguous(), cen, out_f32=True)[:, :self.nlist].contiguous()
-        else:
-            cs = q.float() @ self.centroids.float().t()
-        if self.metric == "l2":
-            cs = 2 * cs - self.centroids.float().pow(2).sum(-1)[None]
-        probes = torch.topk(cs, nprobe, dim=-1).indices
-        if self.gpu and self.metric == "ip" and self.dim % 8 == 0:
-            cand, cid = ops.ivf_scan(q.to(self.dtype), probes, self.offsets, self.vecs, self.ids, max(self.maxlen, 1))
-            kk = min(k, cand.shape[1])
+            cand, cid = ops.ivf_scan(q.to(self.dtype), probes, self.lstart, self.lsize, self.vecs, self.ids, maxlen,
+                                     self.sqnorm, l2)
             v, i = ops.topk(cand, kk)
-            ids = cid.gather(1, i.clamp(min=0))
-            ids = torch.where(torch.isfinite(v), ids, torch.full_like(ids, -1))
-            return v, ids
-        # generic path (CPU / l2)
-        res_v = torch.full((nq, k), float("-inf"), device=self.device)
-        res_i = torch.full((nq, k), -1, dtype=torch.long, device=self.device)
-        off = self.offsets.long().cpu()
-        for qi in range(nq):
-            rows = torch.cat([torch.arange(int(off[l]), int(off[l + 1])) for l in probes[qi].tolist()])
-            if rows.numel() == 0:
-                continue
-            rows = rows.to(self.device)
-            xv = self.vecs[rows].float()
-            s = xv @ q[qi].float()
-            if self.metric == "l2":
-                s = 2 * s - xv.pow(2).sum(-1) - q[qi].float().pow(2).sum()
-            kk = min(k, s.numel())
-            v, i = torch.topk(s, kk)
-            res_v[qi, :kk] = v
-            res_i[qi, :kk] = self.ids[rows[i]]
-        if self.metric == "l2":
-            res_v = -res_v
-        return res_v, res_i
+        else:
+            # same algorithm as the list-scan kernel: [nq, nprobe, maxlen] candidate slots
+            j = torch.arange(maxlen)
+            slot = self.lstart.long()[probes][..., None] + j
+            valid = j < self.lsize.long()[probes][..., None]
+            slot = torch.where(valid, slot, torch.zeros_like(slot)).reshape(q.shape[0], -1)
+            valid = valid.reshape(q.shape[0], -1)
+            xv = self.vecs[slot] if self.vecs.numel() else torch.zeros(*slot.shape, self.dim)
+            cand = (xv * q.float()[:, None, :]).sum(-1)
+            if l2:
+                cand = 2 * cand - self.sqnorm[slot] - q.float().pow(2).sum(-1, keepdim=True)
+            cand = torch.where(valid, cand, torch.full_like(cand, float("-inf")))
+            cid = torch.where(valid, self.ids[slot] if self.ids.numel() else slot, torch.full_like(slot, -1))
+            v, i = torch.topk(cand, kk, dim=-1)
+        out_ids = cid.gather(1, i.clamp(min=0))
+        out_ids = torch.where(torch.isfinite(v), out_ids, torch.full_like(out_ids, -1))
+        if kk < k:
+            v = torch.cat([v, torch.full((v.shape[0], k - kk), float("-inf"), device=v.device)], 1)
+            out_ids = torch.cat([out_ids, torch.full((v.shape[0], k - kk), -1, dtype=torch.long,
+                                                     device=v.device)], 1)
+        if l2:
+            v = -v
+        return v, out_ids
 
     # ------------------------------------------------------------------ persistence
     def state(self):
-        return {"vecs": self.vecs.float().cpu(), "ids": self.ids.cpu(), "offsets": self.offsets.cpu(),
+        """Compacted lists (no spare capacity) + centroids."""
+        lists = torch.repeat_interleave(torch.arange(self.nlist, device=self.device), self.lsize.long())
+        first = (torch.cumsum(self.lsize, 0) - self.lsize).long()
+        src = self.lstart.long()[lists] + torch.arange(lists.numel(), device=self.device) - first[lists]
+        return {"vecs": self.vecs[src].float().cpu(), "ids": self.ids[src].cpu(), "offsets": self.offsets.cpu(),
                 "centroids": self.centroids.float().cpu()}, \
                {"kind": self.kind, "dim": self.dim, "metric": self.metric, "nlist": self.nlist, "nprobe": self.nprobe}
 
     def load_state(self, t):
-        self.vecs = t["vecs"].to(self.device, self.dtype)
+        off = t["offsets"].to(self.device).int()
+        self.nlist = off.numel() - 1
+        self._set_centroids(t["centroids"].to(self.device))
+        self.lstart = off[:-1].contiguous()
+        self.lsize = (off[1:] - off[:-1]).contiguous()
+        self.lcap = self.lsize.clone()
+        self.vecs = t["vecs"].to(self.device, self.dtype).contiguous()
         self.ids = t["ids"].to(self.device)
-        self.offsets = t["offsets"].to(self.device)
-        self.centroids = t["centroids"].to(self.device)
-        sizes = t["offsets"][1:] - t["offsets"][:-1]
-        self.maxlen = int(sizes.max()) if sizes.numel() else 0
+        self.sqnorm = self.vecs.float().pow(2).sum(-1)
+        self._ntotal = self.ids.numel()
+        self.maxlen = int(self.lsize.max()) if self.nlist else 0
 
     def save(self, path: str):
         _save(self, path)

@@ -73,7 +73,7 @@ class RewardModel:
         if maxd:
             pad = torch.tensor([x + [-1] * (maxd - len(x)) for x in d_i], device=dev)
             Dm = emb[pad.clamp(min=0)]                      # [B, maxd, d]
-            sims = torch.einsum("bd,bkd->bk", R, Dm).masked_fill(pad < 0, float("-inf"))
+            sims = (R[:, None, :] * Dm).sum(-1).masked_fill(pad < 0, float("-inf"))
             fact = torch.where(pad.ge(0).any(-1), sims.max(-1).values, torch.zeros_like(rel))
         wc = [len(r.split()) for r in responses]
         conc = torch.tensor([conciseness(w, self.cfg) for w in wc], device=dev)

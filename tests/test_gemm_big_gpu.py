@@ -106,3 +106,15 @@ def test_splitk_small_m(M, N, K, split):
     pre = want.to(torch.bfloat16).float()
     F = N // 2
     _close(f, torch.nn.functional.silu(pre[:, :F]) * pre[:, F:])
+
+
+@pytest.mark.parametrize("M,K,R", [(300, 4096, 64), (1000, 14336, 64), (77, 520, 128)])
+def test_small_tile_narrow(M, K, R):
+    """64x64-tile kernel: U = X A^T (ROW/ROW), dU = dY UB (ROW/KMAJ), bf16 out; TN split-K atomics."""
+    x, a = _r(M, K), _r(R, K, s=1 / math.sqrt(K))
+    _close(ops.native().gemm_small(x, a, ops.ROW, ops.ROW, 0, 1), x.float() @ a.float().t())
+    ub = _r(K, R, s=1 / math.sqrt(K))
+    _close(ops.native().gemm_small(x, ub, ops.ROW, ops.KMAJ, 0, 1), x.float() @ ub.float())
+    t = _r(M, R)
+    _close(ops.gemm_tn(t, x), t.float().t() @ x.float(), rtol=5e-3, atol=5e-3)
+    _close(ops.gemm_tn(x, t), x.float().t() @ t.float(), rtol=5e-3, atol=5e-3)

@@ -420,22 +420,28 @@ def test_pool_topk_ivf_gae():
     v, i = ops.topk(scores, 10)
     vr, ir = torch.topk(scores, 10)
     assert torch.equal(i, ir) and torch.allclose(v, vr)
-    # ivf scan over 3 lists
+    # ivf scan over 3 capacity-padded lists (list 0 holds 7 of its 10 slots), ip and l2
     d = 64
     vecs = torch.randn(50, d, device=DEV, dtype=torch.bfloat16)
     ids = torch.arange(50, device=DEV) + 1000
-    offsets = torch.tensor([0, 10, 35, 50], device=DEV, dtype=torch.int32)
+    lstart = torch.tensor([0, 10, 35], device=DEV, dtype=torch.int32)
+    lsize = torch.tensor([7, 25, 15], device=DEV, dtype=torch.int32)
+    sq = vecs.float().pow(2).sum(-1)
     q = torch.randn(2, d, device=DEV, dtype=torch.bfloat16)
     probes = torch.tensor([[2, 0], [1, 2]], device=DEV, dtype=torch.int32)
-    cand, cid = ops.ivf_scan(q, probes, offsets, vecs, ids, 32)
-    full = q.float() @ vecs.float().t()
-    for qi in range(2):
-        for p in range(2):
-            L = int(probes[qi, p])
-            a, b = int(offsets[L]), int(offsets[L + 1])
-            n = min(b - a, 32)
-            _close(cand[qi, p * 32:p * 32 + n], full[qi, a:a + n], rtol=1e-2, atol=1e-2)
-            assert torch.equal(cid[qi, p * 32:p * 32 + n], ids[a:a + n])
+    for l2 in (False, True):
+        cand, cid = ops.ivf_scan(q, probes, lstart, lsize, vecs, ids, 32, sq, l2)
+        full = q.float() @ vecs.float().t()
+        if l2:
+            full = 2 * full - sq[None] - q.float().pow(2).sum(-1, keepdim=True)
+        for qi in range(2):
+            for p in range(2):
+                L = int(probes[qi, p])
+                a, n = int(lstart[L]), min(int(lsize[L]), 32)
+                _close(cand[qi, p * 32:p * 32 + n], full[qi, a:a + n], rtol=1e-2, atol=3e-2)
+                assert torch.equal(cid[qi, p * 32:p * 32 + n], ids[a:a + n])
+                assert bool((cid[qi, p * 32 + n:(p + 1) * 32] == -1).all())
+                assert bool(torch.isinf(cand[qi, p * 32 + n:(p + 1) * 32]).all())
     r = torch.randn(3, 17, device=DEV)
     val = torch.randn(3, 17, device=DEV)
     mask = (torch.arange(17, device=DEV)[None] < torch.tensor([17, 9, 1], device=DEV)[:, None]).float()

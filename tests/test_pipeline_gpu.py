@@ -137,13 +137,27 @@ def test_rccl_process_group_world1():
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
-def test_reward_stream_overlap_matches_serial():
-    """Reward scoring on the side HIP stream (overlapped with the reference forward) gives the same
-    rewards and losses as the serialized schedule (SURVEY §5.2 stream-overlap correctness)."""
+def test_reward_stream_overlap_matches_serial(monkeypatch):
+    """overlap_reward=True: the reward encoder runs on the side stream WHILE the reference forward
+    runs on the main stream — with a GPU spin injected in front of every reference minibatch, the
+    encoder's last event completes before the reference forward's end event (it would complete
+    after it if the reward waited for the main stream, as a blocking .cpu() of the rollout tokens
+    on the main stream made it do). overlap_reward=False scores first, serially. Both schedules
+    give the same rewards and losses (SURVEY §5.2 stream-overlap correctness)."""
+    import rag_tl_domainllm_optimizer_amd.train.ppo as P
     from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
     from rag_tl_domainllm_optimizer_amd.train.ppo import PPOConfig, PPOTrainer
 
-    res = []
+    orig = P.score_sequences
+    spin = {"on": False}
+
+    def slow_ref(*a, **k):
+        if spin["on"]:
+            torch.cuda._sleep(100_000_000)  # tens of ms of GPU spin on the current (main) stream
+        return orig(*a, **k)
+
+    monkeypatch.setattr(P, "score_sequences", slow_ref)
+    res, evs = [], []
     for overlap in (True, False):
         pol, tok, enc, corpus = _tiny_stack(5)
         items = corpus.sample_queries(8, seed=1)
@@ -152,7 +166,21 @@ def test_reward_stream_overlap_matches_serial():
         tr = PPOTrainer(pol, tok, RewardModel(enc), PPOConfig(max_new_tokens=8, max_prompt_tokens=96,
                                                               minibatch_size=4, lora_r=8, overlap_reward=overlap,
                                                               seed=3), max_batch=8)
-        res.append(tr.step(batch))
+        tr.record_overlap_events = True
+        ro = tr.rollout(batch)
+        spin["on"] = True
+        tr.prepare(ro)
+        spin["on"] = False
+        torch.cuda.synchronize()
+        e = tr.overlap_events
+        t = {k: e["ref_start"].elapsed_time(v) for k, v in e.items()}
+        evs.append(t)
+        upd = tr.update(ro)
+        res.append({"reward_mean": float(ro.scores.mean()), "kl_ref": ro.kl_ref,
+                    "factual_accuracy": float(ro.components["factual_accuracy"].mean()), **upd})
+    ov, ser = evs
+    assert ov["reward_end"] < ov["ref_end"], ov        # encoder finished while the reference ran
+    assert ser["reward_end"] <= 0.0, ser               # serial: scored before the reference started
     a, b = res
-    for k in ("reward_mean", "factual_accuracy", "relevance", "conciseness", "kl_ref", "total_loss"):
+    for k in ("reward_mean", "factual_accuracy", "kl_ref", "total_loss"):
         assert abs(a[k] - b[k]) < 1e-5, (k, a[k], b[k])

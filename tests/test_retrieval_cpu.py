@@ -58,6 +58,49 @@ def test_ivf_full_probe_is_exact_and_recall():
     assert hits / fi.numel() >= 0.8
 
 
+@pytest.mark.parametrize("metric", ["ip", "l2"])
+def test_ivf_incremental_add_and_l2(metric):
+    """Adding in pieces (several list re-layouts) gives the same search results as one add; with
+    nprobe == nlist the IVF search is exact for both metrics."""
+    x = _clustered(1500, 16, seed=2) * (1.0 if metric == "ip" else 3.0)
+    q = _clustered(30, 16, seed=7) * (1.0 if metric == "ip" else 3.0)
+    one = IVFIndex(16, nlist=12, metric=metric, nprobe=12)
+    one.train(x, niter=4)
+    one.add(x)
+    inc = IVFIndex(16, nlist=12, metric=metric, nprobe=12)
+    inc.train(x, niter=4)
+    for s in (0, 7, 300, 301, 900):
+        e = {0: 7, 7: 300, 300: 301, 301: 900, 900: 1500}[s]
+        inc.add(x[s:e])
+    assert inc.ntotal == one.ntotal == 1500
+    assert bool((inc.lcap >= inc.lsize).all()) and int(inc.lsize.sum()) == 1500
+    v0, i0 = one.search(q, 8)
+    v1, i1 = inc.search(q, 8)
+    assert torch.equal(i0, i1)
+    torch.testing.assert_close(v0, v1)
+    flat = FlatIndex(16, metric)
+    flat.add(x)
+    vf, fi = flat.search(q, 8)
+    assert torch.equal(i0, fi)
+    torch.testing.assert_close(v0, vf, rtol=1e-4, atol=1e-4)
+
+
+def test_segment_mean_reference():
+    from rag_tl_domainllm_optimizer_amd.ops import reference as ref
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(50, 8, generator=g)
+    a = torch.randint(0, 6, (50,), generator=g)
+    a[a == 3] = 2  # one empty cluster
+    srt, order = torch.sort(a, stable=True)
+    seg = torch.searchsorted(srt, torch.arange(7)).int()
+    out = torch.full((6, 8), 7.0)
+    ref.segment_mean(x, order, seg, False, out)
+    for c in range(6):
+        want = x[a == c].mean(0) if (a == c).any() else torch.full((8,), 7.0)
+        torch.testing.assert_close(out[c], want)
+
+
 def test_index_save_load_roundtrip(tmp_path):
     x = _clustered(400, 16)
     q = _clustered(8, 16, seed=9)
