@@ -24,7 +24,7 @@ void rt_gemm_set_m64_split(int);
 void rt_gemm_set_decode_split(int);
 int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, long, const void*, long, int,
                 const void*, void*, long, void*, long, const void*, long, int, int, int, int, int, int, const void*,
-                hipStream_t);
+                int, hipStream_t);
 int rt_gemm_small(int, int, const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
                   hipStream_t);
 int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
@@ -202,7 +202,8 @@ const Tensor& zero_page(const Tensor& like) {
 
 Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layout_b, const optional<Tensor>& a2,
                 const optional<Tensor>& b2, const optional<Tensor>& bias, int64_t act, int64_t out_mode,
-                int64_t nsplit, optional<Tensor> out, const optional<Tensor>& out2, const optional<Tensor>& residual) {
+                int64_t nsplit, optional<Tensor> out, const optional<Tensor>& out2, const optional<Tensor>& residual,
+                int64_t bn) {
   CHECK_CUDA(a); CHECK_CUDA(b); CHECK_BF16(a); CHECK_BF16(b); CHECK_ROWS(a); CHECK_ROWS(b);
   CHECK_ALIGN16(a); CHECK_ALIGN16(b);
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_big: row strides must be multiples of 8");
@@ -270,7 +271,8 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
                        ext ? a2->data_ptr() : nullptr, ext ? a2->stride(0) : 0, ext ? b2->data_ptr() : nullptr,
                        ext ? b2->stride(0) : 0, (int)K2, opt_ptr(bias), c.data_ptr(), c.stride(0), c2, ldc2,
                        has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, (int)M,
-                       (int)N, (int)K, (int)act, (int)out_mode, (int)nsplit, zero_page(a).data_ptr(), cur_stream()),
+                       (int)N, (int)K, (int)act, (int)out_mode, (int)nsplit, zero_page(a).data_ptr(), (int)bn,
+                       cur_stream()),
            "gemm_big");
   return c;
 }
@@ -306,7 +308,7 @@ Tensor gemm_small(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t la
 // K split over `nsplit` workgroup rows into fp32 slabs (workspace `slabs`, >= nsplit*M*N floats),
 // then one reduce kernel with the epilogue (bias, act / SwiGLU pairing, residual).
 Tensor gemm_splitk(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor slabs, const optional<Tensor>& bias,
-                   int64_t act, optional<Tensor> out, const optional<Tensor>& residual) {
+                   int64_t act, optional<Tensor> out, const optional<Tensor>& residual, int64_t bn) {
   CHECK_CUDA(a); CHECK_BF16(a); CHECK_BF16(w); CHECK_ROWS(a); CHECK_ROWS(w); CHECK_F32(slabs);
   CHECK_ALIGN16(a); CHECK_ALIGN16(w);
   const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
@@ -334,7 +336,7 @@ Tensor gemm_splitk(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor slab
   if (M == 0) return c;
   check_rc(rt_gemm_big(0, 0, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), nullptr, 0, nullptr, 0, 0,
                        nullptr, slabs.data_ptr(), N, nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, 0, 3,
-                       (int)nsplit, zero_page(a).data_ptr(), cur_stream()),
+                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, cur_stream()),
            "gemm_splitk");
   check_rc(rt_gemm_splitk_reduce(slabs.data_ptr<float>(), (int)nsplit, (int)M, (int)N, opt_ptr(bias), (int)act,
                                  has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, c.data_ptr(),
@@ -838,10 +840,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a"), py::arg("b"), py::arg("layout_a"), py::arg("layout_b"), py::arg("a2") = py::none(),
         py::arg("b2") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("out_mode") = 0,
         py::arg("nsplit") = 1, py::arg("out") = py::none(), py::arg("out2") = py::none(),
-        py::arg("residual") = py::none());
+        py::arg("residual") = py::none(), py::arg("bn") = 0);
   m.def("gemm_splitk", &gemm_splitk, "small-M NT GEMM: split-K fp32 slabs + fused reduce epilogue", py::arg("a"),
         py::arg("w"), py::arg("nsplit"), py::arg("slabs"), py::arg("bias") = py::none(), py::arg("act") = 0,
-        py::arg("out") = py::none(), py::arg("residual") = py::none());
+        py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("bn") = 256);
   m.def("gemm_small", &gemm_small, "64x64-tile GEMM for narrow (LoRA) products", py::arg("a"), py::arg("b"),
         py::arg("layout_a"), py::arg("layout_b"), py::arg("out_mode") = 0, py::arg("nsplit") = 1,
         py::arg("out") = py::none());

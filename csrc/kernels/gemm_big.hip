@@ -84,19 +84,36 @@ __device__ __forceinline__ float act_fn(float x, int act) {
   }
 }
 
-// counted wait: leave n (wave-uniform, 0..4) granules = 2n LDS-DMA instructions per lane in flight
+// counted wait: leave the n newest granules (wave-uniform; n = 4, 2, 1 or 0 at the call sites) in
+// flight. BN = 256: every granule is 2 LDS-DMA instructions per lane -> vmcnt(2n). BN = 128: the B
+// granules are 1 instruction; at every call site the n newest granules are
+//   n = 4: two A + two B granules -> 6;   n = 2: a1 + b1 -> 3;   n = 1: a1 -> 2
+template <int BN>
 __device__ __forceinline__ void wait_granules(int n) {
-  if (n >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (n == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (BN == 256) {
+    if (n >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (n >= 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
 #define GB_BARRIER() asm volatile("s_barrier" ::: "memory")
 
-template <int LA, int LB, int OUT, int EPI>
+// BN = 256 (default) or 128 output columns per tile. The 128-wide form keeps the A side, the phase
+// structure and the issue order; its B granules are 64 rows (one LDS-DMA instruction per wave) and
+// each wave owns 2 B fragments instead of 4 (columns 64 (wc >> 1) + 16 (wc & 1) + 32 s): used for
+// M = 256 decode GEMMs (twice the workgroups, no split-K on the widest weights) and for the last,
+// partial wave of tiles of a large GEMM (rt_gemm_big_planned).
+template <int LA, int LB, int OUT, int EPI, int BN>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
+  static_assert(BN == 256 || BN == 128, "BN");
+  constexpr int NB = BN / 128;  // B fragments per wave and B sub-block; LDS-DMA instructions per B granule
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];  // the only __shared__ object
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -106,7 +123,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
 
   // ---- tile assignment: XCD remap, then GROUP_M-row groups (L2 reuse of B panels) ----
   const int tiles_m = (p.M + 255) / 256;
-  const int tiles_n = EPI == E_SWIGLU ? p.N / 256 : (p.N + 255) / 256;
+  const int tiles_n = EPI == E_SWIGLU ? p.N / BN : (p.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int group = bid / (GROUP_M * tiles_n);
@@ -114,8 +131,9 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   const int gsz = min(tiles_m - first_m, GROUP_M);
   const int tm = first_m + (bid % gsz);
   const int tn = (bid % (GROUP_M * tiles_n)) / gsz;
-  const int m0 = tm * 256, n0 = tn * 256;
+  const int m0 = tm * 256, n0 = tn * BN;
   const int Fh = p.N / 2;  // E_SWIGLU: gate rows [0, F), up rows [F, 2F)
+  constexpr int HALF = BN / 2;  // E_SWIGLU: tile columns [0, HALF) gate, [HALF, BN) up
 
   // ---- K-steps of this split ----
   const int nk1 = (p.K + 63) / 64;
@@ -130,7 +148,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   // KMAJ: 16 k-rows x 64 B of one 32-wide block; lane -> k-row kr0 + lane/4, chunk lane%4 holding
   //       mn-chunk (lane%4) ^ kmaj_swz(kr)
   auto lds_dst = [&](int g, int j) -> int {  // byte offset of the instruction's 1 KiB in the K-step image
-    const int op = g >> 1, s = g & 1, o = wid * 2 + j;
+    const int op = g >> 1, s = g & 1, o = (op == 0 || NB == 2) ? wid * 2 + j : wid;
     if ((op ? LB : LA) == ROW) {
       const int rb = op == 0 ? (o >> 3) * 128 + s * 64 + (o & 7) * 8 : (o >> 2) * 64 + s * 32 + (o & 3) * 8;
       return op * OPB + rb * 128;
@@ -141,14 +159,14 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   // per-lane element offset of the source (relative to the operand base + K-step advance) and the
   // lane's reduction index within the K-step (for ragged tails)
   auto src_off = [&](int g, int j, long ld, bool main_w, int& kin) -> uint32_t {
-    const int op = g >> 1, s = g & 1, o = wid * 2 + j;
+    const int op = g >> 1, s = g & 1, o = (op == 0 || NB == 2) ? wid * 2 + j : wid;
     if ((op ? LB : LA) == ROW) {
       const int rb = op == 0 ? (o >> 3) * 128 + s * 64 + (o & 7) * 8 : (o >> 2) * 64 + s * 32 + (o & 3) * 8;
       const int row = rb + (lane >> 3);
       const int kc = (lane & 7) ^ row_swz(row);
       int grow;
       if (op == 0) grow = min(m0 + row, p.M - 1);
-      else if (EPI == E_SWIGLU && main_w) grow = row < 128 ? tn * 128 + row : Fh + tn * 128 + row - 128;
+      else if (EPI == E_SWIGLU && main_w) grow = row < HALF ? tn * HALF + row : Fh + tn * HALF + row - HALF;
       else grow = min(n0 + row, p.N - 1);
       kin = kc * 8;
       return (uint32_t)grow * (uint32_t)ld + (uint32_t)(kc * 8);
@@ -166,8 +184,8 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      int ki;
-      off[g][j] = src_off(g, j, (g >> 1) ? p.ldb : p.lda, true, ki);
+      int ki = 0;
+      off[g][j] = (g < 2 || j < NB) ? src_off(g, j, (g >> 1) ? p.ldb : p.lda, true, ki) : 0u;
       if (g < 2) kin[g][j] = ki;
     }
   // one granule g of K-step t into buffer t & 1 (g is a literal at every call site)
@@ -180,11 +198,11 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       const bf16_t* base = (op ? p.B : p.A) + adv;
       if (k0 + 64 <= p.K) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < (op ? NB : 2); ++j)
           __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
       } else {  // ragged reduction tail: out-of-range k reads the zero page
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < (op ? NB : 2); ++j) {
           int ki;
           src_off(g, j, 1, true, ki);
           const bf16_t* src = k0 + ki < p.K ? base + off[g][j] : p.zpage + (lane & 7) * 8;
@@ -197,7 +215,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       const long adv = ((op ? LB : LA) == ROW) ? (long)k0 : (long)k0 * ld2;
       const bf16_t* base = (op ? p.B2 : p.A2) + adv;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < (op ? NB : 2); ++j) {
         int ki;
         const uint32_t o2 = src_off(g, j, ld2, false, ki);
         const bf16_t* src = k0 + ki < p.K2 ? base + o2 : p.zpage + (lane & 7) * 8;
@@ -243,8 +261,8 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   auto read_b = [&](int buf, int s, i32x8 (&fb)[2]) {
     const char* img = smem + buf * BUF + OPB;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = (wc >> 1) * 128 + (wc & 1) * 64 + s * 32 + j * 16;
+    for (int j = 0; j < NB; ++j) {
+      const int row = NB == 2 ? (wc >> 1) * 128 + (wc & 1) * 64 + s * 32 + j * 16 : (wc >> 1) * 64 + s * 32 + (wc & 1) * 16;
       fb[j] = LB == ROW ? rd_row(img, row + frow) : rd_kmaj(img, row);
     }
   };
@@ -253,11 +271,13 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
                   : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][2 * NB];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2 * NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // tile column of accumulator column-fragment j (0 .. 2 NB - 1; j / NB = B sub-block)
+  auto col_of = [&](int j) -> int { return NB == 2 ? wc * 64 + j * 16 : (wc >> 1) * 64 + (wc & 1) * 16 + j * 32; };
 
   // SWAP: B fragment as the MFMA's A operand -> the accumulator holds C^T, i.e. every lane owns
   // 4 CONSECUTIVE output columns of one row (16-B fp32 / 8-B bf16 epilogue stores instead of
@@ -270,13 +290,13 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     __builtin_amdgcn_sched_barrier(0);                                                      \
     __builtin_amdgcn_s_setprio(1);                                                          \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                           \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                         \
+      _Pragma("unroll") for (int j = 0; j < NB; ++j)                                        \
         _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                    \
-          acc[(SA) * 4 + i][(SB) * 2 + j] = SWAP                                            \
+          acc[(SA) * 4 + i][(SB) * NB + j] = SWAP                                           \
               ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(half(FB[j], kk), half(fa[i], kk),   \
-                                                        acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0) \
+                                                        acc[(SA) * 4 + i][(SB) * NB + j], 0, 0, 0) \
               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(half(fa[i], kk), half(FB[j], kk),   \
-                                                        acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0); \
+                                                        acc[(SA) * 4 + i][(SB) * NB + j], 0, 0, 0); \
     __builtin_amdgcn_s_setprio(0);                                                          \
     GB_BARRIER();                                                                           \
   } while (0)
@@ -287,7 +307,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     const bool two = t_begin + 1 < t_end;
     stage(0, t_begin); stage(2, t_begin); stage(3, t_begin); stage(1, t_begin);
     if (two) { stage(0, t_begin + 1); stage(2, t_begin + 1); }
-    wait_granules(two ? 4 : 2);  // retire a0, b0 of t_begin
+    wait_granules<BN>(two ? 4 : 2);  // retire a0, b0 of t_begin
     GB_BARRIER();  // raw: a __syncthreads() would drain the granules still in flight
     if (wr == 1) GB_BARRIER();
 
@@ -301,7 +321,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       const bf16_t* base = (op ? p.B : p.A) + adv;
       char* img = smem + (u & 1) * BUF;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < (op ? NB : 2); ++j)
         __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
     };
     int t = t_begin;
@@ -310,17 +330,17 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       read_a(buf, 0);
       read_b(buf, 0, fb0);
       stage_fast(3, t + 1);
-      wait_granules(4);
+      wait_granules<BN>(4);
       GB_MMA(0, 0, fb0);
       read_b(buf, 1, fb1);
       stage_fast(1, t + 1);
-      wait_granules(4);
+      wait_granules<BN>(4);
       GB_MMA(0, 1, fb1);
       read_a(buf, 1);
       stage_fast(0, t + 2);
       GB_MMA(1, 1, fb1);
       stage_fast(2, t + 2);
-      wait_granules(4);
+      wait_granules<BN>(4);
       GB_MMA(1, 0, fb0);
     }
     for (; t < t_end; ++t) {
@@ -330,12 +350,12 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       read_a(buf, 0);
       read_b(buf, 0, fb0);
       if (n1) stage(3, t + 1);
-      wait_granules(n1 ? 4 : 1);
+      wait_granules<BN>(n1 ? 4 : 1);
       GB_MMA(0, 0, fb0);
       // p2: a0 x b1; stage a1(t+1); retire a1(t)
       read_b(buf, 1, fb1);
       if (n1) stage(1, t + 1);
-      wait_granules(n1 ? 4 : 0);
+      wait_granules<BN>(n1 ? 4 : 0);
       GB_MMA(0, 1, fb1);
       // p3: a1 x b1; stage a0(t+2)
       read_a(buf, 1);
@@ -343,7 +363,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       GB_MMA(1, 1, fb1);
       // p4: a1 x b0; stage b0(t+2); retire a0 / b0 of t+1 (after them: b1 / a1 (t+1), a0 / b0 (t+2))
       if (n2) stage(2, t + 2);
-      if (n1) wait_granules(n2 ? 4 : 2);
+      if (n1) wait_granules<BN>(n2 ? 4 : 2);
       GB_MMA(1, 0, fb0);
     }
     if (wr == 0) GB_BARRIER();
@@ -358,8 +378,8 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   if constexpr (OUT == O_F32_ATOMIC) {
     float* C = (float*)p.C;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wc * 64 + j * 16 + frow;
+    for (int j = 0; j < 2 * NB; ++j) {
+      const int col = n0 + col_of(j) + frow;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -374,8 +394,8 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     // splitk_reduce_kernel sums the slabs and runs the epilogue. N % 4 == 0 (launcher).
     float* C = (float*)p.C + (OUT == O_F32_SLAB ? (long)blockIdx.y * p.M * p.ldc : 0L);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wc * 64 + j * 16 + fq * 4;
+    for (int j = 0; j < 2 * NB; ++j) {
+      const int col = n0 + col_of(j) + fq * 4;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       if (OUT == O_F32 && p.bias && col < p.N) {
 #pragma unroll
@@ -397,12 +417,12 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   } else {
     // bf16 through LDS (two 128-row halves; row stride 260 elements = 520 B: the 8-B ds_write of
     // 16 lanes in 16 rows hit 16 distinct bank pairs) for 16-B coalesced global stores
-    constexpr int LDT = 256 + 4;
+    constexpr int LDT = BN + 4;
     bf16_t* tile = (bf16_t*)smem;
-    float bcol[4][4];
+    float bcol[2 * NB][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wc * 64 + j * 16 + fq * 4;
+    for (int j = 0; j < 2 * NB; ++j) {
+      const int col = n0 + col_of(j) + fq * 4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) bcol[j][r] = (EPI != E_SWIGLU && p.bias && col < p.N) ? bf2f(p.bias[col + r]) : 0.f;
     }
@@ -417,8 +437,8 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int row = i * 16 + frow, col = wc * 64 + j * 16 + fq * 4;
+          for (int j = 0; j < 2 * NB; ++j) {
+            const int row = i * 16 + frow, col = col_of(j) + fq * 4;
             float y[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) y[r] = EPI == E_SWIGLU ? acc[i][j][r] : act_fn(acc[i][j][r] + bcol[j][r], EPI);
@@ -430,19 +450,20 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
         // tile columns [0,128) = gate F-cols tn*128.., [128,256) = up; f = silu(g) * u from the
         // bf16-rounded pre-activations (bitwise what a separate SwiGLU kernel would read)
         bf16_t* Cf = (bf16_t*)p.C;
-        const int cc = tid & 15;
+        constexpr int CH = HALF / 8;  // 16-B chunks per row of the gate half
+        const int cc = tid % CH;
 #pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
-          const int row = pass * 32 + (tid >> 4);
+        for (int pass = 0; pass < 128 * CH / 512; ++pass) {
+          const int row = pass * (512 / CH) + tid / CH;
           const int grow = m0 + hh * 128 + row;
           if (grow < p.M) {
-            const uint4 g4 = ld16(row, cc), u4 = ld16(row, 16 + cc);
+            const uint4 g4 = ld16(row, cc), u4 = ld16(row, CH + cc);
             float g[8], u[8], f[8];
             unpack8(g4, g);
             unpack8(u4, u);
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = g[e] / (1.f + __expf(-g[e])) * u[e];
-            const int fcol = tn * 128 + cc * 8;
+            const int fcol = tn * HALF + cc * 8;
             *(uint4*)(Cf + (long)grow * p.ldc + fcol) = pack8(f);
             if (p.C2) {
               *(uint4*)(p.C2 + (long)grow * p.ldc2 + fcol) = g4;
@@ -452,10 +473,11 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
         }
       } else {
         bf16_t* C = (bf16_t*)p.C;
-        const int cc = tid & 31;
+        constexpr int CH = BN / 8;  // 16-B chunks per tile row
+        const int cc = tid % CH;
 #pragma unroll
-        for (int pass = 0; pass < 8; ++pass) {
-          const int row = pass * 16 + (tid >> 5);
+        for (int pass = 0; pass < 128 * CH / 512; ++pass) {
+          const int row = pass * (512 / CH) + tid / CH;
           const int grow = m0 + hh * 128 + row, gcol = n0 + cc * 8;
           if (grow < p.M && gcol < p.N) {
             uint4 v = ld16(row, cc);
@@ -675,10 +697,87 @@ using namespace rt::gb;
 // (split-K; C must be initialised by the caller). Requirements (checked): KMAJ operands have
 // M / N % 8 == 0 and 16-B aligned rows; ROW operands 16-B aligned rows; K, K2 % 8 == 0;
 // E_SWIGLU: ROW/ROW, bf16 out, N % 256 == 0, no K-extension of B beyond the weight rows.
+static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, int out, int bn, hipStream_t stream) {
+  const int tiles_n = act == E_SWIGLU ? p.N / bn : (p.N + bn - 1) / bn;
+  dim3 grid(((p.M + 255) / 256) * tiles_n, p.nsplit), block(512);
+  const int key = layout_a * 100 + layout_b * 10 + out;
+#define GB_LAUNCH(LA, LB, O, E, BN) hipLaunchKernelGGL((gemm_big_kernel<LA, LB, O, E, BN>), grid, block, 0, stream, p)
+  if (bn == 128) {  // the 128-column tile: NT (bf16 / SwiGLU / fp32 / slab) and NN bf16
+    switch (key * 10 + act) {
+      case 0: GB_LAUNCH(ROW, ROW, O_BF16, E_NONE, 128); break;
+      case E_SWIGLU: GB_LAUNCH(ROW, ROW, O_BF16, E_SWIGLU, 128); break;
+      case 10: GB_LAUNCH(ROW, ROW, O_F32, E_NONE, 128); break;
+      case 30: GB_LAUNCH(ROW, ROW, O_F32_SLAB, E_NONE, 128); break;
+      case 100: GB_LAUNCH(ROW, KMAJ, O_BF16, E_NONE, 128); break;
+      default: return -4;
+    }
+  } else if (key == 0) {  // NT, bf16 out: the activation is a template parameter (no runtime switch in the epilogue)
+    switch (act) {
+      case E_NONE: GB_LAUNCH(ROW, ROW, O_BF16, E_NONE, 256); break;
+      case E_RELU: GB_LAUNCH(ROW, ROW, O_BF16, E_RELU, 256); break;
+      case E_GELU: GB_LAUNCH(ROW, ROW, O_BF16, E_GELU, 256); break;
+      case E_GELU_TANH: GB_LAUNCH(ROW, ROW, O_BF16, E_GELU_TANH, 256); break;
+      case E_SILU: GB_LAUNCH(ROW, ROW, O_BF16, E_SILU, 256); break;
+      case E_SWIGLU: GB_LAUNCH(ROW, ROW, O_BF16, E_SWIGLU, 256); break;
+      default: return -4;
+    }
+  } else {
+    if (act != E_NONE) return -5;  // fp32 outputs and the NN / TN forms carry no activation
+    switch (key) {
+      case 1: GB_LAUNCH(ROW, ROW, O_F32, E_NONE, 256); break;
+      case 2: GB_LAUNCH(ROW, ROW, O_F32_ATOMIC, E_NONE, 256); break;
+      case 3: GB_LAUNCH(ROW, ROW, O_F32_SLAB, E_NONE, 256); break;
+      case 10: GB_LAUNCH(ROW, KMAJ, O_BF16, E_NONE, 256); break;
+      case 11: GB_LAUNCH(ROW, KMAJ, O_F32, E_NONE, 256); break;
+      case 12: GB_LAUNCH(ROW, KMAJ, O_F32_ATOMIC, E_NONE, 256); break;
+      case 110: GB_LAUNCH(KMAJ, KMAJ, O_BF16, E_NONE, 256); break;
+      case 111: GB_LAUNCH(KMAJ, KMAJ, O_F32, E_NONE, 256); break;
+      case 112: GB_LAUNCH(KMAJ, KMAJ, O_F32_ATOMIC, E_NONE, 256); break;
+      default: return -4;
+    }
+  }
+#undef GB_LAUNCH
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+static bool bn128_supported(int layout_a, int layout_b, int act, int out) {
+  const int key = layout_a * 100 + layout_b * 10 + out;
+  return (key == 0 && (act == E_NONE || act == E_SWIGLU)) || (act == E_NONE && (key == 1 || key == 3 || key == 10));
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// Ratio of a 256x128 tile's time to a 256x256 tile's (same K), for the wave planner below.
+static float bn128_cost() {
+  static float r = -1.f;
+  if (r < 0.f) {
+    const char* e = getenv("RT_GEMM_BN128_COST");
+    r = e ? (float)atof(e) : 0.55f;
+  }
+  return r;
+}
+
+// layout_a / layout_b: 0 = ROW (K contiguous), 1 = KMAJ (M / N contiguous).
+// out: 0 bf16 (epilogue bias + act, or SwiGLU), 1 fp32 store (bias + act), 2 fp32 atomic add
+// (split-K; C must be initialised by the caller), 3 fp32 split-K slabs. bn: 256, 128, or 0 = plan:
+// the tile rows are cut in two launches — rows [0, 256 m1) on 256x256 tiles, the rest on 256x128
+// tiles — with m1 chosen so that the last, partial wave of workgroups is as short as possible
+// (e.g. M = 9632 tokens x N = 4096: 608 tiles = 2.4 waves of 256 CUs -> 512 tiles + 192 half tiles).
+// Requirements (checked): KMAJ operands have M / N % 8 == 0 and 16-B aligned rows; ROW operands
+// 16-B aligned rows; K, K2 % 8 == 0; E_SWIGLU: ROW/ROW, bf16 out, N % 256 == 0.
 extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb,
                            const void* A2, long lda2, const void* B2, long ldb2, int K2, const void* bias,
                            void* C, long ldc, void* C2, long ldc2, const void* R, long ldr, int M, int N, int K,
-                           int act, int out, int nsplit, const void* zpage, hipStream_t stream) {
+                           int act, int out, int nsplit, const void* zpage, int bn, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   // a ROW operand reads 8-element k-chunks: its reduction length must be a multiple of 8
   const bool any_row = layout_a == ROW || layout_b == ROW;
@@ -693,6 +792,9 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   if (nsplit > 1 && out != O_F32_ATOMIC && out != O_F32_SLAB) return -2;
   if (act == E_SWIGLU && (layout_a != ROW || layout_b != ROW || out != O_BF16 || N % 256)) return -3;
   if (act != E_NONE && (layout_a != ROW || layout_b != ROW || out != O_BF16)) return -5;
+  if (bn != 0 && bn != 128 && bn != 256) return -8;
+  const bool can128 = bn128_supported(layout_a, layout_b, act, out);
+  if (bn == 128 && !can128) return -8;
   Args p;
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
   p.A2 = (A2 && B2) ? (const bf16_t*)A2 : nullptr; p.lda2 = lda2;
@@ -700,38 +802,38 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = (bf16_t*)C2; p.ldc2 = ldc2;
   p.R = (const bf16_t*)R; p.ldr = ldr;
   p.M = M; p.N = N; p.K = K; p.act = act; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
-  const int tiles_n = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
-  dim3 grid(((M + 255) / 256) * tiles_n, nsplit), block(512);
-  const int key = layout_a * 100 + layout_b * 10 + out;
-#define GB_LAUNCH(LA, LB, O, E) hipLaunchKernelGGL((gemm_big_kernel<LA, LB, O, E>), grid, block, 0, stream, p)
-  if (key == 0) {  // NT, bf16 out: the activation is a template parameter (no runtime switch in the epilogue)
-    switch (act) {
-      case E_NONE: GB_LAUNCH(ROW, ROW, O_BF16, E_NONE); break;
-      case E_RELU: GB_LAUNCH(ROW, ROW, O_BF16, E_RELU); break;
-      case E_GELU: GB_LAUNCH(ROW, ROW, O_BF16, E_GELU); break;
-      case E_GELU_TANH: GB_LAUNCH(ROW, ROW, O_BF16, E_GELU_TANH); break;
-      case E_SILU: GB_LAUNCH(ROW, ROW, O_BF16, E_SILU); break;
-      case E_SWIGLU: GB_LAUNCH(ROW, ROW, O_BF16, E_SWIGLU); break;
-      default: return -4;
-    }
-  } else {
-    if (act != E_NONE) return -5;  // fp32 outputs and the NN / TN forms carry no activation
-    switch (key) {
-      case 1: GB_LAUNCH(ROW, ROW, O_F32, E_NONE); break;
-      case 2: GB_LAUNCH(ROW, ROW, O_F32_ATOMIC, E_NONE); break;
-      case 3: GB_LAUNCH(ROW, ROW, O_F32_SLAB, E_NONE); break;
-      case 10: GB_LAUNCH(ROW, KMAJ, O_BF16, E_NONE); break;
-      case 11: GB_LAUNCH(ROW, KMAJ, O_F32, E_NONE); break;
-      case 12: GB_LAUNCH(ROW, KMAJ, O_F32_ATOMIC, E_NONE); break;
-      case 110: GB_LAUNCH(KMAJ, KMAJ, O_BF16, E_NONE); break;
-      case 111: GB_LAUNCH(KMAJ, KMAJ, O_F32, E_NONE); break;
-      case 112: GB_LAUNCH(KMAJ, KMAJ, O_F32_ATOMIC, E_NONE); break;
-      default: return -4;
+  if (bn != 0) return launch_gemm_big(p, layout_a, layout_b, act, out, bn, stream);
+  // ---- plan: m1 row tiles at BN = 256, the rest at BN = 128 ----
+  const int tiles_m = (M + 255) / 256;
+  const int tn256 = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
+  const int tn128 = act == E_SWIGLU ? N / 128 : (N + 127) / 128;
+  const long cus = (long)num_cus() * 1;  // one 512-thread, 128-KiB-LDS workgroup per CU
+  int m1 = tiles_m;
+  if (can128 && nsplit == 1 && (out == O_BF16 || out == O_F32)) {
+    const float r = bn128_cost();
+    float best = 1e30f;
+    for (int m = tiles_m; m >= 0; --m) {
+      const long w256 = ((long)m * tn256 + cus - 1) / cus, w128 = ((long)(tiles_m - m) * tn128 + cus - 1) / cus;
+      const float cost = (float)w256 + r * (float)w128;
+      if (cost < best - 1e-3f) { best = cost; m1 = m; }
     }
   }
-#undef GB_LAUNCH
-  RT_LAUNCH_CHECK();
-  return 0;
+  if (m1 == tiles_m) return launch_gemm_big(p, layout_a, layout_b, act, out, 256, stream);
+  const long r0 = (long)m1 * 256;
+  if (m1 > 0) {
+    Args q = p;
+    q.M = (int)r0;
+    const int rc = launch_gemm_big(q, layout_a, layout_b, act, out, 256, stream);
+    if (rc) return rc;
+  }
+  Args q = p;
+  q.M = M - (int)r0;
+  q.A = p.A + (layout_a == ROW ? r0 * lda : r0);
+  if (p.A2) q.A2 = p.A2 + (layout_a == ROW ? r0 * lda2 : r0);
+  q.C = (char*)C + r0 * ldc * (out == O_BF16 ? 2 : 4);
+  if (p.C2) q.C2 = p.C2 + r0 * ldc2;
+  if (p.R) q.R = p.R + r0 * ldr;
+  return launch_gemm_big(q, layout_a, layout_b, act, out, 128, stream);
 }
 
 extern "C" int rt_gemm_splitk_reduce(const float* slabs, int nsplit, int M, int N, const void* bias, int act,

@@ -31,17 +31,20 @@ ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new":
 ACT_SWIGLU = 5  # w = [gate; up] (2F rows) -> silu(x gate^T) * (x up^T), [.., F]
 
 
-def splitk_plan(M: int, N: int, K: int, act: int = 0) -> int:
-    """Split-K factor for an NT GEMM whose 256x256 tiles cannot fill the 256 CUs (decode at batch
-    65..256, narrow outputs): ~256 workgroups with >= 8 K-steps each (each split streams its weight
-    slice from HBM with ~1 K-step of prefetch; shorter splits pay the pipeline fill and the fp32
-    slab round trip more than they gain — M = 256 sweep, profiles/gemm_r2_m256_split_sweep.log:
-    qkv / o 8-way, gate_up 2-way, down 16-way); 1 = the plain tiled kernel."""
-    tiles = ((M + 255) // 256) * (N // 256 if act == ACT_SWIGLU else (N + 255) // 256)
-    if tiles >= 128 or M > 1024:
-        return 1
+def splitk_plan(M: int, N: int, K: int, act: int = 0):
+    """(nsplit, bn) for a token-parallel NT GEMM. Up to 512 rows (decode at batch 65..512, small
+    prefills) the 256x128 tile doubles the workgroups over the 256x256 one, and the K split fills
+    the rest of the chip (qkv 48 tiles x 5, o / down 32 x 8, gate_up 224 x 1 with the SwiGLU in the
+    epilogue, lm_head 250 x 1). Larger M: one launch planned by rt_gemm_big (bn 0: 256x256 tiles,
+    the last partial wave on 256x128 tiles)."""
+    if M > 512:
+        return 1, 0
+    bn = 128 if act in (0, ACT_SWIGLU) else 256
+    tiles = ((M + 255) // 256) * (N // bn if act == ACT_SWIGLU else (N + bn - 1) // bn)
+    if tiles >= 128:
+        return 1, bn
     nk = (K + 63) // 64
-    return max(1, min(nk // 8, (256 + tiles // 2) // tiles))
+    return max(1, min(nk // 8, (256 + tiles // 2) // tiles)), bn
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None,
@@ -54,11 +57,15 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
         N = w.shape[0]
         if M <= 64 and residual is None and N % 8 == 0:
             return native().gemm(x, w, u, ub, bias, act, out_f32, out)
-        s = nsplit or (splitk_plan(M, N, K, act) if (u is None and not out_f32 and N % 16 == 0) else 1)
+        s, bn = splitk_plan(M, N, K, act)
+        if nsplit:
+            s = nsplit
+        if u is not None or out_f32 or N % 16:
+            s = 1
         if s > 1:
             slabs = torch.empty(s * M * N, dtype=torch.float32, device=x.device)
-            return native().gemm_splitk(x, w, s, slabs, bias, act, out, residual)
-        return native().gemm_big(x, w, ROW, ROW, u, ub, bias, act, 1 if out_f32 else 0, 1, out, None, residual)
+            return native().gemm_splitk(x, w, s, slabs, bias, act, out, residual, bn or 256)
+        return native().gemm_big(x, w, ROW, ROW, u, ub, bias, act, 1 if out_f32 else 0, 1, out, None, residual, bn)
     y = ref.gemm(x, w, u, ub, bias, act, out_f32)
     if residual is not None:
         y = (y.float() + residual.float()).to(y.dtype)
@@ -79,12 +86,13 @@ def _op(t: torch.Tensor, layout: int, trans_for_a: bool) -> torch.Tensor:
 
 
 def gemm_big(a, b, la: int, lb: int, a2=None, b2=None, bias=None, act: int = 0, out_mode: int = 0,
-             nsplit: int = 1, out=None, out2=None):
+             nsplit: int = 1, out=None, out2=None, residual=None, bn: int = 0):
     """C = epi(A·B + A2·B2) with per-operand layouts (ROW: K contiguous, KMAJ: M / N contiguous).
     GPU: one hand-written MFMA kernel (gemm_big_kernel); CPU: fp32 oracle (tests, plumbing).
-    out_mode 0 bf16 / 1 fp32 / 2 fp32 accumulate into ``out``; act 5 = SwiGLU over [gate; up]."""
+    out_mode 0 bf16 / 1 fp32 / 2 fp32 accumulate into ``out``; act 5 = SwiGLU over [gate; up].
+    bn: 256 / 128 output columns per tile, 0 = planned (256, the last partial wave on 128)."""
     if on_gpu(a):
-        return native().gemm_big(a, b, la, lb, a2, b2, bias, act, out_mode, nsplit, out, out2)
+        return native().gemm_big(a, b, la, lb, a2, b2, bias, act, out_mode, nsplit, out, out2, residual, bn)
     A = _op(a, la, True).float()
     B = _op(b, lb, False).float()
     y = A @ B
@@ -101,6 +109,8 @@ def gemm_big(a, b, la: int, lb: int, a2=None, b2=None, bias=None, act: int = 0, 
         if bias is not None:
             y = y + bias.float()
         y = ref.apply_act(y, act)
+        if residual is not None:
+            y = y.to(a.dtype).float() + residual.float()
     if out_mode == 2:
         out.add_(y)
         return out

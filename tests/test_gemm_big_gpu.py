@@ -118,3 +118,48 @@ def test_small_tile_narrow(M, K, R):
     t = _r(M, R)
     _close(ops.gemm_tn(t, x), t.float().t() @ x.float(), rtol=5e-3, atol=5e-3)
     _close(ops.gemm_tn(x, t), x.float().t() @ t.float(), rtol=5e-3, atol=5e-3)
+
+
+# ---- 256x128 tiles (decode at M <= 512, last partial wave of large GEMMs) and the wave planner ----
+@pytest.mark.parametrize("bn", [128, 256, 0])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (300, 520, 200), (77, 136, 4096), (2900, 1024, 192)])
+def test_bn_forms_nt_nn(bn, M, N, K):
+    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
+    ref_nt = a.float() @ w.float().t()
+    _close(ops.gemm_big(a, w, ops.ROW, ops.ROW, bn=bn), ref_nt)
+    _close(ops.gemm_big(a, w, ops.ROW, ops.ROW, out_mode=1, bn=bn), ref_nt, rtol=5e-3, atol=5e-3)
+    wk = _r(K, N, s=1 / math.sqrt(K))  # NN: C = A W, W [K, N]
+    _close(ops.gemm_big(a, wk, ops.ROW, ops.KMAJ, bn=bn), a.float() @ wk.float())
+    # residual epilogue, poisoned output fully written
+    r = _r(M, N)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.gemm_big(a, w, ops.ROW, ops.ROW, out=out, residual=r, bn=bn)
+    assert not torch.isnan(out).any()
+    _close(out, ref_nt + r.float())
+
+
+@pytest.mark.parametrize("bn", [128, 0])
+def test_bn_lora_extension_and_swiglu(bn):
+    M, K, F, R = 700, 512, 384, 64
+    x, w = _r(M, K), _r(2 * F, K, s=1 / math.sqrt(K))
+    u, ub = _r(M, R), _r(2 * F, R, s=0.1)
+    _close(ops.gemm_big(x, w, ops.ROW, ops.ROW, u, ub, bn=bn), x.float() @ w.float().t() + u.float() @ ub.float().t())
+    pre = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    y = ops.gemm_big(x, w, ops.ROW, ops.ROW, act=ops.ACT_SWIGLU, out2=pre, bn=bn)
+    p_ref = (x.float() @ w.float().t()).to(torch.bfloat16)
+    _close(pre, p_ref)
+    g, up = p_ref[:, :F].float(), p_ref[:, F:].float()
+    _close(y, torch.nn.functional.silu(g) * up)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(256, 6144, 4096, 0), (256, 28672, 512, 5), (256, 4096, 14336, 0),
+                                       (200, 1000, 512, 0), (512, 32000, 256, 0)])
+def test_decode_plan_m256(M, N, K, act):
+    """ops.gemm at decode batch sizes (the 256x128 tile, split-K slabs or the SwiGLU epilogue)."""
+    x, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
+    y = ops.gemm(x, w, act=act)
+    ref_ = x.float() @ w.float().t()
+    if act == ops.ACT_SWIGLU:
+        ref_ = ref_.to(torch.bfloat16).float()
+        ref_ = torch.nn.functional.silu(ref_[:, :N // 2]) * ref_[:, N // 2:]
+    _close(y, ref_)

@@ -62,14 +62,20 @@ def main():
                 "lib_k64": lambda: torch.matmul(x[:, :64], w[:, :64].t()),
                 "nt_lora": lambda: ops.gemm_big(x, w, 0, 0, u, ub),
                 "lib_nt": lambda: torch.matmul(x, w.t()),
-                "old256_lora": lambda: (C.gemm_set_variant(2), C.gemm(x, w, u, ub, None, 0, False, None)),
+                "nt256": lambda: ops.gemm_big(x, w, 0, 0, bn=256),
+                "nt128": lambda: ops.gemm_big(x, w, 0, 0, bn=128),
+                "nn256": lambda: ops.gemm_big(dy, w, 0, 1, bn=256),
+                "nn128": lambda: ops.gemm_big(dy, w, 0, 1, bn=128),
+                "nn_lora256": lambda: ops.gemm_big(dy, w, 0, 1, du, ap_, bn=256),
                 "nn": lambda: ops.gemm_big(dy, w, 0, 1),
                 "nn_lora": lambda: ops.gemm_big(dy, w, 0, 1, du, ap_),
                 "lib_nn": lambda: torch.matmul(dy, w),
             }
             if name == "gate_up":
                 cases["nt_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5)
-            for sp in (1, 2, 4, 8, 12, 16):
+            if name == "gate_up":
+                cases["nt128_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5, bn=128)
+            for sp in (1, 2, 4, 5, 8, 12, 16):
                 cases[f"split{sp}"] = (lambda sp=sp: ops.gemm(x, w, nsplit=sp))
                 if name == "gate_up":
                     cases[f"split{sp}_swiglu"] = (lambda sp=sp: ops.gemm(x, w, act=5, nsplit=sp))
