@@ -166,7 +166,9 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       const int kc = (lane & 7) ^ row_swz(row);
       int grow;
       if (op == 0) grow = min(m0 + row, p.M - 1);
-      else if (EPI == E_SWIGLU && main_w) grow = row < HALF ? tn * HALF + row : Fh + tn * HALF + row - HALF;
+      // SwiGLU: tile rows [0, HALF) are gate rows, [HALF, BN) the matching up rows — for the weight
+      // and for its K-extension (LoRA UB rows follow the weight's row order)
+      else if (EPI == E_SWIGLU) grow = row < HALF ? tn * HALF + row : Fh + tn * HALF + row - HALF;
       else grow = min(n0 + row, p.N - 1);
       kin = kc * 8;
       return (uint32_t)grow * (uint32_t)ld + (uint32_t)(kc * 8);

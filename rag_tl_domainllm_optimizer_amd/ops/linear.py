@@ -222,14 +222,27 @@ class LoRAGroup:
         return self.merged
 
 
-def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int) -> torch.Tensor:
+def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0) -> torch.Tensor:
     """a [M, K] (ROW) times a narrow operand b (ROW [R, K] or KMAJ [K, R]; R = padded LoRA rank) ->
-    [M, R] bf16 on the 64x64-tile kernel, one workgroup per 64 tokens over the full reduction
-    (U = X A_pad^T forward, dU = dY UB backward)."""
+    [M, R] bf16 on the 64x64-tile kernel (U = X A_pad^T forward, dU = dY UB backward). One
+    workgroup per 64 tokens leaves most CUs idle at a few thousand tokens (151 workgroups at 9632
+    tokens, each over a K of up to 28672), so the reduction is split until ~3 workgroups per CU
+    are in flight: fp32 atomic partials, rounded to bf16 once."""
     if not on_gpu(a):
         B = b.float().t() if lb == ROW else b.float()
         return (a.float() @ B).to(a.dtype)
-    return native().gemm_small(a, b, ROW, lb, 0, 1)
+    M, K = a.shape
+    R = b.shape[0] if lb == ROW else b.shape[1]
+    tiles = ((M + 63) // 64) * ((R + 63) // 64)
+    # (measured at 9632 tokens: dU 383 -> 172 us at K = 28672; U at K = 4096 is already at 3.2 TB/s
+    # unsplit and only pays the fp32 pass, profiles/lora_narrow_r2.log)
+    auto = 1 if (lb == ROW and K <= 4096) else max(1, min(K // 512, (768 + tiles - 1) // tiles))
+    ns = nsplit or auto
+    if ns == 1:
+        return native().gemm_small(a, b, ROW, lb, 0, 1)
+    out = torch.zeros(M, R, dtype=torch.float32, device=a.device)
+    native().gemm_small(a, b, ROW, lb, 2, ns, out)
+    return out.to(a.dtype)
 
 
 def _dropout_mask(x: torch.Tensor, p: float) -> torch.Tensor:
@@ -249,11 +262,19 @@ class _LinearFn(torch.autograd.Function):
                 xd = x2 * ctx.mask
             u = _narrow(xd, lora.a_pad, ROW)  # [M, Rp] = drop(X) (s A)^T
             ub = lora.ub
-        y = gemm(x2, w, u, ub, bias, act)
         ctx.act = act
         ctx.lora = lora
         ctx.has_bias = bias is not None
-        # with an activation epilogue the pre-activation is recomputed in backward (no extra
+        ctx.pre = None
+        if act == ACT_SWIGLU:
+            # w = [gate; up]: ONE GEMM writes silu(g) * u and the [M, 2F] pre-activation (kept for
+            # the SwiGLU backward) from its epilogue — no separate SwiGLU pass over the activations
+            pre = torch.empty(x2.shape[0], w.shape[0], dtype=x2.dtype, device=x2.device)
+            y = gemm_big(x2, w, ROW, ROW, u, ub, None, ACT_SWIGLU, out2=pre)
+            ctx.pre = pre
+        else:
+            y = gemm(x2, w, u, ub, bias, act)
+        # other activation epilogues: the pre-activation is recomputed in backward (no extra
         # activation-sized tensor is kept alive)
         ctx.save_for_backward(x2, w, u if u is not None else torch.empty(0), bias if bias is not None else torch.empty(0))
         return y
@@ -263,7 +284,12 @@ class _LinearFn(torch.autograd.Function):
         x2, w, u, bias = ctx.saved_tensors
         lora = ctx.lora
         dy = dy.contiguous()
-        if ctx.act != 0:
+        if ctx.act == ACT_SWIGLU:
+            from .misc import _swiglu_grad
+
+            dy = _swiglu_grad(ctx.pre, dy)  # d[gate | up]
+            ctx.pre = None
+        elif ctx.act != 0:
             # recompute pre-activation and apply the activation derivative
             ub = lora.ub if lora is not None else None
             pre = gemm(x2, w, u if lora is not None else None, ub, bias if ctx.has_bias else None, 0, out_f32=True)
@@ -322,8 +348,17 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
         x2.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)
         or (use_lora and any(p.requires_grad for p in lora.a + lora.b)))
     if act_id == ACT_SWIGLU:
-        # no-grad: SwiGLU is the GEMM epilogue (skinny kernels for decode, gemm_big otherwise);
-        # training keeps the [gate | up] pre-activation for the SwiGLU backward
+        # SwiGLU is the GEMM epilogue. no-grad: skinny kernels for decode, gemm_big otherwise;
+        # training (_LinearFn): gemm_big also writes the [gate | up] pre-activation for backward
+        if on_gpu(x2) and grad_needed and bias is None and fp8 is None and w.shape[0] % 256 == 0 \
+                and x2.shape[1] % 8 == 0 and x2.shape[0] > 64 and w.dtype == torch.bfloat16 \
+                and not (use_lora and lora.use_merged):
+            params = []
+            if use_lora:
+                for a, b in zip(lora.a, lora.b):
+                    params += [a, b]
+            y = _LinearFn.apply(x2, w, None, ACT_SWIGLU, lora if use_lora else None, *params)
+            return y.reshape(*shp[:-1], w.shape[0] // 2)
         if on_gpu(x2) and not grad_needed and bias is None and w.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0 \
                 and (x2.shape[0] <= 64 or w.shape[0] % 256 == 0):
             w_eff = lora.merged_weight(w) if use_lora else w

@@ -22,6 +22,17 @@ class _SwiGLUFn(torch.autograd.Function):
         return native().swiglu_bwd(gu, dy.contiguous())
 
 
+def _swiglu_grad(gu: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    """d[gate | up] of silu(gate) * up given the [gate | up] pre-activation and dL/dy."""
+    if on_gpu(gu):
+        return native().swiglu_bwd(gu.contiguous(), dy.contiguous())
+    with torch.enable_grad():
+        p = gu.detach().float().requires_grad_(True)
+        F2 = p.shape[-1]
+        (g,) = torch.autograd.grad(F.silu(p[..., : F2 // 2]) * p[..., F2 // 2:], p, dy.float())
+    return g.to(gu.dtype)
+
+
 def swiglu(gu: torch.Tensor) -> torch.Tensor:
     """silu(gate) * up for gu = [gate | up] along the last dim."""
     if not on_gpu(gu):

@@ -113,6 +113,46 @@ def test_linear_lora_deep(M, N, K):
     _close(ops.gemm_nn(dy, w), dy.float() @ w.float())
 
 
+@pytest.mark.parametrize("M", [300, 1100])
+def test_linear_swiglu_lora_autograd(M):
+    """Training SwiGLU projection: one GEMM writes silu(g) * u and keeps the [gate | up]
+    pre-activation (epilogue), the LoRA K-extension rows follow the gate / up tile mapping, the
+    backward runs the SwiGLU derivative on the kept pre-activation."""
+    torch.manual_seed(4)
+    K, F, r = 256, 384, 8
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = torch.nn.Parameter((torch.randn(2 * F, K, device=DEV) / 16).to(torch.bfloat16), requires_grad=False)
+    a = torch.nn.Parameter(torch.randn(r, K, device=DEV) * 0.05)
+    b = torch.nn.Parameter(torch.randn(2 * F, r, device=DEV) * 0.05)
+    grp = ops.LoRAGroup(["gu"], [a], [b], [0], [2.0], 2 * F)
+    y = ops.linear(x, w, act="swiglu", lora=grp)
+    assert y.shape == (M, F)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    ar, br = a.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    pre = xr @ w.float().t() + 2.0 * (xr @ ar.t()) @ br.t()
+    yr = torch.nn.functional.silu(pre[:, :F]) * pre[:, F:]
+    (yr * g.float()).sum().backward()
+    _close(y, yr)
+    _close(x.grad, xr.grad)
+    _close(a.grad, ar.grad, rtol=3e-2, atol=3e-2)
+    _close(b.grad, br.grad, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("M,K", [(9632, 4096), (700, 14336)])
+def test_lora_narrow_split(M, K):
+    """U = X A_pad^T / dU = dY UB with the reduction split over workgroups (fp32 partials)."""
+    from rag_tl_domainllm_optimizer_amd.ops.linear import _narrow
+
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ap = (torch.randn(64, K, device=DEV) / 64).to(torch.bfloat16)
+    ub = (torch.randn(K, 64, device=DEV) / 64).to(torch.bfloat16)
+    for ns in (1, 0, 7):
+        _close(_narrow(x, ap, ops.ROW, ns), x.float() @ ap.float().t())
+        _close(_narrow(x, ub, ops.KMAJ, ns), x.float() @ ub.float())
+
+
 def test_linear_lora_dropout():
     """PEFT lora_dropout: the adapter sees drop(X); dX / dA follow the same mask."""
     torch.manual_seed(3)

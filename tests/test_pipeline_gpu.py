@@ -166,6 +166,10 @@ def test_reward_stream_overlap_matches_serial(monkeypatch):
         tr = PPOTrainer(pol, tok, RewardModel(enc), PPOConfig(max_new_tokens=8, max_prompt_tokens=96,
                                                               minibatch_size=4, lora_r=8, overlap_reward=overlap,
                                                               seed=3), max_batch=8)
+        # warm-up iteration: the caching allocator's first-time device allocations may synchronise
+        # the host; the measured prepare() below runs on cached blocks like a steady-state step
+        tr.prepare(tr.rollout(batch))
+        torch.cuda.synchronize()
         tr.record_overlap_events = True
         ro = tr.rollout(batch)
         spin["on"] = True
