@@ -48,6 +48,47 @@ __device__ __forceinline__ uint4 load_nt16(const void* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// ---- transposed LDS reads that do not drain LDS-DMA ----
+// hipcc places `s_waitcnt vmcnt(0)` in front of every __builtin_amdgcn_ds_read_tr16_b64 while a
+// global_load_lds is in flight (the intrinsic carries no alias information, so every pending
+// LDS-DMA is assumed to write what it reads), which empties a kernel's prefetch pipeline at each
+// transposed read. These helpers issue the reads in inline asm and end with their own
+// `s_waitcnt lgkmcnt(0)`, so the outputs are complete at ASMEND (cdna_hip_programming.md §5.7:
+// the compiler neither counts nor waits for asm memory operations). The caller orders them behind
+// the LDS-DMA that filled the image (counted vmcnt, + barrier for other waves' DMA). EXEC must be
+// all ones (ISA requirement of ds_read_b64_tr_b16).
+typedef __attribute__((ext_vector_type(4))) short rt_s16x4;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+// 4 reads at a + {0, O1, O2, O3} (byte offsets, compile-time)
+template <int O1, int O2, int O3>
+__device__ __forceinline__ void ds_tr16_x4(uint32_t a, rt_s16x4& r0, rt_s16x4& r1, rt_s16x4& r2, rt_s16x4& r3) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %4\n\t"
+      "ds_read_b64_tr_b16 %1, %4 offset:%5\n\t"
+      "ds_read_b64_tr_b16 %2, %4 offset:%6\n\t"
+      "ds_read_b64_tr_b16 %3, %4 offset:%7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+      : "v"(a), "i"(O1), "i"(O2), "i"(O3)
+      : "memory");
+}
+// 2 x (2 reads at a_i + {0, O1})
+template <int O1>
+__device__ __forceinline__ void ds_tr16_2x2(uint32_t a0, uint32_t a1, rt_s16x4& r0, rt_s16x4& r1, rt_s16x4& r2,
+                                            rt_s16x4& r3) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %4\n\t"
+      "ds_read_b64_tr_b16 %1, %4 offset:%6\n\t"
+      "ds_read_b64_tr_b16 %2, %5\n\t"
+      "ds_read_b64_tr_b16 %3, %5 offset:%6\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+      : "v"(a0), "v"(a1), "i"(O1)
+      : "memory");
+}
+
 __device__ __forceinline__ float bf2f(bf16_t x) {
   return __uint_as_float(((uint32_t)x) << 16);
 }

@@ -744,6 +744,211 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Fused decode step on MFMA (large batch: B * Hkv >= 256, one partition per (batch, kv head))
+// ---------------------------------------------------------------------------------------------
+// At batch 256 the decode attention of a layer streams ~250 MB of K/V (256 x 8 kv-heads x ~240
+// keys x 512 B); the VALU kernel above spends ~120 instructions per key-lane on dot products,
+// 16-lane shuffle reductions and the PV update (~3 TB/s). Here the G query heads of a kv head are
+// the 16 "query rows" of the prefill kernel's swapped product (heads on the lane, G <= 16 valid).
+// One wave per (batch, kv head); per 16-key tile:
+//   * S^T = K·Q^T: 4 MFMAs whose K fragments are loaded straight from the cache into registers
+//     (16 B per lane, no LDS); online softmax on 4 scores per lane (two cross-group shuffles);
+//   * O += P·V: 8 MFMAs (K = 32: k-slots 4..7 are P = 0 against zero LDS rows), P = the packed
+//     S^T accumulator, V through an LDS image (whole 256-B rows stored by ds_write_b128, read by
+//     ds_read_b64_tr_b16).
+// K and V of the next tile are prefetched into a second register set (plain loads only: no
+// LDS-DMA, so hipcc's counted waits keep the prefetch in flight; 178 VGPRs = 2 waves per SIMD:
+// all 2048 waves of a batch-256 layer are resident at once). The prologue issues every q / k_new /
+// v_new / rotary-table load at once (one round trip) behind the first tile's loads. RoPE of q /
+// k_new and the cache append are fused; lanes whose (clamped) key is the new token's slot use
+// k_new / v_new from registers. Measured at batch 256 (Mistral-7B, 174..301 keys): 51 us per
+// layer vs 80 us for the VALU kernel (profiles/decode_attn_r2_mfma.log).
+template <int G>
+__global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a) {
+  constexpr int D = 128, DS = D / 32, DT = D / 16;
+  __shared__ __attribute__((aligned(16))) char vimg[32 * D * 2];  // rows 16..31 stay zero
+  const int lane = threadIdx.x, g = lane >> 4, r16 = lane & 15;
+  const int b = blockIdx.x / a.Hkv, hk = blockIdx.x % a.Hkv;
+  const int len = a.attn_len[b];
+  const int s_new = a.slot[b];
+  RT_ASSERT(len <= a.Smax && s_new >= 0 && s_new < a.Smax);
+  int kbeg = a.kv_start ? a.kv_start[b] : 0;
+  if (a.window > 0) kbeg = max(kbeg, len - a.window);
+  const int p = a.pos ? a.pos[b] : 0;
+  const bf16_t* row = a.qkv + (long)b * a.ldq;
+  const bf16_t* kbase = a.kc + ((long)b * a.Hkv + hk) * a.Smax * D;
+  const bf16_t* vbase = a.vc + ((long)b * a.Hkv + hk) * a.Smax * D;
+
+  // tile of 16 keys from c0 (32 registers per set: two sets keep every wave of a batch-256 layer
+  // resident, 3 per SIMD): K fragments k[s] = K[c0 + r16][32 s + 8 g ..] (A operand of S^T);
+  // V pieces v[i] = V[c0 + 4 i + g][8 r16 ..] (4 whole rows per load instruction).
+  // Keys past len - 1 re-read slot len - 1 (masked).
+  struct Tile { uint4 k[DS]; uint4 v[4]; };
+  auto load = [&](Tile& T, int c0) {
+    const long keyk = min(c0 + r16, len - 1);
+#pragma unroll
+    for (int s2 = 0; s2 < DS; ++s2) T.k[s2] = *(const uint4*)(kbase + keyk * D + 32 * s2 + 8 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long key = min(c0 + 4 * i + g, len - 1);
+      T.v[i] = *(const uint4*)(vbase + key * D + 8 * r16);
+    }
+  };
+  Tile ta, tb;
+  if (kbeg < len) load(ta, kbeg);
+
+  // ---- q / k_new / v_new and the rotary tables, all loads at once. D = 128: chunk 4 s + g's
+  // rotary partner (chunk ^ 8) is the lane's own chunk 4 (s ^ 2) + g, its table offset
+  // ((chunk & 7) * 8) depends on s & 1 only ----
+  const bool rot = a.cosT != nullptr;
+  const bool has_new = s_new >= kbeg && s_new < len;
+  const bf16_t* qrow = row + (long)min(hk * G + r16, a.Hq - 1) * D;
+  const bf16_t* krow = row + (long)(a.Hq + hk) * D;
+  uint4 qraw[DS], kraw[DS];
+#pragma unroll
+  for (int s2 = 0; s2 < DS; ++s2) {
+    qraw[s2] = *(const uint4*)(qrow + (4 * s2 + g) * 8);
+    kraw[s2] = *(const uint4*)(krow + (4 * s2 + g) * 8);
+  }
+  const uint4 vx = *(const uint4*)(row + (long)(a.Hq + a.Hkv + hk) * D + r16 * 8);
+  float4 cq[2][2], sq[2][2];
+  {
+    // unconditional (no branch between load batches): without tables read the qkv row
+    const float* ct = rot ? a.cosT + (long)p * (D / 2) : (const float*)row;
+    const float* stb = rot ? a.sinT + (long)p * (D / 2) : (const float*)row;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int j0 = (4 * par + g) * 8;
+      cq[par][0] = *(const float4*)(ct + j0); cq[par][1] = *(const float4*)(ct + j0 + 4);
+      sq[par][0] = *(const float4*)(stb + j0); sq[par][1] = *(const float4*)(stb + j0 + 4);
+    }
+  }
+  // x rotated with partner y: lo half (chunk < 8) x c - y s', hi half x c + y s' (s' = sign sin),
+  // rounded to bf16 as the unfused rope kernel stores it
+  auto rope8 = [&](const uint4& xv, const uint4& yv, const float4 (&c)[2], const float4 (&sn)[2], bool lo) -> uint4 {
+    if (!rot) return xv;
+    float x[8], y[8], o8[8];
+    unpack8(xv, x);
+    unpack8(yv, y);
+    const float cs[8] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w};
+    const float sv[8] = {sn[0].x, sn[0].y, sn[0].z, sn[0].w, sn[1].x, sn[1].y, sn[1].z, sn[1].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float t = a.sign * sv[e];
+      o8[e] = lo ? x[e] * cs[e] - y[e] * t : x[e] * cs[e] + y[e] * t;
+    }
+    return pack8(o8);
+  };
+  bf16x8 qf[DS];   // B operand of S^T = K·Q^T: Q[head r16][32 s + 8 g ..]
+  uint4 knew[DS];  // rotated k_new chunks 4 s + g (the lane's K-fragment chunks)
+#pragma unroll
+  for (int s2 = 0; s2 < DS; ++s2) {
+    const uint4 qv = rope8(qraw[s2], qraw[s2 ^ 2], cq[s2 & 1], sq[s2 & 1], s2 < 2);
+    qf[s2] = __builtin_bit_cast(bf16x8, r16 < G ? qv : make_uint4(0, 0, 0, 0));
+    knew[s2] = rope8(kraw[s2], kraw[s2 ^ 2], cq[s2 & 1], sq[s2 & 1], s2 < 2);
+  }
+  // cache append: lane (g, 0) stores its 4 k chunks 4 s + g, lane group 1 the v chunks
+  if (has_new) {
+    bf16_t* kdst = a.kc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
+    bf16_t* vdst = a.vc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
+    if (r16 == 0) {
+#pragma unroll
+      for (int s2 = 0; s2 < DS; ++s2) *(uint4*)(kdst + (4 * s2 + g) * 8) = knew[s2];
+    }
+    if (g == 1) *(uint4*)(vdst + r16 * 8) = vx;
+  }
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int c = 0; c < DT; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;  // of head r16 (identical over the 4 lane groups)
+  // P·V runs K = 32 MFMAs on 16-key tiles: k-slots 4..7 carry P = 0 against zero V rows 16..31
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *(uint4*)(vimg + v_off<D>(16 + 4 * i + g, r16)) = make_uint4(0, 0, 0, 0);
+
+  auto consume = [&](Tile& T, int c0) {
+    if (has_new && s_new >= c0 && s_new < c0 + 16) {
+      if (min(c0 + r16, len - 1) == s_new) {
+#pragma unroll
+        for (int s2 = 0; s2 < DS; ++s2) T.k[s2] = knew[s2];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (min(c0 + 4 * i + g, len - 1) == s_new) T.v[i] = vx;
+    }
+    // V image rows 0..15 (the previous tile's transposed reads precede these writes in this
+    // wave's LDS queue)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(uint4*)(vimg + v_off<D>(4 * i + g, r16)) = T.v[i];
+    // S^T: lane holds the scores of keys c0 + 4 g + i for head r16
+    f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < DS; ++s2)
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, T.k[s2]), qf[s2], st, 0, 0, 0);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = c0 + 4 * g + i < len ? st[i] * a.scale_log2 : -INFINITY;
+      st[i] = x;
+      mx = fmaxf(mx, x);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);  // finite: every tile holds >= 1 valid key
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float pv = exp2f(st[i] - mn);
+      st[i] = pv;
+      rs += pv;
+    }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    // O rows are heads 4 g + i: their factors live in lanes 4 g + i
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float al = __shfl(alpha, 4 * g + i, 64);
+#pragma unroll
+      for (int c = 0; c < DT; ++c) o[c][i] *= al;
+    }
+    // O += P·V: P (A operand) = the packed S^T accumulators, V (B operand) by transposed reads
+    const bf16x8 pa = pack_bf16x8(st, f32x4{0.f, 0.f, 0.f, 0.f});
+    const int qrow_ = lane >> 2 & 3, pcol = lane & 3;
+#pragma unroll
+    for (int c = 0; c < DT; ++c) {
+      const int key_a = 4 * g + qrow_, col = 16 * c + 4 * pcol;
+      const s16x4 lo = ds_tr16(vimg + v_off<D>(key_a, col >> 3) + ((col & 7) << 1));
+      const s16x4 hi = ds_tr16(vimg + v_off<D>(key_a + 16, col >> 3) + ((col & 7) << 1));
+      o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, cat_tr(lo, hi), o[c], 0, 0, 0);
+    }
+  };
+
+  for (int c0 = kbeg; c0 < len; c0 += 32) {
+    if (c0 + 16 < len) load(tb, c0 + 16);
+    consume(ta, c0);
+    if (c0 + 16 < len) {
+      if (c0 + 32 < len) load(ta, c0 + 32);
+      consume(tb, c0 + 16);
+    }
+  }
+  // ---- normalise and store: lane holds O[head 4 g + i][d = 16 c + r16] ----
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = 4 * g + i;
+    const float lh = __shfl(l, h, 64);
+    const float inv = lh > 0.f ? 1.f / lh : 0.f;
+    if (h < G) {
+      bf16_t* orow = a.o + (long)b * a.ldo + (long)(hk * G + h) * D;
+#pragma unroll
+      for (int c = 0; c < DT; ++c) orow[16 * c + r16] = f2bf(o[c][i] * inv);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Batch-1 decode: attention + o_proj + residual in ONE launch (RAG answer latency path)
 // ---------------------------------------------------------------------------------------------
 // At batch 1 the attention of a layer is latency-bound (~1.8 MB of K/V over 8 kv-heads) and the
@@ -1344,6 +1549,20 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -1;
+  // large batch, one partition per (batch, kv head): the MFMA kernel (RT_DECODE_MFMA=0 disables)
+  static const int use_mfma = getenv("RT_DECODE_MFMA") ? atoi(getenv("RT_DECODE_MFMA")) : 1;
+  if (use_mfma && NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) {
+    dim3 mgrid((unsigned)(B * Hkv)), mblock(64);
+    switch (G) {
+      case 1: hipLaunchKernelGGL(attn_decode_mfma_kernel<1>, mgrid, mblock, 0, stream, a); break;
+      case 2: hipLaunchKernelGGL(attn_decode_mfma_kernel<2>, mgrid, mblock, 0, stream, a); break;
+      case 4: hipLaunchKernelGGL(attn_decode_mfma_kernel<4>, mgrid, mblock, 0, stream, a); break;
+      case 8: hipLaunchKernelGGL(attn_decode_mfma_kernel<8>, mgrid, mblock, 0, stream, a); break;
+      default: hipLaunchKernelGGL(attn_decode_mfma_kernel<16>, mgrid, mblock, 0, stream, a); break;
+    }
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
   const int nk = g_dec_nk > 0 ? g_dec_nk : 4;  // keys per lane per chunk; PS must be a multiple of the chunk
   if (PS % (4 * (64 / (D / 8)) * nk) != 0) return -1;
   dim3 grid(NP, Hkv, B), block(256);

@@ -530,7 +530,10 @@ def test_gemm_256_identity():
 
 @pytest.mark.parametrize("B,Hq,Hkv,D,Smax,rot,window", [(1, 32, 8, 128, 456, True, 0), (64, 32, 8, 128, 456, True, 0),
                                                         (3, 8, 8, 64, 200, False, 0), (5, 8, 2, 32, 300, True, 64),
-                                                        (2, 16, 2, 128, 64, True, 0)])
+                                                        (2, 16, 2, 128, 64, True, 0),
+                                                        # B * Hkv >= 256: the MFMA kernel (G = 4, 8, 1)
+                                                        (40, 32, 8, 128, 300, True, 64), (32, 64, 8, 128, 200, True, 0),
+                                                        (16, 16, 16, 128, 97, False, 0)])
 @pytest.mark.parametrize("poison", [False, True])
 def test_decode_step_fused(B, Hq, Hkv, D, Smax, rot, window, poison):
     """Fused RoPE + append + attention + in-launch combine == rope_qkv_ + decode_attention.
