@@ -74,6 +74,49 @@ __device__ __forceinline__ void ds_tr16_x4(uint32_t a, rt_s16x4& r0, rt_s16x4& r
       : "v"(a), "i"(O1), "i"(O2), "i"(O3)
       : "memory");
 }
+// F fragments x 4 reads at a_f + {0, O1, O2, O3}: r[4 f + h]
+template <int O1, int O2, int O3>
+__device__ __forceinline__ void ds_tr16_frag2(uint32_t a0, uint32_t a1, rt_s16x4 (&r)[8]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8\n\t"
+      "ds_read_b64_tr_b16 %1, %8 offset:%10\n\t"
+      "ds_read_b64_tr_b16 %2, %8 offset:%11\n\t"
+      "ds_read_b64_tr_b16 %3, %8 offset:%12\n\t"
+      "ds_read_b64_tr_b16 %4, %9\n\t"
+      "ds_read_b64_tr_b16 %5, %9 offset:%10\n\t"
+      "ds_read_b64_tr_b16 %6, %9 offset:%11\n\t"
+      "ds_read_b64_tr_b16 %7, %9 offset:%12\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+      : "v"(a0), "v"(a1), "i"(O1), "i"(O2), "i"(O3)
+      : "memory");
+}
+template <int O1, int O2, int O3>
+__device__ __forceinline__ void ds_tr16_frag4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, rt_s16x4 (&r)[16]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %16\n\t"
+      "ds_read_b64_tr_b16 %1, %16 offset:%20\n\t"
+      "ds_read_b64_tr_b16 %2, %16 offset:%21\n\t"
+      "ds_read_b64_tr_b16 %3, %16 offset:%22\n\t"
+      "ds_read_b64_tr_b16 %4, %17\n\t"
+      "ds_read_b64_tr_b16 %5, %17 offset:%20\n\t"
+      "ds_read_b64_tr_b16 %6, %17 offset:%21\n\t"
+      "ds_read_b64_tr_b16 %7, %17 offset:%22\n\t"
+      "ds_read_b64_tr_b16 %8, %18\n\t"
+      "ds_read_b64_tr_b16 %9, %18 offset:%20\n\t"
+      "ds_read_b64_tr_b16 %10, %18 offset:%21\n\t"
+      "ds_read_b64_tr_b16 %11, %18 offset:%22\n\t"
+      "ds_read_b64_tr_b16 %12, %19\n\t"
+      "ds_read_b64_tr_b16 %13, %19 offset:%20\n\t"
+      "ds_read_b64_tr_b16 %14, %19 offset:%21\n\t"
+      "ds_read_b64_tr_b16 %15, %19 offset:%22\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
+        "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]), "=&v"(r[15])
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "i"(O1), "i"(O2), "i"(O3)
+      : "memory");
+}
+
 // 2 x (2 reads at a_i + {0, O1})
 template <int O1>
 __device__ __forceinline__ void ds_tr16_2x2(uint32_t a0, uint32_t a1, rt_s16x4& r0, rt_s16x4& r1, rt_s16x4& r2,

@@ -110,7 +110,7 @@ __device__ __forceinline__ void wait_granules(int n) {
 // each wave owns 2 B fragments instead of 4 (columns 64 (wc >> 1) + 16 (wc & 1) + 32 s): used for
 // M = 256 decode GEMMs (twice the workgroups, no split-K on the widest weights) and for the last,
 // partial wave of tiles of a large GEMM (rt_gemm_big_planned).
-template <int LA, int LB, int OUT, int EPI, int BN>
+template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   static_assert(BN == 256 || BN == 128, "BN");
   constexpr int NB = BN / 128;  // B fragments per wave and B sub-block; LDS-DMA instructions per B granule
@@ -234,38 +234,70 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     const i32x4 hi = *(const i32x4*)(img + row * 128 + (((4 + fq) ^ row_swz(row)) << 4));
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   };
-  // KMAJ: fragment of 16 mn starting at mn (multiple of 16) — both 32-deep k halves
-  auto rd_kmaj = [&](const char* img, int mn) -> i32x8 {
+  // KMAJ fragments by inline-asm transposed reads (the builtin makes hipcc drain every LDS-DMA in
+  // flight before each read: rt_common.h). The 4 reads of a fragment are at +0, +256, +2048, +2304
+  // bytes from its first (rows kr, kr + 4, kr + 32, kr + 36 share the chunk swizzle).
+  auto kmaj_addr = [&](const char* img, int mn) -> uint32_t {
     const int blk = mn >> 5, c0 = mn & 31;
     const int q = frow >> 2, pp = frow & 3;
     const int col = c0 + 4 * pp;
-    const char* b = img + blk * 4096;
-    s16x4 v[4];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {  // h = 2 kk + half
-      const int kr = (h >> 1) * 32 + fq * 8 + (h & 1) * 4 + q;
-      const int ch = (col >> 3) ^ kmaj_swz(kr);
-      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + kr * 64 + ch * 16 + (col & 7) * 2));
-    }
+    const int kr = fq * 8 + q;
+    const int ch = (col >> 3) ^ kmaj_swz(kr);
+    return lds_addr(img + blk * 4096 + kr * 64 + ch * 16 + (col & 7) * 2);
+  };
+  auto frag_of = [](const rt_s16x4* v) -> i32x8 {
     typedef __attribute__((ext_vector_type(16))) short s16x16;
     const s16x16 w = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3],
                       v[2][0], v[2][1], v[2][2], v[2][3], v[3][0], v[3][1], v[3][2], v[3][3]};
     return __builtin_bit_cast(i32x8, w);
   };
+  // TRB (A/B reference, RT_GEMM_TR_BUILTIN=1): the same reads through the builtin
+  auto rd_kmaj_builtin = [&](const char* img, int mn) -> i32x8 {
+    const uint32_t a0 = kmaj_addr(img, mn);
+    const char* base = img + (a0 - lds_addr(img));
+    rt_s16x4 v[4];
+    v[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+    v[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 256));
+    v[2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 2048));
+    v[3] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 2304));
+    return frag_of(v);
+  };
   auto read_a = [&](int buf, int s) {
     const char* img = smem + buf * BUF;
+    if constexpr (LA == KMAJ && TRB) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wr * 128 + s * 64 + i * 16;
-      fa[i] = LA == ROW ? rd_row(img, row + frow) : rd_kmaj(img, row);
+      for (int i = 0; i < 4; ++i) fa[i] = rd_kmaj_builtin(img, wr * 128 + s * 64 + i * 16);
+    } else if constexpr (LA == ROW) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = rd_row(img, wr * 128 + s * 64 + i * 16 + frow);
+    } else {
+      rt_s16x4 v[16];
+      ds_tr16_frag4<256, 2048, 2304>(kmaj_addr(img, wr * 128 + s * 64), kmaj_addr(img, wr * 128 + s * 64 + 16),
+                                     kmaj_addr(img, wr * 128 + s * 64 + 32), kmaj_addr(img, wr * 128 + s * 64 + 48), v);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_of(v + 4 * i);
     }
   };
   auto read_b = [&](int buf, int s, i32x8 (&fb)[2]) {
     const char* img = smem + buf * BUF + OPB;
+    auto brow = [&](int j) {
+      return NB == 2 ? (wc >> 1) * 128 + (wc & 1) * 64 + s * 32 + j * 16 : (wc >> 1) * 64 + s * 32 + (wc & 1) * 16;
+    };
+    if constexpr (LB == ROW) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int row = NB == 2 ? (wc >> 1) * 128 + (wc & 1) * 64 + s * 32 + j * 16 : (wc >> 1) * 64 + s * 32 + (wc & 1) * 16;
-      fb[j] = LB == ROW ? rd_row(img, row + frow) : rd_kmaj(img, row);
+      for (int j = 0; j < NB; ++j) fb[j] = rd_row(img, brow(j) + frow);
+    } else if constexpr (TRB) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) fb[j] = rd_kmaj_builtin(img, brow(j));
+    } else if constexpr (NB == 2) {
+      rt_s16x4 v[8];
+      ds_tr16_frag2<256, 2048, 2304>(kmaj_addr(img, brow(0)), kmaj_addr(img, brow(1)), v);
+      fb[0] = frag_of(v);
+      fb[1] = frag_of(v + 4);
+    } else {
+      rt_s16x4 v[4];
+      ds_tr16_x4<256, 2048, 2304>(kmaj_addr(img, brow(0)), v[0], v[1], v[2], v[3]);
+      fb[0] = frag_of(v);
     }
   };
   auto half = [](const i32x8& v, int h) -> bf16x8 {
@@ -561,18 +593,15 @@ __global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
     const i32x4 hi = *(const i32x4*)(img + row * 128 + (((4 + fq) ^ row_swz(row)) << 4));
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   };
-  auto rd_kmaj = [&](const char* img, int mn) -> i32x8 {
+  auto kmaj_addr = [&](const char* img, int mn) -> uint32_t {  // first of a fragment's 4 reads
     const int blk = mn >> 5, c0 = mn & 31;
     const int q = frow >> 2, pp = frow & 3;
     const int col = c0 + 4 * pp;
-    const char* b = img + blk * 4096;
-    s16x4 v[4];
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int kr = (h >> 1) * 32 + fq * 8 + (h & 1) * 4 + q;
-      const int ch = (col >> 3) ^ kmaj_swz(kr);
-      v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b + kr * 64 + ch * 16 + (col & 7) * 2));
-    }
+    const int kr = fq * 8 + q;
+    const int ch = (col >> 3) ^ kmaj_swz(kr);
+    return lds_addr(img + blk * 4096 + kr * 64 + ch * 16 + (col & 7) * 2);
+  };
+  auto frag_of = [](const rt_s16x4* v) -> i32x8 {
     typedef __attribute__((ext_vector_type(16))) short s16x16;
     const s16x16 w = {v[0][0], v[0][1], v[0][2], v[0][3], v[1][0], v[1][1], v[1][2], v[1][3],
                       v[2][0], v[2][1], v[2][2], v[2][3], v[3][0], v[3][1], v[3][2], v[3][3]};
@@ -601,11 +630,25 @@ __global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
       if (t + 2 < t_end) stage(t + 2);
       const char* slot = smem + ((t - t_begin) % SM_SLOTS) * SM_SLOT;
       i32x8 fa[2], fb[2];
+      // KMAJ fragments by inline-asm transposed reads (the builtin drains the LDS-DMA ring)
+      if constexpr (LA == ROW) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = LA == ROW ? rd_row(slot, wr * 32 + i * 16 + frow) : rd_kmaj(slot, wr * 32 + i * 16);
+        for (int i = 0; i < 2; ++i) fa[i] = rd_row(slot, wr * 32 + i * 16 + frow);
+      } else {
+        rt_s16x4 v[8];
+        ds_tr16_frag2<256, 2048, 2304>(kmaj_addr(slot, wr * 32), kmaj_addr(slot, wr * 32 + 16), v);
+        fa[0] = frag_of(v);
+        fa[1] = frag_of(v + 4);
+      }
+      if constexpr (LB == ROW) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[j] = LB == ROW ? rd_row(slot + 8192, wc * 32 + j * 16 + frow) : rd_kmaj(slot + 8192, wc * 32 + j * 16);
+        for (int j = 0; j < 2; ++j) fb[j] = rd_row(slot + 8192, wc * 32 + j * 16 + frow);
+      } else {
+        rt_s16x4 v[8];
+        ds_tr16_frag2<256, 2048, 2304>(kmaj_addr(slot + 8192, wc * 32), kmaj_addr(slot + 8192, wc * 32 + 16), v);
+        fb[0] = frag_of(v);
+        fb[1] = frag_of(v + 4);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -703,6 +746,15 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
   const int tiles_n = act == E_SWIGLU ? p.N / bn : (p.N + bn - 1) / bn;
   dim3 grid(((p.M + 255) / 256) * tiles_n, p.nsplit), block(512);
   const int key = layout_a * 100 + layout_b * 10 + out;
+  // A/B switch: the NN / TN forms with the compiler's transposed-read builtin
+  static const bool trb = getenv("RT_GEMM_TR_BUILTIN") && atoi(getenv("RT_GEMM_TR_BUILTIN"));
+  if (trb && act == E_NONE && (key == 10 || key == 112)) {
+    if (key == 10 && bn == 128) hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 128, true>), grid, block, 0, stream, p);
+    else if (key == 10) hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 256, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((gemm_big_kernel<KMAJ, KMAJ, O_F32_ATOMIC, E_NONE, 256, true>), grid, block, 0, stream, p);
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
 #define GB_LAUNCH(LA, LB, O, E, BN) hipLaunchKernelGGL((gemm_big_kernel<LA, LB, O, E, BN>), grid, block, 0, stream, p)
   if (bn == 128) {  // the 128-column tile: NT (bf16 / SwiGLU / fp32 / slab) and NN bf16
     switch (key * 10 + act) {
