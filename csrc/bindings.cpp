@@ -613,7 +613,9 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   CHECK_CUDA(q); CHECK_ROWS(q); CHECK_ROWS(k); CHECK_ROWS(v); CHECK_ROWS(o); CHECK_ROWS(dout);
   CHECK_ROWS(dq); CHECK_ROWS(dk); CHECK_ROWS(dv); CHECK_F32(lse);
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
-  auto dq32 = at::empty({B * S, Hq * D}, q.options().dtype(at::kFloat));
+  // fp32 dQ accumulator: only the atomic form (RT_ATTN_BWD_ATOMIC_DQ=1) uses it
+  static const bool atomic_dq = getenv("RT_ATTN_BWD_ATOMIC_DQ") && atoi(getenv("RT_ATTN_BWD_ATOMIC_DQ"));
+  auto dq32 = at::empty({atomic_dq ? B * S : 1, atomic_dq ? Hq * D : 1}, q.options().dtype(at::kFloat));
   if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
   check_rc(rt_attn_bwd(q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0), o.data_ptr(),
                        o.stride(0), dout.data_ptr(), dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(),

@@ -1230,7 +1230,8 @@ struct AttnBwdArgs {
   const bf16_t* dout; long lddo;
   const float* lse;            // [B, Hq, S]
   float* delta;                // [B, Hq, S]
-  float* dq;                   // fp32 [B*S, Hq*D] (zeroed)
+  float* dq;                   // fp32 [B*S, Hq*D] (zeroed; atomic form only)
+  bf16_t* dqb; long lddq;      // bf16 dQ (separate dQ kernel)
   bf16_t* dk; long lddk;       // may alias into a d_qkv buffer
   bf16_t* dv; long lddv;
   const int* kv_start;
@@ -1270,7 +1271,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
   }
 }
 
-template <int D>
+template <int D, bool DQ>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnBwdArgs a) {
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TB = 64 * D * 2;
@@ -1415,6 +1416,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnBwdArgs a) {
           dk[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qT, db, dk[c], 0, 0, 0);
         }
       }
+      if constexpr (!DQ) continue;  // dQ comes from attn_bwd_dq_kernel (no atomics)
       // dS -> LDS as [q][key] (16-B chunk swizzle by q&7) for dQ = dS · K
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -1468,6 +1470,140 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnBwdArgs a) {
         a.dk[((long)b * a.S + mykey) * a.lddk + (long)hk * D + d] = f2bf(dk[c][i] * a.scale);
         a.dv[((long)b * a.S + mykey) * a.lddv + (long)hk * D + d] = f2bf(dvv[c][i]);
       }
+  }
+}
+
+// dQ without atomics: one workgroup = 64 query rows of one (batch, head), 4 waves x 16 rows (the
+// forward's swapped geometry). Per 64-key tile (K and V register-prefetched into K-style LDS
+// images): S^T = K·Q^T and dP^T = V·dO^T with the key on the MFMA row and the query on the lane;
+// P = exp2(S·scale·log2e − lse·log2e) (no online softmax: lse is known), dS = P (dP − delta),
+// masks; dQ += dS·K with dS (packed accumulators) as the A operand and K^T by transposed reads of
+// the same K image. Each dQ element is written once, in bf16 (the atomic form added one fp32 row
+// per key block: ~0.5 GB of atomics per Mistral-7B layer at 9.6k tokens, bound at ~1.3 TB/s).
+template <int D>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+  constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
+  constexpr int TILE_BYTES = 64 * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+  char* Ks = smem;
+  char* Vs = smem + TILE_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int hk = h / (a.Hq / a.Hkv);
+  const int qblk0 = blockIdx.x * 64;
+  const int q0 = qblk0 + wid * 16;
+  const int start = a.kv_start ? a.kv_start[b] : 0;
+  int kend = a.S;
+  if (a.causal) kend = min(kend, min(qblk0 + 63, a.S - 1) + 1);
+  int kbeg = start;
+  if (a.window > 0) kbeg = max(kbeg, qblk0 - a.window + 1);
+  kbeg = max(kbeg, 0) & ~63;
+
+  // Q and dO fragments (B operands): lane holds X[q0 + r16][32 s + 8 g .. +8]
+  const int qrow = min(q0 + r16, a.S - 1);
+  bf16x8 qf[DS], of[DS];
+  {
+    const bf16_t* qp = a.q + ((long)b * a.S + qrow) * a.ldq + (long)h * D + 8 * g;
+    const bf16_t* op = a.dout + ((long)b * a.S + qrow) * a.lddo + (long)h * D + 8 * g;
+#pragma unroll
+    for (int s2 = 0; s2 < DS; ++s2) {
+      qf[s2] = *(const bf16x8*)(qp + 32 * s2);
+      of[s2] = *(const bf16x8*)(op + 32 * s2);
+    }
+  }
+  const long li = ((long)b * a.Hq + h) * a.S + qrow;
+  const float lse2 = a.lse[li] * 1.4426950408889634f, del = a.delta[li];
+  // retire these loads here (else hipcc re-waits vmcnt(0) for them inside the loop)
+#pragma unroll
+  for (int s2 = 0; s2 < DS; ++s2) asm volatile("" : "+v"(qf[s2]), "+v"(of[s2]));
+
+  f32x4 dq[DT];
+#pragma unroll
+  for (int c = 0; c < DT; ++c) dq[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int CPT = 64 * NCH / 256;  // 16-B chunks per thread per tile
+  constexpr int KSTEP = 256 / NCH;
+  const int lc = tid % NCH, lkey = tid / NCH;
+  const bf16_t* kb = a.k + (long)b * a.S * a.ldk + (long)hk * D + lc * 8;
+  const bf16_t* vb = a.v + (long)b * a.S * a.ldv + (long)hk * D + lc * 8;
+  u32x4 kreg[CPT], vreg[CPT];
+  auto load_tile = [&](int kv0) {
+#pragma unroll
+    for (int r = 0; r < CPT; ++r) {
+      const long kk = min(kv0 + lkey + KSTEP * r, a.S - 1);
+      kreg[r] = *(const u32x4*)(kb + kk * a.ldk);
+      vreg[r] = *(const u32x4*)(vb + kk * a.ldv);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int r = 0; r < CPT; ++r) {
+      *(u32x4*)(Ks + k_off<D>(lkey + KSTEP * r, lc)) = kreg[r];
+      *(u32x4*)(Vs + k_off<D>(lkey + KSTEP * r, lc)) = vreg[r];
+    }
+  };
+  if (kbeg < kend) {
+    load_tile(kbeg);
+    store_tile();
+  }
+  __syncthreads();
+
+  const int qq = q0 + r16;  // this lane's query row
+  for (int kv0 = kbeg; kv0 < kend; kv0 += 64) {
+    const bool has_next = kv0 + 64 < kend;
+    if (has_next) load_tile(kv0 + 64);
+    // S^T[t], dP^T[t]: lane holds (key kv0 + 16 t + 4 g + i, query qq)
+    f32x4 st[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      st[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < DS; ++s2) {
+        const bf16x8 kf = *(const bf16x8*)(Ks + k_off<D>(16 * t + r16, 4 * s2 + g));
+        const bf16x8 vf = *(const bf16x8*)(Vs + k_off<D>(16 * t + r16, 4 * s2 + g));
+        st[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s2], st[t], 0, 0, 0);
+        dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, of[s2], dp[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kk = kv0 + 16 * t + 4 * g + i;
+        bool ok = kk >= start && kk < a.S && qq < a.S;
+        if (a.causal) ok = ok && kk <= qq;
+        if (a.window > 0) ok = ok && (qq - kk) < a.window;
+        const float pv = ok ? exp2f(st[t][i] * a.scale_log2 - lse2) : 0.f;
+        st[t][i] = pv * (dp[t][i] - del);  // dS^T
+      }
+    // dQ += dS · K: A = packed dS^T accumulators [q][keys], B = K^T by transposed reads
+    const int qr = lane >> 2 & 3, pcol = lane & 3;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 da = pack_bf16x8(st[2 * ks], st[2 * ks + 1]);
+#pragma unroll
+      for (int c = 0; c < DT; ++c) {
+        const int key_a = 32 * ks + 4 * g + qr, col = 16 * c + 4 * pcol;
+        const s16x4 lo = ds_tr16(Ks + k_off<D>(key_a, col >> 3) + ((col & 7) << 1));
+        const s16x4 hi = ds_tr16(Ks + k_off<D>(key_a + 16, col >> 3) + ((col & 7) << 1));
+        dq[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, cat_tr(lo, hi), dq[c], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (has_next) store_tile();
+    __syncthreads();
+  }
+  // lane holds dQ[q0 + 4 g + i][16 c + r16]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qo = q0 + 4 * g + i;
+    if (qo < a.S) {
+      bf16_t* dst = a.dqb + ((long)b * a.S + qo) * a.lddq + (long)h * D;
+#pragma unroll
+      for (int c = 0; c < DT; ++c) dst[16 * c + r16] = f2bf(dq[c][i] * a.scale);
+    }
   }
 }
 
@@ -1590,24 +1726,31 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.window = window;
   a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
   if (B == 0 || S == 0) return 0;
-  RT_HIP_CHECK(hipMemsetAsync(dq_f32, 0, (size_t)B * S * Hq * D * sizeof(float), stream));
+  a.dqb = (bf16_t*)dq; a.lddq = lddq;
   const long rows = (long)B * S * Hq;
   const long rows_per_block = 4L * (64 / (D / 8));
   dim3 pgrid((unsigned)((rows + rows_per_block - 1) / rows_per_block)), grid((S + 63) / 64, Hkv, B);
-  switch (D) {
-    case 64:
-      hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, pgrid, dim3(256), 0, stream, a);
-      hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, stream, a);
-      break;
-    case 128:
-      hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, pgrid, dim3(256), 0, stream, a);
-      hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, stream, a);
-      break;
-    default: return -1;
+  // dQ: a separate kernel per 64-query block (default) or fp32 atomics from the key-block kernel
+  // (RT_ATTN_BWD_ATOMIC_DQ=1, the round-1 form)
+  static const bool atomic_dq = getenv("RT_ATTN_BWD_ATOMIC_DQ") && atoi(getenv("RT_ATTN_BWD_ATOMIC_DQ"));
+  if (D != 64 && D != 128) return -1;
+  if (atomic_dq) RT_HIP_CHECK(hipMemsetAsync(dq_f32, 0, (size_t)B * S * Hq * D * sizeof(float), stream));
+  dim3 qgrid((S + 63) / 64, Hq, B);
+#define BWD_CASE(DD)                                                                              \
+  hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, pgrid, dim3(256), 0, stream, a);                    \
+  if (atomic_dq) {                                                                                \
+    hipLaunchKernelGGL((attn_bwd_kernel<DD, true>), grid, dim3(256), 0, stream, a);               \
+  } else {                                                                                        \
+    hipLaunchKernelGGL((attn_bwd_kernel<DD, false>), grid, dim3(256), 0, stream, a);              \
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<DD>, qgrid, dim3(256), 0, stream, a);                   \
   }
-  const long n = (long)B * S * Hq * D;
-  hipLaunchKernelGGL(f32_to_bf16_strided_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_f32,
-                     (long)Hq * D, (bf16_t*)dq, lddq, (long)B * S);
+  if (D == 64) { BWD_CASE(64) } else { BWD_CASE(128) }
+#undef BWD_CASE
+  if (atomic_dq) {
+    const long n = (long)B * S * Hq * D;
+    hipLaunchKernelGGL(f32_to_bf16_strided_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_f32,
+                       (long)Hq * D, (bf16_t*)dq, lddq, (long)B * S);
+  }
   RT_LAUNCH_CHECK();
   return 0;
 }
