@@ -139,7 +139,7 @@ def test_rccl_process_group_world1():
 
 def test_reward_stream_overlap_matches_serial(monkeypatch):
     """overlap_reward=True: the reward encoder runs on the side stream WHILE the reference forward
-    runs on the main stream — with a GPU spin injected in front of every reference minibatch, the
+    runs on the main stream — with a GPU spin injected behind every reference minibatch, the
     encoder's last event completes before the reference forward's end event (it would complete
     after it if the reward waited for the main stream, as a blocking .cpu() of the rollout tokens
     on the main stream made it do). overlap_reward=False scores first, serially. Both schedules
@@ -152,9 +152,13 @@ def test_reward_stream_overlap_matches_serial(monkeypatch):
     spin = {"on": False}
 
     def slow_ref(*a, **k):
+        out = orig(*a, **k)
         if spin["on"]:
-            torch.cuda._sleep(100_000_000)  # tens of ms of GPU spin on the current (main) stream
-        return orig(*a, **k)
+            # tens of ms of GPU spin on the main stream AFTER the reference kernels are queued: one
+            # queue packet, so the host is never held back by a full hardware queue (a spin in
+            # front of hundreds of kernel launches stalled the host once the queue ring filled)
+            torch.cuda._sleep(100_000_000)
+        return out
 
     monkeypatch.setattr(P, "score_sequences", slow_ref)
     res, evs = [], []
