@@ -72,6 +72,8 @@ int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const int*, 
                 int, int, float*, long*,
                 hipStream_t);
 int rt_gae(const float*, const float*, const float*, int, int, float, float, float*, float*, hipStream_t);
+int rt_ppo_advantages(const float*, const float*, const float*, const float*, const int*, int, int, float, float, float,
+                      int, float, float*, float*, float*, float*, hipStream_t);
 void rt_attn_decode_set_nk(int nk);
 void rt_attn_o_set_stamps(long long* p);
 int rt_ppo_loss(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
@@ -774,6 +776,25 @@ Tensor segment_mean(const Tensor& x, const Tensor& order, const Tensor& seg, boo
   return out;
 }
 
+// (adv, returns, token rewards, per-sequence KL) of a rollout: see ppo_advantages_kernel
+std::vector<Tensor> ppo_advantages(const Tensor& old_lp, const Tensor& ref_lp, const Tensor& values, const Tensor& score,
+                                   const Tensor& len, double kl_coef, double gamma, double lam, bool whiten, double eps) {
+  CHECK_CUDA(old_lp); CHECK_F32(old_lp); CHECK_F32(ref_lp); CHECK_F32(values); CHECK_F32(score); CHECK_I32(len);
+  TORCH_CHECK(old_lp.is_contiguous() && ref_lp.is_contiguous() && values.is_contiguous() && score.is_contiguous() &&
+              len.is_contiguous());
+  const int64_t B = old_lp.size(0), T = old_lp.size(1);
+  TORCH_CHECK(ref_lp.sizes() == old_lp.sizes() && values.sizes() == old_lp.sizes() && score.numel() == B &&
+              len.numel() == B, "ppo_advantages: shapes");
+  auto adv = at::empty_like(old_lp), ret = at::empty_like(old_lp), rew = at::empty_like(old_lp);
+  auto kl = at::empty({B}, old_lp.options());
+  check_rc(rt_ppo_advantages(old_lp.data_ptr<float>(), ref_lp.data_ptr<float>(), values.data_ptr<float>(),
+                             score.data_ptr<float>(), len.data_ptr<int>(), (int)B, (int)T, (float)kl_coef, (float)gamma,
+                             (float)lam, whiten ? 1 : 0, (float)eps, adv.data_ptr<float>(), ret.data_ptr<float>(),
+                             rew.data_ptr<float>(), kl.data_ptr<float>(), cur_stream()),
+           "ppo_advantages");
+  return {adv, ret, rew, kl};
+}
+
 std::vector<Tensor> gae(const Tensor& rewards, const Tensor& values, const Tensor& mask, double gamma, double lam) {
   CHECK_CUDA(rewards); CHECK_F32(rewards); CHECK_F32(values); CHECK_F32(mask);
   TORCH_CHECK(rewards.is_contiguous() && values.is_contiguous() && mask.is_contiguous() && rewards.dim() == 2);
@@ -877,6 +898,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "debug: int64 [NB, 8] buffer receiving per-block s_memrealtime phase stamps of attn_o_fused (None = off)");
   m.def("attn_o_fused", &attn_o_fused, "batch-1 decode: attention + o_proj + residual in one launch (false = unsupported)");
   m.def("gae", &gae);
+  m.def("ppo_advantages", &ppo_advantages, "token KL rewards + GAE + advantage whitening in one launch");
   m.def("ppo_loss", &ppo_loss, "fused token-level PPO loss: {stats[6], dlp, dv, dent}");
   m.def("decode_update", &decode_update);
   ragtl::bind_tokenizer(m);

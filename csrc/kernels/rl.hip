@@ -30,6 +30,69 @@ __global__ void gae_kernel(const float* __restrict__ rewards, const float* __res
   }
 }
 
+// PPO advantages in one launch (one workgroup; a thread per sequence, then block reductions):
+//   kl[b,t]   = old_logp - ref_logp                      (t < len[b])
+//   r[b,t]    = -kl_coef kl + (t == len[b] - 1) score[b]  (reward at the last response token)
+//   GAE over r with V = old values (the reverse scan of gae_kernel)
+//   whiten: adv = (adv - mean) / sqrt(var + eps) over the valid tokens (masked_whiten)
+//   kl_seq[b] = sum_t kl                                  (the KL-to-reference statistic)
+// Replaces ~15 small ATen launches between the reference forward and the update
+// (reinforcement_learning_optimization_after_rag.py:176-191 GAE, with the SURVEY B3 KL term).
+__global__ __launch_bounds__(256) void ppo_advantages_kernel(const float* __restrict__ old_lp, const float* __restrict__ ref_lp,
+                                                             const float* __restrict__ values, const float* __restrict__ score,
+                                                             const int* __restrict__ len, int B, int T, float kl_coef,
+                                                             float gamma, float lam, int whiten, float eps,
+                                                             float* __restrict__ adv, float* __restrict__ ret,
+                                                             float* __restrict__ rew, float* __restrict__ kl_seq) {
+  __shared__ float sb[4];
+  float s1 = 0.f, n = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int L = min(max(len[b], 0), T);
+    float nextv = 0.f, last = 0.f, klsum = 0.f;
+    for (int t = T - 1; t >= 0; --t) {
+      const long i = (long)b * T + t;
+      if (t >= L) {
+        adv[i] = 0.f; ret[i] = 0.f; rew[i] = 0.f;
+        continue;
+      }
+      const float kl = old_lp[i] - ref_lp[i];
+      klsum += kl;
+      const float r = -kl_coef * kl + (t == L - 1 ? score[b] : 0.f);
+      rew[i] = r;
+      const float v = values[i];
+      const float delta = r + gamma * nextv - v;
+      last = delta + gamma * lam * last;
+      adv[i] = last;
+      ret[i] = last + v;
+      nextv = v;
+      s1 += last;
+    }
+    n += (float)L;
+    kl_seq[b] = klsum;
+  }
+  if (!whiten) return;
+  const float tot = block_sum(s1, sb);
+  const float cnt = block_sum(n, sb);
+  const float mean = tot / fmaxf(cnt, 1.f);
+  float s2 = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int L = min(max(len[b], 0), T);
+    for (int t = 0; t < L; ++t) {
+      const float d = adv[(long)b * T + t] - mean;
+      s2 += d * d;
+    }
+  }
+  const float var = block_sum(s2, sb) / fmaxf(cnt, 1.f);
+  const float inv = rsqrtf(var + eps);
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const int L = min(max(len[b], 0), T);
+    for (int t = 0; t < L; ++t) {
+      const long i = (long)b * T + t;
+      adv[i] = (adv[i] - mean) * inv;
+    }
+  }
+}
+
 // After sampling token `tok[b]` at decode step `step`: record it, update finished flags (eos or
 // length budget), advance per-row cache length/position, bump the RNG offset and step counter.
 // Rows that are finished keep emitting pad and stop advancing.
@@ -180,6 +243,16 @@ extern "C" int rt_gae(const float* rewards, const float* values, const float* ma
   if (B == 0) return 0;
   hipLaunchKernelGGL(gae_kernel, dim3((B + 63) / 64), dim3(64), 0, stream, rewards, values, mask, B, T, gamma, lam, adv,
                      ret);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int rt_ppo_advantages(const float* old_lp, const float* ref_lp, const float* values, const float* score,
+                                 const int* len, int B, int T, float kl_coef, float gamma, float lam, int whiten,
+                                 float eps, float* adv, float* ret, float* rew, float* kl_seq, hipStream_t stream) {
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(ppo_advantages_kernel, dim3(1), dim3(256), 0, stream, old_lp, ref_lp, values, score, len, B, T,
+                     kl_coef, gamma, lam, whiten, eps, adv, ret, rew, kl_seq);
   RT_LAUNCH_CHECK();
   return 0;
 }

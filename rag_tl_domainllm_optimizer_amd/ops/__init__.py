@@ -8,7 +8,7 @@ from .attention import (  # noqa: F401
     attention, decode_attention, decode_step_attention, decode_step_attention_o, decode_workspace, flash_attention_qkv,
     rope_qkv, rope_qkv_,
 )
-from .misc import (embedding, gae, ivf_scan, pool_normalize, ppo_loss, sample, segment_mean, swiglu,  # noqa: F401
+from .misc import (embedding, gae, ivf_scan, ppo_advantages, pool_normalize, ppo_loss, sample, segment_mean, swiglu,  # noqa: F401
                    token_logprobs, topk)
 from .optim import FlatParams, FusedAdamW, MixedFlatParams, flat_params  # noqa: F401
 from .fp8 import Fp8Cache, dequantize_fp8, gemm_fp8, quantize_fp8  # noqa: F401

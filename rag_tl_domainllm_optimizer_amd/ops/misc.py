@@ -194,6 +194,19 @@ def ppo_loss(lp, vals, ent, old, adv, ret, mask, eps: float, c_v: float, c_e: fl
     return ref.ppo_loss(lp, old, adv, vals, ret, ent, mask.float(), eps, c_v, c_e, vclip, vold)
 
 
+def ppo_advantages(old_logp, ref_logp, values, scores, resp_len, kl_coef: float, gamma: float, lam: float,
+                   whiten: bool = True, eps: float = 1e-8):
+    """Token rewards (-kl_coef (old - ref) per token + the score at the last response token), GAE
+    over the old values and masked advantage whitening in one launch on GPU.
+    -> (advantages, returns, token rewards, per-sequence KL sum)."""
+    f = lambda t: t.float().contiguous()  # noqa: E731
+    if on_gpu(old_logp):
+        return native().ppo_advantages(f(old_logp), f(ref_logp), f(values), f(scores), resp_len.int().contiguous(),
+                                       kl_coef, gamma, lam, whiten, eps)
+    return ref.ppo_advantages(f(old_logp), f(ref_logp), f(values), f(scores), resp_len, kl_coef, gamma, lam, whiten,
+                              eps)
+
+
 def gae(rewards, values, mask, gamma: float, lam: float):
     if on_gpu(rewards):
         return native().gae(rewards.float().contiguous(), values.float().contiguous(), mask.float().contiguous(),

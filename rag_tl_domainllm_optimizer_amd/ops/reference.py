@@ -289,3 +289,22 @@ def segment_mean(x, order, seg, normalize: bool, out):
     nz = cnt > 0
     out[nz] = m[nz].to(out.dtype)
     return out
+
+
+def ppo_advantages(old_logp, ref_logp, values, scores, resp_len, kl_coef, gamma, lam, whiten=True, eps=1e-8):
+    """fp32 oracle of the ppo_advantages kernel (the eager token-reward + GAE + whitening path)."""
+    B, T = old_logp.shape
+    mask = torch.arange(T, device=old_logp.device)[None, :] < resp_len.long()[:, None]
+    kl = (old_logp - ref_logp) * mask
+    rewards = -kl_coef * kl
+    last = (resp_len.long() - 1).clamp(min=0)
+    rewards[torch.arange(B, device=old_logp.device), last] += scores
+    rewards = rewards * mask
+    adv, ret = gae(rewards, values * mask, mask.float(), gamma, lam)
+    if whiten:
+        m = mask.float()
+        n = m.sum().clamp(min=1)
+        mean = (adv * m).sum() / n
+        var = (((adv - mean) ** 2) * m).sum() / n
+        adv = (adv - mean) * torch.rsqrt(var + eps) * m
+    return adv, ret, rewards, kl.sum(-1)

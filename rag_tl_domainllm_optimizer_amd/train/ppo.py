@@ -37,7 +37,7 @@ from ..parallel import GradSync, info as dist_info, reduce_metrics
 from ..rag.prompt import build_prompt, extract_answer
 from ..runtime import PhaseTimer, StreamPair
 from ..utils import MetricsSink, maybe_inject_fault
-from .common import lr_at, masked_mean, masked_whiten, response_mask, score_sequences
+from .common import lr_at, score_sequences
 
 
 @dataclass
@@ -328,17 +328,13 @@ class PPOTrainer:
             # the whole reference forward is queued and nothing above waited for the device: the
             # host detokenises now and the reward encoder runs on the side stream beside it
             self._collect_rewards(ro)
-        mask = response_mask(ro.resp_len, ro.resp.shape[1])
-        kl = (ro.old_logp - ro.ref_logp) * mask
-        rewards = -self.kl_coef * kl
-        last = (ro.resp_len - 1).clamp(min=0)
-        rewards[torch.arange(len(last), device=rewards.device), last] += ro.scores
-        rewards = rewards * mask
-        adv, ret = ops.gae(rewards, ro.old_values * mask, mask.float(), c.gamma, c.lam)
-        if c.whiten_advantages:
-            adv = masked_whiten(adv, mask)
+        # token rewards (-beta * KL per token, score at the last token), GAE and whitening: one
+        # kernel on GPU (ops.ppo_advantages; the eager oracle on CPU)
+        adv, ret, rewards, kl_seq = ops.ppo_advantages(ro.old_logp, ro.ref_logp, ro.old_values, ro.scores,
+                                                       ro.resp_len, self.kl_coef, c.gamma, c.lam,
+                                                       c.whiten_advantages)
         ro.adv, ro.returns, ro.rewards_tok = adv, ret, rewards
-        ro.kl_ref = float(kl.sum(-1).mean())
+        ro.kl_ref = float(kl_seq.mean())
         return ro
 
     # ------------------------------------------------------------------ update

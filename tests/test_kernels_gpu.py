@@ -773,3 +773,18 @@ def test_attn_o_fused_generation_matches_unfused():
         outs.append(Generator(m, 1, 64, DEV).generate(prompt, p, pad_id=0, eos_ids=[-1]))
     assert torch.equal(outs[0].tokens, outs[1].tokens)
     torch.testing.assert_close(outs[0].logprobs, outs[1].logprobs, rtol=0, atol=0.05)
+
+
+def test_ppo_advantages_kernel():
+    """Fused token rewards + GAE + whitening == the fp32 oracle (ragged lengths incl. 0 and T)."""
+    torch.manual_seed(5)
+    B, T = 300, 128
+    old, refl, vals = (torch.randn(B, T, device=DEV) for _ in range(3))
+    scores = torch.randn(B, device=DEV)
+    lens = torch.randint(0, T + 1, (B,), device=DEV)
+    lens[0], lens[1] = 0, T
+    for whiten in (False, True):
+        got = ops.ppo_advantages(old, refl, vals, scores, lens, 0.05, 0.99, 0.95, whiten)
+        want = ref.ppo_advantages(old.cpu(), refl.cpu(), vals.cpu(), scores.cpu(), lens.cpu(), 0.05, 0.99, 0.95, whiten)
+        for a, b in zip(got, want):
+            _close(a.cpu(), b, rtol=1e-4, atol=1e-4)

@@ -106,3 +106,30 @@ def test_fault_injection_then_resume_matches(tmp_path, monkeypatch):
     got = tr3.step(batches[1])
     for k in ("reward_mean", "total_loss", "policy_loss", "kl_ref"):
         assert abs(got[k] - ref[k]) < 1e-6, (k, got[k], ref[k])
+
+
+def test_ppo_advantages_oracle_matches_eager_path():
+    """ops.ppo_advantages (CPU oracle) == the eager token-reward + GAE + whitening composition."""
+    import torch
+
+    from rag_tl_domainllm_optimizer_amd import ops
+    from rag_tl_domainllm_optimizer_amd.train.common import masked_whiten, response_mask
+
+    g = torch.Generator().manual_seed(0)
+    B, T = 6, 9
+    old, refl, vals = (torch.randn(B, T, generator=g) for _ in range(3))
+    scores = torch.randn(B, generator=g)
+    lens = torch.tensor([9, 1, 0, 5, 8, 3])
+    mask = response_mask(lens, T)
+    kl = (old - refl) * mask
+    rew = -0.1 * kl
+    last = (lens - 1).clamp(min=0)
+    rew[torch.arange(B), last] += scores
+    rew = rew * mask
+    adv, ret = ops.gae(rew, vals * mask, mask.float(), 0.99, 0.95)
+    adv = masked_whiten(adv, mask)
+    a2, r2, w2, k2 = ops.ppo_advantages(old, refl, vals, scores, lens, 0.1, 0.99, 0.95, True)
+    torch.testing.assert_close(a2, adv, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(r2, ret)
+    torch.testing.assert_close(w2, rew)
+    torch.testing.assert_close(k2, kl.sum(-1))
