@@ -32,7 +32,7 @@ int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*
                 int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
 int rt_quant_fp8_rows(const void*, long, void*, long, float*, long, int, hipStream_t);
 int rt_norm_fwd(int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
-                hipStream_t);
+                const float*, int, hipStream_t);
 int rt_norm_bwd(int, const void*, const void*, const void*, const float*, const float*, const void*, void*, float*,
                 float*, int, int, hipStream_t);
 int rt_rope_qkv(void*, long, const int*, const float*, const float*, int, int, int, int, int, float, void*, void*,
@@ -48,6 +48,8 @@ int rt_attn_decode_fused(const void*, long, void*, void*, int, const int*, const
                          const float*, const float*, float, int, float*, unsigned*, int, int, void*, long, int, int, int,
                          int, float, hipStream_t);
 int rt_attn_decode_fused_ps(int, int);
+void rt_attn_decode_set_qkv_slabs(const float*, int);
+int rt_attn_decode_mfma_ok(int, int, int, int, int);
 int rt_attn_o_fused(const void*, void*, void*, int, const int*, const int*, const int*, const int*, const float*,
                     const float*, float, int, float*, int, int, int, int, int, float, const void*, long, const void*,
                     void*, int, unsigned*, int*, hipStream_t);
@@ -421,9 +423,54 @@ std::vector<Tensor> norm_fwd(bool layernorm, const Tensor& x, const optional<Ten
   Tensor mean = layernorm ? at::empty({T}, x.options().dtype(at::kFloat)) : Tensor();
   check_rc(rt_norm_fwd(layernorm, x.data_ptr(), opt_ptr(res), w.data_ptr(), opt_ptr(b), y.data_ptr(),
                        h.defined() ? h.data_ptr() : nullptr, rstd.data_ptr<float>(),
-                       layernorm ? mean.data_ptr<float>() : nullptr, (int)T, (int)H, (float)eps, cur_stream()),
+                       layernorm ? mean.data_ptr<float>() : nullptr, (int)T, (int)H, (float)eps, nullptr, 0,
+                       cur_stream()),
            "norm_fwd");
   return {y, h, rstd, mean};
+}
+
+// reduce of split-K slabs [nsplit, M, N] -> bf16 [M, N] (fallback when a consumer cannot fuse it)
+Tensor splitk_reduce(const Tensor& slabs, int64_t nsplit, int64_t M, int64_t N, Tensor out) {
+  CHECK_CUDA(slabs); CHECK_F32(slabs); CHECK_BF16(out);
+  TORCH_CHECK(slabs.is_contiguous() && slabs.numel() >= nsplit * M * N && out.size(0) == M && out.size(1) == N &&
+              out.stride(1) == 1 && out.stride(0) % 8 == 0, "splitk_reduce: shapes");
+  check_rc(rt_gemm_splitk_reduce(slabs.data_ptr<float>(), (int)nsplit, (int)M, (int)N, nullptr, 0, nullptr, 0,
+                                 out.data_ptr(), out.stride(0), cur_stream()),
+           "splitk_reduce");
+  return out;
+}
+
+// norm_fwd whose input is the sum of `nsplit` fp32 split-K slabs [nsplit, T, H] (the reduce of a
+// split-K GEMM fused into the norm; residual required: returns y and the new residual stream)
+std::vector<Tensor> norm_fwd_slabs(bool layernorm, const Tensor& slabs, int64_t nsplit, int64_t T, int64_t H,
+                                   const Tensor& res, const Tensor& w, const optional<Tensor>& b, double eps) {
+  CHECK_CUDA(slabs); CHECK_F32(slabs); CHECK_BF16(res); CHECK_BF16(w);
+  TORCH_CHECK(slabs.is_contiguous() && slabs.numel() >= nsplit * T * H && res.is_contiguous() && res.numel() == T * H,
+              "norm_fwd_slabs: shapes");
+  auto y = at::empty({T, H}, res.options());
+  auto h = at::empty({T, H}, res.options());
+  auto rstd = at::empty({T}, res.options().dtype(at::kFloat));
+  Tensor mean = layernorm ? at::empty({T}, res.options().dtype(at::kFloat)) : Tensor();
+  check_rc(rt_norm_fwd(layernorm, nullptr, res.data_ptr(), w.data_ptr(), opt_ptr(b), y.data_ptr(), h.data_ptr(),
+                       rstd.data_ptr<float>(), layernorm ? mean.data_ptr<float>() : nullptr, (int)T, (int)H,
+                       (float)eps, slabs.data_ptr<float>(), (int)nsplit, cur_stream()),
+           "norm_fwd_slabs");
+  return {y, h};
+}
+
+// split-K partial slabs only (the reduce is fused into the consumer): slabs [nsplit, M, N] fp32
+void gemm_splitk_raw(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor slabs, int64_t bn) {
+  CHECK_CUDA(a); CHECK_BF16(a); CHECK_BF16(w); CHECK_ROWS(a); CHECK_ROWS(w); CHECK_F32(slabs);
+  CHECK_ALIGN16(a); CHECK_ALIGN16(w);
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 8 == 0 && N % 8 == 0, "gemm_splitk_raw: shapes");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "gemm_splitk_raw: row strides % 8");
+  TORCH_CHECK(slabs.is_contiguous() && slabs.numel() >= nsplit * M * N, "gemm_splitk_raw: workspace too small");
+  if (M == 0) return;
+  check_rc(rt_gemm_big(0, 0, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), nullptr, 0, nullptr, 0, 0,
+                       nullptr, slabs.data_ptr(), N, nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, 0, 3,
+                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, cur_stream()),
+           "gemm_splitk_raw");
 }
 
 std::vector<Tensor> norm_bwd(bool layernorm, const Tensor& dy, const Tensor& h, const Tensor& w, const Tensor& rstd,
@@ -571,6 +618,46 @@ void attn_decode_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& sl
                                 out.data_ptr(), out.stride(0), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
                                 cur_stream()),
            "attn_decode_fused");
+}
+
+// The same decode step with q | k | v given as the qkv GEMM's nsplit fp32 split-K slabs
+// [nsplit, B, (Hq + 2 Hkv) D]: the MFMA kernel sums them in its prologue (no reduce launch).
+// Returns false (nothing launched) when the MFMA kernel does not apply to the shape.
+bool attn_decode_fused_slabs(const Tensor& slabs, int64_t nsplit, Tensor kc, Tensor vc, const Tensor& slot,
+                             const Tensor& attn_len, const optional<Tensor>& kv_start, const optional<Tensor>& pos,
+                             const optional<Tensor>& cos, const optional<Tensor>& sin, double sign, int64_t window,
+                             double scale, int64_t Hq, Tensor part, Tensor tickets, int64_t PS, Tensor out) {
+  CHECK_CUDA(slabs); CHECK_F32(slabs); CHECK_BF16(kc); CHECK_BF16(vc); CHECK_I32(slot); CHECK_I32(attn_len);
+  CHECK_F32(part); CHECK_I32(tickets); CHECK_BF16(out); CHECK_ROWS(out);
+  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes(),
+              "attn_decode_fused_slabs: cache layout");
+  const int64_t B = kc.size(0), Hkv = kc.size(1), Smax = kc.size(2), D = kc.size(3);
+  const int64_t NP = (Smax + PS - 1) / PS, G = Hq / Hkv;
+  TORCH_CHECK(G * Hkv == Hq, "attn_decode_fused_slabs: Hq must be a multiple of Hkv");
+  if (!rt_attn_decode_mfma_ok((int)B, (int)Hq, (int)Hkv, (int)D, (int)NP)) return false;
+  const int64_t W = (Hq + 2 * Hkv) * D;
+  TORCH_CHECK(slabs.is_contiguous() && slabs.numel() >= nsplit * B * W && nsplit >= 1, "attn_decode_fused_slabs: slabs");
+  TORCH_CHECK(out.size(0) == B && slot.numel() == B && attn_len.numel() == B && out.size(1) >= Hq * D,
+              "attn_decode_fused_slabs: batch");
+  TORCH_CHECK(tickets.numel() >= B * Hkv && part.numel() >= B * Hkv * NP * G * (D + 2), "attn_decode_fused_slabs: ws");
+  const bool rot = cos.has_value() && cos->defined();
+  if (rot) {
+    CHECK_F32(*cos); CHECK_F32(*sin);
+    TORCH_CHECK(pos.has_value() && pos->defined(), "attn_decode_fused_slabs: rotary needs pos");
+    CHECK_I32(*pos);
+    TORCH_CHECK(cos->size(-1) == D / 2 && cos->is_contiguous() && sin->is_contiguous(), "attn_decode_fused_slabs: tables");
+  }
+  if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
+  rt_attn_decode_set_qkv_slabs(slabs.data_ptr<float>(), (int)nsplit);
+  check_rc(rt_attn_decode_fused(slabs.data_ptr(), W, kc.data_ptr(), vc.data_ptr(), (int)Smax, slot.data_ptr<int>(),
+                                attn_len.data_ptr<int>(), (const int*)opt_ptr(kv_start),
+                                rot ? pos->data_ptr<int>() : nullptr, rot ? cos->data_ptr<float>() : nullptr,
+                                rot ? sin->data_ptr<float>() : nullptr, (float)sign, (int)window,
+                                part.data_ptr<float>(), (unsigned*)tickets.data_ptr<int>(), (int)NP, (int)PS,
+                                out.data_ptr(), out.stride(0), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
+                                cur_stream()),
+           "attn_decode_fused_slabs");
+  return true;
 }
 
 // batch-1 decode step of one layer: attention (RoPE + append + split-K) and o_proj + residual in
@@ -857,6 +944,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_decode_split", &rt_gemm_set_decode_split, "tuning: fixed split-K of the M<=16 decode kernel (0 = auto)");
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
+  m.def("attn_decode_fused_slabs", &attn_decode_fused_slabs, "decode attention with the qkv split-K reduce fused");
   m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");
   m.def("quant_fp8", &quant_fp8, "per-row absmax e4m3fn quantisation -> (uint8 [R,C], scale fp32 [R])");
   m.def("gemm_big", &gemm_big, "token-parallel GEMM family (NT / NN / TN, LoRA K-extension, split-K, SwiGLU)",
@@ -874,6 +962,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sa") = py::none(), py::arg("wq"), py::arg("sw"), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("norm_eps") = 0.0);
   m.def("norm_fwd", &norm_fwd);
+  m.def("splitk_reduce", &splitk_reduce, "sum of split-K slabs -> bf16");
+  m.def("norm_fwd_slabs", &norm_fwd_slabs, "residual-add + norm whose input is a sum of split-K slabs");
+  m.def("gemm_splitk_raw", &gemm_splitk_raw, "split-K NT GEMM into fp32 slabs (reduce fused into the consumer)");
   m.def("norm_bwd", &norm_bwd);
   m.def("rope_qkv", &rope_qkv);
   m.def("swiglu_fwd", &swiglu_fwd);

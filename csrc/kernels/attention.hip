@@ -473,6 +473,9 @@ struct DecodeFusedArgs {
   bf16_t* o; long ldo;
   int B, Hq, Hkv, NP, PS;
   float scale_log2;
+  // optional: qkv as nsplit fp32 split-K slabs [nsplit][B][ldq] (the qkv GEMM's reduce fused into
+  // the MFMA kernel's prologue); qkv above is then unused
+  const float* qkv_slabs; int qkv_nsplit; long qkv_sstride;
 };
 
 template <int D>
@@ -767,6 +770,7 @@ template <int G>
 __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a) {
   constexpr int D = 128, DS = D / 32, DT = D / 16;
   __shared__ __attribute__((aligned(16))) char vimg[32 * D * 2];  // rows 16..31 stay zero
+  __shared__ __attribute__((aligned(16))) bf16_t qkv_st[(G + 2) * D];  // slab path: reduced q | k | v
   const int lane = threadIdx.x, g = lane >> 4, r16 = lane & 15;
   const int b = blockIdx.x / a.Hkv, hk = blockIdx.x % a.Hkv;
   const int len = a.attn_len[b];
@@ -804,13 +808,35 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a)
   const bool has_new = s_new >= kbeg && s_new < len;
   const bf16_t* qrow = row + (long)min(hk * G + r16, a.Hq - 1) * D;
   const bf16_t* krow = row + (long)(a.Hq + hk) * D;
+  const bf16_t* vrow = row + (long)(a.Hq + a.Hkv + hk) * D;
+  if (a.qkv_slabs) {
+    // split-K slabs of the qkv GEMM: this wave sums its (G + 2) x D slice once (in the order and
+    // with the bf16 rounding of splitk_reduce_kernel) into LDS, and reads q / k / v from there
+    constexpr int NCHK = (G + 2) * (D / 8);
+    for (int ch = lane; ch < NCHK; ch += 64) {
+      const int seg = ch / (D / 8), c8 = ch % (D / 8);
+      const int head = seg < G ? hk * G + seg : (seg == G ? a.Hq + hk : a.Hq + a.Hkv + hk);
+      const float* sp = a.qkv_slabs + (long)b * a.ldq + (long)head * D + c8 * 8;
+      float4 a0 = *(const float4*)sp, a1 = *(const float4*)(sp + 4);
+      for (int q = 1; q < a.qkv_nsplit; ++q) {
+        const float4 b0 = *(const float4*)(sp + q * a.qkv_sstride), b1 = *(const float4*)(sp + q * a.qkv_sstride + 4);
+        a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+        a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+      }
+      const float t8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      *(uint4*)(qkv_st + seg * D + c8 * 8) = pack8(t8);
+    }
+    qrow = qkv_st + min(r16, G - 1) * D;
+    krow = qkv_st + G * D;
+    vrow = qkv_st + (G + 1) * D;
+  }
   uint4 qraw[DS], kraw[DS];
 #pragma unroll
   for (int s2 = 0; s2 < DS; ++s2) {
     qraw[s2] = *(const uint4*)(qrow + (4 * s2 + g) * 8);
     kraw[s2] = *(const uint4*)(krow + (4 * s2 + g) * 8);
   }
-  const uint4 vx = *(const uint4*)(row + (long)(a.Hq + a.Hkv + hk) * D + r16 * 8);
+  const uint4 vx = *(const uint4*)(vrow + r16 * 8);
   float4 cq[2][2], sq[2][2];
   {
     // unconditional (no branch between load batches): without tables read the qkv row
@@ -1671,6 +1697,15 @@ extern "C" int rt_attn_decode_fused_ps(int D, int nk) { return 4 * (64 / (D / 8)
 // keys per lane per chunk (bytes in flight per block); 0 = default 4. Tuning hook.
 static int g_dec_nk = 0;
 extern "C" void rt_attn_decode_set_nk(int nk) { g_dec_nk = nk; }
+// qkv given as split-K slabs for the NEXT rt_attn_decode_fused call (set by the binding)
+static const float* g_dec_qkv_slabs = nullptr;
+static int g_dec_qkv_nsplit = 0;
+extern "C" void rt_attn_decode_set_qkv_slabs(const float* p, int nsplit) { g_dec_qkv_slabs = p; g_dec_qkv_nsplit = nsplit; }
+extern "C" int rt_attn_decode_mfma_ok(int B, int Hq, int Hkv, int D, int NP) {
+  static const int use_mfma = getenv("RT_DECODE_MFMA") ? atoi(getenv("RT_DECODE_MFMA")) : 1;
+  const int G = Hkv ? Hq / Hkv : 0;
+  return use_mfma && NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
+}
 
 extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* vc, int Smax, const int* slot,
                                     const int* attn_len, const int* kv_start, const int* pos, const float* cosT,
@@ -1682,12 +1717,13 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   a.slot = slot; a.attn_len = attn_len; a.kv_start = kv_start; a.pos = pos; a.cosT = cosT; a.sinT = sinT;
   a.sign = sign; a.window = window; a.part = part; a.tickets = tickets; a.o = (bf16_t*)o; a.ldo = ldo;
   a.B = B; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
+  a.qkv_slabs = g_dec_qkv_slabs; a.qkv_nsplit = g_dec_qkv_nsplit; a.qkv_sstride = (long)B * ldq;
+  g_dec_qkv_slabs = nullptr;  // one launch only
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -1;
   // large batch, one partition per (batch, kv head): the MFMA kernel (RT_DECODE_MFMA=0 disables)
-  static const int use_mfma = getenv("RT_DECODE_MFMA") ? atoi(getenv("RT_DECODE_MFMA")) : 1;
-  if (use_mfma && NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) {
+  if (rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
     dim3 mgrid((unsigned)(B * Hkv)), mblock(64);
     switch (G) {
       case 1: hipLaunchKernelGGL(attn_decode_mfma_kernel<1>, mgrid, mblock, 0, stream, a); break;
@@ -1699,6 +1735,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     RT_LAUNCH_CHECK();
     return 0;
   }
+  if (a.qkv_slabs) return -2;  // the slab form exists only in the MFMA kernel (caller reduces first)
   const int nk = g_dec_nk > 0 ? g_dec_nk : 4;  // keys per lane per chunk; PS must be a multiple of the chunk
   if (PS % (4 * (64 / (D / 8)) * nk) != 0) return -1;
   dim3 grid(NP, Hkv, B), block(256);
@@ -1771,6 +1808,7 @@ extern "C" int rt_attn_o_fused(const void* qkv, void* kc, void* vc, int Smax, co
   a.slot = slot; a.attn_len = attn_len; a.kv_start = kv_start; a.pos = pos; a.cosT = cosT; a.sinT = sinT;
   a.sign = sign; a.window = window; a.part = part; a.tickets = nullptr; a.o = nullptr; a.ldo = 0;
   a.B = 1; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
+  a.qkv_slabs = nullptr; a.qkv_nsplit = 0; a.qkv_sstride = 0;
   g.w = (const bf16_t*)w; g.ldw = ldw; g.res = (const bf16_t*)res; g.out = (bf16_t*)out; g.H = H;
   g.sync = sync; g.err = err; g.stamps = g_ao_stamps;
   const int G = Hq / Hkv;

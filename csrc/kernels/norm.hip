@@ -19,7 +19,10 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
                                                        bf16_t* __restrict__ y, bf16_t* __restrict__ h_out,
                                                        float* __restrict__ rstd_out, float* __restrict__ mean_out,
-                                                       int H, float eps) {
+                                                       int H, float eps, const float* __restrict__ xs, int nsplit,
+                                                       long sstride) {
+  // xs != null: x is the bf16-rounded sum of nsplit fp32 split-K slabs (stride sstride floats):
+  // the split-K reduce of the producing GEMM fused into this pass (decode at batch 65..512)
   __shared__ float sbuf[8];
   const long row = blockIdx.x;
   const int nv = H / 8;
@@ -41,7 +44,20 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
   for (int i = 0; i < NV; ++i) {
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nv) {
-      unpack8(*(const uint4*)(xr + c * 8), v[i]);
+      if (xs) {
+        const float* sp = xs + row * H + c * 8;
+        float4 a0 = *(const float4*)sp, a1 = *(const float4*)(sp + 4);
+        for (int q = 1; q < nsplit; ++q) {
+          const float4 b0 = *(const float4*)(sp + q * sstride), b1 = *(const float4*)(sp + q * sstride + 4);
+          a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+          a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+        }
+        const float t8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[i][k] = bf2f(f2bf(t8[k]));  // = the reduce kernel's bf16 output
+      } else {
+        unpack8(*(const uint4*)(xr + c * 8), v[i]);
+      }
       if (res) {
         float r[8];
         unpack8(*(const uint4*)(res + row * H + c * 8), r);
@@ -189,17 +205,20 @@ using namespace rt;
   }
 
 extern "C" int rt_norm_fwd(int layernorm, const void* x, const void* res, const void* w, const void* b, void* y,
-                           void* h_out, float* rstd, float* mean, int T, int H, float eps, hipStream_t stream) {
+                           void* h_out, float* rstd, float* mean, int T, int H, float eps, const float* xs,
+                           int nsplit, hipStream_t stream) {
   if (H % 8 != 0 || H > 256 * 8 * NORM_MAXV) return -1;
   if (T == 0) return 0;
   int threads, nvpt;
   norm_geom(H, threads, nvpt);
   if (layernorm) {
     NORM_DISPATCH(true, norm_fwd_kernel, dim3(T), dim3(threads), 0, stream, (const bf16_t*)x, (const bf16_t*)res,
-                  (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (bf16_t*)h_out, rstd, mean, H, eps)
+                  (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (bf16_t*)h_out, rstd, mean, H, eps, xs, nsplit,
+                  (long)T * H)
   } else {
     NORM_DISPATCH(false, norm_fwd_kernel, dim3(T), dim3(threads), 0, stream, (const bf16_t*)x, (const bf16_t*)res,
-                  (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (bf16_t*)h_out, rstd, mean, H, eps)
+                  (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (bf16_t*)h_out, rstd, mean, H, eps, xs, nsplit,
+                  (long)T * H)
   }
   RT_LAUNCH_CHECK();
   return 0;

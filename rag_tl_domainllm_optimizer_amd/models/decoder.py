@@ -115,18 +115,24 @@ class DecoderLayer(nn.Module):
         f = ops.gemm_decode(h, wgu, act=ops.ACT_SWIGLU, norm_eps=eps, fp8=self._f8("gate_up_folded"))
         return ops.gemm_decode(f, self._w_eff("down_w", "down"), residual=h, fp8=self._f8("down"))
 
-    def attn_in(self, x, residual):
+    def attn_in(self, x, residual, defer: bool = False):
+        """``defer`` (no-grad decode, batch > 64): the qkv GEMM may return unreduced split-K
+        partials (ops.SplitK) for the attention kernel to sum; ``x`` may itself be the previous
+        layer's unreduced down projection (summed inside the norm)."""
         cfg = self.cfg
         if cfg.arch == "opt":
             h, residual = ops.layer_norm(x, self.ln1_w, self.ln1_b, cfg.norm_eps, residual)
         else:
             h, residual = ops.rms_norm(x, self.ln1_w, cfg.norm_eps, residual)
-        qkv = ops.linear(h, self.qkv_w, self._b("qkv_b"), lora=self._lg("qkv"), fp8=self._f8("qkv"))
+        lin = ops.linear_deferred if (defer and cfg.arch != "opt") else ops.linear
+        qkv = lin(h, self.qkv_w, self._b("qkv_b"), lora=self._lg("qkv"), fp8=self._f8("qkv"))
         return qkv, residual
 
-    def mlp(self, a, residual):
+    def mlp(self, a, residual, defer: bool = False):
         cfg = self.cfg
-        a = ops.linear(a, self.o_w, self._b("o_b"), lora=self._lg("o"), fp8=self._f8("o"))
+        defer = defer and cfg.arch != "opt"
+        lin = ops.linear_deferred if defer else ops.linear
+        a = lin(a, self.o_w, self._b("o_b"), lora=self._lg("o"), fp8=self._f8("o"))
         if cfg.arch == "opt":
             h, residual = ops.layer_norm(a, self.ln2_w, self.ln2_b, cfg.norm_eps, residual)
             f = ops.linear(h, self.fc1_w, self.fc1_b, act=cfg.hidden_act, lora=self._lg("fc1"), fp8=self._f8("fc1"))
@@ -135,7 +141,7 @@ class DecoderLayer(nn.Module):
             h, residual = ops.rms_norm(a, self.ln2_w, cfg.norm_eps, residual)
             # act="swiglu": one fused skinny GEMM in no-grad decode, GEMM + SwiGLU kernel otherwise
             f = ops.linear(h, self.gate_up_w, act="swiglu", lora=self._lg("gate_up"), fp8=self._f8("gate_up"))
-            d = ops.linear(f, self.down_w, lora=self._lg("down"), fp8=self._f8("down"))
+            d = lin(f, self.down_w, lora=self._lg("down"), fp8=self._f8("down"))
         return d, residual
 
 
@@ -160,6 +166,8 @@ class CausalLM(nn.Module):
         # (MI355X, Mistral-7B: batch 1 4.15 -> 4.0 ms/token fused; batch 64 5.1 -> 5.5 ms/step)
         self.fused_decode = True
         self.fused_decode_max_batch = 16
+        # decode at batch > 64: leave split-K partials for the consumer kernels to sum
+        self.defer_splitk = True
         # batch 1: attention + o_proj + residual in one launch (ops.decode_step_attention_o). Off by
         # default: measured 26.4 vs 25.0 us per layer for the two-kernel path (docs/DESIGN.md,
         # profiles/kernels_attn_o_fused_rejected.log); RAGTL_ATTN_O=1 turns it on
@@ -291,12 +299,14 @@ class CausalLM(nn.Module):
             y, _ = ops.rms_norm(h, self.norm_w, cfg.norm_eps)
             return y
         residual = None
+        # batch > 64: split-K GEMM partials flow unreduced into the attention prologue and the norms
+        defer = x.is_cuda and x.shape[0] > 64 and self.defer_splitk
         for li, layer in enumerate(self.layers):
-            qkv, residual = layer.attn_in(x, residual)
+            qkv, residual = layer.attn_in(x, residual, defer)
             # one fused kernel: RoPE(q, k_new) + cache append + split-K attention + combine
             o = ops.decode_step_attention(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads, pos, cos, sin,
                                           kv_start, cfg.sliding_window, workspace=workspace)
-            x, residual = layer.mlp(o, residual)
+            x, residual = layer.mlp(o, residual, defer)
         return self.final_norm(x, residual)
 
     # ------------------------------------------------------------------ LoRA

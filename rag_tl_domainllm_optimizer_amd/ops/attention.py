@@ -186,8 +186,21 @@ def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, c
     """One decode step of a layer, fused: rotate q / k_new (if ``cos`` is given), append k_new and
     v_new at cache slot ``slot[b]``, attend over ``attn_len[b]`` keys -> [B, Hq*D].
     ``qkv`` [B, (Hq + 2 Hkv) D] is left unrotated (the fused kernel rotates in registers)."""
+    from .linear import SplitK
+
     B, Hkv, Smax, D = k_cache.shape
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if isinstance(qkv, SplitK):
+        # the qkv GEMM's split-K partials: summed in the MFMA kernel's prologue when it applies
+        if workspace is None or len(workspace) < 3:
+            workspace = decode_workspace(B, Hq, Hkv, D, Smax, k_cache.device)
+        if out is None:
+            out = torch.empty(B, Hq * D, dtype=qkv.dtype, device=qkv.device)
+        if native().attn_decode_fused_slabs(qkv.slabs, qkv.nsplit, k_cache, v_cache, slot, attn_len, kv_start, pos,
+                                            cos, sin, sign, window, scale, Hq, workspace[0], workspace[2],
+                                            workspace[1], out):
+            return out
+        qkv = qkv.reduce()
     if not on_gpu(qkv):
         q = rope_qkv_(qkv.clone(), pos, cos, sin, Hq, Hkv, D, S=1, k_cache=k_cache, v_cache=v_cache,
                       slot_base=slot, sign=sign)

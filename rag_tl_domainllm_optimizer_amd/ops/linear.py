@@ -397,6 +397,46 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
     return y.reshape(*shp[:-1], w.shape[0])
 
 
+class SplitK:
+    """Unreduced split-K partial sums of an NT GEMM, ``slabs`` [nsplit, M, N] fp32: the reduce is
+    left to the consumer (``ops.rms_norm`` with a residual, ``ops.decode_step_attention``), which
+    sums the slabs in its own pass (decode at batch 65..512: no reduce launch, no bf16 round trip)."""
+
+    __slots__ = ("slabs", "nsplit", "M", "N", "dtype", "device")
+
+    def __init__(self, slabs, nsplit, M, N, dtype):
+        self.slabs, self.nsplit, self.M, self.N, self.dtype = slabs, nsplit, M, N, dtype
+        self.device = slabs.device
+
+    @property
+    def shape(self):
+        return torch.Size((self.M, self.N))
+
+    def reduce(self) -> torch.Tensor:
+        out = torch.empty(self.M, self.N, dtype=self.dtype, device=self.device)
+        return native().splitk_reduce(self.slabs, self.nsplit, self.M, self.N, out)
+
+
+def linear_deferred(x: torch.Tensor, w: torch.Tensor, bias=None, lora: Optional[LoRAGroup] = None, fp8=None):
+    """``linear`` for no-grad decode steps that may return a :class:`SplitK` (unreduced) when the
+    plan splits K (bf16 weights, no bias / activation, merged or absent LoRA); else a tensor."""
+    x2 = x.reshape(-1, x.shape[-1])
+    use_lora = lora is not None and lora.enabled
+    if (not on_gpu(x2) or torch.is_grad_enabled() or bias is not None or fp8 is not None or w.dtype != torch.bfloat16
+            or x2.dtype != torch.bfloat16 or (use_lora and not lora.use_merged) or x2.shape[0] <= 64
+            or w.shape[0] % 16 or x2.shape[1] % 8):
+        return linear(x, w, bias, None, lora, fp8)
+    w_eff = lora.merged_weight(w) if use_lora else w
+    M, K = x2.shape
+    N = w_eff.shape[0]
+    s, bn = splitk_plan(M, N, K, 0)
+    if s <= 1:
+        return gemm(x2.contiguous(), w_eff).reshape(*x.shape[:-1], N)
+    slabs = torch.empty(s * M * N, dtype=torch.float32, device=x2.device)
+    native().gemm_splitk_raw(x2.contiguous(), w_eff, s, slabs, bn or 256)
+    return SplitK(slabs, s, M, N, x2.dtype)
+
+
 def gemm_decode(x: torch.Tensor, w: torch.Tensor, act: int = 0, residual=None, norm_eps: float = 0.0, fp8=None):
     """Decode-step GEMM (M <= 64) with the fused prologue/epilogue of the skinny kernels:
     ``C = act(rstd(x) * x w^T) + residual`` where ``rstd`` (``norm_eps > 0``) is the RMS-norm of

@@ -66,6 +66,14 @@ class _NormFn(torch.autograd.Function):
 
 
 def _norm(x, w, b, eps, residual, layernorm):
+    from .linear import SplitK
+
+    if isinstance(x, SplitK):  # the producing GEMM's split-K reduce fused into this pass
+        if residual is None:
+            x = x.reduce()
+        else:
+            return tuple(native().norm_fwd_slabs(layernorm, x.slabs, x.nsplit, x.M, x.N, residual.contiguous(), w, b,
+                                                 eps))
     grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or (residual is not None and residual.requires_grad))
     if not grad:
         xs = x.contiguous()
