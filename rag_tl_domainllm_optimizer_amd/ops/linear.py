@@ -55,9 +55,16 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
     if on_gpu(x):
         M, K = x.shape
         N = w.shape[0]
-        if M <= 64 and residual is None and N % 8 == 0:
+        # 32 <= M <= 64 on narrow weights (qkv / o): the 256x128-tile split-K form beats the ring
+        # kernel by 2-4 us (profiles/gemm_r2_m32_m64_ring_vs_splitk.log); wide / deep weights and
+        # M < 32 stay on the weight-streaming ring / GEMV kernels
+        narrow_split = 32 <= M <= 64 and N <= 8192 and K <= 8192 and N % 16 == 0 and act == 0 and u is None \
+            and not out_f32 and bias is None and residual is None and nsplit == 0
+        if M <= 64 and residual is None and N % 8 == 0 and not narrow_split:
             return native().gemm(x, w, u, ub, bias, act, out_f32, out)
         s, bn = splitk_plan(M, N, K, act)
+        if narrow_split:
+            s, bn = max(s, 2), 128
         if nsplit:
             s = nsplit
         if u is not None or out_f32 or N % 16:

@@ -151,8 +151,8 @@ def test_odd_vocab_generation_gpu():
     torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=0.08)
 
 
-@pytest.mark.parametrize("merged_lora", [False, True])
-def test_batched_decode_deferred_splitk_bitwise(merged_lora):
+@pytest.mark.parametrize("merged_lora,batch", [(False, 160), (True, 160), (False, 100)])
+def test_batched_decode_deferred_splitk_bitwise(merged_lora, batch):
     """Batch > 64 decode with the split-K reduces fused into their consumers (qkv partials summed in
     the MFMA attention prologue, o / down partials summed inside the RMSNorms) == the same decode
     with separate reduce launches, bitwise; greedy generation on the graph path agrees too."""
@@ -171,14 +171,16 @@ def test_batched_decode_deferred_splitk_bitwise(merged_lora):
                     g.refresh()
         m.set_lora_merged(True)
     g = torch.Generator().manual_seed(0)
-    prompts = [torch.randint(3, 512, (int(n),), generator=g).tolist() for n in torch.randint(5, 40, (160,), generator=g)]
+    # batch 160 x 2 kv-heads = 320 pairs: the MFMA attention sums the qkv partials; batch 100 = 200
+    # pairs: the VALU kernel, so the partials are reduced first
+    prompts = [torch.randint(3, 512, (int(n),), generator=g).tolist() for n in torch.randint(5, 40, (batch,), generator=g)]
     p = SamplingParams(max_new_tokens=6, do_sample=False)
     m.defer_splitk = True
-    a = Generator(m, 160, 64, DEV, use_graph=False).generate(prompts, p, pad_id=0, eos_ids=[-1])
+    a = Generator(m, batch, 64, DEV, use_graph=False).generate(prompts, p, pad_id=0, eos_ids=[-1])
     m.defer_splitk = False
-    b = Generator(m, 160, 64, DEV, use_graph=False).generate(prompts, p, pad_id=0, eos_ids=[-1])
+    b = Generator(m, batch, 64, DEV, use_graph=False).generate(prompts, p, pad_id=0, eos_ids=[-1])
     assert torch.equal(a.tokens, b.tokens)
     torch.testing.assert_close(a.logprobs, b.logprobs, rtol=0, atol=0)
     m.defer_splitk = True
-    c = Generator(m, 160, 64, DEV, use_graph=True).generate(prompts, p, pad_id=0, eos_ids=[-1])
+    c = Generator(m, batch, 64, DEV, use_graph=True).generate(prompts, p, pad_id=0, eos_ids=[-1])
     assert torch.equal(a.tokens, c.tokens)

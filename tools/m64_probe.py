@@ -37,7 +37,7 @@ def main():
             ws = [((torch.rand(N, K, device="cuda") - 0.5) / 64).to(torch.bfloat16) for _ in range(4)]  # > MALL
             act = 5 if name == "gate_up" else 0
             slabs = torch.empty(16 * M * N, device="cuda")
-            cases = {"ring": lambda w: C.gemm(x, w, None, None, None, act, False, None)}
+            cases = {"ring": lambda w: C.gemm(x, w, None, None, None, act, False, None)} if M <= 64 else {}
             for s in (1, 2, 4, 5, 8, 16):
                 if act == 5 and s == 1:
                     cases["bn128_s1"] = lambda w: C.gemm_big(x, w, 0, 0, None, None, None, 5, 0, 1, None, None, None, 128)
