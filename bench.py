@@ -61,6 +61,9 @@ def main():
     ap.add_argument("--nprobe", type=int, default=16)
     ap.add_argument("--latency-queries", type=int, default=16)
     ap.add_argument("--skip-latency", action="store_true")
+    ap.add_argument("--vary-docs", action="store_true",
+                    help="1..top-k retrieved docs per query (variable prompt lengths: exercises the varlen "
+                         "packed forwards; RAGTL_PACK=0 for the padded comparison)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--mode", default="ppo", choices=["ppo", "sft", "pipeline"])
@@ -132,6 +135,8 @@ def main():
         qs = [it.query for it in items]
         _, ids = index.search(encoder.encode(qs), args.top_k_docs)
         docs = [[corpus.docs[i] for i in row if i >= 0] for row in ids.tolist()]
+        if args.vary_docs:
+            docs = [d[:rng.randint(1, len(d))] if d else d for d in docs]
         return {"query": qs, "retrieved_docs": docs, "ground_truth": [it.ground_truth for it in items]}
 
     # ---- p50 RAG answer latency (batch 1, retrieve + generate) ----
@@ -196,7 +201,9 @@ def main():
                    "seq_len": args.max_prompt + args.new_tokens, "parallelism": f"dp{di.world}",
                    "new_tokens": args.new_tokens, "lora_r": None if args.full_ft else 16,
                    "full_finetune": bool(args.full_ft), "encoder": args.encoder, "ndocs": args.ndocs,
-                   "index": f"ivf{index.nlist}/nprobe{args.nprobe}", "minibatch": args.minibatch},
+                   "index": f"ivf{index.nlist}/nprobe{args.nprobe}", "minibatch": args.minibatch,
+                   **({"docs_per_query": f"1-{args.top_k_docs}",
+                       "packed": os.environ.get("RAGTL_PACK", "1") != "0"} if args.vary_docs else {})},
         "backend": di.backend or "none",
         "world": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
         "p50_rag_latency_s": lat["p50_s"] if lat else None,

@@ -13,9 +13,11 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from .. import ops
+from ..models.decoder import pack_enabled, packed_index
 
 
 @dataclass
@@ -204,7 +206,13 @@ class Generator:
 
     def _enqueue(self, params, B, S, T, ids, start, eos, eos_list, pad_id, sub, early_stop, t0, ev):
         cfg, dev, MB = self.cfg, self.device, self.max_batch
-        h_last = self.model.prefill(ids, self.kv_start[:B], sub)
+        packed = None
+        n_real = B * S - int(start.sum())
+        if pack_enabled() and n_real < 0.97 * B * S:
+            # varlen prefill: the projection GEMMs run on the real prompt tokens only
+            packed = packed_index(start.numpy(), np.full(B, S), S, dev)
+        h_last = self.model.prefill(ids, self.kv_start[:B], sub, packed=packed) if packed is not None else \
+            self.model.prefill(ids, self.kv_start[:B], sub)
         if hasattr(self.model, "refresh_decode_weights"):
             self.model.refresh_decode_weights()  # merged / folded / fp8 images used by graph replays
         h = torch.zeros(MB, cfg.hidden_size, dtype=h_last.dtype, device=dev)

@@ -6,7 +6,7 @@ import os
 import torch
 
 from .config import PRESETS, ModelConfig, resolve_preset  # noqa: F401
-from .decoder import CausalLM, fast_random_init_  # noqa: F401
+from .decoder import CausalLM, fast_random_init_, pack_enabled, packed_index  # noqa: F401
 from .encoder import SentenceEncoder  # noqa: F401
 from .lora import LoraConfig, attach_lora, load_adapter, merge_lora, save_adapter  # noqa: F401
 from .value_head import ValueHead  # noqa: F401

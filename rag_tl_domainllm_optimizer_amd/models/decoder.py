@@ -17,6 +17,7 @@ import math
 import os
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -226,53 +227,79 @@ class CausalLM(nn.Module):
 
     # ------------------------------------------------------------------ full forward
     def forward(self, input_ids: torch.Tensor, kv_start: Optional[torch.Tensor] = None,
-                gradient_checkpointing: bool = False) -> torch.Tensor:
-        """input_ids [B, S] (left-padded; kv_start[b] = first real token) -> final hidden [B*S, H]."""
+                gradient_checkpointing: bool = False, packed_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """input_ids [B, S] (left-padded; kv_start[b] = first real token) -> final hidden [B*S, H].
+
+        ``packed_idx`` [N] (grid positions b*S + s of the tokens to compute, see ``packed_index``):
+        varlen form — embeddings, norms and every projection GEMM run on the N real tokens only
+        (attention scatters them into the [B, S] grid it tiles); returns [N, H] in that order."""
         cfg = self.cfg
         B, S = input_ids.shape
         dev = input_ids.device
         pos = self.positions(B, S, kv_start, dev)
         cos, sin = self.rope(dev)
         ks = kv_start.to(torch.int32) if kv_start is not None else None
-        x = self.embed_tokens(input_ids.reshape(-1), pos)
+        if packed_idx is not None:
+            x = self.embed_tokens(input_ids.reshape(-1).index_select(0, packed_idx), pos.index_select(0, packed_idx))
+        else:
+            x = self.embed_tokens(input_ids.reshape(-1), pos)
         residual = None
         for layer in self.layers:
             if gradient_checkpointing and torch.is_grad_enabled():
                 x, residual = torch.utils.checkpoint.checkpoint(self._layer_fwd, layer, x, residual, pos, cos, sin,
-                                                                B, S, ks, use_reentrant=False)
+                                                                B, S, ks, packed_idx, use_reentrant=False)
             else:
-                x, residual = self._layer_fwd(layer, x, residual, pos, cos, sin, B, S, ks)
+                x, residual = self._layer_fwd(layer, x, residual, pos, cos, sin, B, S, ks, packed_idx)
         return self.final_norm(x, residual)
 
-    def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks):
+    def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks, packed_idx=None):
         cfg = self.cfg
         qkv, residual = layer.attn_in(x, residual)
-        o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
-                                    cfg.sliding_window, kv_start=ks,
-                                    rope=(pos, cos, sin) if cos is not None else None)
+        rope = (pos, cos, sin) if cos is not None else None
+        if packed_idx is not None:
+            o = ops.flash_attention_packed(qkv, packed_idx, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
+                                           cfg.sliding_window, kv_start=ks, rope=rope)
+        else:
+            o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
+                                        cfg.sliding_window, kv_start=ks, rope=rope)
         return layer.mlp(o, residual)
 
     # ------------------------------------------------------------------ generation
     @torch.no_grad()
-    def prefill(self, input_ids, kv_start, cache) -> torch.Tensor:
+    def prefill(self, input_ids, kv_start, cache, packed=None) -> torch.Tensor:
         """Prompt forward writing K/V into ``cache`` slots [0, S); returns final hidden at the last
-        position of every row [B, H] (rows are left-padded so all end at S-1)."""
+        position of every row [B, H] (rows are left-padded so all end at S-1).
+
+        ``packed`` = (idx [N] device grid positions, off host row offsets) from ``packed_index``:
+        the projection GEMMs skip the left pads; each layer's qkv is scattered into the zeroed
+        [B*S] grid for RoPE + cache append + attention, and the outputs gathered back."""
         cfg = self.cfg
         B, S = input_ids.shape
         dev = input_ids.device
         pos = self.positions(B, S, kv_start, dev)
         cos, sin = self.rope(dev)
         ks = kv_start.to(torch.int32)
-        x = self.embed_tokens(input_ids.reshape(-1), pos)
+        idx = packed[0] if packed is not None else None
+        if idx is not None:
+            x = self.embed_tokens(input_ids.reshape(-1).index_select(0, idx), pos.index_select(0, idx))
+        else:
+            x = self.embed_tokens(input_ids.reshape(-1), pos)
         residual = None
         for li, layer in enumerate(self.layers):
             qkv, residual = layer.attn_in(x, residual)
+            if idx is not None:
+                qkv = qkv.new_zeros(B * S, qkv.shape[1]).index_copy_(0, idx, qkv)
             ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S,
                           k_cache=cache.k[li], v_cache=cache.v[li], slot_base=None)
             o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
                                         cfg.sliding_window, kv_start=ks)
+            if idx is not None:
+                o = o.index_select(0, idx)
             x, residual = layer.mlp(o, residual)
-        last = torch.arange(B, device=dev) * S + (S - 1)
+        if idx is not None:
+            last = torch.from_numpy(packed[1][1:] - 1).to(dev)
+        else:
+            last = torch.arange(B, device=dev) * S + (S - 1)
         return self.final_norm(x[last].contiguous(), residual[last].contiguous())
 
     @torch.no_grad()
@@ -359,6 +386,24 @@ class CausalLM(nn.Module):
         for n, p in self.named_parameters():
             if "lora" not in n:
                 p.requires_grad_(False)
+
+
+def packed_index(lo, hi, L: int, device):
+    """Varlen packing of a [B, L] token grid: row b keeps its positions [lo[b], hi[b]) (host integer
+    arrays). Returns (idx, off): ``idx`` [N] int64 on ``device`` = grid position b*L + s of every
+    kept token in row-major order; ``off`` [B+1] host offsets of each row's first packed token."""
+    lo = np.asarray(lo, dtype=np.int64).reshape(-1)
+    hi = np.maximum(np.asarray(hi, dtype=np.int64).reshape(-1), lo)
+    n = hi - lo
+    off = np.zeros(len(n) + 1, dtype=np.int64)
+    np.cumsum(n, out=off[1:])
+    idx = np.repeat(np.arange(len(n), dtype=np.int64) * L - off[:-1] + lo, n) + np.arange(off[-1], dtype=np.int64)
+    return torch.from_numpy(idx).to(device), off
+
+
+def pack_enabled() -> bool:
+    """Varlen packing of training / scoring / prefill forwards (RAGTL_PACK=0 turns it off)."""
+    return os.environ.get("RAGTL_PACK", "1") != "0"
 
 
 def _normal_(p: torch.Tensor, std: float, g: torch.Generator):

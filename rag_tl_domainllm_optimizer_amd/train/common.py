@@ -5,9 +5,11 @@ from __future__ import annotations
 import math
 from typing import Optional
 
+import numpy as np
 import torch
 
 from .. import ops
+from ..models.decoder import pack_enabled, packed_index
 
 
 def masked_mean(x: torch.Tensor, mask: torch.Tensor, dim=None) -> torch.Tensor:
@@ -32,21 +34,55 @@ def response_mask(lengths: torch.Tensor, T: int) -> torch.Tensor:
 
 def score_sequences(model, prompt_ids: torch.Tensor, start: torch.Tensor, resp: torch.Tensor,
                     resp_len: torch.Tensor, inv_temp: float = 1.0, value_head=None,
-                    gradient_checkpointing: bool = False):
+                    gradient_checkpointing: bool = False, lengths=None):
     """One forward over [prompt | response] -> per-response-token (logp, entropy, values).
 
     The hidden state at position S-1+t produces the distribution of response token t and is also
     the state whose value is V_t (the reference instead runs two forwards and scores a response
-    against a different prompt)."""
+    against a different prompt).
+
+    ``lengths`` = host (start, resp_len) integer arrays: varlen form. Row b needs only the inputs
+    [start_b, S + resp_len_b - 1); when that drops >= 3 % of the [B, S+T] grid the forward runs
+    packed (``CausalLM.forward(packed_idx=...)``: no GEMM / norm work on left or right pads), the
+    lm_head / log-softmax / value head run on the sum(resp_len) scored rows only, and the outputs
+    are scattered back to [B, T] (zeros at masked positions)."""
     B, S = prompt_ids.shape
     T = resp.shape[1]
     seq = torch.cat([prompt_ids, resp], 1)
+    mask = response_mask(resp_len, T)
+    grad = torch.is_grad_enabled()
+    if lengths is not None and pack_enabled():
+        st = np.asarray(lengths[0], dtype=np.int64).reshape(-1)
+        rl = np.asarray(lengths[1], dtype=np.int64).reshape(-1)
+        lo, hi = st, S + np.maximum(rl - 1, 0)
+        n_tok = int(np.maximum(hi - lo, 0).sum())
+        n_sc = int(rl.sum())
+        if n_sc > 0 and n_tok < 0.97 * B * (S + T):
+            dev = prompt_ids.device
+            idx, off = packed_index(lo, hi, S + T, dev)
+            h = model(seq, kv_start=start.to(torch.int32), gradient_checkpointing=gradient_checkpointing,
+                      packed_idx=idx)
+            b = np.repeat(np.arange(B, dtype=np.int64), rl)
+            t = np.arange(n_sc, dtype=np.int64) - np.repeat(np.cumsum(rl) - rl, rl)
+            sel = torch.from_numpy(off[:-1][b] + (S - 1 + t) - lo[b]).to(dev)
+            dst = torch.from_numpy(b * T + t).to(dev)
+            hs = h.index_select(0, sel)
+            tgt = resp.reshape(-1).index_select(0, dst)
+            logits = ops.linear(hs, model.head_weight) if (grad and hs.requires_grad) else \
+                ops.gemm(hs.contiguous(), model.head_weight)
+            lp, ent = ops.token_logprobs(logits, tgt, inv_temp)
+            logp = lp.new_zeros(B * T).index_copy(0, dst, lp).view(B, T)
+            entf = ent.new_zeros(B * T).index_copy(0, dst, ent).view(B, T)
+            values = None
+            if value_head is not None:
+                v = value_head(hs).reshape(-1)
+                values = v.new_zeros(B * T).index_copy(0, dst, v).view(B, T)
+            return logp, entf, values, mask
     h = model(seq, kv_start=start.to(torch.int32), gradient_checkpointing=gradient_checkpointing)
     H = h.shape[-1]
     h = h.view(B, S + T, H)[:, S - 1:S + T - 1].reshape(B * T, H)
-    mask = response_mask(resp_len, T)
     tgt = torch.where(mask, resp, torch.full_like(resp, -100)).reshape(-1)
-    logits = ops.linear(h, model.head_weight) if (torch.is_grad_enabled() and h.requires_grad) else \
+    logits = ops.linear(h, model.head_weight) if (grad and h.requires_grad) else \
         ops.gemm(h.contiguous(), model.head_weight)
     logp, ent = ops.token_logprobs(logits, tgt, inv_temp)
     values = value_head(h).view(B, T) if value_head is not None else None

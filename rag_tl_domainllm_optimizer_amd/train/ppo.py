@@ -127,6 +127,8 @@ class Rollout:
     rewards_tok: Optional[torch.Tensor] = None
     n_tokens: int = 0
     kl_ref: float = 0.0
+    # host copies of (start, resp_len) for the varlen (packed) scoring forwards
+    host_lengths: Optional[tuple] = None
 
 
 class PPOTrainer:
@@ -254,7 +256,10 @@ class PPOTrainer:
                      cat_pad([o.tokens for o in outs], T, False, pad), torch.cat([o.lengths for o in outs], 0),
                      cat_pad([o.logprobs for o in outs], T, False, 0.0),
                      cat_pad([o.values for o in outs], T, False, 0.0), None, {}, [], list(queries))
-        ro.n_tokens = int(ro.resp_len.sum())
+        # generation has completed (result() waited): one small D2H copy of the response lengths
+        rl_host = ro.resp_len.cpu().numpy()
+        ro.host_lengths = (np.array([S - len(p) for p in prompts], dtype=np.int64), rl_host.astype(np.int64))
+        ro.n_tokens = int(rl_host.sum())
         ro._outs, ro._pending, ro._batch = outs, pending, (queries, docs, gts)
         if not pending:
             # generation is complete here (result() waited): one D2H copy per output while the GPU
@@ -315,10 +320,12 @@ class PPOTrainer:
             try:
                 ref_lp = []
                 mb = max(c.minibatch_size, c.ref_minibatch_size)  # no-grad: larger GEMMs, no saved activations
+                hl = ro.host_lengths
                 for s in range(0, ro.resp.shape[0], mb):
                     lp, _, _, _ = score_sequences(ref_model, ro.prompt_ids[s:s + mb], ro.start[s:s + mb],
                                                   ro.resp[s:s + mb], ro.resp_len[s:s + mb],
-                                                  1.0 / c.temperature)
+                                                  1.0 / c.temperature,
+                                                  lengths=(hl[0][s:s + mb], hl[1][s:s + mb]) if hl else None)
                     ref_lp.append(lp)
                 ro.ref_logp = torch.cat(ref_lp, 0)
             finally:
@@ -347,11 +354,14 @@ class PPOTrainer:
         with self.timer.phase("update"):
             for _ in range(c.ppo_epochs):
                 perm = torch.randperm(B, generator=g).tolist()
+                hl = ro.host_lengths
                 for s in range(0, B, c.minibatch_size):
-                    idx = torch.tensor(perm[s:s + c.minibatch_size], device=self.device)
+                    rows = perm[s:s + c.minibatch_size]
+                    idx = torch.tensor(rows, device=self.device)
                     lp, ent, vals, mask = score_sequences(self.policy, ro.prompt_ids[idx], ro.start[idx],
                                                           ro.resp[idx], ro.resp_len[idx], inv_t, self.value_head,
-                                                          c.gradient_checkpointing)
+                                                          c.gradient_checkpointing,
+                                                          lengths=(hl[0][rows], hl[1][rows]) if hl else None)
                     # fused token-level objective (clipped surrogate + value + entropy) and its
                     # gradient in one kernel on the GPU (ops.ppo_loss; eager oracle on CPU)
                     loss, st = ops.ppo_loss(lp, vals, ent, ro.old_logp[idx], ro.adv[idx], ro.returns[idx], mask,

@@ -13,9 +13,11 @@ import time
 from dataclasses import asdict, dataclass
 from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from .. import ops
+from ..models.decoder import pack_enabled, packed_index
 from ..parallel import GradSync, info as dist_info, reduce_metrics
 from ..utils import MetricsSink, maybe_inject_fault
 from .common import lr_at
@@ -93,10 +95,22 @@ class SFTTrainer:
         return ids.to(self.device), start.to(self.device), tgt.to(self.device)
 
     def loss(self, ids, start, tgt):
-        h = self.model(ids, kv_start=start, gradient_checkpointing=self.cfg.gradient_checkpointing)
         flat_t = tgt.reshape(-1)
         rows = (flat_t >= 0).nonzero().squeeze(-1)
-        hs = h[rows]
+        B, S = ids.shape
+        st = start.cpu().numpy().astype(np.int64) if pack_enabled() else None
+        if st is not None and B * (S - 1) - int(st.sum()) < 0.97 * B * S:
+            # varlen: row b's inputs are [start_b, S - 1) (the last token predicts nothing); the
+            # GEMMs skip the left pads, the scored rows are looked up in the packed order
+            idx, _ = packed_index(st, np.full(B, S - 1), S, ids.device)
+            h = self.model(ids, kv_start=start, gradient_checkpointing=self.cfg.gradient_checkpointing,
+                           packed_idx=idx)
+            inv = torch.full((B * S,), -1, dtype=torch.long, device=ids.device)
+            inv.index_copy_(0, idx, torch.arange(idx.numel(), device=ids.device))
+            hs = h.index_select(0, inv.index_select(0, rows))
+        else:
+            h = self.model(ids, kv_start=start, gradient_checkpointing=self.cfg.gradient_checkpointing)
+            hs = h[rows]
         logits = ops.linear(hs, self.model.head_weight)
         lp, _ = ops.token_logprobs(logits, flat_t[rows], 1.0)
         return -lp.mean(), int(rows.numel())
