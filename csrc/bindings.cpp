@@ -112,9 +112,17 @@ const void* opt_ptr(const optional<Tensor>& t) { return t.has_value() && t->defi
 struct DecodeWS {
   Tensor slabs, tickets;
 };
+static std::mutex g_ws_mu;
+static std::unordered_map<uint64_t, DecodeWS*>* g_ws_map = new std::unordered_map<uint64_t, DecodeWS*>();
+std::vector<Tensor> decode_ws_all() {
+  std::lock_guard<std::mutex> g(g_ws_mu);
+  std::vector<Tensor> v;
+  for (auto& kv : *g_ws_map) v.push_back(kv.second->tickets);
+  return v;
+}
 DecodeWS& decode_ws(const Tensor& like, hipStream_t st) {
-  static std::mutex mu;
-  static auto* map = new std::unordered_map<uint64_t, DecodeWS*>();
+  auto& mu = g_ws_mu;
+  auto* map = g_ws_map;
   std::lock_guard<std::mutex> g(mu);
   const uint64_t key = (uint64_t)like.get_device() << 56 ^ (uint64_t)(uintptr_t)st;
   auto it = map->find(key);
@@ -124,6 +132,14 @@ DecodeWS& decode_ws(const Tensor& like, hipStream_t st) {
   w->tickets = at::zeros({RT_SPLITK_TICKETS}, like.options().dtype(at::kInt));
   (*map)[key] = w;
   return *w;
+}
+
+// diagnostics: per decode workspace, the number of arrival tickets not back at zero (every
+// split-K launch leaves them at zero; a non-zero count means two launches raced on one workspace)
+std::vector<int64_t> decode_ws_dirty_tickets() {
+  std::vector<int64_t> out;
+  for (auto& t : decode_ws_all()) out.push_back((t.ne(0)).sum().item<int64_t>());
+  return out;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -936,6 +952,7 @@ void decode_update(const Tensor& tok, Tensor out_tokens, const optional<Tensor>&
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels + native host runtime";
+  m.def("decode_ws_dirty_tickets", &decode_ws_dirty_tickets, "per decode workspace: tickets not at zero");
   m.def("gemm", &gemm, "bf16 MFMA GEMM C = act(rstd(A) A W^T + U UB^T + bias) + R", py::arg("a"), py::arg("w"),
         py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out_f32") = false, py::arg("out") = py::none(), py::arg("residual") = py::none(),

@@ -260,6 +260,11 @@ class Generator:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._step(params, eos, pad_id)
+        # the graph reads the EOS id list through this tensor's address: keep it alive for as long
+        # as the graph is replayed (replays are keyed on the same EOS values). A per-call tensor
+        # freed after the capturing call left later replays reading a recycled block, so their EOS
+        # test compared against whatever the allocator had put there.
+        self._graph_eos = eos
         for t, v in zip(self._state(), saved):
             t.copy_(v)
         torch.cuda.synchronize()

@@ -238,3 +238,26 @@ def test_varlen_packed_scoring_and_prefill_gpu(monkeypatch):
         toks.append(out.tokens.cpu())
     agree = float((toks[0] == toks[1]).float().mean())
     assert agree >= 0.9, (agree, toks)
+
+
+def test_graph_replay_eos_after_allocator_churn():
+    """Replays of the captured decode graph keep testing the EOS ids they were captured with: the
+    second generation on one Generator stops at EOS even after the allocator has recycled the
+    first call's small blocks (the graph once read a freed per-call EOS tensor)."""
+    cfg = PRESETS["tiny-llama"]
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
+    gen = Generator(m, max_batch=2, max_seq=64, device=DEV)
+    prompts = [[5, 9, 33, 41, 7], [12, 300, 4, 8]]
+    ref = gen.generate(prompts, SamplingParams(max_new_tokens=12, do_sample=False), pad_id=0, eos_ids=[-7])
+    eos = int(ref.tokens[0, 3])
+    first = [t for t in range(4) if int(ref.tokens[0, t]) == eos][0] + 1
+    lens = []
+    for _ in range(3):
+        out = gen.generate(prompts, SamplingParams(max_new_tokens=12, do_sample=False), pad_id=0, eos_ids=[eos])
+        lens.append(int(out.lengths[0]))
+        assert out.tokens[0, :first].tolist() == ref.tokens[0, :first].tolist()
+        # churn: small device blocks of the EOS tensor's size, holding other ids
+        junk = [torch.full((1,), 123456 + i, dtype=torch.long, device=DEV) for i in range(64)]
+        torch.cuda.synchronize()
+        del junk
+    assert lens == [first] * 3, (lens, first)
