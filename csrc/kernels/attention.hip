@@ -85,7 +85,7 @@ __device__ __forceinline__ int v_off(int r, int c) {
 // forward
 // ---------------------------------------------------------------------------------------------
 template <int D>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fwd_kernel(AttnArgs a) {
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TILE_BYTES = 64 * D * 2;
   constexpr int OROW = D + 8;  // O staging row stride (elements)
@@ -1298,7 +1298,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 }
 
 template <int D, bool DQ>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TB = 64 * D * 2;
   // LDS: K tile (block keys) | Q tile | dO tile | dS tile [64 q][64 keys] | lse[64] | delta[64]
