@@ -18,6 +18,7 @@ import torch
 
 from .. import ops
 from ..models.decoder import pack_enabled, packed_index
+from ..runtime import GraphRunner
 
 
 @dataclass
@@ -96,8 +97,7 @@ class Generator:
         self.sampled_lp = torch.zeros(B, dtype=torch.float32, device=dev)
         self.values = torch.zeros(B, dtype=torch.float32, device=dev)
         self.out_tokens = None
-        self.graph = None
-        self._graph_key = None
+        self.runner = GraphRunner()  # captured decode step (runtime.GraphRunner, shared graph pool)
 
     # ------------------------------------------------------------------ one decode step (device only)
     def _step(self, params: SamplingParams, eos_ids: torch.Tensor, pad_id: int):
@@ -186,7 +186,7 @@ class Generator:
             self.out_tokens = torch.full((MB, T), pad_id, dtype=torch.long, device=dev)
             self.out_logp = torch.zeros(MB, T, dtype=torch.float32, device=dev)
             self.out_values = torch.zeros(MB, T, dtype=torch.float32, device=dev)
-            self.graph = None
+            self.runner.reset()
         else:
             self.out_tokens.fill_(pad_id)
             self.out_logp.zero_()
@@ -227,14 +227,15 @@ class Generator:
         steps = T - 1
         if steps > 0:
             if self.use_graph:
-                if self.graph is None or self._graph_key != key:
-                    self._capture(params, eos, pad_id)
-                    self._graph_key = key
+                if self.runner.needs(key):
+                    # the EOS tensor is created per call: the runner keeps the captured one alive
+                    self.runner.capture(lambda: self._step(params, eos, pad_id), key, keep=(eos,),
+                                        restore=self._state())
                 done = 0
                 while done < steps:
                     n = min(self.sync_every, steps - done) if early_stop else steps - done
                     for _ in range(n):
-                        self.graph.replay()
+                        self.runner.replay()
                     done += n
                     if early_stop and done < steps and int(self.active.sum().item()) == 0:
                         break
@@ -246,29 +247,6 @@ class Generator:
         if ev:
             ev[2].record()
         return _Pending(self, B, ids, start, t0, ev)
-
-    def _capture(self, params, eos, pad_id):
-        # snapshot the state the warm-up step mutates, then restore it after capture
-        saved = [t.clone() for t in self._state()]
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            self._step(params, eos, pad_id)  # warm-up (allocations, lazy init)
-        torch.cuda.current_stream().wait_stream(s)
-        for t, v in zip(self._state(), saved):
-            t.copy_(v)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._step(params, eos, pad_id)
-        # the graph reads the EOS id list through this tensor's address: keep it alive for as long
-        # as the graph is replayed (replays are keyed on the same EOS values). A per-call tensor
-        # freed after the capturing call left later replays reading a recycled block, so their EOS
-        # test compared against whatever the allocator had put there.
-        self._graph_eos = eos
-        for t, v in zip(self._state(), saved):
-            t.copy_(v)
-        torch.cuda.synchronize()
-        self.graph = g
 
     def _state(self):
         return [self.tok_in, self.kv_len, self.pos, self.attn_len, self.active, self.gen_len, self.step,

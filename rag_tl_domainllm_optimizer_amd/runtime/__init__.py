@@ -103,3 +103,83 @@ class StreamPair:
     def join(self):
         if self.enabled:
             torch.cuda.current_stream().wait_stream(self.side)
+
+
+# ---------------------------------------------------------------------------------------------
+# hipGraph capture / replay
+# ---------------------------------------------------------------------------------------------
+_GRAPH_POOL = {}
+
+
+def graph_pool(device=None):
+    """One graph memory pool per device, shared by every ``GraphRunner`` of the process: the
+    rollout decode graph (batch 256) and the RAG-answer decode graph (batch 1) then draw their
+    captured intermediates from one reservation instead of one each. Graphs of a shared pool must
+    not replay concurrently (they are replayed from one stream here)."""
+    dev = torch.device(device or "cuda")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _GRAPH_POOL:
+        handle = torch.cuda.graph_pool_handle()
+        # a pool lives while some graph captured into it lives: an anchor graph (one tiny kernel)
+        # keeps it valid after every generator that used it has been freed
+        with torch.cuda.device(idx):
+            x = torch.zeros(1, device=f"cuda:{idx}")
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                x.add_(1)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=handle):
+                x.add_(1)
+        _GRAPH_POOL[idx] = (handle, g, x)
+    return _GRAPH_POOL[idx][0]
+
+
+class GraphRunner:
+    """Capture a device-only step once as a hipGraph and replay it (SURVEY T1 ``GraphRunner``).
+
+    ``capture(fn, key, keep, restore)``:
+      * runs ``fn`` once eagerly on a side stream first, so lazy allocations (workspaces, folded
+        weights, library handles) happen outside the capture;
+      * snapshots the tensors in ``restore`` before that warm-up and restores them after the
+        warm-up and after the capture (a step that mutates device state must not advance it);
+      * captures ``fn`` into a graph on ``pool`` (default: the process-wide ``graph_pool``);
+      * keeps a reference to every tensor in ``keep``: a graph reads its inputs through the
+        addresses it captured, so a tensor created per call (e.g. an EOS-id list) must live as long
+        as the graph, not as long as the call that captured it.
+    ``replay()`` launches the graph; ``needs(key)`` says whether a capture with ``key`` is current.
+    """
+
+    def __init__(self, pool=None):
+        self.pool = pool
+        self.graph = None
+        self.key = None
+        self._keep = ()
+
+    def needs(self, key) -> bool:
+        return self.graph is None or self.key != key
+
+    def reset(self):
+        self.graph, self.key, self._keep = None, None, ()
+
+    def capture(self, fn, key=None, keep=(), restore=()):
+        saved = [t.clone() for t in restore]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fn()  # warm-up: lazy allocations and caches outside the capture
+        torch.cuda.current_stream().wait_stream(s)
+        for t, v in zip(restore, saved):
+            t.copy_(v)
+        g = torch.cuda.CUDAGraph()
+        pool = self.pool if self.pool is not None else graph_pool()
+        with torch.cuda.graph(g, pool=pool):
+            fn()
+        for t, v in zip(restore, saved):
+            t.copy_(v)
+        torch.cuda.synchronize()
+        self.graph, self.key, self._keep = g, key, tuple(keep)
+
+    def replay(self):
+        self.graph.replay()

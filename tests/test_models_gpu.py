@@ -261,3 +261,41 @@ def test_graph_replay_eos_after_allocator_churn():
         torch.cuda.synchronize()
         del junk
     assert lens == [first] * 3, (lens, first)
+
+
+def test_graph_runner_keep_restore_and_shared_pool():
+    """runtime.GraphRunner: the warm-up / capture do not advance restored state, replays read the
+    kept per-call tensor, a key change recaptures, and two runners share the process graph pool."""
+    from rag_tl_domainllm_optimizer_amd import runtime
+
+    acc = torch.zeros(4, device=DEV)
+    step = torch.zeros(1, dtype=torch.long, device=DEV)
+
+    def make(delta):
+        d = torch.full((4,), float(delta), device=DEV)  # per-call input, captured by address
+
+        def fn():
+            acc.add_(d * 2.0)  # intermediate from the graph pool, then accumulate
+            step.add_(1)
+        return fn, d
+
+    r1, r2 = runtime.GraphRunner(), runtime.GraphRunner()
+    fn, d = make(1.5)
+    assert r1.needs("a")
+    r1.capture(fn, "a", keep=(d,), restore=[acc, step])
+    del d, fn
+    junk = [torch.full((4,), 9.0, device=DEV) for _ in range(32)]  # recycle small blocks
+    del junk
+    assert float(acc.sum()) == 0.0 and int(step) == 0  # warm-up and capture restored the state
+    for _ in range(3):
+        r1.replay()
+    torch.cuda.synchronize()
+    assert torch.allclose(acc, torch.full((4,), 9.0, device=DEV)) and int(step) == 3
+    fn2, d2 = make(-1.0)
+    r2.capture(fn2, "b", keep=(d2,), restore=[acc, step])
+    r2.replay()
+    r1.replay()
+    torch.cuda.synchronize()
+    assert torch.allclose(acc, torch.full((4,), 10.0, device=DEV)) and int(step) == 5
+    assert not r1.needs("a") and r1.needs("c")
+    assert runtime.graph_pool() == runtime.graph_pool(DEV)
