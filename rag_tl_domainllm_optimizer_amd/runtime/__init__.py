@@ -85,7 +85,15 @@ class StreamPair:
     def __init__(self, device=None):
         self.enabled = torch.cuda.is_available() and (device is None or torch.device(device).type == "cuda")
         self.main = torch.cuda.current_stream() if self.enabled else None
-        self.side = torch.cuda.Stream() if self.enabled else None
+        # the side stream is created at the highest priority: HIP maps streams onto a few hardware
+        # queues (GPU_MAX_HW_QUEUES), round-robin by creation order among streams of one priority,
+        # so a normal-priority side stream can land on the main stream's queue and then waits
+        # behind every kernel queued there (no overlap at all); high-priority streams get queues
+        # of their own, and the small reward / scoring kernels are the latency-critical ones
+        self.side = None
+        if self.enabled:
+            hi = torch.cuda.Stream.priority_range()[1] if hasattr(torch.cuda.Stream, "priority_range") else -1
+            self.side = torch.cuda.Stream(priority=min(hi, 0))
 
     @contextlib.contextmanager
     def on_side(self, wait: bool = False):
