@@ -299,3 +299,29 @@ def test_graph_runner_keep_restore_and_shared_pool():
     assert torch.allclose(acc, torch.full((4,), 10.0, device=DEV)) and int(step) == 5
     assert not r1.needs("a") and r1.needs("c")
     assert runtime.graph_pool() == runtime.graph_pool(DEV)
+
+
+def test_split_k_tickets_return_to_zero_after_generation():
+    """Race detector for the in-launch split-K hand-off: every arrival ticket of every per-stream
+    decode workspace is back at zero after graph-replayed generations (a launch that raced another
+    on a shared workspace, or lost an arrival, leaves a non-zero count behind)."""
+    from rag_tl_domainllm_optimizer_amd.ops import native
+
+    cfg = PRESETS["tiny-llama"]
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
+    for B in (1, 4, 40):
+        gen = Generator(m, max_batch=B, max_seq=96, device=DEV)
+        prompts = [[5 + i, 9, 33, 41, 7][: 3 + i % 3] for i in range(B)]
+        for _ in range(2):
+            gen.generate(prompts, SamplingParams(max_new_tokens=10, temperature=0.9), pad_id=0, eos_ids=[-1])
+    torch.cuda.synchronize()
+    dirty = native().decode_ws_dirty_tickets()
+    assert len(dirty) >= 1 and all(d == 0 for d in dirty), dirty
+
+
+def test_side_stream_is_high_priority():
+    from rag_tl_domainllm_optimizer_amd.runtime import StreamPair
+
+    sp = StreamPair(DEV)
+    lo, hi = torch.cuda.Stream.priority_range()
+    assert sp.side.priority == hi and hi < lo
