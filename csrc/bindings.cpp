@@ -81,7 +81,7 @@ void rt_attn_o_set_stamps(long long* p);
 int rt_ppo_loss(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
                 const float*, long, float, float, float, float, float*, float*, float*, float*, hipStream_t);
 int rt_decode_update(const long*, long*, int, float*, const float*, float*, const float*, uint8_t*, int*, int*, long*,
-                     int*, int64_t*, int64_t*, int, const long*, int, long, hipStream_t);
+                     int*, int64_t*, int64_t*, int, const long*, int, long, int*, const int*, hipStream_t);
 }
 
 namespace {
@@ -935,8 +935,15 @@ std::vector<Tensor> ppo_loss(const Tensor& lp, const Tensor& old, const Tensor& 
 void decode_update(const Tensor& tok, Tensor out_tokens, const optional<Tensor>& out_logp,
                    const optional<Tensor>& logp, const optional<Tensor>& out_values, const optional<Tensor>& values,
                    Tensor active, Tensor kv_len, Tensor pos, Tensor next_input, Tensor gen_len, Tensor step,
-                   Tensor rng_offset, const Tensor& eos_ids, int64_t pad_id) {
+                   Tensor rng_offset, const Tensor& eos_ids, int64_t pad_id, const optional<Tensor>& attn_len,
+                   const optional<Tensor>& kv_start) {
   CHECK_I64(tok); CHECK_I64(out_tokens); CHECK_I32(kv_len); CHECK_I32(pos); CHECK_I64(next_input); CHECK_I32(gen_len);
+  const bool al = attn_len.has_value() && attn_len->defined();
+  if (al) {
+    CHECK_I32(*attn_len);
+    TORCH_CHECK(attn_len->numel() >= tok.numel(), "decode_update: attn_len");
+  }
+  if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
   CHECK_I64(step); CHECK_I64(rng_offset); CHECK_I64(eos_ids);
   TORCH_CHECK(active.scalar_type() == at::kByte || active.scalar_type() == at::kBool);
   check_rc(rt_decode_update((const long*)tok.data_ptr(), (long*)out_tokens.data_ptr(), (int)out_tokens.size(1),
@@ -944,7 +951,8 @@ void decode_update(const Tensor& tok, Tensor out_tokens, const optional<Tensor>&
                             (const float*)opt_ptr(values), (uint8_t*)active.data_ptr(), kv_len.data_ptr<int>(),
                             pos.data_ptr<int>(), (long*)next_input.data_ptr(), gen_len.data_ptr<int>(),
                             (int64_t*)step.data_ptr(), (int64_t*)rng_offset.data_ptr(), (int)tok.numel(),
-                            (const long*)eos_ids.data_ptr(), (int)eos_ids.numel(), (long)pad_id, cur_stream()),
+                            (const long*)eos_ids.data_ptr(), (int)eos_ids.numel(), (long)pad_id,
+                            al ? attn_len->data_ptr<int>() : nullptr, (const int*)opt_ptr(kv_start), cur_stream()),
            "decode_update");
 }
 

@@ -102,7 +102,8 @@ __global__ void decode_update_kernel(const long* __restrict__ tok, long* __restr
                                      uint8_t* __restrict__ active, int* __restrict__ kv_len, int* __restrict__ pos,
                                      long* __restrict__ next_input, int* __restrict__ gen_len,
                                      int64_t* __restrict__ step, int64_t* __restrict__ rng_offset, int B,
-                                     const long* __restrict__ eos_ids, int n_eos, long pad_id) {
+                                     const long* __restrict__ eos_ids, int n_eos, long pad_id,
+                                     int* __restrict__ attn_len, const int* __restrict__ kv_start) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t s = *step;
   if (b < B) {
@@ -121,6 +122,13 @@ __global__ void decode_update_kernel(const long* __restrict__ tok, long* __restr
       next_input[b] = t;
     } else {
       next_input[b] = pad_id;
+    }
+    // the next step's attention length and rotary position (kept here, not as two extra
+    // elementwise launches at the head of every decode step)
+    if (attn_len) {
+      const int kl = kv_len[b];
+      attn_len[b] = kl + 1;
+      pos[b] = kl - (kv_start ? kv_start[b] : 0);
     }
   }
   __syncthreads();
@@ -260,11 +268,12 @@ extern "C" int rt_ppo_advantages(const float* old_lp, const float* ref_lp, const
 extern "C" int rt_decode_update(const long* tok, long* out_tokens, int max_new, float* out_logp, const float* logp,
                                 float* out_values, const float* values, uint8_t* active, int* kv_len, int* pos,
                                 long* next_input, int* gen_len, int64_t* step, int64_t* rng_offset, int B,
-                                const long* eos_ids, int n_eos, long pad_id, hipStream_t stream) {
+                                const long* eos_ids, int n_eos, long pad_id, int* attn_len, const int* kv_start,
+                                hipStream_t stream) {
   if (B > 1024) return -1;
   hipLaunchKernelGGL(decode_update_kernel, dim3(1), dim3(((B + 63) / 64) * 64), 0, stream, tok, out_tokens, max_new,
                      out_logp, logp, out_values, values, active, kv_len, pos, next_input, gen_len, step, rng_offset, B,
-                     eos_ids, n_eos, pad_id);
+                     eos_ids, n_eos, pad_id, attn_len, kv_start);
   RT_LAUNCH_CHECK();
   return 0;
 }

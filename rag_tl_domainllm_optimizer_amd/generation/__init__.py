@@ -101,8 +101,8 @@ class Generator:
 
     # ------------------------------------------------------------------ one decode step (device only)
     def _step(self, params: SamplingParams, eos_ids: torch.Tensor, pad_id: int):
-        torch.add(self.kv_len, 1, out=self.attn_len)
-        torch.sub(self.kv_len, self.kv_start, out=self.pos)
+        # attn_len = kv_len + 1 and pos = kv_len - kv_start were set by the previous bookkeeping
+        # (decode_update on the GPU, _update_cpu on the CPU) — no elementwise launches here
         h = self.model.decode(self.tok_in, self.pos, self.kv_len, self.attn_len, self.kv_start, self.cache,
                               self.workspace)
         self._emit(h, params, eos_ids, pad_id)
@@ -118,7 +118,7 @@ class Generator:
                                        self.out_values if self.value_head is not None else None,
                                        self.values if self.value_head is not None else None, self.active,
                                        self.kv_len, self.pos, self.tok_in, self.gen_len, self.step, self.rng_offset,
-                                       eos_ids, pad_id)
+                                       eos_ids, pad_id, self.attn_len, self.kv_start)
         else:
             self._update_cpu(eos_ids, pad_id)
 
@@ -139,6 +139,8 @@ class Generator:
             self.active[act & fin] = 0
         self.step += 1
         self.rng_offset += 1
+        torch.add(self.kv_len, 1, out=self.attn_len)
+        torch.sub(self.kv_len, self.kv_start, out=self.pos)
 
     # ------------------------------------------------------------------ public
     @torch.no_grad()
