@@ -88,10 +88,13 @@ class RagPipeline:
         return out
 
     def latency_stats(self, queries: Sequence[str], warmup: int = 2) -> dict:
+        """p50 / p90 of single-query answers over ``queries[warmup:]``; the first ``warmup`` queries
+        only warm up (graph capture, workspaces) and are not measured."""
         for q in queries[:warmup]:
             self.answer([q])
+        measured = queries[warmup:] if len(queries) > warmup else queries
         lat, toks, stages = [], [], {}
-        for q in queries:
+        for q in measured:
             a = self.answer([q])[0]
             lat.append(a.timings["total_s"])
             toks.append(a.timings["new_tokens"])
