@@ -18,10 +18,12 @@
 
 extern "C" {
 int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
-               long, int, int, int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
+               long, int, int, int, int, int, float*, unsigned*, const void*, long, float, int, hipStream_t);
+int rt_shuffle_decode_weight(const void*, void*, long, long, hipStream_t);
 void rt_gemm_set_variant(int);
 void rt_gemm_set_m64_split(int);
 void rt_gemm_set_decode_split(int);
+void rt_gemm_set_decode_depth(int);
 int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, long, const void*, long, int,
                 const void*, void*, long, void*, long, const void*, long, int, int, int, int, int, int, const void*,
                 int, hipStream_t);
@@ -145,8 +147,11 @@ std::vector<int64_t> decode_ws_dirty_tickets() {
 // ---------------------------------------------------------------------------------------------
 Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const optional<Tensor>& ub,
             const optional<Tensor>& bias, int64_t act, bool out_f32, optional<Tensor> out,
-            const optional<Tensor>& residual, double norm_eps) {
+            const optional<Tensor>& residual, double norm_eps, bool w_shuffled) {
   CHECK_CUDA(a); CHECK_CUDA(w); CHECK_BF16(a); CHECK_BF16(w); CHECK_ROWS(a); CHECK_ROWS(w);
+  if (w_shuffled)
+    TORCH_CHECK(a.size(0) <= 64 && w.size(0) % 16 == 0 && w.is_contiguous(),
+                "gemm: a shuffled decode weight needs M <= 64, N % 16 == 0 and a contiguous image");
   CHECK_ALIGN16(a); CHECK_ALIGN16(w);
   const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "gemm: K mismatch ", w.size(1), " vs ", K);
@@ -198,9 +203,24 @@ Tensor gemm(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const o
   check_rc(rt_gemm_nt(a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), opt_ptr(u), Rp ? u->stride(0) : 0,
                       opt_ptr(ub), Rp ? ub->stride(0) : 0, Rp, opt_ptr(bias), c.data_ptr(), c.stride(0), (int)M,
                       (int)N, (int)K, (int)act, out_f32 ? 1 : 0, slabs, tickets,
-                      has_res ? residual->data_ptr() : nullptr, has_res ? residual->stride(0) : 0, (float)norm_eps, st),
+                      has_res ? residual->data_ptr() : nullptr, has_res ? residual->stride(0) : 0, (float)norm_eps,
+                      w_shuffled ? 1 : 0, st),
            "gemm");
   return c;
+}
+
+// W [N, K] -> the decode kernel's tile-ordered image (same shape, permuted content; gemm(...,
+// w_shuffled=True) reads it). Written into `out` when given (in-place refresh of a captured buffer).
+Tensor shuffle_decode_weight(const Tensor& w, optional<Tensor> out) {
+  CHECK_CUDA(w); CHECK_BF16(w);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "shuffle_decode_weight: contiguous [N, K] weight expected");
+  const int64_t N = w.size(0), K = w.size(1);
+  TORCH_CHECK(N % 16 == 0 && K % 64 == 0, "shuffle_decode_weight: needs N % 16 == 0 and K % 64 == 0");
+  Tensor o = (out.has_value() && out->defined()) ? *out : at::empty_like(w);
+  TORCH_CHECK(o.sizes() == w.sizes() && o.is_contiguous() && o.scalar_type() == w.scalar_type(), "shuffle_decode_weight: bad out");
+  TORCH_CHECK(o.data_ptr() != w.data_ptr(), "shuffle_decode_weight: out must not alias w");
+  check_rc(rt_shuffle_decode_weight(w.data_ptr(), o.data_ptr(), N, K, cur_stream()), "shuffle_decode_weight");
+  return o;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -964,9 +984,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, "bf16 MFMA GEMM C = act(rstd(A) A W^T + U UB^T + bias) + R", py::arg("a"), py::arg("w"),
         py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out_f32") = false, py::arg("out") = py::none(), py::arg("residual") = py::none(),
-        py::arg("norm_eps") = 0.0);
+        py::arg("norm_eps") = 0.0, py::arg("w_shuffled") = false);
+  m.def("shuffle_decode_weight", &shuffle_decode_weight, "W [N, K] -> tile-ordered decode image (gemm w_shuffled=True)",
+        py::arg("w"), py::arg("out") = py::none());
   m.def("gemm_set_m64_split", &rt_gemm_set_m64_split, "tuning: fixed split-K of the M<=64 ring kernel (0 = auto)");
   m.def("gemm_set_decode_split", &rt_gemm_set_decode_split, "tuning: fixed split-K of the M<=16 decode kernel (0 = auto)");
+  m.def("gemm_set_decode_depth", &rt_gemm_set_decode_depth, "tuning: weight-pipeline depth (2 / 4) of the M<=16 decode kernel (0 = auto)");
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
   m.def("attn_decode_fused_slabs", &attn_decode_fused_slabs, "decode attention with the qkv split-K reduce fused");

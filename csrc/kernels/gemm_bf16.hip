@@ -64,6 +64,9 @@ struct GemmArgs {
   // into B'; rstd(X_row) = rsqrt(mean(X_row^2) + eps) is computed inside the GEMM, 0 = off)
   const bf16_t* R; long ldr;
   float norm_eps;
+  // decode kernel only: B is in the MFMA-fragment order of shuffle_decode_weight (each 16-row x
+  // 64-k tile = 2 KiB contiguous, one 1-KiB run per load instruction) instead of row-major
+  int wshuf;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -529,15 +532,16 @@ struct DGRegs {
 // 64-deep chunk and is widened to two bf16x8 fragments in registers (per-column scale applied in
 // the epilogue). The k order matches the bf16 X fragments (lane group g owns k [16g, 16g+16)).
 template <int MT, bool W8>
-__device__ __forceinline__ void dg_load(DGRegs<MT>& r, const char* const* wrow, const bf16_t* const* xrow, long c) {
+__device__ __forceinline__ void dg_load(DGRegs<MT>& r, const char* const* wrow, const bf16_t* const* xrow, long c,
+                                        long wstep, long hoff) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     // weights are read once per launch: non-temporal (MI355X_MICROARCH.md 'nt-weights')
     if constexpr (W8) {
       r.w[j][0] = load_nt16(wrow[j] + c * 64);
     } else {
-      r.w[j][0] = load_nt16(wrow[j] + c * 128);
-      r.w[j][1] = load_nt16(wrow[j] + c * 128 + 64);
+      r.w[j][0] = load_nt16(wrow[j] + c * wstep);
+      r.w[j][1] = load_nt16(wrow[j] + c * wstep + hoff);
     }
   }
 #pragma unroll
@@ -578,7 +582,7 @@ __device__ __forceinline__ void dg_mma(const DGRegs<MT>& r, f32x4 (&acc)[MT][4])
     }
 }
 
-template <int MT, bool OUT_F32, bool W8>
+template <int MT, bool OUT_F32, bool W8, int DEPTH>
 __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* __restrict__ slabs,
                                                           unsigned* __restrict__ tickets, int split) {
   constexpr int ROWS = MT * 16;
@@ -604,8 +608,11 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
                          : min(n0 + j * 16 + frow, p.N - 1);
     // bf16: lane group g holds k [8g, 8g+8) and [32+8g, 32+8g+8) of each 64-deep chunk (the MFMA's
     // own layout: each load instruction reads 64 contiguous bytes per row); fp8: [16g, 16g+16)
-    wrow[j] = (const char*)p.B + ((long)wr_ * p.ldb + g * (W8 ? 16 : 8)) * WSZ;
+    wrow[j] = (!W8 && p.wshuf) ? (const char*)p.B + ((long)(wr_ >> 4) * nc * 2048 + lane * 16)
+                               : (const char*)p.B + ((long)wr_ * p.ldb + g * (W8 ? 16 : 8)) * WSZ;
   }
+  // bytes between consecutive k-chunks of one lane / between its two 16-B loads of a chunk
+  const long wstep = p.wshuf ? 2048 : 128, hoff = p.wshuf ? 1024 : 64;
 #pragma unroll
   for (int m = 0; m < MT; ++m) xrow[m] = p.A + (long)min(m * 16 + frow, p.M - 1) * p.lda + g * (W8 ? 16 : 8);
 
@@ -632,18 +639,27 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
     }
   };
 
-  DGRegs<MT> ra, rb;
-  if (c_begin < c_end) dg_load<MT, W8>(ra, wrow, xrow, c_begin);
-  for (int c = c_begin; c < c_end; c += 2) {
-    if (c + 1 < c_end) dg_load<MT, W8>(rb, wrow, xrow, c + 1);
-    dg_mma<MT, W8>(ra, acc);
-    if (normed) xsq(ra);
-    if (c + 2 < c_end) dg_load<MT, W8>(ra, wrow, xrow, c + 2);
-    if (c + 1 < c_end) {
-      dg_mma<MT, W8>(rb, acc);
-      if (normed) xsq(rb);
+  // DEPTH register sets: DEPTH-1 chunks stay in flight while one is consumed (chunk c lives in set
+  // (c - c_begin) % DEPTH; every index below is a compile-time constant after unrolling)
+  DGRegs<MT> r[DEPTH];
+#pragma unroll
+  for (int i = 0; i < DEPTH - 1; ++i)
+    if (c_begin + i < c_end) dg_load<MT, W8>(r[i], wrow, xrow, c_begin + i, wstep, hoff);
+  int c = c_begin;
+  for (; c + DEPTH <= c_end; c += DEPTH) {
+#pragma unroll
+    for (int i = 0; i < DEPTH; ++i) {
+      if (c + i + DEPTH - 1 < c_end) dg_load<MT, W8>(r[(i + DEPTH - 1) % DEPTH], wrow, xrow, c + i + DEPTH - 1, wstep, hoff);
+      dg_mma<MT, W8>(r[i], acc);
+      if (normed) xsq(r[i]);
     }
   }
+#pragma unroll
+  for (int i = 0; i < DEPTH - 1; ++i)
+    if (c + i < c_end) {
+      dg_mma<MT, W8>(r[i], acc);
+      if (normed) xsq(r[i]);
+    }
 
   // ---- intra-block reduction: acc[m][j] lane holds C[m*16 + 4g + r][j*16 + frow] ----
 #pragma unroll
@@ -1013,6 +1029,17 @@ static int m64_split(int N, int K) {
 // (M = 1: qkv 16.5 -> 13.7 us, o 11.8 -> 10.9, down 29.4 -> 28.4 at split 8 vs 4).
 static int g_decode_split = 0;  // 0 = heuristic below; tuning override (rt_gemm_set_decode_split)
 
+// Tile-ordered (shuffled) weights stream best with ~8 blocks per column group at every width
+// (gate_up 52.0 -> 43.2 us, lm_head 52.2 -> 47.7 at split 8 vs unsplit row-major; qkv / o / down
+// as the row-major heuristic), keeping >= 2 k-chunks per wave (profiles/kernels_decode_depth_shuffle.log).
+static int decode_split_shuf(int K) {
+  if (g_decode_split > 0) return g_decode_split;
+  const int nc = K / 64;
+  int split = 8;
+  while (split > 1 && nc / (4 * split) < 2) split >>= 1;
+  return split;
+}
+
 static int decode_split(int N, int K) {
   if (g_decode_split > 0) return g_decode_split;
   const int groups = (N + DG_COLS - 1) / DG_COLS;
@@ -1041,6 +1068,19 @@ extern "C" void rt_gemm_set_variant(int v) { g_gemm_variant = v; }
 extern "C" void rt_gemm_set_m64_split(int s) { g_m64_split = s; }
 extern "C" void rt_gemm_set_decode_split(int s) { g_decode_split = s; }
 
+// register sets of the M <= 16 kernel's weight pipeline (DEPTH - 1 k-chunks in flight per wave).
+// 4 sets cost ~85 VGPRs at MT = 1 (occupancy 3 -> 2 blocks per CU; MT = 2 would spill) and
+// measured no faster even on the unsplit wide GEMMs (gate_up 48.9 vs 48.7 us, lm_head 52.8 vs
+// 52.6; profiles/kernels_decode_depth_shuffle.log): the default stays 2. 2 / 4 force (tuning).
+static int g_decode_depth = 0;
+extern "C" void rt_gemm_set_decode_depth(int d) { g_decode_depth = d; }
+static int decode_depth(int MT, long blocks) {
+  if (MT > 1) return 2;
+  if (g_decode_depth == 2 || g_decode_depth == 4) return g_decode_depth;
+  (void)blocks;
+  return 2;
+}
+
 
 // Wave quantisation decides between the kernels: the 256-tile kernel runs one workgroup per CU
 // (256 slots), the 128-tile kernel two (512 slots); the 256 kernel is ~10 % faster per FLOP
@@ -1059,7 +1099,7 @@ static bool use_256(int M, int N) {
 extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, const void* U, long ldu,
                           const void* UB, long ldub, int Rp, const void* bias, void* C, long ldc, int M,
                           int N, int K, int act, int out_f32, float* slabs, unsigned* tickets,
-                          const void* R, long ldr, float norm_eps, hipStream_t stream) {
+                          const void* R, long ldr, float norm_eps, int wshuf, hipStream_t stream) {
   GemmArgs p;
   p.A = (const bf16_t*)A; p.lda = lda;
   p.B = (const bf16_t*)B; p.ldb = ldb;
@@ -1070,25 +1110,32 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   p.C = C; p.ldc = ldc;
   p.M = M; p.N = N; p.K = K; p.act = act;
   p.sa = nullptr; p.sb = nullptr;
-  p.R = (const bf16_t*)R; p.ldr = ldr; p.norm_eps = norm_eps;
+  p.R = (const bf16_t*)R; p.ldr = ldr; p.norm_eps = norm_eps; p.wshuf = wshuf;
   if (M <= 0 || N <= 0) return 0;
+  if (wshuf && (M > 64 || N % 16 != 0 || K % 64 != 0)) return -4;  // shuffled weights: decode kernel only
   if (act == ACT_SWIGLU && (M > 64 || N % 64 != 0 || (U && UB))) return -2;
   if ((R || norm_eps > 0.f) && M > 64) return -3;  // residual / in-GEMM norm: skinny kernels only
-  if (M > 16 && M <= 64 && p.Rp == 0 && g_gemm_variant != 1) {
+  if (M > 16 && M <= 64 && p.Rp == 0 && g_gemm_variant != 1 && !wshuf) {
     const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64 + 64) : 1;
     dim3 grid(((N + 63) / 64) * split), block(256);
     if (out_f32) hipLaunchKernelGGL((gemm_m64_kernel<true>), grid, block, 0, stream, p, slabs, tickets, split);
     else hipLaunchKernelGGL((gemm_m64_kernel<false>), grid, block, 0, stream, p, slabs, tickets, split);
   } else if (M <= 64) {
     const int MT = (M + 15) / 16;
-    const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * (DG_COLS + 1)) : 1;
+    const int want = wshuf ? decode_split_shuf(K) : decode_split(N, K);
+    const int split = (slabs && tickets) ? fit_split(want, (N + DG_COLS - 1) / DG_COLS, MT * 16 * (DG_COLS + 1)) : 1;
     dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
-#define DG_CASE(mt)                                                                                        \
-  case mt:                                                                                                 \
-    if (out_f32) hipLaunchKernelGGL((gemm_decode_kernel<mt, true, false>), grid, block, 0, stream, p, slabs, tickets, split); \
-    else hipLaunchKernelGGL((gemm_decode_kernel<mt, false, false>), grid, block, 0, stream, p, slabs, tickets, split);       \
-    break;
-    switch (MT) { DG_CASE(1) DG_CASE(2) DG_CASE(3) DG_CASE(4) default: return -1; }
+    const bool deep = decode_depth(MT, (long)grid.x) == 4;
+#define DG_CASE(mt, d)                                                                                     \
+  if (out_f32) hipLaunchKernelGGL((gemm_decode_kernel<mt, true, false, d>), grid, block, 0, stream, p, slabs, tickets, split); \
+  else hipLaunchKernelGGL((gemm_decode_kernel<mt, false, false, d>), grid, block, 0, stream, p, slabs, tickets, split);
+    switch (MT) {
+      case 1: if (deep) { DG_CASE(1, 4) } else { DG_CASE(1, 2) } break;
+      case 2: DG_CASE(2, 2) break;
+      case 3: DG_CASE(3, 2) break;
+      case 4: DG_CASE(4, 2) break;
+      default: return -1;
+    }
 #undef DG_CASE
   } else if (use_256(M, N) && (N % 8) == 0 && (ldc % 8) == 0) {
     const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
@@ -1117,7 +1164,7 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
   p.U = nullptr; p.ldu = 0; p.UB = nullptr; p.ldub = 0; p.Rp = 0;
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K; p.act = act;
   p.sa = sa; p.sb = sb;
-  p.R = (const bf16_t*)R; p.ldr = ldr; p.norm_eps = norm_eps;
+  p.R = (const bf16_t*)R; p.ldr = ldr; p.norm_eps = norm_eps; p.wshuf = 0;
   if (M <= 0 || N <= 0) return 0;
   if ((R || norm_eps > 0.f) && !a_is_bf16) return -3;
   if (a_is_bf16) {
@@ -1126,10 +1173,13 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
     const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * (DG_COLS + 1)) : 1;
     dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
     switch (MT) {
-      case 1: hipLaunchKernelGGL((gemm_decode_kernel<1, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;
-      case 2: hipLaunchKernelGGL((gemm_decode_kernel<2, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;
-      case 3: hipLaunchKernelGGL((gemm_decode_kernel<3, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;
-      case 4: hipLaunchKernelGGL((gemm_decode_kernel<4, false, true>), grid, block, 0, stream, p, slabs, tickets, split); break;
+      case 1:
+        if (decode_depth(1, (long)grid.x) == 4) hipLaunchKernelGGL((gemm_decode_kernel<1, false, true, 4>), grid, block, 0, stream, p, slabs, tickets, split);
+        else hipLaunchKernelGGL((gemm_decode_kernel<1, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split);
+        break;
+      case 2: hipLaunchKernelGGL((gemm_decode_kernel<2, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
+      case 3: hipLaunchKernelGGL((gemm_decode_kernel<3, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
+      case 4: hipLaunchKernelGGL((gemm_decode_kernel<4, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
       default: return -1;
     }
   } else {
@@ -1137,6 +1187,37 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
     const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
     hipLaunchKernelGGL((gemm_256_kernel<false, true>), dim3(tiles), dim3(512), 0, stream, p);
   }
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+// Decode-weight image for the M <= 64 kernel: W [N, K] row-major -> per (16-row group G, 64-k chunk
+// c) one 2-KiB tile in the order the kernel's lanes load it (lane l = 16 g + r of load h reads
+// W[16 G + r][64 c + 32 h + 8 g .. +8]), tiles of one row group consecutive in c. Every 16-B load
+// instruction of a wave then reads one contiguous 1-KiB run (tools/microbench/hbm_pattern.hip:
+// 6.3-6.7 TB/s vs 5.9 for the row-major 16-rows x 128-B pattern). Measured at M = 1 (graph replay,
+// cold weights, profiles/kernels_decode_depth_shuffle.log): the split-K launches gain (qkv 14.2 ->
+// 12.8 us, o 11.0 -> 10.3, down 28.5 -> 21.9), the unsplit wide ones do not (gate_up 52.7 -> 51.3,
+// lm_head 49.7 -> 56.9; rotating each block's k walk made both worse) until they are split 8 ways
+// too (decode_split_shuf: gate_up 43.2, lm_head 47.7). At the same split the results are bitwise
+// identical to the row-major launch. One thread per 16 B.
+__global__ __launch_bounds__(256) void shuffle_decode_weight_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                                     long N, long K) {
+  const long nc = K / 64;
+  const long total = N * K / 8;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long l = i & 63, h = (i >> 6) & 1, tile = i >> 7;
+    const long G = tile / nc, c = tile % nc;
+    const long row = G * 16 + (l & 15), k = c * 64 + h * 32 + (l >> 4) * 8;
+    dst[i] = src[(row * K + k) / 8];
+  }
+}
+
+extern "C" int rt_shuffle_decode_weight(const void* src, void* dst, long N, long K, hipStream_t stream) {
+  if (N % 16 || K % 64) return -1;
+  const long total = N * K / 8;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(shuffle_decode_weight_kernel, dim3(blocks), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst, N, K);
   RT_LAUNCH_CHECK();
   return 0;
 }

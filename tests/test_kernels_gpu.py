@@ -384,6 +384,39 @@ def test_decode_gemm_split_k_repeated(M, N, K):
     _close(ops.gemm(a, w, u, ub, out_f32=True), ref.gemm(a, w, u, ub, out_f32=True), rtol=5e-3, atol=5e-3)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (5, 4096, 14336), (16, 1040, 448), (12, 2048, 1024),
+                                   (1, 28672, 4096)])
+def test_decode_gemm_shuffled_weight_bitwise(M, N, K):
+    """The tile-ordered weight image feeds the same MFMAs in the same order: at the same split-K the
+    results are bitwise equal to the row-major launch, with the in-GEMM norm, SwiGLU pair and
+    residual epilogues (the default splits differ per layout: close, not equal)."""
+    C = ops.native()
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / math.sqrt(K)
+    ws = C.shuffle_decode_weight(w)
+    # the image is a permutation of w (every element kept)
+    assert torch.equal(torch.sort(ws.flatten().float())[0], torch.sort(w.flatten().float())[0])
+    res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    for kw in (dict(), dict(norm_eps=1e-5), dict(residual=res), dict(act=ops.ACT_SWIGLU, norm_eps=1e-5)):
+        if kw.get("act") == ops.ACT_SWIGLU and N % 64:
+            continue
+        args = (None, None, None, kw.get("act", 0), False, None, kw.get("residual"), kw.get("norm_eps", 0.0))
+        try:
+            for split in (0, 2):  # 0: each layout's own split heuristic; forced: the same split-K
+                C.gemm_set_decode_split(split)
+                base = C.gemm(a, w, *args)
+                for _ in range(2):  # split-K tickets re-arm
+                    got = C.gemm(a, ws, *args, True)
+                    if split:
+                        assert torch.equal(got, base), kw
+                    else:
+                        _close(got, base, rtol=1e-2, atol=1e-2)
+        finally:
+            C.gemm_set_decode_split(0)
+    with pytest.raises(RuntimeError):
+        C.gemm(torch.randn(65, K, device=DEV, dtype=torch.bfloat16), ws, w_shuffled=True)
+
+
 def test_sampler_bf16_topk_topp_vocab():
     # LDS fast path on a realistic vocabulary: only top-k survivors are ever drawn
     B, V = 64, 32000

@@ -69,6 +69,60 @@ def test_decode_matches_teacher_forcing():
     torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=0.08)
 
 
+def test_fused_decode_follows_adapter_updates():
+    """Batch-1 decode reads weights derived in place from the adapters (merged W + UB A, then the
+    norm fold): after an optimizer-style adapter update + refresh_lora, the next generation must
+    score like teacher forcing under the NEW adapter (a stale derived weight would not)."""
+    from rag_tl_domainllm_optimizer_amd.train.common import score_sequences
+
+    cfg = PRESETS["tiny-mistral"]
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=4)
+    m.add_lora(8, 16.0, "all", seed=1)
+    gen = Generator(m, 1, 64, DEV)
+    p = SamplingParams(max_new_tokens=10, temperature=0.7, top_k=0, seed=5)
+    prompts = [[5, 9, 33, 41, 7, 8, 9, 10]]
+    for step in range(3):
+        with torch.no_grad():
+            for q in m.lora_parameters():
+                q.normal_(0, 0.08)
+        m.refresh_lora()
+        out = gen.generate(prompts, p, pad_id=0, eos_ids=[-1])
+        with torch.no_grad():
+            lp, _, _, _ = score_sequences(m, out.prompt_ids, out.prompt_start, out.tokens, out.lengths, 1 / 0.7)
+        torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=0.08, msg=f"step {step}")
+
+
+def test_shuffled_decode_weights_match_row_major(monkeypatch):
+    """Batch-1 decode on the tile-ordered weight images (qkv, o, gate_up, down, lm_head) == the
+    row-major weights, bitwise at a common split-K, including after an adapter update (the images
+    follow the merged / folded sources)."""
+    cfg = PRESETS["tiny-mistral"]
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=6)
+    m.add_lora(8, 16.0, "all", seed=2)
+    p = SamplingParams(max_new_tokens=12, temperature=0.7, top_k=0, seed=9)
+    prompts = [[5, 9, 33, 41, 7, 8, 9, 10, 11]]
+    outs = {}
+    ops.native().gemm_set_decode_split(2)  # same split-K for both layouts -> bitwise comparable
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RAGTL_DECODE_SHUF", flag)
+        gen = Generator(m, 1, 64, DEV)
+        res = []
+        for step in range(2):
+            with torch.no_grad():
+                g = torch.Generator(device=DEV).manual_seed(step)
+                for q in m.lora_parameters():
+                    q.copy_(torch.randn(q.shape, device=DEV, generator=g, dtype=q.dtype) * 0.05)
+            m.refresh_lora()
+            out = gen.generate(prompts, p, pad_id=0, eos_ids=[-1])
+            res.append((out.tokens.clone(), out.logprobs.clone()))
+        outs[flag] = res
+    ops.native().gemm_set_decode_split(0)
+    assert any(len(layer._shufc) for layer in m.layers) and m._head_shuf is not None
+    for (t1, l1), (t0, l0) in zip(outs["1"], outs["0"]):
+        assert torch.equal(t1, t0)
+        assert torch.equal(l1, l0)
+
+
 def test_encoder_gpu_matches_cpu():
     cfg = PRESETS["tiny-mpnet"]
     cpu = models.SentenceEncoder(cfg, dtype=torch.float32, seed=3)

@@ -2,7 +2,8 @@
 
 For each Mistral-7B decode shape, captures `reps` back-to-back GEMMs over distinct weight copies
 (> 256 MB total, so every launch streams its weights from HBM like a real decode step) and reports
-kernel time per GEMM and effective weight bandwidth, for each split-K setting and for hipBLASLt.
+kernel time per GEMM and effective weight bandwidth, for each split-K / pipeline-depth setting and
+for the tile-ordered (shuffled) weight image.
 
     python tools/sweep_decode.py [--M 1] [--splits 0,2,4,8,16]
 """
@@ -45,6 +46,8 @@ def main():
     ap.add_argument("--M", default="1")
     ap.add_argument("--splits", default="0,1,2,4,8,16")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--depths", default="0", help="weight-pipeline depths of the M<=16 kernel (0 = auto)")
+    ap.add_argument("--shuf-splits", default="0", help="split-K settings for the shuffled-weight runs")
     args = ap.parse_args()
     C = ops.native()
     dev = "cuda"
@@ -58,27 +61,34 @@ def main():
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(reps)]
             byts = N * K * 2
-            for sp in [int(v) for v in args.splits.split(",")]:
+            for sp, dp in [(int(v), int(d)) for v in args.splits.split(",") for d in args.depths.split(",")]:
                 (C.gemm_set_m64_split if M > 16 else C.gemm_set_decode_split)(sp)
+                C.gemm_set_decode_depth(dp)
 
                 def run():
                     for w, o in zip(ws, outs):
                         ops.gemm(x, w, out=o)
                 t = graph_time(run) / reps
-                r = dict(kind="decode_gemm", name=name, M=M, N=N, K=K, split=sp, us=round(t, 2),
+                r = dict(kind="decode_gemm", name=name, M=M, N=N, K=K, split=sp, depth=dp, us=round(t, 2),
                          tbs=round(byts / t / 1e6, 2))
                 print(json.dumps(r), flush=True)
             C.gemm_set_decode_split(0)
+            C.gemm_set_decode_depth(0)
             C.gemm_set_m64_split(0)
-            prev = None  # single (hand-written) GEMM path since round 2
+            # tile-ordered weight image (shuffle_decode_weight): same kernel, contiguous 1-KiB loads
+            ref = C.gemm(x, ws[0])
+            ws = [C.shuffle_decode_weight(w) for w in ws]
 
-            def run_lib():
+            def run_shuf():
                 for w, o in zip(ws, outs):
-                    ops.gemm(x, w, out=o)
-            t = graph_time(run_lib) / reps
-            pass  # single (hand-written) GEMM path since round 2
-            print(json.dumps(dict(kind="decode_gemm", name=name, M=M, N=N, K=K, split="lib", us=round(t, 2),
-                                  tbs=round(byts / t / 1e6, 2))), flush=True)
+                    C.gemm(x, w, out=o, w_shuffled=True)
+            for sp in [int(v) for v in args.shuf_splits.split(",")]:
+                C.gemm_set_decode_split(sp)
+                t = graph_time(run_shuf) / reps
+                err = float((ref.float() - outs[0].float()).abs().max() / ref.float().abs().max())
+                print(json.dumps(dict(kind="decode_gemm", name=name, M=M, N=N, K=K, split=f"shuf{sp}",
+                                      us=round(t, 2), tbs=round(byts / t / 1e6, 2), rel_err=err)), flush=True)
+            C.gemm_set_decode_split(0)
             del ws, outs
             torch.cuda.empty_cache()
 
