@@ -42,6 +42,7 @@ int rt_rope_qkv(void*, long, const int*, const float*, const float*, int, int, i
 int rt_swiglu_fwd(const void*, void*, long, int, hipStream_t);
 int rt_swiglu_bwd(const void*, const void*, void*, long, int, hipStream_t);
 int rt_embed(const void*, const long*, const void*, const long*, void*, long, int, hipStream_t);
+int rt_rows_scatter(const void*, long, const int*, void*, long, int, long, hipStream_t);
 int rt_attn_fwd(const void*, long, const void*, long, const void*, long, void*, long, float*, const int*, const int*,
                 const float*, int, int, int, int, int, int, int, int, int, float, hipStream_t);
 int rt_attn_decode(const void*, long, const void*, const void*, int, const int*, const int*, int, float*, int, int,
@@ -580,6 +581,20 @@ Tensor embed(const Tensor& table, const Tensor& ids, const optional<Tensor>& pta
   return out;
 }
 
+// src [N, H] (row stride % 8 == 0) -> out [R, H]: out[r] = src[inv[r]] or zeros where inv[r] < 0
+Tensor rows_scatter(const Tensor& src, const Tensor& inv, int64_t R) {
+  CHECK_CUDA(src); CHECK_BF16(src); CHECK_CUDA(inv);
+  TORCH_CHECK(src.dim() == 2 && src.stride(1) == 1 && src.stride(0) % 8 == 0, "rows_scatter: [N, H] rows expected");
+  TORCH_CHECK(inv.scalar_type() == at::kInt && inv.is_contiguous() && inv.numel() == R, "rows_scatter: inv int32 [R]");
+  const int64_t H = src.size(1);
+  TORCH_CHECK(H % 8 == 0, "rows_scatter: H % 8");
+  auto out = at::empty({R, H}, src.options());
+  check_rc(rt_rows_scatter(src.data_ptr(), src.stride(0), inv.data_ptr<int>(), out.data_ptr(), R, (int)H, src.size(0),
+                           cur_stream()),
+           "rows_scatter");
+  return out;
+}
+
 // ---------------------------------------------------------------------------------------------
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, int64_t B, int64_t Sq, int64_t Sk,
                              int64_t Hq, int64_t Hkv, int64_t D, bool causal, int64_t window, double scale,
@@ -985,6 +1000,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out_f32") = false, py::arg("out") = py::none(), py::arg("residual") = py::none(),
         py::arg("norm_eps") = 0.0, py::arg("w_shuffled") = false);
+  m.def("rows_scatter", &rows_scatter, "varlen: out[r] = src[inv[r]] (zeros where inv[r] < 0)", py::arg("src"),
+        py::arg("inv"), py::arg("R"));
   m.def("shuffle_decode_weight", &shuffle_decode_weight, "W [N, K] -> tile-ordered decode image (gemm w_shuffled=True)",
         py::arg("w"), py::arg("out") = py::none());
   m.def("gemm_set_m64_split", &rt_gemm_set_m64_split, "tuning: fixed split-K of the M<=64 ring kernel (0 = auto)");

@@ -263,26 +263,28 @@ class CausalLM(nn.Module):
         pos = self.positions(B, S, kv_start, dev)
         cos, sin = self.rope(dev)
         ks = kv_start.to(torch.int32) if kv_start is not None else None
+        packed_inv = None
         if packed_idx is not None:
             x = self.embed_tokens(input_ids.reshape(-1).index_select(0, packed_idx), pos.index_select(0, packed_idx))
+            packed_inv = ops.packed_inverse(packed_idx, B * S)
         else:
             x = self.embed_tokens(input_ids.reshape(-1), pos)
         residual = None
         for layer in self.layers:
             if gradient_checkpointing and torch.is_grad_enabled():
                 x, residual = torch.utils.checkpoint.checkpoint(self._layer_fwd, layer, x, residual, pos, cos, sin,
-                                                                B, S, ks, packed_idx, use_reentrant=False)
+                                                                B, S, ks, packed_idx, packed_inv, use_reentrant=False)
             else:
-                x, residual = self._layer_fwd(layer, x, residual, pos, cos, sin, B, S, ks, packed_idx)
+                x, residual = self._layer_fwd(layer, x, residual, pos, cos, sin, B, S, ks, packed_idx, packed_inv)
         return self.final_norm(x, residual)
 
-    def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks, packed_idx=None):
+    def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks, packed_idx=None, packed_inv=None):
         cfg = self.cfg
         qkv, residual = layer.attn_in(x, residual)
         rope = (pos, cos, sin) if cos is not None else None
         if packed_idx is not None:
             o = ops.flash_attention_packed(qkv, packed_idx, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
-                                           cfg.sliding_window, kv_start=ks, rope=rope)
+                                           cfg.sliding_window, kv_start=ks, rope=rope, inv=packed_inv)
         else:
             o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
                                         cfg.sliding_window, kv_start=ks, rope=rope)
@@ -306,19 +308,20 @@ class CausalLM(nn.Module):
         idx = packed[0] if packed is not None else None
         if idx is not None:
             x = self.embed_tokens(input_ids.reshape(-1).index_select(0, idx), pos.index_select(0, idx))
+            inv = ops.packed_inverse(idx, B * S)
         else:
             x = self.embed_tokens(input_ids.reshape(-1), pos)
         residual = None
         for li, layer in enumerate(self.layers):
             qkv, residual = layer.attn_in(x, residual)
             if idx is not None:
-                qkv = qkv.new_zeros(B * S, qkv.shape[1]).index_copy_(0, idx, qkv)
+                qkv = ops.scatter_rows(qkv, idx, inv, B * S)
             ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S,
                           k_cache=cache.k[li], v_cache=cache.v[li], slot_base=None)
             o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
                                         cfg.sliding_window, kv_start=ks)
             if idx is not None:
-                o = o.index_select(0, idx)
+                o = ops.gather_rows(o, idx, inv)
             x, residual = layer.mlp(o, residual)
         if idx is not None:
             last = torch.from_numpy(packed[1][1:] - 1).to(dev)

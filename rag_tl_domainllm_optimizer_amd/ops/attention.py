@@ -122,8 +122,64 @@ def flash_attention_qkv(qkv, B, S, Hq, Hkv, D, causal=True, window=0, scale=None
     return native().attn_fwd(q, k, v, B, S, S, Hq, Hkv, D, causal, window, scale, kv_start, None, None, 0, False)[0]
 
 
+def packed_inverse(idx: torch.Tensor, R: int) -> torch.Tensor:
+    """int32 [R]: the packed row of every grid row (-1 for pad rows) — the scatter's index."""
+    inv = torch.full((R,), -1, dtype=torch.int32, device=idx.device)
+    inv[idx] = torch.arange(idx.numel(), dtype=torch.int32, device=idx.device)
+    return inv
+
+
+def _scatter_rows_raw(src, idx, inv, R):
+    if on_gpu(src) and src.dtype == torch.bfloat16:
+        return native().rows_scatter(src, inv, R)
+    return src.new_zeros(R, src.shape[1]).index_copy(0, idx, src)
+
+
+def _gather_rows_raw(src, idx):
+    if on_gpu(src) and src.dtype == torch.bfloat16:
+        return native().embed(src.contiguous(), idx, None, None)
+    return src.index_select(0, idx)
+
+
+class _ScatterRows(torch.autograd.Function):
+    """[N, W] packed rows -> [R, W] grid (zeros on pad rows) in one native pass; backward gathers."""
+
+    @staticmethod
+    def forward(ctx, src, idx, inv, R):
+        ctx.save_for_backward(idx)
+        return _scatter_rows_raw(src, idx, inv, R)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        return _gather_rows_raw(g, idx), None, None, None
+
+
+class _GatherRows(torch.autograd.Function):
+    """[R, W] grid -> its [N, W] real rows (native gather); backward scatters with zero pads."""
+
+    @staticmethod
+    def forward(ctx, src, idx, inv):
+        ctx.save_for_backward(idx, inv)
+        ctx.R = src.shape[0]
+        return _gather_rows_raw(src, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, inv = ctx.saved_tensors
+        return _scatter_rows_raw(g.contiguous(), idx, inv, ctx.R), None, None
+
+
+def scatter_rows(src, idx, inv, R):
+    return _ScatterRows.apply(src, idx, inv, R)
+
+
+def gather_rows(src, idx, inv):
+    return _GatherRows.apply(src, idx, inv)
+
+
 def flash_attention_packed(qkv_p, idx, B, S, Hq, Hkv, D, causal=True, window=0, scale=None, kv_start=None,
-                           rope=None):
+                           rope=None, inv=None):
     """Varlen self-attention over PACKED token rows (no pad rows in the GEMMs around it).
 
     ``qkv_p`` [N, W] holds only real tokens; ``idx`` [N] (int64) is each row's position b*S + s in
@@ -131,10 +187,13 @@ def flash_attention_packed(qkv_p, idx, B, S, Hq, Hkv, D, causal=True, window=0, 
     keys stay zero: left pads are masked by ``kv_start``, right pads lie after every real query of
     their row under the causal mask), attended with the usual kernels, and the real output rows
     gathered back. Scatter / gather move ~40 KB per token per layer against ~0.4 GFLOP of
-    projection GEMMs per token per layer that no longer run on pads (both differentiable)."""
-    grid = qkv_p.new_zeros(B * S, qkv_p.shape[1]).index_copy(0, idx, qkv_p)
+    projection GEMMs per token per layer that no longer run on pads (both differentiable, one
+    native pass each: ``inv`` = packed_inverse(idx, B*S), computed once per forward)."""
+    if inv is None:
+        inv = packed_inverse(idx, B * S)
+    grid = scatter_rows(qkv_p, idx, inv, B * S)
     o = flash_attention_qkv(grid, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope)
-    return o.index_select(0, idx)
+    return gather_rows(o, idx, inv)
 
 
 def attention(q, k, v, B, Sq, Sk, Hq, Hkv, D, causal=False, window=0, scale=None, kv_start=None, kv_len=None,

@@ -417,6 +417,28 @@ def test_decode_gemm_shuffled_weight_bitwise(M, N, K):
         C.gemm(torch.randn(65, K, device=DEV, dtype=torch.bfloat16), ws, w_shuffled=True)
 
 
+def test_varlen_rows_scatter_gather_autograd():
+    """Native varlen scatter (one pass, zero pad rows) / gather and their autograd duals equal the
+    index_copy / index_select forms exactly (pure data movement)."""
+    R, N, W = 1000, 700, 392
+    idx = torch.randperm(R, device=DEV)[:N].sort().values
+    inv = ops.packed_inverse(idx, R)
+    assert int((inv >= 0).sum()) == N and torch.equal(inv[idx].long(), torch.arange(N, device=DEV))
+    base = torch.randn(N, W + 8, device=DEV, dtype=torch.bfloat16)
+    src = base[:, :W].detach().requires_grad_(True)  # row stride != W
+    grid = ops.scatter_rows(src, idx, inv, R)
+    assert torch.equal(grid, torch.zeros(R, W, device=DEV, dtype=torch.bfloat16).index_copy(0, idx, src.detach()))
+    g = torch.randn_like(grid)
+    grid.backward(g)
+    assert torch.equal(src.grad, g.index_select(0, idx))
+    full = torch.randn(R, W, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = ops.gather_rows(full, idx, inv)
+    assert torch.equal(o, full.detach().index_select(0, idx))
+    h = torch.randn_like(o)
+    o.backward(h)
+    assert torch.equal(full.grad, torch.zeros_like(full).index_copy(0, idx, h))
+
+
 def test_sampler_bf16_topk_topp_vocab():
     # LDS fast path on a realistic vocabulary: only top-k survivors are ever drawn
     B, V = 64, 32000
