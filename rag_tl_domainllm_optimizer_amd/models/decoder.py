@@ -251,12 +251,17 @@ class CausalLM(nn.Module):
 
     # ------------------------------------------------------------------ full forward
     def forward(self, input_ids: torch.Tensor, kv_start: Optional[torch.Tensor] = None,
-                gradient_checkpointing: bool = False, packed_idx: Optional[torch.Tensor] = None) -> torch.Tensor:
+                gradient_checkpointing: bool = False, packed_idx: Optional[torch.Tensor] = None,
+                out_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """input_ids [B, S] (left-padded; kv_start[b] = first real token) -> final hidden [B*S, H].
 
         ``packed_idx`` [N] (grid positions b*S + s of the tokens to compute, see ``packed_index``):
         varlen form — embeddings, norms and every projection GEMM run on the N real tokens only
-        (attention scatters them into the [B, S] grid it tiles); returns [N, H] in that order."""
+        (attention scatters them into the [B, S] grid it tiles); returns [N, H] in that order.
+
+        ``out_rows`` [R] (int64 rows of that [B*S] / [N] order): only these rows' hidden states are
+        wanted (the scored positions). The last layer's K/V still cover every row, but its o_proj,
+        MLP and the final norm run on the R rows only; returns [R, H]."""
         cfg = self.cfg
         B, S = input_ids.shape
         dev = input_ids.device
@@ -270,15 +275,19 @@ class CausalLM(nn.Module):
         else:
             x = self.embed_tokens(input_ids.reshape(-1), pos)
         residual = None
-        for layer in self.layers:
+        nl = len(self.layers)
+        for li, layer in enumerate(self.layers):
+            rows = out_rows if li == nl - 1 else None
             if gradient_checkpointing and torch.is_grad_enabled():
                 x, residual = torch.utils.checkpoint.checkpoint(self._layer_fwd, layer, x, residual, pos, cos, sin,
-                                                                B, S, ks, packed_idx, packed_inv, use_reentrant=False)
+                                                                B, S, ks, packed_idx, packed_inv, rows,
+                                                                use_reentrant=False)
             else:
-                x, residual = self._layer_fwd(layer, x, residual, pos, cos, sin, B, S, ks, packed_idx, packed_inv)
+                x, residual = self._layer_fwd(layer, x, residual, pos, cos, sin, B, S, ks, packed_idx, packed_inv, rows)
         return self.final_norm(x, residual)
 
-    def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks, packed_idx=None, packed_inv=None):
+    def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks, packed_idx=None, packed_inv=None,
+                   out_rows=None):
         cfg = self.cfg
         qkv, residual = layer.attn_in(x, residual)
         rope = (pos, cos, sin) if cos is not None else None
@@ -288,6 +297,11 @@ class CausalLM(nn.Module):
         else:
             o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
                                         cfg.sliding_window, kv_start=ks, rope=rope)
+        if out_rows is not None:
+            # everything after attention is row-local: drop the rows nobody reads before o_proj
+            inv = ops.packed_inverse(out_rows, o.shape[0])
+            o = ops.gather_rows(o, out_rows, inv)
+            residual = ops.gather_rows(residual, out_rows, inv)
         return layer.mlp(o, residual)
 
     # ------------------------------------------------------------------ generation
@@ -320,14 +334,17 @@ class CausalLM(nn.Module):
                           k_cache=cache.k[li], v_cache=cache.v[li], slot_base=None)
             o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
                                         cfg.sliding_window, kv_start=ks)
-            if idx is not None:
+            if li == len(self.layers) - 1:
+                # only the last position of every row is sampled from: the last layer's o_proj and
+                # MLP run on B rows (its K/V above still covered the whole prompt)
+                last = torch.arange(B, device=dev) * S + (S - 1)
+                o = o.index_select(0, last)
+                residual = residual.index_select(0, torch.from_numpy(packed[1][1:] - 1).to(dev)
+                                                 if idx is not None else last)
+            elif idx is not None:
                 o = ops.gather_rows(o, idx, inv)
             x, residual = layer.mlp(o, residual)
-        if idx is not None:
-            last = torch.from_numpy(packed[1][1:] - 1).to(dev)
-        else:
-            last = torch.arange(B, device=dev) * S + (S - 1)
-        return self.final_norm(x[last].contiguous(), residual[last].contiguous())
+        return self.final_norm(x, residual)
 
     @torch.no_grad()
     def decode(self, tokens, pos, slot, attn_len, kv_start, cache, workspace=None) -> torch.Tensor:

@@ -60,13 +60,13 @@ def score_sequences(model, prompt_ids: torch.Tensor, start: torch.Tensor, resp: 
         if n_sc > 0 and n_tok < 0.97 * B * (S + T):
             dev = prompt_ids.device
             idx, off = packed_index(lo, hi, S + T, dev)
-            h = model(seq, kv_start=start.to(torch.int32), gradient_checkpointing=gradient_checkpointing,
-                      packed_idx=idx)
             b = np.repeat(np.arange(B, dtype=np.int64), rl)
             t = np.arange(n_sc, dtype=np.int64) - np.repeat(np.cumsum(rl) - rl, rl)
             sel = torch.from_numpy(off[:-1][b] + (S - 1 + t) - lo[b]).to(dev)
             dst = torch.from_numpy(b * T + t).to(dev)
-            hs = h.index_select(0, sel)
+            # hidden states of the scored rows only (the last layer's o_proj / MLP skip the rest)
+            hs = model(seq, kv_start=start.to(torch.int32), gradient_checkpointing=gradient_checkpointing,
+                       packed_idx=idx, out_rows=sel)
             tgt = resp.reshape(-1).index_select(0, dst)
             logits = ops.linear(hs, model.head_weight) if (grad and hs.requires_grad) else \
                 ops.gemm(hs.contiguous(), model.head_weight)
@@ -78,9 +78,9 @@ def score_sequences(model, prompt_ids: torch.Tensor, start: torch.Tensor, resp: 
                 v = value_head(hs).reshape(-1)
                 values = v.new_zeros(B * T).index_copy(0, dst, v).view(B, T)
             return logp, entf, values, mask
-    h = model(seq, kv_start=start.to(torch.int32), gradient_checkpointing=gradient_checkpointing)
-    H = h.shape[-1]
-    h = h.view(B, S + T, H)[:, S - 1:S + T - 1].reshape(B * T, H)
+    rows = (torch.arange(B, device=seq.device)[:, None] * (S + T) +
+            torch.arange(S - 1, S + T - 1, device=seq.device)[None, :]).reshape(-1)
+    h = model(seq, kv_start=start.to(torch.int32), gradient_checkpointing=gradient_checkpointing, out_rows=rows)
     tgt = torch.where(mask, resp, torch.full_like(resp, -100)).reshape(-1)
     logits = ops.linear(h, model.head_weight) if (grad and h.requires_grad) else \
         ops.gemm(h.contiguous(), model.head_weight)

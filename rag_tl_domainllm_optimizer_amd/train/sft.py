@@ -103,14 +103,14 @@ class SFTTrainer:
             # varlen: row b's inputs are [start_b, S - 1) (the last token predicts nothing); the
             # GEMMs skip the left pads, the scored rows are looked up in the packed order
             idx, _ = packed_index(st, np.full(B, S - 1), S, ids.device)
-            h = self.model(ids, kv_start=start, gradient_checkpointing=self.cfg.gradient_checkpointing,
-                           packed_idx=idx)
             inv = torch.full((B * S,), -1, dtype=torch.long, device=ids.device)
             inv.index_copy_(0, idx, torch.arange(idx.numel(), device=ids.device))
-            hs = h.index_select(0, inv.index_select(0, rows))
+            # hidden states of the answer rows only (last layer's o_proj / MLP skip the rest)
+            hs = self.model(ids, kv_start=start, gradient_checkpointing=self.cfg.gradient_checkpointing,
+                            packed_idx=idx, out_rows=inv.index_select(0, rows))
         else:
-            h = self.model(ids, kv_start=start, gradient_checkpointing=self.cfg.gradient_checkpointing)
-            hs = h[rows]
+            hs = self.model(ids, kv_start=start, gradient_checkpointing=self.cfg.gradient_checkpointing,
+                            out_rows=rows)
         logits = ops.linear(hs, self.model.head_weight)
         lp, _ = ops.token_logprobs(logits, flat_t[rows], 1.0)
         return -lp.mean(), int(rows.numel())

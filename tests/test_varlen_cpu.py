@@ -120,3 +120,44 @@ def test_prefill_packed_matches_padded(preset, monkeypatch):
         res.append((out.tokens.clone(), out.logprobs.clone()))
     assert torch.equal(res[0][0], res[1][0])
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("preset", ["tiny-mistral", "tiny-opt"])
+@pytest.mark.parametrize("packed", [False, True])
+def test_forward_out_rows_matches_full(preset, packed):
+    """``out_rows``: the last layer's o_proj / MLP / final norm on the selected rows only gives the
+    same hidden states (and LoRA gradients) as the full forward indexed afterwards."""
+    from rag_tl_domainllm_optimizer_amd.generation import KVCache
+
+    cfg = PRESETS[preset]
+    m = models.CausalLM(cfg, dtype=torch.float32, seed=7)
+    m.add_lora(4, 8.0, None, seed=2)
+    with torch.no_grad():
+        for p in m.lora_parameters():
+            p.normal_(0, 0.05)
+    m.refresh_lora()
+    pid, start, resp, rlen, st, rl = _batch(cfg, seed=3)
+    B, S = pid.shape
+    idx = packed_index(st, np.full(B, S), S, "cpu")[0] if packed else None
+    n = idx.numel() if packed else B * S
+    rows = torch.tensor(sorted({0, 1, n // 2, n - 3, n - 1, 2}), dtype=torch.long)
+    res = []
+    for sel in (None, rows):
+        for p in m.lora_parameters():
+            p.grad = None
+        h = m(pid, kv_start=start, packed_idx=idx, out_rows=sel)
+        if sel is None:
+            h = h[rows]
+        (h * torch.linspace(-1, 1, h.shape[1])).sum().backward()
+        res.append((h.detach(), [p.grad.clone() for p in m.lora_parameters()]))
+    assert res[1][0].shape == (rows.numel(), cfg.hidden_size)
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-5, atol=1e-5)
+    for ga, gb in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=2e-5)
+    # prefill: hidden of the last position of every row == the full forward's
+    if not packed:
+        with torch.no_grad():
+            cache = KVCache(cfg.num_layers, B, cfg.num_kv_heads, S + 4, cfg.head_dim, "cpu", torch.float32)
+            hp = m.prefill(pid, start, cache)
+            hf = m(pid, kv_start=start)
+        torch.testing.assert_close(hp, hf[torch.arange(B) * S + S - 1], rtol=1e-5, atol=1e-5)
