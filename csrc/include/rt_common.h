@@ -166,6 +166,34 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return v;
 }
 
+// Sum of `ns` fp32 split-K slabs of 8 consecutive floats (slab q at p + q * stride), added in
+// slab order from slab 0 (bitwise equal to a rolled `for q` loop). The loads of the first 8 slabs
+// are issued unconditionally (indices clamped to ns - 1, the surplus ones hit cache) before the
+// first add: ONE L2/MALL round trip, where a rolled loop with a runtime trip count waits for every
+// slab's loads in turn (docs/DESIGN.md 'A rolled reduction loop ... Unroll it').
+__device__ __forceinline__ void sum_slabs8(const float* p, long stride, int ns, float (&out)[8]) {
+  float4 lo[8], hi[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float* sp = p + (long)min(q, ns - 1) * stride;
+    lo[q] = *(const float4*)sp;
+    hi[q] = *(const float4*)(sp + 4);
+  }
+  out[0] = lo[0].x; out[1] = lo[0].y; out[2] = lo[0].z; out[3] = lo[0].w;
+  out[4] = hi[0].x; out[5] = hi[0].y; out[6] = hi[0].z; out[7] = hi[0].w;
+#pragma unroll
+  for (int q = 1; q < 8; ++q)
+    if (q < ns) {
+      out[0] += lo[q].x; out[1] += lo[q].y; out[2] += lo[q].z; out[3] += lo[q].w;
+      out[4] += hi[q].x; out[5] += hi[q].y; out[6] += hi[q].z; out[7] += hi[q].w;
+    }
+  for (int q = 8; q < ns; ++q) {
+    const float4 a = *(const float4*)(p + (long)q * stride), b = *(const float4*)(p + (long)q * stride + 4);
+    out[0] += a.x; out[1] += a.y; out[2] += a.z; out[3] += a.w;
+    out[4] += b.x; out[5] += b.y; out[6] += b.z; out[7] += b.w;
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

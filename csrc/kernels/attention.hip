@@ -615,6 +615,9 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
     const bf16_t* vbase = a.vc + ((long)b * a.Hkv + hk) * a.Smax * D;
     KVChunk<D, NK> ca, cb;
     load_chunk<D, NK>(ca, kbase, vbase, p0, p1, wid, sub, dl);
+    // the second chunk is issued with the first, before q (waiting for q drains both): a
+    // partition of <= 2 chunks (the batch-1 partition plan) costs one memory round trip, not two
+    if (p0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, p0 + CH, p1, wid, sub, dl);
     float qv[G][8];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) rope_chunk<D>(row + (long)(hk * G + gg) * D, dl, a, p, qv[gg]);
@@ -640,7 +643,7 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
       for (int e = 0; e < 8; ++e) acc[gg][e] = 0.f;
     }
     for (int c0 = p0; c0 < p1; c0 += 2 * CH) {
-      if (c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl);
+      if (c0 != p0 && c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl);
       consume_chunk<D, G, NK>(ca, c0, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
       if (c0 + CH < p1) {
         if (c0 + 2 * CH < p1) load_chunk<D, NK>(ca, kbase, vbase, c0 + 2 * CH, p1, wid, sub, dl);
@@ -816,14 +819,8 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a)
     for (int ch = lane; ch < NCHK; ch += 64) {
       const int seg = ch / (D / 8), c8 = ch % (D / 8);
       const int head = seg < G ? hk * G + seg : (seg == G ? a.Hq + hk : a.Hq + a.Hkv + hk);
-      const float* sp = a.qkv_slabs + (long)b * a.ldq + (long)head * D + c8 * 8;
-      float4 a0 = *(const float4*)sp, a1 = *(const float4*)(sp + 4);
-      for (int q = 1; q < a.qkv_nsplit; ++q) {
-        const float4 b0 = *(const float4*)(sp + q * a.qkv_sstride), b1 = *(const float4*)(sp + q * a.qkv_sstride + 4);
-        a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
-        a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
-      }
-      const float t8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      float t8[8];
+      sum_slabs8(a.qkv_slabs + (long)b * a.ldq + (long)head * D + c8 * 8, a.qkv_sstride, a.qkv_nsplit, t8);
       *(uint4*)(qkv_st + seg * D + c8 * 8) = pack8(t8);
     }
     qrow = qkv_st + min(r16, G - 1) * D;

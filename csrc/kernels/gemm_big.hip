@@ -698,17 +698,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const int m = (int)(e / cpr), c0 = (int)(e % cpr) * 8;
   const long sstride = (long)M * N;
   float a[8], b[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) a[q] = b[q] = 0.f;
   const float* base = slabs + (long)m * N + c0;
-  for (int s = 0; s < nsplit; ++s) {
-    const float4 x0 = *(const float4*)(base + s * sstride), x1 = *(const float4*)(base + s * sstride + 4);
-    a[0] += x0.x; a[1] += x0.y; a[2] += x0.z; a[3] += x0.w; a[4] += x1.x; a[5] += x1.y; a[6] += x1.z; a[7] += x1.w;
-    if (swiglu) {
-      const float4 y0 = *(const float4*)(base + s * sstride + Nout), y1 = *(const float4*)(base + s * sstride + Nout + 4);
-      b[0] += y0.x; b[1] += y0.y; b[2] += y0.z; b[3] += y0.w; b[4] += y1.x; b[5] += y1.y; b[6] += y1.z; b[7] += y1.w;
-    }
-  }
+  sum_slabs8(base, sstride, nsplit, a);
+  if (swiglu) sum_slabs8(base + Nout, sstride, nsplit, b);
   float y[8];
   if (swiglu) {
 #pragma unroll

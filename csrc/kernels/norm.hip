@@ -45,14 +45,8 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nv) {
       if (xs) {
-        const float* sp = xs + row * H + c * 8;
-        float4 a0 = *(const float4*)sp, a1 = *(const float4*)(sp + 4);
-        for (int q = 1; q < nsplit; ++q) {
-          const float4 b0 = *(const float4*)(sp + q * sstride), b1 = *(const float4*)(sp + q * sstride + 4);
-          a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
-          a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
-        }
-        const float t8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        float t8[8];
+        sum_slabs8(xs + row * H + c * 8, sstride, nsplit, t8);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[i][k] = bf2f(f2bf(t8[k]));  // = the reduce kernel's bf16 output
       } else {
