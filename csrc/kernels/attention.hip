@@ -476,6 +476,7 @@ struct DecodeFusedArgs {
   // optional: qkv as nsplit fp32 split-K slabs [nsplit][B][ldq] (the qkv GEMM's reduce fused into
   // the MFMA kernel's prologue); qkv above is then unused
   const float* qkv_slabs; int qkv_nsplit; long qkv_sstride;
+  int kv_nt;                        // MFMA kernel: non-temporal K/V cache loads (each read once per step)
 };
 
 template <int D>
@@ -518,13 +519,22 @@ struct KVChunk {
 
 template <int D, int NK>
 __device__ __forceinline__ void load_chunk(KVChunk<D, NK>& c, const bf16_t* kbase, const bf16_t* vbase, int c0,
-                                           int p1, int wid, int sub, int dl) {
+                                           int p1, int wid, int sub, int dl, bool nt) {
   constexpr int KPW = 64 / (D / 8);
+  if (nt) {
 #pragma unroll
-  for (int i = 0; i < NK; ++i) {
-    const int key = min(c0 + (i * 4 + wid) * KPW + sub, p1 - 1);
-    c.k[i] = *(const uint4*)(kbase + (long)key * D + dl * 8);
-    c.v[i] = *(const uint4*)(vbase + (long)key * D + dl * 8);
+    for (int i = 0; i < NK; ++i) {
+      const int key = min(c0 + (i * 4 + wid) * KPW + sub, p1 - 1);
+      c.k[i] = load_nt16(kbase + (long)key * D + dl * 8);
+      c.v[i] = load_nt16(vbase + (long)key * D + dl * 8);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+      const int key = min(c0 + (i * 4 + wid) * KPW + sub, p1 - 1);
+      c.k[i] = *(const uint4*)(kbase + (long)key * D + dl * 8);
+      c.v[i] = *(const uint4*)(vbase + (long)key * D + dl * 8);
+    }
   }
 }
 
@@ -614,10 +624,10 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
     const bf16_t* kbase = a.kc + ((long)b * a.Hkv + hk) * a.Smax * D;
     const bf16_t* vbase = a.vc + ((long)b * a.Hkv + hk) * a.Smax * D;
     KVChunk<D, NK> ca, cb;
-    load_chunk<D, NK>(ca, kbase, vbase, p0, p1, wid, sub, dl);
+    load_chunk<D, NK>(ca, kbase, vbase, p0, p1, wid, sub, dl, a.kv_nt);
     // the second chunk is issued with the first, before q (waiting for q drains both): a
     // partition of <= 2 chunks (the batch-1 partition plan) costs one memory round trip, not two
-    if (p0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, p0 + CH, p1, wid, sub, dl);
+    if (p0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, p0 + CH, p1, wid, sub, dl, a.kv_nt);
     float qv[G][8];
 #pragma unroll
     for (int gg = 0; gg < G; ++gg) rope_chunk<D>(row + (long)(hk * G + gg) * D, dl, a, p, qv[gg]);
@@ -643,10 +653,10 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
       for (int e = 0; e < 8; ++e) acc[gg][e] = 0.f;
     }
     for (int c0 = p0; c0 < p1; c0 += 2 * CH) {
-      if (c0 != p0 && c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl);
+      if (c0 != p0 && c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl, a.kv_nt);
       consume_chunk<D, G, NK>(ca, c0, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
       if (c0 + CH < p1) {
-        if (c0 + 2 * CH < p1) load_chunk<D, NK>(ca, kbase, vbase, c0 + 2 * CH, p1, wid, sub, dl);
+        if (c0 + 2 * CH < p1) load_chunk<D, NK>(ca, kbase, vbase, c0 + 2 * CH, p1, wid, sub, dl, a.kv_nt);
         consume_chunk<D, G, NK>(cb, c0 + CH, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
       }
     }
@@ -793,12 +803,19 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a)
   struct Tile { uint4 k[DS]; uint4 v[4]; };
   auto load = [&](Tile& T, int c0) {
     const long keyk = min(c0 + r16, len - 1);
+    if (a.kv_nt) {
 #pragma unroll
-    for (int s2 = 0; s2 < DS; ++s2) T.k[s2] = *(const uint4*)(kbase + keyk * D + 32 * s2 + 8 * g);
+      for (int s2 = 0; s2 < DS; ++s2) T.k[s2] = load_nt16(kbase + keyk * D + 32 * s2 + 8 * g);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const long key = min(c0 + 4 * i + g, len - 1);
-      T.v[i] = *(const uint4*)(vbase + key * D + 8 * r16);
+      for (int i = 0; i < 4; ++i) T.v[i] = load_nt16(vbase + (long)min(c0 + 4 * i + g, len - 1) * D + 8 * r16);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < DS; ++s2) T.k[s2] = *(const uint4*)(kbase + keyk * D + 32 * s2 + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long key = min(c0 + 4 * i + g, len - 1);
+        T.v[i] = *(const uint4*)(vbase + key * D + 8 * r16);
+      }
     }
   };
   Tile ta, tb;
@@ -1049,7 +1066,7 @@ __global__ __launch_bounds__(256) void attn_o_fused_kernel(AttnOArgs args) {
       const bf16_t* kbase = a.kc + (long)hk * a.Smax * D;
       const bf16_t* vbase = a.vc + (long)hk * a.Smax * D;
       KVChunk<D, NK> ca, cb;
-      load_chunk<D, NK>(ca, kbase, vbase, p0, p1, wid, sub, dl);
+      load_chunk<D, NK>(ca, kbase, vbase, p0, p1, wid, sub, dl, a.kv_nt);
       float qv[G][8];
 #pragma unroll
       for (int gg = 0; gg < G; ++gg) rope_chunk<D>(a.qkv + (long)(hk * G + gg) * D, dl, a, p, qv[gg]);
@@ -1075,10 +1092,10 @@ __global__ __launch_bounds__(256) void attn_o_fused_kernel(AttnOArgs args) {
         for (int e = 0; e < 8; ++e) acc[gg][e] = 0.f;
       }
       for (int c0 = p0; c0 < p1; c0 += 2 * CH) {
-        if (c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl);
+        if (c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl, a.kv_nt);
         consume_chunk<D, G, NK>(ca, c0, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
         if (c0 + CH < p1) {
-          if (c0 + 2 * CH < p1) load_chunk<D, NK>(ca, kbase, vbase, c0 + 2 * CH, p1, wid, sub, dl);
+          if (c0 + 2 * CH < p1) load_chunk<D, NK>(ca, kbase, vbase, c0 + 2 * CH, p1, wid, sub, dl, a.kv_nt);
           consume_chunk<D, G, NK>(cb, c0 + CH, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
         }
       }
@@ -1716,6 +1733,10 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   a.B = B; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
   a.qkv_slabs = g_dec_qkv_slabs; a.qkv_nsplit = g_dec_qkv_nsplit; a.qkv_sstride = (long)B * ldq;
   g_dec_qkv_slabs = nullptr;  // one launch only
+  // K/V cache bytes are read once per decode step: non-temporal loads (batch 256: 56 -> 50 us per
+  // layer, profiles/decode_nt_ab.log); RT_ATTN_KV_NT=0 for A/B runs
+  static const int kv_nt_env = getenv("RT_ATTN_KV_NT") ? atoi(getenv("RT_ATTN_KV_NT")) : 1;
+  a.kv_nt = kv_nt_env;
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -1;
@@ -1805,7 +1826,7 @@ extern "C" int rt_attn_o_fused(const void* qkv, void* kc, void* vc, int Smax, co
   a.slot = slot; a.attn_len = attn_len; a.kv_start = kv_start; a.pos = pos; a.cosT = cosT; a.sinT = sinT;
   a.sign = sign; a.window = window; a.part = part; a.tickets = nullptr; a.o = nullptr; a.ldo = 0;
   a.B = 1; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
-  a.qkv_slabs = nullptr; a.qkv_nsplit = 0; a.qkv_sstride = 0;
+  a.qkv_slabs = nullptr; a.qkv_nsplit = 0; a.qkv_sstride = 0; a.kv_nt = 0;
   g.w = (const bf16_t*)w; g.ldw = ldw; g.res = (const bf16_t*)res; g.out = (bf16_t*)out; g.H = H;
   g.sync = sync; g.err = err; g.stamps = g_ao_stamps;
   const int G = Hq / Hkv;

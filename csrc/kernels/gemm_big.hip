@@ -66,6 +66,7 @@ struct Args {
   int act;
   int nsplit;                     // split-K factor (gridDim.y)
   const bf16_t* zpage;            // >= 128 zero bytes
+  int b_nt;                       // B (weight) stream read once per launch: non-temporal LDS-DMA
 };
 
 __device__ __forceinline__ int row_swz(int row) { return (row >> 1) & 7; }
@@ -199,9 +200,18 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       const long adv = ((op ? LB : LA) == ROW) ? (long)k0 : (long)k0 * (op ? p.ldb : p.lda);
       const bf16_t* base = (op ? p.B : p.A) + adv;
       if (k0 + 64 <= p.K) {
+        if (op && p.b_nt) {
+          // a single row tile (M <= 256, decode): every weight byte is read by ONE workgroup once
+          // per launch and the other layers' weights evict it before the next step
+          // (MI355X_MICROARCH.md 'nt-weights')
 #pragma unroll
-        for (int j = 0; j < (op ? NB : 2); ++j)
-          __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+          for (int j = 0; j < NB; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 2);
+        } else {
+#pragma unroll
+          for (int j = 0; j < (op ? NB : 2); ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+        }
       } else {  // ragged reduction tail: out-of-range k reads the zero page
 #pragma unroll
         for (int j = 0; j < (op ? NB : 2); ++j) {
@@ -848,6 +858,10 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = (bf16_t*)C2; p.ldc2 = ldc2;
   p.R = (const bf16_t*)R; p.ldr = ldr;
   p.M = M; p.N = N; p.K = K; p.act = act; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
+  // non-temporal weight stream when one row tile covers M (each B byte read once per launch);
+  // RT_GEMM_B_NT=0/1 forces it off/on for A/B runs
+  static const int bnt_env = getenv("RT_GEMM_B_NT") ? atoi(getenv("RT_GEMM_B_NT")) : -1;
+  p.b_nt = layout_b == ROW && (bnt_env >= 0 ? bnt_env : (M <= 256 ? 1 : 0));
   if (bn != 0) return launch_gemm_big(p, layout_a, layout_b, act, out, bn, stream);
   // ---- plan: m1 row tiles at BN = 256, the rest at BN = 128 ----
   const int tiles_m = (M + 255) / 256;
