@@ -858,10 +858,10 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = (bf16_t*)C2; p.ldc2 = ldc2;
   p.R = (const bf16_t*)R; p.ldr = ldr;
   p.M = M; p.N = N; p.K = K; p.act = act; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
-  // non-temporal weight stream when one row tile covers M (each B byte read once per launch);
-  // RT_GEMM_B_NT=0/1 forces it off/on for A/B runs
-  static const int bnt_env = getenv("RT_GEMM_B_NT") ? atoi(getenv("RT_GEMM_B_NT")) : -1;
-  p.b_nt = layout_b == ROW && (bnt_env >= 0 ? bnt_env : (M <= 256 ? 1 : 0));
+  // RT_GEMM_B_NT=1: non-temporal weight stream when one row tile covers M (each B byte read once
+  // per launch). Measured neutral on the batch-256 decode GEMMs (profiles/decode_nt_ab.log): off
+  static const int bnt_env = getenv("RT_GEMM_B_NT") ? atoi(getenv("RT_GEMM_B_NT")) : 0;
+  p.b_nt = layout_b == ROW && M <= 256 && bnt_env > 0;
   if (bn != 0) return launch_gemm_big(p, layout_a, layout_b, act, out, bn, stream);
   // ---- plan: m1 row tiles at BN = 256, the rest at BN = 128 ----
   const int tiles_m = (M + 255) / 256;
