@@ -499,7 +499,8 @@ __device__ __forceinline__ void rope_chunk(const bf16_t* head, int dl, const Dec
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float sv = a.sign * sn[k];
-      out[k] = lo ? x[k] * cs[k] - y[k] * sv : x[k] * cs[k] + y[k] * sv;
+      // explicit fma order shared by every RoPE site (rope_qkv_kernel): bitwise-equal appends
+      out[k] = fmaf(x[k], cs[k], lo ? -(y[k] * sv) : y[k] * sv);
     }
   } else {
 #pragma unroll
@@ -779,12 +780,20 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
 // k_new and the cache append are fused; lanes whose (clamped) key is the new token's slot use
 // k_new / v_new from registers. Measured at batch 256 (Mistral-7B, 174..301 keys): 51 us per
 // layer vs 80 us for the VALU kernel (profiles/decode_attn_r2_mfma.log).
-template <int G>
-__global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a) {
+//
+// W > 1 (small batch, B * Hkv < 256 — the batch-1 RAG answer path): W waves share one (batch, kv
+// head); wave w takes the 16-key tiles w, w + W, w + 2W, ... (its first two tiles' loads issued
+// with the prologue's), and the W partial (m, l, O) states merge through LDS in the same launch —
+// no cross-workgroup partition combine, so a layer's attention is one memory round trip plus a
+// workgroup barrier instead of the split kernel's publish / ticket / merge chain.
+template <int G, int W>
+__global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArgs a) {
   constexpr int D = 128, DS = D / 32, DT = D / 16;
-  __shared__ __attribute__((aligned(16))) char vimg[32 * D * 2];  // rows 16..31 stay zero
-  __shared__ __attribute__((aligned(16))) bf16_t qkv_st[(G + 2) * D];  // slab path: reduced q | k | v
-  const int lane = threadIdx.x, g = lane >> 4, r16 = lane & 15;
+  __shared__ __attribute__((aligned(16))) char vimg_all[W][32 * D * 2];  // per wave; rows 16..31 stay zero
+  __shared__ __attribute__((aligned(16))) bf16_t qkv_st[(G + 2) * D];  // slab path (W == 1): reduced q | k | v
+  const int lane = threadIdx.x & 63, g = lane >> 4, r16 = lane & 15;
+  const int w = W > 1 ? (int)(threadIdx.x >> 6) : 0;
+  char* vimg = vimg_all[w];
   const int b = blockIdx.x / a.Hkv, hk = blockIdx.x % a.Hkv;
   const int len = a.attn_len[b];
   const int s_new = a.slot[b];
@@ -818,8 +827,11 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a)
       }
     }
   };
-  Tile ta, tb;
-  if (kbeg < len) load(ta, kbeg);
+  Tile ta, tb, tc;
+  const int cfirst = kbeg + 16 * w, cstep = 16 * W;  // this wave's tiles: cfirst + j * cstep
+  if (cfirst < len) load(ta, cfirst);
+  if (W > 1 && cfirst + cstep < len) load(tb, cfirst + cstep);
+  if (W > 1 && cfirst + 2 * cstep < len) load(tc, cfirst + 2 * cstep);
 
   // ---- q / k_new / v_new and the rotary tables, all loads at once. D = 128: chunk 4 s + g's
   // rotary partner (chunk ^ 8) is the lane's own chunk 4 (s ^ 2) + g, its table offset
@@ -875,7 +887,7 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float t = a.sign * sv[e];
-      o8[e] = lo ? x[e] * cs[e] - y[e] * t : x[e] * cs[e] + y[e] * t;
+      o8[e] = fmaf(x[e], cs[e], lo ? -(y[e] * t) : y[e] * t);  // = rope_qkv_kernel's rounding
     }
     return pack8(o8);
   };
@@ -887,8 +899,8 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a)
     qf[s2] = __builtin_bit_cast(bf16x8, r16 < G ? qv : make_uint4(0, 0, 0, 0));
     knew[s2] = rope8(kraw[s2], kraw[s2 ^ 2], cq[s2 & 1], sq[s2 & 1], s2 < 2);
   }
-  // cache append: lane (g, 0) stores its 4 k chunks 4 s + g, lane group 1 the v chunks
-  if (has_new) {
+  // cache append: lane (g, 0) stores its 4 k chunks 4 s + g, lane group 1 the v chunks (wave 0)
+  if (has_new && w == 0) {
     bf16_t* kdst = a.kc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
     bf16_t* vdst = a.vc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
     if (r16 == 0) {
@@ -966,24 +978,78 @@ __global__ __launch_bounds__(64) void attn_decode_mfma_kernel(DecodeFusedArgs a)
     }
   };
 
-  for (int c0 = kbeg; c0 < len; c0 += 32) {
-    if (c0 + 16 < len) load(tb, c0 + 16);
-    consume(ta, c0);
-    if (c0 + 16 < len) {
-      if (c0 + 32 < len) load(ta, c0 + 32);
-      consume(tb, c0 + 16);
+  if constexpr (W == 1) {
+    for (int c0 = cfirst; c0 < len; c0 += 2 * cstep) {
+      if (c0 + cstep < len) load(tb, c0 + cstep);
+      consume(ta, c0);
+      if (c0 + cstep < len) {
+        if (c0 + 2 * cstep < len) load(ta, c0 + 2 * cstep);
+        consume(tb, c0 + cstep);
+      }
+    }
+  } else {
+    // three tiles in flight (all of a wave's tiles at up to 24 W keys: one memory round trip);
+    // a register set is refilled right after its tile is consumed
+    for (int c0 = cfirst; c0 < len; c0 += 3 * cstep) {
+      consume(ta, c0);
+      if (c0 + 3 * cstep < len) load(ta, c0 + 3 * cstep);
+      if (c0 + cstep < len) {
+        consume(tb, c0 + cstep);
+        if (c0 + 4 * cstep < len) load(tb, c0 + 4 * cstep);
+      }
+      if (c0 + 2 * cstep < len) {
+        consume(tc, c0 + 2 * cstep);
+        if (c0 + 5 * cstep < len) load(tc, c0 + 5 * cstep);
+      }
     }
   }
-  // ---- normalise and store: lane holds O[head 4 g + i][d = 16 c + r16] ----
+  if constexpr (W == 1) {
+    // ---- normalise and store: lane holds O[head 4 g + i][d = 16 c + r16] ----
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int h = 4 * g + i;
-    const float lh = __shfl(l, h, 64);
-    const float inv = lh > 0.f ? 1.f / lh : 0.f;
-    if (h < G) {
-      bf16_t* orow = a.o + (long)b * a.ldo + (long)(hk * G + h) * D;
+    for (int i = 0; i < 4; ++i) {
+      const int h = 4 * g + i;
+      const float lh = __shfl(l, h, 64);
+      const float inv = lh > 0.f ? 1.f / lh : 0.f;
+      if (h < G) {
+        bf16_t* orow = a.o + (long)b * a.ldo + (long)(hk * G + h) * D;
 #pragma unroll
-      for (int c = 0; c < DT; ++c) orow[16 * c + r16] = f2bf(o[c][i] * inv);
+        for (int c = 0; c < DT; ++c) orow[16 * c + r16] = f2bf(o[c][i] * inv);
+      }
+    }
+  } else {
+    // ---- merge the W waves' states (m = -inf, l = 0 for a wave without tiles) ----
+    __shared__ float mst[W][16], lst[W][16];
+    __shared__ float ost[W][G][D];
+    if (g == 0) {
+      mst[w][r16] = m;
+      lst[w][r16] = l;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = 4 * g + i;
+      if (h < G) {
+#pragma unroll
+        for (int c = 0; c < DT; ++c) ost[w][h][16 * c + r16] = o[c][i];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < G * D; e += 64 * W) {
+      const int h = e / D, d = e % D;
+      float M = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < W; ++q) M = fmaxf(M, mst[q][h]);
+      float L = 0.f, O = 0.f;
+      if (M != -INFINITY) {
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+          const float mq = mst[q][h];
+          if (mq == -INFINITY) continue;
+          const float f = exp2f(mq - M);
+          L += lst[q][h] * f;
+          O += ost[q][h][d] * f;
+        }
+      }
+      a.o[(long)b * a.ldo + (long)(hk * G + h) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
     }
   }
 }
@@ -1715,6 +1781,14 @@ extern "C" void rt_attn_decode_set_nk(int nk) { g_dec_nk = nk; }
 static const float* g_dec_qkv_slabs = nullptr;
 static int g_dec_qkv_nsplit = 0;
 extern "C" void rt_attn_decode_set_qkv_slabs(const float* p, int nsplit) { g_dec_qkv_slabs = p; g_dec_qkv_nsplit = nsplit; }
+// waves per (batch, kv head) of the small-batch MFMA decode attention; caches up to 1024 slots
+// (<= 8 tiles per wave: the 2-tile register prefetch still covers the memory round trip)
+constexpr int DEC_MW = 8;
+static bool rt_attn_decode_mw_ok(int B, int Hq, int Hkv, int D, int Smax) {
+  static const int use_mw = getenv("RT_DECODE_MW") ? atoi(getenv("RT_DECODE_MW")) : 1;
+  const int G = Hkv ? Hq / Hkv : 0;
+  return use_mw && D == 128 && (long)B * Hkv < 256 && Smax <= 1024 && (G == 1 || G == 2 || G == 4 || G == 8);
+}
 extern "C" int rt_attn_decode_mfma_ok(int B, int Hq, int Hkv, int D, int NP) {
   static const int use_mfma = getenv("RT_DECODE_MFMA") ? atoi(getenv("RT_DECODE_MFMA")) : 1;
   const int G = Hkv ? Hq / Hkv : 0;
@@ -1744,11 +1818,23 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   if (rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
     dim3 mgrid((unsigned)(B * Hkv)), mblock(64);
     switch (G) {
-      case 1: hipLaunchKernelGGL(attn_decode_mfma_kernel<1>, mgrid, mblock, 0, stream, a); break;
-      case 2: hipLaunchKernelGGL(attn_decode_mfma_kernel<2>, mgrid, mblock, 0, stream, a); break;
-      case 4: hipLaunchKernelGGL(attn_decode_mfma_kernel<4>, mgrid, mblock, 0, stream, a); break;
-      case 8: hipLaunchKernelGGL(attn_decode_mfma_kernel<8>, mgrid, mblock, 0, stream, a); break;
-      default: hipLaunchKernelGGL(attn_decode_mfma_kernel<16>, mgrid, mblock, 0, stream, a); break;
+      case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, 1>), mgrid, mblock, 0, stream, a); break;
+      case 2: hipLaunchKernelGGL((attn_decode_mfma_kernel<2, 1>), mgrid, mblock, 0, stream, a); break;
+      case 4: hipLaunchKernelGGL((attn_decode_mfma_kernel<4, 1>), mgrid, mblock, 0, stream, a); break;
+      case 8: hipLaunchKernelGGL((attn_decode_mfma_kernel<8, 1>), mgrid, mblock, 0, stream, a); break;
+      default: hipLaunchKernelGGL((attn_decode_mfma_kernel<16, 1>), mgrid, mblock, 0, stream, a); break;
+    }
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
+  // small batch, short caches: 8 waves per (batch, kv head), merged in LDS (RT_DECODE_MW=0 disables)
+  if (rt_attn_decode_mw_ok(B, Hq, Hkv, D, Smax) && !a.qkv_slabs) {
+    dim3 mgrid((unsigned)(B * Hkv)), mblock(64 * DEC_MW);
+    switch (G) {
+      case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, DEC_MW>), mgrid, mblock, 0, stream, a); break;
+      case 2: hipLaunchKernelGGL((attn_decode_mfma_kernel<2, DEC_MW>), mgrid, mblock, 0, stream, a); break;
+      case 4: hipLaunchKernelGGL((attn_decode_mfma_kernel<4, DEC_MW>), mgrid, mblock, 0, stream, a); break;
+      default: hipLaunchKernelGGL((attn_decode_mfma_kernel<8, DEC_MW>), mgrid, mblock, 0, stream, a); break;
     }
     RT_LAUNCH_CHECK();
     return 0;

@@ -45,8 +45,9 @@ __global__ __launch_bounds__(256) void rope_qkv_kernel(bf16_t* __restrict__ qkv,
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float x1 = a[k], x2 = b[k], s = sign * sn[k];
-      a[k] = x1 * cs[k] - x2 * s;
-      b[k] = x2 * cs[k] + x1 * s;
+      // explicit fma order (the fused decode kernels round identically: bitwise-equal cache appends)
+      a[k] = fmaf(x1, cs[k], -(x2 * s));
+      b[k] = fmaf(x2, cs[k], x1 * s);
     }
     *(uint4*)(row + e1) = pack8(a);
     *(uint4*)(row + e2) = pack8(b);

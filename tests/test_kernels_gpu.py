@@ -586,6 +586,8 @@ def test_gemm_256_identity():
 @pytest.mark.parametrize("B,Hq,Hkv,D,Smax,rot,window", [(1, 32, 8, 128, 456, True, 0), (64, 32, 8, 128, 456, True, 0),
                                                         (3, 8, 8, 64, 200, False, 0), (5, 8, 2, 32, 300, True, 64),
                                                         (2, 16, 2, 128, 64, True, 0),
+                                                        # B * Hkv < 256, D = 128: the 8-wave MFMA kernel (window; G = 2)
+                                                        (3, 32, 8, 128, 300, True, 100), (3, 16, 8, 128, 300, True, 0),
                                                         # B * Hkv >= 256: the MFMA kernel (G = 4, 8, 1)
                                                         (40, 32, 8, 128, 300, True, 64), (32, 64, 8, 128, 200, True, 0),
                                                         (16, 16, 16, 128, 97, False, 0)])
