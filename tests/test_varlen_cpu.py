@@ -55,7 +55,7 @@ def test_score_sequences_packed_matches_padded(preset):
         torch.testing.assert_close(x * mask, y * mask, rtol=1e-5, atol=1e-5)
     assert float((b_lp * ~mask).abs().max()) == 0.0  # masked positions are zero in the packed form
     for ga, gb in zip(*grads):
-        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-5)  # fp32 summation order
 
 
 def test_score_sequences_no_padding_stays_unpacked(monkeypatch):
@@ -104,7 +104,7 @@ def test_sft_loss_packed_matches_padded(monkeypatch):
     assert res[0][1] == res[1][1]
     assert abs(res[0][0] - res[1][0]) < 1e-5
     for ga, gb in zip(res[0][2], res[1][2]):
-        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-5)  # fp32 summation order
 
 
 @pytest.mark.parametrize("preset", ["tiny-llama", "tiny-opt"])
