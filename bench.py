@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--new-tokens", type=int, default=128)
     ap.add_argument("--max-prompt", type=int, default=320)
     ap.add_argument("--minibatch", type=int, default=None, help="PPO minibatch (default 32; 16 for pipeline)")
+    ap.add_argument("--ref-minibatch", type=int, default=None,
+                    help="sequences per reference-scoring forward (default: PPOConfig.ref_minibatch_size)")
     ap.add_argument("--top-k-docs", type=int, default=3)
     ap.add_argument("--ndocs", type=int, default=100_000)
     ap.add_argument("--doc-words", type=int, default=48)
@@ -124,7 +126,8 @@ def main():
     # ---- PPO trainer ----
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
                    lora_r=16, lora_alpha=32.0, seed=0, rollout_chunks=1, overlap_reward=True,
-                   full_finetune=args.full_ft)
+                   full_finetune=args.full_ft,
+                   **({"ref_minibatch_size": args.ref_minibatch} if args.ref_minibatch else {}))
     trainer = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
     if args.no_graph:
         trainer.gen.use_graph = False
