@@ -799,6 +799,111 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batch-1 GEMV without split-K: one workgroup per 16 output rows of a tile-ordered weight image
+// ---------------------------------------------------------------------------------------------
+// The split-K decode kernel above ends in a serial hand-off (write-through slab stores drained,
+// an arrival ticket, the last arriver's slab loads): about three dependent device-memory round
+// trips after the last weight byte lands. Here a workgroup owns one 16-row group of the
+// tile-ordered image (its K chunks are ONE contiguous run of nc x 2 KiB) and its 4 waves split K;
+// the partial sums meet in LDS, so the tail is a workgroup barrier. N / 16 workgroups (256 for
+// o / down, 384 for qkv) fill the chip without a K split. Each wave keeps DEPTH - 1 k-chunks in
+// flight (non-temporal: every weight byte is read once per token). Same epilogue contract as
+// gemm_decode_kernel at M = 1: in-GEMM RMS norm (folded weight, rstd from the X fragments), bias,
+// activation (not SwiGLU), residual, bf16 / fp32 store.
+//
+// PAIR (SwiGLU, weight = [gate; up], 2F rows): the workgroup owns output columns [16 grp, 16 grp +
+// 16) and streams the gate row group grp and the up row group F / 16 + grp side by side.
+template <bool OUT_F32, int DEPTH, bool PAIR>
+__global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
+  __shared__ float red[4][PAIR ? 32 : 16];
+  __shared__ float rsq[4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int frow = lane & 15, g = lane >> 4;
+  const int grp = blockIdx.x;  // 16-row group (of the gate rows when PAIR)
+  const int nc = p.K / 64;
+  const int c_begin = wid * nc / 4, c_end = (wid + 1) * nc / 4;
+  const char* wbase = (const char*)p.B + (long)grp * nc * 2048 + lane * 16;
+  const char* ubase = PAIR ? (const char*)p.B + ((long)(p.N / 32) + grp) * nc * 2048 + lane * 16 : wbase;
+  const bf16_t* xrow = p.A + g * 8;
+  struct Regs { uint4 w0, w1, u0, u1, x0, x1; };
+  auto ld = [&](Regs& r, int c) {
+    r.w0 = load_nt16(wbase + (long)c * 2048);
+    r.w1 = load_nt16(wbase + (long)c * 2048 + 1024);
+    if constexpr (PAIR) {
+      r.u0 = load_nt16(ubase + (long)c * 2048);
+      r.u1 = load_nt16(ubase + (long)c * 2048 + 1024);
+    }
+    r.x0 = *(const uint4*)(xrow + c * 64);
+    r.x1 = *(const uint4*)(xrow + c * 64 + 32);
+  };
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f}, accu = acc;
+  float sq = 0.f;
+  const bool normed = p.norm_eps > 0.f;
+  auto mma = [&](const Regs& r) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x0), __builtin_bit_cast(bf16x8, r.w0), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x1), __builtin_bit_cast(bf16x8, r.w1), acc, 0, 0, 0);
+    if constexpr (PAIR) {
+      accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x0), __builtin_bit_cast(bf16x8, r.u0), accu, 0, 0, 0);
+      accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x1), __builtin_bit_cast(bf16x8, r.u1), accu, 0, 0, 0);
+    }
+    if (normed && frow == 0) {
+      float f[8];
+      unpack8(r.x0, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sq += f[e] * f[e];
+      unpack8(r.x1, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sq += f[e] * f[e];
+    }
+  };
+  Regs r[DEPTH];
+#pragma unroll
+  for (int i = 0; i < DEPTH - 1; ++i)
+    if (c_begin + i < c_end) ld(r[i], c_begin + i);
+  int c = c_begin;
+  for (; c + DEPTH <= c_end; c += DEPTH) {
+#pragma unroll
+    for (int i = 0; i < DEPTH; ++i) {
+      if (c + i + DEPTH - 1 < c_end) ld(r[(i + DEPTH - 1) % DEPTH], c + i + DEPTH - 1);
+      mma(r[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < DEPTH - 1; ++i)
+    if (c + i < c_end) mma(r[i]);
+  // acc[0] of lanes 0..15 (g = 0) = C[row 0][16 grp + frow] over this wave's k range; X row
+  // sums of squares live in the g lanes of frow 0
+  if (g == 0) {
+    red[wid][frow] = acc[0];
+    if constexpr (PAIR) red[wid][16 + frow] = accu[0];
+  }
+  if (normed) {
+    float t = sq;
+    t += __shfl_xor(t, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    if (lane == 0) rsq[wid] = t;
+  }
+  __syncthreads();
+  if (tid < 16) {
+    const int col = grp * 16 + tid;
+    const float rs = normed ? rsqrtf((rsq[0] + rsq[1] + rsq[2] + rsq[3]) / (float)p.K + p.norm_eps) : 1.f;
+    float y = (red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]) * rs;
+    if constexpr (PAIR) {
+      const int F = p.N / 2;
+      float up = (red[0][16 + tid] + red[1][16 + tid] + red[2][16 + tid] + red[3][16 + tid]) * rs;
+      if (p.bias) { y += bf2f(p.bias[col]); up += bf2f(p.bias[F + col]); }
+      y = y / (1.f + __expf(-y)) * up;
+    } else {
+      if (p.bias) y += bf2f(p.bias[col]);
+      y = apply_act(y, p.act);
+      if (p.R) y += bf2f(p.R[col]);
+    }
+    if constexpr (OUT_F32) ((float*)p.C)[col] = y;
+    else ((bf16_t*)p.C)[col] = f2bf(y);
+  }
+}
+
 // Shared tail of the M <= 64 kernels: split-K hand-off (write-through slabs + ticket, last arriver
 // reduces), in-GEMM RMS-norm scaling, SwiGLU pair / bias + activation + residual epilogues.
 // acc[j][r] = C[16 wid + 4 fq + r][16 j + frow] of the block's 64 columns; sq = sum of squares of
@@ -1074,6 +1179,17 @@ extern "C" void rt_gemm_set_decode_split(int s) { g_decode_split = s; }
 // 52.6; profiles/kernels_decode_depth_shuffle.log): the default stays 2. 2 / 4 force (tuning).
 static int g_decode_depth = 0;
 extern "C" void rt_gemm_set_decode_depth(int d) { g_decode_depth = d; }
+// batch-1 GEMVs on the 16-row no-split kernel: narrow outputs (qkv, o, down) whose split-K tail
+// costs more than a second round of workgroups; RT_GEMV16=0 keeps them on gemm_decode_kernel
+// RT_GEMV16: 0 off, 1 narrow outputs only (N <= 8192: qkv, o, down), 2 also wide ones (SwiGLU
+// gate_up, lm_head)
+static bool use_gemv16(int N, int K, int act) {
+  static const int env = getenv("RT_GEMV16") ? atoi(getenv("RT_GEMV16")) : 2;
+  if (!env || K % 64 || K < 1024) return false;
+  if (act == ACT_SWIGLU) return env >= 2 && N % 32 == 0 && N / 32 >= 256;
+  return N % 16 == 0 && N / 16 >= 256 && (N <= 8192 || env >= 2);
+}
+
 static int decode_depth(int MT, long blocks) {
   if (MT > 1) return 2;
   if (g_decode_depth == 2 || g_decode_depth == 4) return g_decode_depth;
@@ -1120,6 +1236,14 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
     dim3 grid(((N + 63) / 64) * split), block(256);
     if (out_f32) hipLaunchKernelGGL((gemm_m64_kernel<true>), grid, block, 0, stream, p, slabs, tickets, split);
     else hipLaunchKernelGGL((gemm_m64_kernel<false>), grid, block, 0, stream, p, slabs, tickets, split);
+  } else if (M == 1 && wshuf && g_decode_split == 0 && use_gemv16(N, K, act) && p.Rp == 0) {
+    const bool pair = act == ACT_SWIGLU;
+    dim3 grid(pair ? N / 32 : N / 16), block(256);
+    static const int gd = getenv("RT_GEMV16_DEPTH") ? atoi(getenv("RT_GEMV16_DEPTH")) : 4;
+#define G16(D, P) if (out_f32) hipLaunchKernelGGL((gemv16_kernel<true, D, P>), grid, block, 0, stream, p); \
+                  else hipLaunchKernelGGL((gemv16_kernel<false, D, P>), grid, block, 0, stream, p);
+    if (pair) { G16(4, true) } else if (gd == 6) { G16(6, false) } else if (gd == 8) { G16(8, false) } else { G16(4, false) }
+#undef G16
   } else if (M <= 64) {
     const int MT = (M + 15) / 16;
     const int want = wshuf ? decode_split_shuf(K) : decode_split(N, K);
