@@ -477,6 +477,7 @@ struct DecodeFusedArgs {
   // the MFMA kernel's prologue); qkv above is then unused
   const float* qkv_slabs; int qkv_nsplit; long qkv_sstride;
   int kv_nt;                        // MFMA kernel: non-temporal K/V cache loads (each read once per step)
+  long long* stamps;                // debug (W > 1 kernel): [blocks * W][8] s_memrealtime phase stamps, or null
 };
 
 template <int D>
@@ -794,6 +795,15 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
   const int lane = threadIdx.x & 63, g = lane >> 4, r16 = lane & 15;
   const int w = W > 1 ? (int)(threadIdx.x >> 6) : 0;
   char* vimg = vimg_all[w];
+  // debug phase stamps (a.stamps set by rt_attn_o_set_stamps): every load drained first
+  auto stamp = [&](int k) {
+    if (W > 1 && a.stamps) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const long long t = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) a.stamps[((long)blockIdx.x * W + w) * 8 + k] = t;
+    }
+  };
+  stamp(0);
   const int b = blockIdx.x / a.Hkv, hk = blockIdx.x % a.Hkv;
   const int len = a.attn_len[b];
   const int s_new = a.slot[b];
@@ -899,6 +909,7 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
     qf[s2] = __builtin_bit_cast(bf16x8, r16 < G ? qv : make_uint4(0, 0, 0, 0));
     knew[s2] = rope8(kraw[s2], kraw[s2 ^ 2], cq[s2 & 1], sq[s2 & 1], s2 < 2);
   }
+  stamp(1);  // q / k_new / v_new / tables and the first tiles landed, RoPE done
   // cache append: lane (g, 0) stores its 4 k chunks 4 s + g, lane group 1 the v chunks (wave 0)
   if (has_new && w == 0) {
     bf16_t* kdst = a.kc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
@@ -1017,6 +1028,7 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
       }
     }
   } else {
+    stamp(2);  // this wave's tiles consumed
     // ---- merge the W waves' states (m = -inf, l = 0 for a wave without tiles) ----
     __shared__ float mst[W][16], lst[W][16];
     __shared__ float ost[W][G][D];
@@ -1051,6 +1063,7 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
       }
       a.o[(long)b * a.ldo + (long)(hk * G + h) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
     }
+    stamp(3);
   }
 }
 
@@ -1781,6 +1794,8 @@ extern "C" void rt_attn_decode_set_nk(int nk) { g_dec_nk = nk; }
 static const float* g_dec_qkv_slabs = nullptr;
 static int g_dec_qkv_nsplit = 0;
 extern "C" void rt_attn_decode_set_qkv_slabs(const float* p, int nsplit) { g_dec_qkv_slabs = p; g_dec_qkv_nsplit = nsplit; }
+static long long* g_ao_stamps = nullptr;  // debug hook: per-block phase stamps (attn_o and 8-wave kernels)
+extern "C" void rt_attn_o_set_stamps(long long* p) { g_ao_stamps = p; }
 // waves per (batch, kv head) of the small-batch MFMA decode attention; caches up to 1024 slots
 // (<= 8 tiles per wave: the 2-tile register prefetch still covers the memory round trip)
 constexpr int DEC_MW = 8;
@@ -1811,6 +1826,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   // layer, profiles/decode_nt_ab.log); RT_ATTN_KV_NT=0 for A/B runs
   static const int kv_nt_env = getenv("RT_ATTN_KV_NT") ? atoi(getenv("RT_ATTN_KV_NT")) : 1;
   a.kv_nt = kv_nt_env;
+  a.stamps = g_ao_stamps;
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -1;
@@ -1896,8 +1912,7 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
   return 0;
 }
 
-static long long* g_ao_stamps = nullptr;  // debug hook: per-block phase stamps
-extern "C" void rt_attn_o_set_stamps(long long* p) { g_ao_stamps = p; }
+
 
 // batch-1 attention + o_proj (+ residual); returns -1 when the shape is not supported (caller
 // falls back to the two-kernel path)
@@ -1912,7 +1927,7 @@ extern "C" int rt_attn_o_fused(const void* qkv, void* kc, void* vc, int Smax, co
   a.slot = slot; a.attn_len = attn_len; a.kv_start = kv_start; a.pos = pos; a.cosT = cosT; a.sinT = sinT;
   a.sign = sign; a.window = window; a.part = part; a.tickets = nullptr; a.o = nullptr; a.ldo = 0;
   a.B = 1; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
-  a.qkv_slabs = nullptr; a.qkv_nsplit = 0; a.qkv_sstride = 0; a.kv_nt = 0;
+  a.qkv_slabs = nullptr; a.qkv_nsplit = 0; a.qkv_sstride = 0; a.kv_nt = 0; a.stamps = nullptr;
   g.w = (const bf16_t*)w; g.ldw = ldw; g.res = (const bf16_t*)res; g.out = (bf16_t*)out; g.H = H;
   g.sync = sync; g.err = err; g.stamps = g_ao_stamps;
   const int G = Hq / Hkv;
