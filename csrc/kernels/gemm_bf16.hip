@@ -816,8 +816,9 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
 // 16) and streams the gate row group grp and the up row group F / 16 + grp side by side.
 template <bool OUT_F32, int DEPTH, bool PAIR>
 __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
-  __shared__ float red[4][PAIR ? 32 : 16];
-  __shared__ float rsq[4];
+  // M <= 16 rows of X: the MFMA's 16 A rows (row frow of lane (frow, g); rows >= M repeat M - 1)
+  __shared__ float red[4][16][PAIR ? 33 : 17];
+  __shared__ float rsq[4][16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int frow = lane & 15, g = lane >> 4;
   const int grp = blockIdx.x;  // 16-row group (of the gate rows when PAIR)
@@ -825,7 +826,7 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
   const int c_begin = wid * nc / 4, c_end = (wid + 1) * nc / 4;
   const char* wbase = (const char*)p.B + (long)grp * nc * 2048 + lane * 16;
   const char* ubase = PAIR ? (const char*)p.B + ((long)(p.N / 32) + grp) * nc * 2048 + lane * 16 : wbase;
-  const bf16_t* xrow = p.A + g * 8;
+  const bf16_t* xrow = p.A + (long)min(frow, p.M - 1) * p.lda + g * 8;
   struct Regs { uint4 w0, w1, u0, u1, x0, x1; };
   auto ld = [&](Regs& r, int c) {
     r.w0 = load_nt16(wbase + (long)c * 2048);
@@ -847,7 +848,7 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
       accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x0), __builtin_bit_cast(bf16x8, r.u0), accu, 0, 0, 0);
       accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x1), __builtin_bit_cast(bf16x8, r.u1), accu, 0, 0, 0);
     }
-    if (normed && frow == 0) {
+    if (normed) {
       float f[8];
       unpack8(r.x0, f);
 #pragma unroll
@@ -872,35 +873,38 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
 #pragma unroll
   for (int i = 0; i < DEPTH - 1; ++i)
     if (c + i < c_end) mma(r[i]);
-  // acc[0] of lanes 0..15 (g = 0) = C[row 0][16 grp + frow] over this wave's k range; X row
-  // sums of squares live in the g lanes of frow 0
-  if (g == 0) {
-    red[wid][frow] = acc[0];
-    if constexpr (PAIR) red[wid][16 + frow] = accu[0];
+  // acc[r] of lane (frow, g) = C[row 4 g + r][16 grp + frow] over this wave's k range; the X row
+  // sum of squares of row frow is spread over its 4 g lanes
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    red[wid][4 * g + rr][frow] = acc[rr];
+    if constexpr (PAIR) red[wid][4 * g + rr][16 + frow] = accu[rr];
   }
   if (normed) {
     float t = sq;
     t += __shfl_xor(t, 16, 64);
     t += __shfl_xor(t, 32, 64);
-    if (lane == 0) rsq[wid] = t;
+    if (g == 0) rsq[wid][frow] = t;
   }
   __syncthreads();
-  if (tid < 16) {
-    const int col = grp * 16 + tid;
-    const float rs = normed ? rsqrtf((rsq[0] + rsq[1] + rsq[2] + rsq[3]) / (float)p.K + p.norm_eps) : 1.f;
-    float y = (red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]) * rs;
+  const int row = tid >> 4, ci = tid & 15;
+  if (row < p.M) {
+    const int col = grp * 16 + ci;
+    const float rs = normed ? rsqrtf((rsq[0][row] + rsq[1][row] + rsq[2][row] + rsq[3][row]) / (float)p.K + p.norm_eps)
+                            : 1.f;
+    float y = (red[0][row][ci] + red[1][row][ci] + red[2][row][ci] + red[3][row][ci]) * rs;
     if constexpr (PAIR) {
       const int F = p.N / 2;
-      float up = (red[0][16 + tid] + red[1][16 + tid] + red[2][16 + tid] + red[3][16 + tid]) * rs;
+      float up = (red[0][row][16 + ci] + red[1][row][16 + ci] + red[2][row][16 + ci] + red[3][row][16 + ci]) * rs;
       if (p.bias) { y += bf2f(p.bias[col]); up += bf2f(p.bias[F + col]); }
       y = y / (1.f + __expf(-y)) * up;
     } else {
       if (p.bias) y += bf2f(p.bias[col]);
       y = apply_act(y, p.act);
-      if (p.R) y += bf2f(p.R[col]);
+      if (p.R) y += bf2f(p.R[(long)row * p.ldr + col]);
     }
-    if constexpr (OUT_F32) ((float*)p.C)[col] = y;
-    else ((bf16_t*)p.C)[col] = f2bf(y);
+    if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
+    else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
   }
 }
 
@@ -1183,6 +1187,11 @@ extern "C" void rt_gemm_set_decode_depth(int d) { g_decode_depth = d; }
 // costs more than a second round of workgroups; RT_GEMV16=0 keeps them on gemm_decode_kernel
 // RT_GEMV16: 0 off, 1 narrow outputs only (N <= 8192: qkv, o, down), 2 also wide ones (SwiGLU
 // gate_up, lm_head)
+// rows of X on the no-split kernel (1..16; RT_GEMV16_MAXM)
+static int gemv16_max_m() {
+  static const int m = getenv("RT_GEMV16_MAXM") ? atoi(getenv("RT_GEMV16_MAXM")) : 16;
+  return m < 1 ? 1 : (m > 16 ? 16 : m);
+}
 static bool use_gemv16(int N, int K, int act) {
   static const int env = getenv("RT_GEMV16") ? atoi(getenv("RT_GEMV16")) : 2;
   if (!env || K % 64 || K < 1024) return false;
@@ -1236,7 +1245,7 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
     dim3 grid(((N + 63) / 64) * split), block(256);
     if (out_f32) hipLaunchKernelGGL((gemm_m64_kernel<true>), grid, block, 0, stream, p, slabs, tickets, split);
     else hipLaunchKernelGGL((gemm_m64_kernel<false>), grid, block, 0, stream, p, slabs, tickets, split);
-  } else if (M == 1 && wshuf && g_decode_split == 0 && use_gemv16(N, K, act) && p.Rp == 0) {
+  } else if (M <= gemv16_max_m() && wshuf && g_decode_split == 0 && use_gemv16(N, K, act) && p.Rp == 0) {
     const bool pair = act == ACT_SWIGLU;
     dim3 grid(pair ? N / 32 : N / 16), block(256);
     static const int gd = getenv("RT_GEMV16_DEPTH") ? atoi(getenv("RT_GEMV16_DEPTH")) : 4;
