@@ -800,7 +800,7 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Batch-1 GEMV without split-K: one workgroup per 16 output rows of a tile-ordered weight image
+// Decode GEMV (M <= 16) without split-K: one workgroup per 16 weight rows of a tile-ordered image
 // ---------------------------------------------------------------------------------------------
 // The split-K decode kernel above ends in a serial hand-off (write-through slab stores drained,
 // an arrival ticket, the last arriver's slab loads): about three dependent device-memory round
@@ -808,9 +808,10 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
 // tile-ordered image (its K chunks are ONE contiguous run of nc x 2 KiB) and its 4 waves split K;
 // the partial sums meet in LDS, so the tail is a workgroup barrier. N / 16 workgroups (256 for
 // o / down, 384 for qkv) fill the chip without a K split. Each wave keeps DEPTH - 1 k-chunks in
-// flight (non-temporal: every weight byte is read once per token). Same epilogue contract as
-// gemm_decode_kernel at M = 1: in-GEMM RMS norm (folded weight, rstd from the X fragments), bias,
-// activation (not SwiGLU), residual, bf16 / fp32 store.
+// flight (non-temporal: every weight byte is read once per step). The M <= 16 rows of X are the
+// MFMA's 16 A rows. Same epilogue contract as gemm_decode_kernel: in-GEMM RMS norm (folded weight,
+// per-row rstd from the X fragments), bias, activation, residual, bf16 / fp32 store; SwiGLU as a
+// gate / up row-group pair. Batch 1: 3.28 -> 2.92 ms/token (profiles/decode_b1_gemv16_ab.log).
 //
 // PAIR (SwiGLU, weight = [gate; up], 2F rows): the workgroup owns output columns [16 grp, 16 grp +
 // 16) and streams the gate row group grp and the up row group F / 16 + grp side by side.
