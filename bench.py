@@ -97,6 +97,9 @@ def main():
 
     di = parallel.init()
     dev = di.device
+    if args.gpus != di.world:
+        log(f"[bench] warning: --gpus {args.gpus} but {di.world} rank(s); launch one process per GPU "
+            f"(python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py ...)")
     assert dev.type == "cuda", "bench.py needs a GPU"
     torch.manual_seed(1234)
     t_setup = time.perf_counter()
