@@ -848,3 +848,26 @@ def test_ppo_advantages_kernel():
         want = ref.ppo_advantages(old.cpu(), refl.cpu(), vals.cpu(), scores.cpu(), lens.cpu(), 0.05, 0.99, 0.95, whiten)
         for a, b in zip(got, want):
             _close(a.cpu(), b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (5, 4096, 14336), (16, 4096, 4096), (1, 28672, 4096),
+                                   (3, 32000, 4096)])
+def test_gemv16_no_split_matches_fp32(M, N, K):
+    """Decode GEMV without split-K (M <= 16 over the tile-ordered image, N / 16 >= 256 workgroups):
+    in-GEMM RMS norm, residual, SwiGLU pair vs an fp32 PyTorch reference."""
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2
+    lnw = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    wf = ops.FoldCache().get(w, lnw)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * lnw.float()
+    shuf = ops.ShufCache()
+    _close(ops.gemm_decode(x, w, shuf=shuf), x.float() @ w.float().t())
+    shuf_f = ops.ShufCache()
+    _close(ops.gemm_decode(x, wf, residual=res, norm_eps=1e-5, shuf=shuf_f), xn @ w.float().t() + res.float())
+    if N % 32 == 0 and N <= 28672:
+        F = N // 2
+        g, u = xn @ w[:F].float().t(), xn @ w[F:].float().t()
+        _close(ops.gemm_decode(x, wf, act=ops.ACT_SWIGLU, norm_eps=1e-5, shuf=shuf_f),
+               torch.nn.functional.silu(g) * u)
