@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes for the batch-1 RAG-answer decode loop (Mistral-7B + LoRA r16, prompt 173): bytes moved
-# by the weight-streaming GEMVs (gemm_decode_kernel, tile-ordered weights) and the fused decode
+# by the weight-streaming GEMVs (gemv16_kernel, tile-ordered weights, no split-K) and the fused decode
 # attention (8-wave attn_decode_mfma_kernel). One counter group per run, kernel trace only.
 # Usage (GPU box, repo root): tools/pmc_decode_b1.sh ; summary: python tools/pmc_summary.py gpurun_out/pmc_b1/*.csv
 set -o pipefail
@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 run() {
   local name=$1 cnt=$2
   rm -rf /tmp/pmcb1_$name
-  timeout -s KILL 150 rocprofv3 --pmc $cnt --kernel-include-regex "gemm_decode|attn_decode" -f csv \
+  timeout -s KILL 150 rocprofv3 --pmc $cnt --kernel-include-regex "gemm_decode|gemv16|attn_decode" -f csv \
     -d /tmp/pmcb1_$name -o run -- python3 $R/tools/decode_profile.py --batch 1 --prompt 173 --new 16 \
     > $out/log_$name.txt 2>&1 || return $?
   find /tmp/pmcb1_$name -name "*counter_collection.csv" -exec cp {} $out/b1_$name.csv \;
