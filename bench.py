@@ -69,7 +69,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--mode", default="ppo", choices=["ppo", "sft", "pipeline"])
-    ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3fn) weights for no-grad forwards (config 5)")
+    ap.add_argument("--fp8", action=argparse.BooleanOptionalAction, default=None,
+                    help="fp8 (e4m3fn) weights for no-grad forwards (default: on for --mode pipeline, config 5)")
     ap.add_argument("--sft-batch", type=int, default=64, help="SFT sequences per GPU per step")
     ap.add_argument("--full-ft", action="store_true",
                     help="PPO over every policy weight (the reference's full-parameter mode: bf16 compute copies "
@@ -84,6 +85,8 @@ def main():
         args.rollout_batch = 64 if args.mode == "pipeline" else 256
     if args.minibatch is None:
         args.minibatch = 16 if args.mode == "pipeline" else 32
+    if args.fp8 is None:
+        args.fp8 = args.mode == "pipeline"
 
     from rag_tl_domainllm_optimizer_amd import models, parallel
     from rag_tl_domainllm_optimizer_amd.data import SyntheticCorpus
@@ -172,6 +175,7 @@ def main():
             f"reward={m['reward_mean']:.3f}")
     parallel.barrier()
     torch.cuda.synchronize()
+    trainer.sync.comm_bytes = 0
     t0 = time.perf_counter()
     tokens = 0.0
     phase = {}
@@ -185,10 +189,13 @@ def main():
                 phase[k] = phase.get(k, 0.0) + v
         log(f"[bench] step {s}: {m['step_time_s']:.2f}s loss={m['total_loss']:.4f} kl_ref={m['kl_ref']:.4f}")
     torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0  # this rank's wall time, before waiting for the others
     parallel.barrier()
     elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     parallel.all_reduce_(elapsed, "max")
     elapsed = float(elapsed)
+    spread = rank_spread(t_local / args.steps, dev)
+    comm_bytes = trainer.sync.comm_bytes / args.steps
     value = tokens / elapsed
     res = {
         "metric": "PPO rollout tokens/sec (node) + p50 RAG answer latency, Mistral-7B 1/2/4/8 GPU",
@@ -216,6 +223,10 @@ def main():
         "p90_rag_latency_s": lat["p90_s"] if lat else None,
         "rag_latency_vs_baseline": (REF_LATENCY_S / lat["p50_s"]) if lat else None,
         "phase_s_per_step": {k: v / args.steps for k, v in phase.items()},
+        # data-parallel diagnostics: gradient payload each rank hands to RCCL per step, and the
+        # spread of the per-rank step times (before the closing barrier) in seconds
+        "allreduce_bytes_per_step": comm_bytes,
+        "rank_step_s": spread,
     }
     if di.is_main:
         print(json.dumps(res), flush=True)
@@ -223,6 +234,19 @@ def main():
             with open(args.json_out, "w") as f:
                 json.dump(res, f, indent=2)
     parallel.shutdown()
+
+
+def rank_spread(step_s: float, dev) -> dict:
+    """min / mean / max over ranks of one rank-local per-step wall time."""
+    from rag_tl_domainllm_optimizer_amd import parallel
+
+    t = torch.tensor([step_s], dtype=torch.float64, device=dev)
+    lo, hi, sm = t.clone(), t.clone(), t.clone()
+    parallel.all_reduce_(lo, "min")
+    parallel.all_reduce_(hi, "max")
+    parallel.all_reduce_(sm, "sum")
+    world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    return {"min": float(lo), "mean": float(sm) / world, "max": float(hi)}
 
 
 def _timed(di, fn, steps):
@@ -296,8 +320,8 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
 
     for w in range(args.warmup):
         ppo.step(make_batch())
-    batches = [make_batch() for _ in range(args.steps)]
-    el2, pm = _timed(di, lambda i: ppo.step(batches[i]), args.steps)
+    # retrieval (query encode + IVF search) inside the timed region, as in the headline mode
+    el2, pm = _timed(di, lambda i: ppo.step(make_batch()), args.steps)
     toks = sum(m["rollout_tokens"] for m in pm) * di.world
     res2 = {"metric": "RAG -> LoRA SFT -> PPO pipeline, " + args.model, "value": toks / el2, "unit": "tokens/s",
             "n_gpus": di.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el2 / args.steps * 1e3,

@@ -20,6 +20,7 @@ extern "C" {
 int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
                long, int, int, int, int, int, float*, unsigned*, const void*, long, float, int, hipStream_t);
 int rt_shuffle_decode_weight(const void*, void*, long, long, hipStream_t);
+int rt_shuffle_decode_weight_fp8(const void*, void*, long, long, hipStream_t);
 void rt_gemm_set_variant(int);
 void rt_gemm_set_m64_split(int);
 void rt_gemm_set_decode_split(int);
@@ -31,7 +32,7 @@ int rt_gemm_small(int, int, const void*, long, const void*, long, void*, long, i
                   hipStream_t);
 int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
 int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
-                int, int, int, float*, unsigned*, const void*, long, float, hipStream_t);
+                int, int, int, float*, unsigned*, const void*, long, float, int, hipStream_t);
 int rt_quant_fp8_rows(const void*, long, void*, long, float*, long, int, hipStream_t);
 int rt_norm_fwd(int, const void*, const void*, const void*, const void*, void*, void*, float*, float*, int, int, float,
                 const float*, int, hipStream_t);
@@ -224,6 +225,21 @@ Tensor shuffle_decode_weight(const Tensor& w, optional<Tensor> out) {
   return o;
 }
 
+// q [N, K] e4m3fn bytes -> the fp8 tile-ordered image of gemv16_kernel<W8> (same shape, permuted).
+Tensor shuffle_decode_weight_fp8(const Tensor& q, optional<Tensor> out) {
+  CHECK_CUDA(q);
+  TORCH_CHECK(q.scalar_type() == at::kByte && q.dim() == 2 && q.is_contiguous(),
+              "shuffle_decode_weight_fp8: contiguous uint8 [N, K] expected");
+  const int64_t N = q.size(0), K = q.size(1);
+  TORCH_CHECK(N % 16 == 0 && K % 128 == 0, "shuffle_decode_weight_fp8: needs N % 16 == 0 and K % 128 == 0");
+  Tensor o = (out.has_value() && out->defined()) ? *out : at::empty_like(q);
+  TORCH_CHECK(o.sizes() == q.sizes() && o.is_contiguous() && o.scalar_type() == at::kByte,
+              "shuffle_decode_weight_fp8: bad out");
+  TORCH_CHECK(o.data_ptr() != q.data_ptr(), "shuffle_decode_weight_fp8: out must not alias q");
+  check_rc(rt_shuffle_decode_weight_fp8(q.data_ptr(), o.data_ptr(), N, K, cur_stream()), "shuffle_decode_weight_fp8");
+  return o;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Token-parallel GEMM family (csrc/kernels/gemm_big.hip). 2-D operands with unit column stride:
 //   layout_a 0: a = [M, K]   1: a = [K, M]        layout_b 0: b = [N, K]   1: b = [K, N]
@@ -279,6 +295,13 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
     TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == Nout && c.stride(1) == 1, "gemm_big: bad out shape");
     TORCH_CHECK(c.scalar_type() == odt, "gemm_big: bad out dtype");
     TORCH_CHECK(out_mode == 2 || c.stride(0) % 8 == 0, "gemm_big: out row stride must be a multiple of 8");
+    // the epilogue stores whole 16-B (bf16) / 4-float chunks: a ragged last chunk of the last row
+    // must still land inside the tensor's storage
+    const int64_t chunk = out_mode == 0 ? 8 : 4;
+    TORCH_CHECK(out_mode == 2 || Nout % chunk == 0 ||
+                    (c.storage_offset() + (M - 1) * c.stride(0) + (Nout + chunk - 1) / chunk * chunk) * c.element_size() <=
+                        (int64_t)c.storage().nbytes(),
+                "gemm_big: out width ", Nout, " is not a multiple of ", chunk, " and its storage has no padding");
     CHECK_ALIGN16(c);
   } else {
     TORCH_CHECK(out_mode != 2, "gemm_big: atomic accumulation needs an initialised out");
@@ -305,6 +328,9 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
     TORCH_CHECK(out_mode == 0 && !swiglu && residual->dim() == 2 && residual->size(0) == M && residual->size(1) == N &&
                     residual->stride(1) == 1 && residual->stride(0) % 8 == 0,
                 "gemm_big: residual must be bf16 [M, N] (bf16 output, no SwiGLU)");
+    // the epilogue reads the residual in 16-B chunks: the last chunk of the last row must not
+    // run past the end of the tensor
+    TORCH_CHECK(N % 8 == 0, "gemm_big: a residual needs N % 8 == 0, got N = ", N);
     CHECK_ALIGN16(*residual);
   }
   if (M == 0 || N == 0) return c;
@@ -401,8 +427,9 @@ std::vector<Tensor> quant_fp8(const Tensor& x) {
 
 Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, const Tensor& sw,
                 const optional<Tensor>& bias, int64_t act, optional<Tensor> out, const optional<Tensor>& residual,
-                double norm_eps) {
-  // a: bf16 [M, K] (W8A16, M <= 64) or uint8 e4m3fn [M, K] with sa [M] (W8A8)
+                double norm_eps, bool w_shuffled) {
+  // a: bf16 [M, K] (W8A16, M <= 64) or uint8 e4m3fn [M, K] with sa [M] (W8A8). w_shuffled: wq is
+  // the tile-ordered fp8 image of shuffle_decode_weight_fp8 (W8A16 at M <= 16 only)
   CHECK_CUDA(a); CHECK_CUDA(wq); CHECK_ROWS(a); CHECK_ROWS(wq); CHECK_F32(sw);
   TORCH_CHECK(wq.scalar_type() == at::kByte, "gemm_fp8: weight must be uint8 (e4m3fn bits)");
   const bool a_bf16 = a.scalar_type() == at::kBFloat16;
@@ -410,7 +437,11 @@ Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, c
   TORCH_CHECK(wq.size(1) == K && sw.numel() == N, "gemm_fp8: shapes");
   if (a_bf16) {
     TORCH_CHECK(M <= 64 && K % 64 == 0, "gemm_fp8: bf16 activations only for M <= 64");
+    if (w_shuffled)
+      TORCH_CHECK(K % 128 == 0 && N % (act == 5 ? 64 : 16) == 0 && wq.is_contiguous(),
+                  "gemm_fp8: the tile-ordered fp8 image needs K % 128 == 0, N % 16 == 0 (SwiGLU: N % 64 == 0)");
   } else {
+    TORCH_CHECK(!w_shuffled, "gemm_fp8: tile-ordered weights are a W8A16 decode layout");
     TORCH_CHECK(a.scalar_type() == at::kByte && sa.has_value() && sa->numel() == M, "gemm_fp8: W8A8 needs sa [M]");
     TORCH_CHECK(K % 128 == 0 && N % 8 == 0, "gemm_fp8: K % 128 == 0, N % 8 == 0");
   }
@@ -438,7 +469,8 @@ Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, c
   check_rc(rt_gemm_fp8(a.data_ptr(), a.stride(0), sa.has_value() && sa->defined() ? sa->data_ptr<float>() : nullptr,
                        wq.data_ptr(), wq.stride(0), sw.data_ptr<float>(), opt_ptr(bias), c.data_ptr(), c.stride(0),
                        (int)M, (int)N, (int)K, (int)act, a_bf16 ? 1 : 0, slabs, tickets,
-                       has_res ? residual->data_ptr() : nullptr, has_res ? residual->stride(0) : 0, (float)norm_eps, st),
+                       has_res ? residual->data_ptr() : nullptr, has_res ? residual->stride(0) : 0, (float)norm_eps,
+                       w_shuffled ? 1 : 0, st),
            "gemm_fp8");
   return c;
 }
@@ -1004,6 +1036,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("inv"), py::arg("R"));
   m.def("shuffle_decode_weight", &shuffle_decode_weight, "W [N, K] -> tile-ordered decode image (gemm w_shuffled=True)",
         py::arg("w"), py::arg("out") = py::none());
+  m.def("shuffle_decode_weight_fp8", &shuffle_decode_weight_fp8,
+        "fp8 W [N, K] -> tile-ordered W8A16 decode image (gemm_fp8 w_shuffled=True)", py::arg("q"),
+        py::arg("out") = py::none());
   m.def("gemm_set_m64_split", &rt_gemm_set_m64_split, "tuning: fixed split-K of the M<=64 ring kernel (0 = auto)");
   m.def("gemm_set_decode_split", &rt_gemm_set_decode_split, "tuning: fixed split-K of the M<=16 decode kernel (0 = auto)");
   m.def("gemm_set_decode_depth", &rt_gemm_set_decode_depth, "tuning: weight-pipeline depth (2 / 4) of the M<=16 decode kernel (0 = auto)");
@@ -1025,7 +1060,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none());
   m.def("gemm_fp8", &gemm_fp8, "fp8 GEMM: W8A8 (MX MFMA 256x256) or W8A16 (skinny, M <= 64)", py::arg("a"),
         py::arg("sa") = py::none(), py::arg("wq"), py::arg("sw"), py::arg("bias") = py::none(), py::arg("act") = 0,
-        py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("norm_eps") = 0.0);
+        py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("norm_eps") = 0.0,
+        py::arg("w_shuffled") = false);
   m.def("norm_fwd", &norm_fwd);
   m.def("splitk_reduce", &splitk_reduce, "sum of split-K slabs -> bf16");
   m.def("norm_fwd_slabs", &norm_fwd_slabs, "residual-add + norm whose input is a sum of split-K slabs");

@@ -815,7 +815,13 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
 //
 // PAIR (SwiGLU, weight = [gate; up], 2F rows): the workgroup owns output columns [16 grp, 16 grp +
 // 16) and streams the gate row group grp and the up row group F / 16 + grp side by side.
-template <bool OUT_F32, int DEPTH, bool PAIR>
+//
+// W8 (W8A16, config 5): the image is the fp8 tile order of shuffle_decode_weight_fp8 — per 16-row
+// group, 2-KiB chunks of 128 k; load h of lane l = 16 g + r holds the 16 e4m3fn bytes of row r at
+// k [128 c + 64 h + 16 g, +16), widened in registers to two bf16x8 fragments (k-slot permutation
+// shared with the X fragments, so the MFMA sums the same products). Half the bytes per chunk of k
+// of the bf16 image; per-column scales sb[col] applied in the epilogue.
+template <bool OUT_F32, int DEPTH, bool PAIR, bool W8 = false>
 __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
   // M <= 16 rows of X: the MFMA's 16 A rows (row frow of lane (frow, g); rows >= M repeat M - 1)
   __shared__ float red[4][16][PAIR ? 33 : 17];
@@ -823,12 +829,13 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int frow = lane & 15, g = lane >> 4;
   const int grp = blockIdx.x;  // 16-row group (of the gate rows when PAIR)
-  const int nc = p.K / 64;
+  constexpr int KC = W8 ? 128 : 64;  // k per 2-KiB chunk
+  const int nc = p.K / KC;
   const int c_begin = wid * nc / 4, c_end = (wid + 1) * nc / 4;
   const char* wbase = (const char*)p.B + (long)grp * nc * 2048 + lane * 16;
   const char* ubase = PAIR ? (const char*)p.B + ((long)(p.N / 32) + grp) * nc * 2048 + lane * 16 : wbase;
-  const bf16_t* xrow = p.A + (long)min(frow, p.M - 1) * p.lda + g * 8;
-  struct Regs { uint4 w0, w1, u0, u1, x0, x1; };
+  const bf16_t* xrow = p.A + (long)min(frow, p.M - 1) * p.lda + g * (W8 ? 16 : 8);
+  struct Regs { uint4 w0, w1, u0, u1, x0, x1, x2, x3; };
   auto ld = [&](Regs& r, int c) {
     r.w0 = load_nt16(wbase + (long)c * 2048);
     r.w1 = load_nt16(wbase + (long)c * 2048 + 1024);
@@ -836,18 +843,40 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
       r.u0 = load_nt16(ubase + (long)c * 2048);
       r.u1 = load_nt16(ubase + (long)c * 2048 + 1024);
     }
-    r.x0 = *(const uint4*)(xrow + c * 64);
-    r.x1 = *(const uint4*)(xrow + c * 64 + 32);
+    if constexpr (W8) {  // k [128 c + 64 h + 16 g, +16) as two 8-element halves, h = 0, 1
+      r.x0 = *(const uint4*)(xrow + c * 128);
+      r.x1 = *(const uint4*)(xrow + c * 128 + 8);
+      r.x2 = *(const uint4*)(xrow + c * 128 + 64);
+      r.x3 = *(const uint4*)(xrow + c * 128 + 72);
+    } else {
+      r.x0 = *(const uint4*)(xrow + c * 64);
+      r.x1 = *(const uint4*)(xrow + c * 64 + 32);
+    }
   };
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f}, accu = acc;
   float sq = 0.f;
   const bool normed = p.norm_eps > 0.f;
   auto mma = [&](const Regs& r) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x0), __builtin_bit_cast(bf16x8, r.w0), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x1), __builtin_bit_cast(bf16x8, r.w1), acc, 0, 0, 0);
-    if constexpr (PAIR) {
-      accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x0), __builtin_bit_cast(bf16x8, r.u0), accu, 0, 0, 0);
-      accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x1), __builtin_bit_cast(bf16x8, r.u1), accu, 0, 0, 0);
+    if constexpr (W8) {
+      const bf16x8 x0 = __builtin_bit_cast(bf16x8, r.x0), x1 = __builtin_bit_cast(bf16x8, r.x1);
+      const bf16x8 x2 = __builtin_bit_cast(bf16x8, r.x2), x3 = __builtin_bit_cast(bf16x8, r.x3);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, fp8x8_to_bf16(r.w0.x, r.w0.y), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, fp8x8_to_bf16(r.w0.z, r.w0.w), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, fp8x8_to_bf16(r.w1.x, r.w1.y), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x3, fp8x8_to_bf16(r.w1.z, r.w1.w), acc, 0, 0, 0);
+      if constexpr (PAIR) {
+        accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, fp8x8_to_bf16(r.u0.x, r.u0.y), accu, 0, 0, 0);
+        accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, fp8x8_to_bf16(r.u0.z, r.u0.w), accu, 0, 0, 0);
+        accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, fp8x8_to_bf16(r.u1.x, r.u1.y), accu, 0, 0, 0);
+        accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x3, fp8x8_to_bf16(r.u1.z, r.u1.w), accu, 0, 0, 0);
+      }
+    } else {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x0), __builtin_bit_cast(bf16x8, r.w0), acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x1), __builtin_bit_cast(bf16x8, r.w1), acc, 0, 0, 0);
+      if constexpr (PAIR) {
+        accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x0), __builtin_bit_cast(bf16x8, r.u0), accu, 0, 0, 0);
+        accu = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, r.x1), __builtin_bit_cast(bf16x8, r.u1), accu, 0, 0, 0);
+      }
     }
     if (normed) {
       float f[8];
@@ -857,6 +886,14 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
       unpack8(r.x1, f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) sq += f[e] * f[e];
+      if constexpr (W8) {
+        unpack8(r.x2, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sq += f[e] * f[e];
+        unpack8(r.x3, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sq += f[e] * f[e];
+      }
     }
   };
   Regs r[DEPTH];
@@ -897,9 +934,11 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
     if constexpr (PAIR) {
       const int F = p.N / 2;
       float up = (red[0][row][16 + ci] + red[1][row][16 + ci] + red[2][row][16 + ci] + red[3][row][16 + ci]) * rs;
+      if constexpr (W8) { y *= p.sb[col]; up *= p.sb[F + col]; }
       if (p.bias) { y += bf2f(p.bias[col]); up += bf2f(p.bias[F + col]); }
       y = y / (1.f + __expf(-y)) * up;
     } else {
+      if constexpr (W8) y *= p.sb[col];
       if (p.bias) y += bf2f(p.bias[col]);
       y = apply_act(y, p.act);
       if (p.R) y += bf2f(p.R[(long)row * p.ldr + col]);
@@ -913,7 +952,7 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
 // reduces), in-GEMM RMS-norm scaling, SwiGLU pair / bias + activation + residual epilogues.
 // acc[j][r] = C[16 wid + 4 fq + r][16 j + frow] of the block's 64 columns; sq = sum of squares of
 // X row (16 wid + frow) over this block's K range (norm only).
-template <bool OUT_F32>
+template <bool OUT_F32, bool W8 = false>
 __device__ __forceinline__ void m64_finish(const GemmArgs& p, f32x4 (&acc)[4], float sq, float* __restrict__ slabs,
                                            unsigned* __restrict__ tickets, int split, int cg, int sp, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -989,11 +1028,12 @@ __device__ __forceinline__ void m64_finish(const GemmArgs& p, f32x4 (&acc)[4], f
     for (int j = 0; j < 2; ++j) {
       const int col = cg * 32 + j * 16 + frow;
       const float bg = p.bias ? bf2f(p.bias[col]) : 0.f, bu = p.bias ? bf2f(p.bias[F + col]) : 0.f;
+      const float sg = W8 ? p.sb[col] : 1.f, su = W8 ? p.sb[F + col] : 1.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wid * 16 + fq * 4 + r;
         if (row >= p.M) continue;
-        const float gt = acc[j][r] + bg, up = acc[j + 2][r] + bu;
+        const float gt = acc[j][r] * sg + bg, up = acc[j + 2][r] * su + bu;
         const float y = gt / (1.f + __expf(-gt)) * up;
         if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
         else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
@@ -1006,11 +1046,12 @@ __device__ __forceinline__ void m64_finish(const GemmArgs& p, f32x4 (&acc)[4], f
     const int col = n0 + j * 16 + frow;
     if (col >= p.N) continue;
     const float bv = p.bias ? bf2f(p.bias[col]) : 0.f;
+    const float sc = W8 ? p.sb[col] : 1.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = wid * 16 + fq * 4 + r;
       if (row >= p.M) continue;
-      float y = apply_act(acc[j][r] + bv, p.act);
+      float y = apply_act(acc[j][r] * sc + bv, p.act);
       if (p.R) y += bf2f(p.R[(long)row * p.ldr + col]);
       if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
       else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
@@ -1030,8 +1071,16 @@ __device__ __forceinline__ void m64_finish(const GemmArgs& p, f32x4 (&acc)[4], f
 // ticket hand-off of gemm_decode_kernel.
 constexpr int R64_SLOTS = 4;
 constexpr int R64_SLOT = 2 * 64 * 128;  // X + W, 64 rows x 128 B each
-
-template <bool OUT_F32>
+//
+// W8 (W8A16, config 5): B is the fp8 tile-ordered image of shuffle_decode_weight_fp8 (16-row
+// groups, 2-KiB chunks of 128 k; lane l = 16 g + r of half h holds row r, k [64 h + 16 g, +16)).
+// A 64-deep K-step of one 16-row group is ONE contiguous 1-KiB run: each wave stages one group
+// with one 16-B LDS-DMA per lane (half the weight bytes of the bf16 ring, and 1-KiB DRAM runs
+// instead of 64-B row pieces — the row-major fp8 form of this ring measured slower than bf16).
+// The fragment of lane (frow, fq) for MFMA step kk is k [32 kk + 8 fq, +8) of row frow = the
+// 8-B half (fq & 1) of unit g = 2 kk + (fq >> 1): conflict-free ds_read_b64 (4 r + 2 fq + e),
+// widened to bf16 in registers; per-column scales in the epilogue.
+template <bool OUT_F32, bool W8 = false>
 __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __restrict__ slabs,
                                                           unsigned* __restrict__ tickets, int split) {
   __shared__ __attribute__((aligned(16))) char smem[R64_SLOTS * R64_SLOT];  // the only __shared__ object
@@ -1054,12 +1103,20 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
       const int lr = (wid * 2 + j) * 8 + srow;  // 0..63
       const int ck = (lane & 7) ^ lds_swz(lr);
       const bf16_t* xa = p.A + (long)min(lr, p.M - 1) * p.lda + (long)t * 64 + ck * 8;
-      const int wrow_ = pair ? (lr < 32 ? cg * 32 + lr : F + cg * 32 + lr - 32) : min(n0 + lr, p.N - 1);
-      const bf16_t* wb = p.B + (long)wrow_ * p.ldb + (long)t * 64 + ck * 8;
       __builtin_amdgcn_global_load_lds((const void*)xa, (lds_void*)(slot + (wid * 2 + j) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)wb, (lds_void*)(slot + 8192 + (wid * 2 + j) * 1024), 16, 0, 0);
+      if constexpr (!W8) {
+        const int wrow_ = pair ? (lr < 32 ? cg * 32 + lr : F + cg * 32 + lr - 32) : min(n0 + lr, p.N - 1);
+        const bf16_t* wb = p.B + (long)wrow_ * p.ldb + (long)t * 64 + ck * 8;
+        __builtin_amdgcn_global_load_lds((const void*)wb, (lds_void*)(slot + 8192 + (wid * 2 + j) * 1024), 16, 0, 0);
+      }
+    }
+    if constexpr (W8) {  // wave wid stages 16-row group G, k-half t & 1 of chunk t >> 1: one 1-KiB run
+      const int G = pair ? (wid < 2 ? 2 * cg + wid : F / 16 + 2 * cg + wid - 2) : min(4 * cg + wid, p.N / 16 - 1);
+      const char* wb = (const char*)p.B + ((long)G * (p.K / 128) + (t >> 1)) * 2048 + (t & 1) * 1024 + lane * 16;
+      __builtin_amdgcn_global_load_lds((const void*)wb, (lds_void*)(slot + 8192 + wid * 1024), 16, 0, 0);
     }
   };
+  constexpr int PER = W8 ? 3 : 4;  // LDS-DMAs per lane per K-step
 
   f32x4 acc[4];
 #pragma unroll
@@ -1073,10 +1130,10 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
     if (i < nt) stage(t0 + i);
 
   for (int i = 0; i < nt; ++i) {
-    // retire step i (each step = 4 DMAs per lane); later steps stay in flight
+    // retire step i (PER DMAs per lane per step); later steps stay in flight
     const int ahead = min(R64_SLOTS - 2, nt - 1 - i);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
     // refill the slot read in the previous iteration (every wave is past it: barrier above)
@@ -1091,7 +1148,13 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int br = j * 16 + frow;
-        b[j][kk] = *(const bf16x8*)(slot + 8192 + br * 128 + ((c ^ lds_swz(br)) << 4));
+        if constexpr (W8) {
+          // fp8 bytes of row frow, k [8c, 8c + 8) = [32 kk + 8 fq, +8): unit 2 kk + (fq >> 1), half fq & 1
+          const uint2 w8 = *(const uint2*)(slot + 8192 + j * 1024 + ((2 * kk + (fq >> 1)) * 16 + frow) * 16 + (fq & 1) * 8);
+          b[j][kk] = fp8x8_to_bf16(w8.x, w8.y);
+        } else {
+          b[j][kk] = *(const bf16x8*)(slot + 8192 + br * 128 + ((c ^ lds_swz(br)) << 4));
+        }
       }
     }
 #pragma unroll
@@ -1113,7 +1176,7 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
     sq += __shfl_xor(sq, 16, 64);
     sq += __shfl_xor(sq, 32, 64);
   }
-  m64_finish<OUT_F32>(p, acc, sq, slabs, tickets, split, cg, sp, smem);
+  m64_finish<OUT_F32, W8>(p, acc, sq, slabs, tickets, split, cg, sp, smem);
 }
 
 // split-K for the ring kernel, from a cold-weight sweep on MI355X (profiles/kernels_m64_split.log,
@@ -1288,10 +1351,14 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
 
 // fp8 GEMMs: C[M,N] (bf16) = act( (A_q B_q^T) * sa[row] * sb[col] + bias ), A_q / B_q OCP e4m3fn.
 //  * M > 64 : W8A8, 256x256 8-phase kernel on MX-scaled mfma_16x16x128_f8f6f4 (2x the bf16 rate)
-//  * M <= 64: W8A16 skinny kernel (A = bf16 activations, sa ignored): half the weight bytes
+//  * M <= 64: W8A16 (A = bf16 activations, sa ignored): half the weight bytes.
+//      - M <= 16 with the tile-ordered fp8 image (wshuf, shuffle_decode_weight_fp8): gemv16_kernel<W8>,
+//        one workgroup per 16 weight rows, no split-K;
+//      - 16 < M <= 64 with the image: the LDS-DMA ring gemm_m64_kernel<W8> (split-K slabs);
+//      - row-major fp8 weights (no image: small / odd shapes): the split-K register-streaming kernel.
 extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void* B, long ldb, const float* sb,
                            const void* bias, void* C, long ldc, int M, int N, int K, int act, int a_is_bf16,
-                           float* slabs, unsigned* tickets, const void* R, long ldr, float norm_eps,
+                           float* slabs, unsigned* tickets, const void* R, long ldr, float norm_eps, int wshuf,
                            hipStream_t stream) {
   GemmArgs p;
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
@@ -1303,18 +1370,34 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
   if ((R || norm_eps > 0.f) && !a_is_bf16) return -3;
   if (a_is_bf16) {
     if (M > 64 || K % 64) return -1;
-    const int MT = (M + 15) / 16;
-    const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * (DG_COLS + 1)) : 1;
-    dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
-    switch (MT) {
-      case 1:
-        if (decode_depth(1, (long)grid.x) == 4) hipLaunchKernelGGL((gemm_decode_kernel<1, false, true, 4>), grid, block, 0, stream, p, slabs, tickets, split);
-        else hipLaunchKernelGGL((gemm_decode_kernel<1, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split);
-        break;
-      case 2: hipLaunchKernelGGL((gemm_decode_kernel<2, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
-      case 3: hipLaunchKernelGGL((gemm_decode_kernel<3, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
-      case 4: hipLaunchKernelGGL((gemm_decode_kernel<4, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
-      default: return -1;
+    const bool pair = act == ACT_SWIGLU;
+    if (wshuf) {
+      // tile-ordered fp8 image: the no-split 16-row kernel up to 16 rows (or RT variant 4), the
+      // LDS-DMA ring above
+      if (K % 128 || N % 16 || (pair && N % 64)) return -4;
+      if (M <= 16 && g_gemm_variant != 4) {
+        dim3 grid(pair ? N / 32 : N / 16), block(256);
+        if (pair) hipLaunchKernelGGL((gemv16_kernel<false, 4, true, true>), grid, block, 0, stream, p);
+        else hipLaunchKernelGGL((gemv16_kernel<false, 4, false, true>), grid, block, 0, stream, p);
+      } else {
+        const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64 + 64) : 1;
+        dim3 grid(((N + 63) / 64) * split), block(256);
+        hipLaunchKernelGGL((gemm_m64_kernel<false, true>), grid, block, 0, stream, p, slabs, tickets, split);
+      }
+    } else {
+      const int MT = (M + 15) / 16;
+      const int split = (slabs && tickets) ? fit_split(decode_split(N, K), (N + DG_COLS - 1) / DG_COLS, MT * 16 * (DG_COLS + 1)) : 1;
+      dim3 grid(((N + DG_COLS - 1) / DG_COLS) * split), block(256);
+      switch (MT) {
+        case 1:
+          if (decode_depth(1, (long)grid.x) == 4) hipLaunchKernelGGL((gemm_decode_kernel<1, false, true, 4>), grid, block, 0, stream, p, slabs, tickets, split);
+          else hipLaunchKernelGGL((gemm_decode_kernel<1, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split);
+          break;
+        case 2: hipLaunchKernelGGL((gemm_decode_kernel<2, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
+        case 3: hipLaunchKernelGGL((gemm_decode_kernel<3, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
+        case 4: hipLaunchKernelGGL((gemm_decode_kernel<4, false, true, 2>), grid, block, 0, stream, p, slabs, tickets, split); break;
+        default: return -1;
+      }
     }
   } else {
     if (K % 128 || N % 8) return -1;
@@ -1352,6 +1435,32 @@ extern "C" int rt_shuffle_decode_weight(const void* src, void* dst, long N, long
   const long total = N * K / 8;
   const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(shuffle_decode_weight_kernel, dim3(blocks), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst, N, K);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+// fp8 decode-weight image for gemv16_kernel<W8>: q [N, K] e4m3fn bytes row-major -> per (16-row
+// group G, 128-k chunk c) one 2-KiB tile; 16-B unit i of a tile: lane l = i & 63 of load h =
+// (i >> 6) & 1 holds row 16 G + (l & 15), k [128 c + 64 h + 16 (l >> 4), +16). Every load
+// instruction of a wave then reads one contiguous 1-KiB run. One thread per 16 B.
+__global__ __launch_bounds__(256) void shuffle_decode_weight_fp8_kernel(const uint4* __restrict__ src,
+                                                                        uint4* __restrict__ dst, long N, long K) {
+  const long nc = K / 128;
+  const long total = N * K / 16;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long l = i & 63, h = (i >> 6) & 1, tile = i >> 7;
+    const long G = tile / nc, c = tile % nc;
+    const long row = G * 16 + (l & 15), k = c * 128 + h * 64 + (l >> 4) * 16;
+    dst[i] = src[(row * K + k) / 16];
+  }
+}
+
+extern "C" int rt_shuffle_decode_weight_fp8(const void* src, void* dst, long N, long K, hipStream_t stream) {
+  if (N % 16 || K % 128) return -1;
+  const long total = N * K / 16;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(shuffle_decode_weight_fp8_kernel, dim3(blocks), dim3(256), 0, stream, (const uint4*)src,
+                     (uint4*)dst, N, K);
   RT_LAUNCH_CHECK();
   return 0;
 }

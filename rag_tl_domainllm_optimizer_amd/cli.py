@@ -103,8 +103,9 @@ def cmd_index(cfg, args):
     print(json.dumps({"index": path, "ntotal": st["index"].ntotal, "kind": st["index"].kind}))
 
 
-def latest_checkpoint(run_dir: str):
-    """Prefix of the checkpoint with the highest global step in ``run_dir`` (or None)."""
+def latest_checkpoint(run_dir: str, kind: str = "ppo"):
+    """Prefix of the ``kind`` ("ppo" / "sft") checkpoint with the highest global step in
+    ``run_dir`` (or None). States written before the kind field existed count as PPO."""
     if not os.path.isdir(run_dir):
         return None
     cands = []
@@ -112,8 +113,19 @@ def latest_checkpoint(run_dir: str):
         sf = os.path.join(run_dir, d, "state.json")
         if d.endswith("_trainer_state") and os.path.exists(sf):
             with open(sf) as f:
-                cands.append((int(json.load(f).get("global_step", 0)), os.path.join(run_dir, d[:-len("_trainer_state")])))
+                st = json.load(f)
+            if st.get("kind", "ppo") != kind:
+                continue
+            cands.append((int(st.get("global_step", 0)), os.path.join(run_dir, d[:-len("_trainer_state")])))
     return max(cands)[1] if cands else None
+
+
+def _apply_fp8(cfg, policy):
+    """config 5: fp8 e4m3fn weight images for the no-grad forwards (``model.fp8``)."""
+    if policy is not None and getattr(cfg.model, "fp8", False) and hasattr(policy, "set_fp8"):
+        if next(policy.parameters()).is_cuda:
+            policy.set_fp8(True)
+    return policy
 
 
 def cmd_rag(cfg, args):
@@ -122,6 +134,7 @@ def cmd_rag(cfg, args):
 
     di = _device()
     st = build_stack(cfg, di.device)
+    _apply_fp8(cfg, st["policy"])
     sp = SamplingParams(max_new_tokens=cfg.ppo.max_new_tokens, temperature=cfg.eval.temperature,
                         do_sample=cfg.eval.do_sample, top_k=cfg.eval.top_k)
     rag = RagPipeline(st["encoder"], st["index"], st["docs"], st["policy"], st["tokenizer"], cfg.retrieval.top_k, sp,
@@ -131,12 +144,12 @@ def cmd_rag(cfg, args):
         print(json.dumps({"query": a.query, "answer": a.answer, "doc_ids": a.doc_ids, "timings": a.timings}))
 
 
-def cmd_sft(cfg, args):
+def cmd_sft(cfg, args, stack=None):
     from .train import SFTTrainer, build_raft_examples
     from .utils import MetricsSink
 
     di = _device()
-    st = build_stack(cfg, di.device)
+    st = stack or build_stack(cfg, di.device)
     recs = _records(cfg, st, cfg.data.n_queries)
     items = [r for r in recs if "gold_doc" in r] or recs
     examples = build_raft_examples(items, st["docs"], cfg.raft) if "gold_doc" in items[0] else \
@@ -145,23 +158,28 @@ def cmd_sft(cfg, args):
     run_dir = os.path.join(cfg.out_dir, cfg.name)
     sink = MetricsSink(run_dir if di.is_main else None, config=C.to_dict(cfg), use_wandb=cfg.use_wandb)
     tr = SFTTrainer(st["policy"], st["tokenizer"], cfg.sft, sink)
-    hist = tr.fit(examples, epochs=cfg.data.epochs)
-    tr.save(os.path.join(run_dir, "sft"), full_policy=getattr(cfg.sft, "save_full_policy", True))
+    # best / per-epoch / mid-epoch checkpoints (rl.py:357-363) in their own directory; --resume
+    # continues from the most advanced of them
+    hist = tr.fit(examples, epochs=cfg.data.epochs, ckpt_dir=os.path.join(run_dir, "sft_ckpt"),
+                  save_every=cfg.sft.save_every, resume=bool(getattr(args, "resume", False)))
+    tr.save(os.path.join(run_dir, "sft"), full_policy=getattr(cfg.sft, "save_full_policy", True),
+            epoch=cfg.data.epochs)
     if di.is_main:
-        print(json.dumps({"final_loss": hist[-1]["loss"] if hist else None, "steps": len(hist)}))
-    return tr
+        print(json.dumps({"final_loss": hist[-1]["loss"] if hist else None, "steps": tr.global_step}))
+    return tr, st
 
 
-def cmd_ppo(cfg, args, policy=None):
+def cmd_ppo(cfg, args, policy=None, stack=None):
     from .data import RecordLoader
     from .rewards import RewardModel
     from .train import PPOTrainer
     from .utils import MetricsSink
 
     di = _device()
-    st = build_stack(cfg, di.device, need_policy=policy is None)
+    st = stack or build_stack(cfg, di.device, need_policy=policy is None)
     if policy is not None:
         st["policy"] = policy
+    _apply_fp8(cfg, st["policy"])
     recs = _records(cfg, st, cfg.data.n_queries)
     run_dir = os.path.join(cfg.out_dir, cfg.name)
     sink = MetricsSink(run_dir if di.is_main else None, config=C.to_dict(cfg), use_wandb=cfg.use_wandb)
@@ -227,18 +245,26 @@ def cmd_eval(cfg, args):
 
 
 def cmd_pipeline(cfg, args):
-    """Config 5: RAG index -> RAFT LoRA SFT -> PPO, chained THROUGH CHECKPOINTS: the SFT stage
-    writes its PEFT adapter to disk, the PPO stage builds a fresh policy and loads that adapter
-    from the directory (as the reference hands stages over by path, rl.py:365-379,494-498)."""
+    """Config 5: RAG index -> RAFT LoRA SFT -> PPO on ONE stack (tokenizer, encoder, embeddings and
+    index are built once), with the policy handed from SFT to PPO THROUGH the SFT checkpoint on disk
+    (as the reference hands stages over by path, rl.py:365-379,494-498): the PEFT adapter is
+    re-read into the policy (LoRA), or the saved HF policy weights (``sft.full_finetune``). The SFT
+    trainer (optimizer moments, flat buffers) is dropped before PPO builds its own."""
+    from .models import io as mio
     from .models import load_adapter
 
-    tr = cmd_sft(cfg, args)
-    adapter_dir = os.path.join(cfg.out_dir, cfg.name, "sft_adapter")
+    tr, st = cmd_sft(cfg, args)
+    run_dir = os.path.join(cfg.out_dir, cfg.name)
+    policy = tr.model
     del tr
-    di = _device()
-    st = build_stack(cfg, di.device)
-    load_adapter(st["policy"], adapter_dir)
-    return cmd_ppo(cfg, args, policy=st["policy"])
+    if cfg.sft.full_finetune:
+        mio.load_hf_state_dict(policy, mio.read_state_dict(os.path.join(run_dir, "sft_policy")))
+        policy.requires_grad_(False)
+    else:
+        load_adapter(policy, os.path.join(run_dir, "sft_adapter"))
+    if policy.embed.is_cuda:
+        torch.cuda.empty_cache()
+    return cmd_ppo(cfg, args, policy=policy, stack=st)
 
 
 def cmd_serve(cfg, args):
@@ -280,7 +306,8 @@ def main(argv: Optional[List[str]] = None):
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--nproc", type=int, default=1)
     ap.add_argument("--env", action="append", default=[], help="launch: KEY=VALUE set for every rank (repeatable)")
-    ap.add_argument("--resume", action="store_true", help="ppo: continue from the run's latest epoch checkpoint")
+    ap.add_argument("--resume", action="store_true",
+                    help="sft / ppo / pipeline: continue from the run's latest checkpoint")
     if argv and argv[0] == "launch":
         a, rest = ap.parse_known_args(argv)
         return cmd_launch(a, [x for x in rest])

@@ -26,6 +26,9 @@ class ModelSection:
     encoder: str = "minilm-l6:random"
     dtype: str = "bfloat16"
     seed: int = 0
+    # fp8 (OCP e4m3fn) weight images for every no-grad policy forward: rollout prefill / decode,
+    # reference scoring, RAG answers (config 5). Training forwards keep the bf16 weights.
+    fp8: bool = False
 
 
 @dataclass
@@ -79,7 +82,8 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # 4: Mistral-7B PPO (actor+ref+reward colocated), DP=8, hipGraph decode
     "config4_ppo_mistral7b": {"model.policy": "mistral-7b:random", "ppo.lora_r": 16, "data.batch_size": 64},
     # 5: Llama-2-13B full pipeline (RAG -> LoRA SFT -> PPO) on 8 GPUs
-    "config5_pipeline_llama13b": {"model.policy": "llama2-13b:random", "sft.lora_r": 16, "ppo.lora_r": 16},
+    "config5_pipeline_llama13b": {"model.policy": "llama2-13b:random", "sft.lora_r": 16, "ppo.lora_r": 16,
+                                  "model.fp8": True},
 }
 
 

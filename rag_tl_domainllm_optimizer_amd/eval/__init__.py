@@ -17,7 +17,7 @@ import torch
 
 from ..generation import Generator, SamplingParams
 from ..metrics import bleu, rouge_scores
-from ..rag.prompt import build_prompt, extract_answer
+from ..rag.prompt import encode_prompt, extract_answer
 
 METRIC_KEYS = ["rouge1", "rouge2", "rougeL", "bleu", "relevance", "factual_accuracy", "overall_score"]
 
@@ -43,10 +43,15 @@ class Evaluator:
     def generate(self, model, tokenizer, items: Sequence[dict]) -> List[str]:
         c = self.cfg
         prompts = []
+        # the prompt keeps room for the answer: documents are dropped lowest-ranked first (as in
+        # the rollouts) instead of cutting "Query: ..." off the front
+        budget = max(1, c.max_length - c.max_new_tokens)
         for it in items:
-            text = build_prompt(it["query"], it.get("retrieved_docs") or []) if c.include_docs else it["query"]
-            ids = tokenizer.encode(text)
-            prompts.append(ids[-(c.max_length - 1):])
+            if c.include_docs:
+                prompts.append(encode_prompt(tokenizer, it["query"], it.get("retrieved_docs") or [], budget))
+            else:
+                ids = tokenizer.encode(it["query"])
+                prompts.append(ids[-(c.max_length - 1):])
         S = max(len(p) for p in prompts)
         T = max(1, min(c.max_new_tokens, c.max_length - S))
         gen = Generator(model, min(c.batch_size, len(prompts)), S + T + 1)

@@ -179,10 +179,14 @@ class CausalLM(nn.Module):
         self._rope = None
         self._head_shuf = None  # ShufCache of the LM head for decode at batch <= 16
         # decode steps run the fused 4-GEMM layer (norms folded into GEMMs, residual epilogues) up to
-        # this batch; above it the hipBLASLt GEMMs + separate norm kernels measured faster
-        # (MI355X, Mistral-7B: batch 1 4.15 -> 4.0 ms/token fused; batch 64 5.1 -> 5.5 ms/step)
+        # this batch: bf16 on the no-split tile-ordered GEMVs (M <= 16); above it the bf16 decode
+        # layer uses the token-parallel 256x128 split-K GEMMs with the split-K partials summed inside
+        # the norm and attention-prologue kernels (``defer_splitk``). With fp8 weights (config 5)
+        # the fused layer runs up to batch 64: W8A16 tile-ordered GEMVs to 16 rows, then the fp8
+        # LDS-DMA ring with the same folded-norm / SwiGLU / residual epilogues
         self.fused_decode = True
         self.fused_decode_max_batch = 16
+        self.fused_decode_max_batch_fp8 = 64
         # decode at batch > 64: leave split-K partials for the consumer kernels to sum
         self.defer_splitk = True
         # batch 1: attention + o_proj + residual in one launch (ops.decode_step_attention_o). Off by
@@ -353,7 +357,9 @@ class CausalLM(nn.Module):
         cfg = self.cfg
         cos, sin = self.rope(tokens.device)
         x = self.embed_tokens(tokens, pos)
-        if (self.fused_decode and cfg.arch != "opt" and x.is_cuda and x.shape[0] <= self.fused_decode_max_batch
+        fp8 = bool(self.layers) and self.layers[0].fp8_enabled
+        max_b = self.fused_decode_max_batch_fp8 if fp8 else self.fused_decode_max_batch
+        if (self.fused_decode and cfg.arch != "opt" and x.is_cuda and x.shape[0] <= max_b
                 and not torch.is_grad_enabled()):
             h = x
             for li, layer in enumerate(self.layers):

@@ -4,8 +4,9 @@
 * M > 64 (prefill / reference-model scoring): W8A8 — activations quantised per token, one
   MX-scaled ``mfma_f32_16x16x128_f8f6f4`` 256x256 GEMM (2x the bf16 MFMA rate), scales in the
   epilogue;
-* M <= 64 (decode): W8A16 — bf16 activations, fp8 weights widened in registers by the split-K
-  skinny kernel: half the weight bytes streamed per token.
+* M <= 64 (decode): W8A16 — bf16 activations, fp8 weights widened to bf16 in registers: half the
+  weight bytes streamed per token, from a tile-ordered fp8 image (``Fp8Cache.shuf``): one
+  workgroup per 16 weight rows (no split-K) up to M = 16, the LDS-DMA ring above.
 gfx950 uses OCP e4m3fn (max 448), not the MI300 fnuz variant (cdna_hip_programming.md §3).
 """
 from __future__ import annotations
@@ -62,7 +63,8 @@ def fp8_supported(w: torch.Tensor) -> bool:
 
 class Fp8Cache(dict):
     """fp8 image of one weight, refreshed in place when the source tensor changes (address or
-    in-place version, e.g. a re-merged LoRA weight) so graph-captured decode steps stay valid."""
+    in-place version, e.g. a re-merged LoRA weight) so graph-captured decode steps stay valid.
+    ``shuf`` adds the tile-ordered decode image (built on first use, then kept in step)."""
 
     @torch.no_grad()
     def get(self, w: torch.Tensor):
@@ -75,7 +77,30 @@ class Fp8Cache(dict):
             else:
                 self["q"], self["s"] = q, s
             self["key"] = key
+            if "qs" in self:
+                self._shuffle()
         return self["q"], self["s"]
+
+    def _shuffle(self):
+        q = self["q"]
+        qs = dict.get(self, "qs")
+        if qs is None or qs.shape != q.shape or qs.device != q.device:
+            qs = torch.empty_like(q)
+            self["qs"] = qs
+        native().shuffle_decode_weight_fp8(q, qs)
+
+    @torch.no_grad()
+    def shuf(self, w: torch.Tensor):
+        """(tile-ordered fp8 image, scales) for the M <= 16 W8A16 kernel."""
+        self.get(w)
+        if "qs" not in self:
+            self._shuffle()
+        return self["qs"], self["s"]
+
+    @staticmethod
+    def shuf_ok(w: torch.Tensor, m: int, act: int = 0) -> bool:
+        """The tile-ordered fp8 image serves every W8A16 decode GEMM (M <= 64) of these shapes."""
+        return m <= 64 and w.shape[1] % 128 == 0 and w.shape[0] % (64 if act == 5 else 16) == 0
 
     def get_key(self):
         return dict.get(self, "key")

@@ -211,9 +211,11 @@ class LoRAGroup:
 
     @torch.no_grad()
     def merged_weight(self, w: torch.Tensor, rows_per_chunk: int = 4096) -> torch.Tensor:
-        """W + UB A_pad (fp32 accumulate, one bf16 rounding), updated IN PLACE so captured graphs
-        that read it stay valid across adapter updates. On the GPU one NN GEMM (K = Rp) with W as
-        the residual input of its epilogue: 4 B of traffic per weight element."""
+        """W + UB A_pad, updated IN PLACE so captured graphs that read it stay valid across adapter
+        updates. On the GPU one NN GEMM (K = Rp) with W as the residual input of its epilogue: 4 B
+        of traffic per weight element. Rounding: UB A_pad is accumulated in fp32 and rounded to
+        bf16, then W is added in fp32 and the sum rounded again — two bf16 roundings, bitwise what
+        a GEMM followed by a separate add kernel gives (the CPU path rounds once)."""
         if self.merged is None or self.merged.shape != w.shape or self.merged.device != w.device:
             self.merged = torch.empty(w.shape, dtype=w.dtype, device=w.device)
             self.merged_dirty = True
@@ -265,40 +267,44 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], *lora_params):
         u = ub = xd = None
+        mask = None
         if lora is not None:
             xd = x2
             if lora.dropout > 0:
-                ctx.mask = _dropout_mask(x2, lora.dropout)
-                xd = x2 * ctx.mask
+                mask = _dropout_mask(x2, lora.dropout)
+                xd = x2 * mask
             u = _narrow(xd, lora.a_pad, ROW)  # [M, Rp] = drop(X) (s A)^T
             ub = lora.ub
         ctx.act = act
         ctx.lora = lora
         ctx.has_bias = bias is not None
-        ctx.pre = None
+        pre = None
         if act == ACT_SWIGLU:
             # w = [gate; up]: ONE GEMM writes silu(g) * u and the [M, 2F] pre-activation (kept for
             # the SwiGLU backward) from its epilogue — no separate SwiGLU pass over the activations
             pre = torch.empty(x2.shape[0], w.shape[0], dtype=x2.dtype, device=x2.device)
             y = gemm_big(x2, w, ROW, ROW, u, ub, None, ACT_SWIGLU, out2=pre)
-            ctx.pre = pre
         else:
             y = gemm(x2, w, u, ub, bias, act)
         # other activation epilogues: the pre-activation is recomputed in backward (no extra
-        # activation-sized tensor is kept alive)
-        ctx.save_for_backward(x2, w, u if u is not None else torch.empty(0), bias if bias is not None else torch.empty(0))
+        # activation-sized tensor is kept alive). The SwiGLU pre-activation and the dropout mask go
+        # through save_for_backward like everything else, so non-reentrant activation
+        # checkpointing frees them between forward and backward (and recomputes them)
+        e = torch.empty(0)
+        ctx.save_for_backward(x2, w, u if u is not None else e, bias if bias is not None else e,
+                              pre if pre is not None else e, mask if mask is not None else e)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w, u, bias = ctx.saved_tensors
+        x2, w, u, bias, pre, mask = ctx.saved_tensors
+        mask = mask if mask.numel() else None
         lora = ctx.lora
         dy = dy.contiguous()
         if ctx.act == ACT_SWIGLU:
             from .misc import _swiglu_grad
 
-            dy = _swiglu_grad(ctx.pre, dy)  # d[gate | up]
-            ctx.pre = None
+            dy = _swiglu_grad(pre, dy)  # d[gate | up]
         elif ctx.act != 0:
             # recompute pre-activation and apply the activation derivative
             ub = lora.ub if lora is not None else None
@@ -312,7 +318,6 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         gpu = on_gpu(dy)
         du = _narrow(dy, lora.ub, KMAJ) if lora is not None else None  # [M, Rp] = dL/dU
-        mask = getattr(ctx, "mask", None)
         if needs[0]:
             if lora is not None and mask is None:
                 # dX = dY W + dU A_pad in ONE NN GEMM (the adapter term as K-extension steps)
@@ -376,8 +381,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
                 from .fp8 import fp8_supported
 
                 if fp8_supported(w_eff):
-                    q, sc = fp8.get(w_eff)
-                    y = native().gemm_fp8(x2, None, q, sc, None, ACT_SWIGLU, None)
+                    shuf = fp8.shuf_ok(w_eff, x2.shape[0], ACT_SWIGLU)
+                    q, sc = fp8.shuf(w_eff) if shuf else fp8.get(w_eff)
+                    y = native().gemm_fp8(x2, None, q, sc, None, ACT_SWIGLU, None, None, 0.0, shuf)
                     return y.reshape(*shp[:-1], w.shape[0] // 2)
             y = gemm(x2, w_eff, None, None, None, ACT_SWIGLU)
             return y.reshape(*shp[:-1], w.shape[0] // 2)
@@ -389,8 +395,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
 
         w_eff = lora.merged_weight(w) if use_lora else w
         if fp8_supported(w_eff) and (x2.shape[0] > 64 or x2.shape[1] % 64 == 0):
-            q, s = fp8.get(w_eff)
-            y = gemm_fp8(x2, q, s, bias, act_id)
+            if on_gpu(x2) and fp8.shuf_ok(w_eff, x2.shape[0], act_id):
+                qs, s = fp8.shuf(w_eff)
+                y = native().gemm_fp8(x2, None, qs, s, bias, act_id, None, None, 0.0, True)
+            else:
+                q, s = fp8.get(w_eff)
+                y = gemm_fp8(x2, q, s, bias, act_id)
             return y.reshape(*shp[:-1], w.shape[0])
     if use_lora and lora.use_merged and not torch.is_grad_enabled():
         y = gemm(x2, lora.merged_weight(w), None, None, bias, act_id)
@@ -460,6 +470,9 @@ def gemm_decode(x: torch.Tensor, w: torch.Tensor, act: int = 0, residual=None, n
             from .fp8 import fp8_supported
 
             if fp8_supported(w):
+                if fp8.shuf_ok(w, x.shape[0], act):
+                    qs, sc = fp8.shuf(w)
+                    return native().gemm_fp8(x, None, qs, sc, None, act, None, residual, norm_eps, True)
                 q, sc = fp8.get(w)
                 return native().gemm_fp8(x, None, q, sc, None, act, None, residual, norm_eps)
         if shuf is not None and x.shape[0] <= 16 and w.shape[0] % 16 == 0:

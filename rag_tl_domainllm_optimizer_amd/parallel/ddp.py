@@ -11,10 +11,20 @@ buckets and averages.
 Bucket sizing for xGMI: a ring all-reduce moves 2(N-1)/N x bytes through each link; LoRA grads are
 latency-bound (tens to ~170 MB), so a few large buckets (default 64 MB) amortise the per-collective
 latency while still leaving the last buckets to overlap with the tail of backward.
+
+bf16 gradient slices (full-parameter training, ``ops.MixedFlatParams``) are NOT summed in bf16: a
+ring all-reduce rounds the running sum to 8 significant bits at every hop (about 3 bits lost at
+world 8). Mode ``"rs32"`` (default): the slice is widened to an fp32 staging buffer and
+reduce-scattered in fp32 (overlapped with backward, (N-1)/N x 4 B per weight), each rank rounds its
+summed shard to bf16 once, and a bf16 all-gather ((N-1)/N x 2 B) completes it in ``finish()`` —
+6 B of link traffic per weight against 4 B for a bf16 all-reduce and 8 B for an fp32 one, with a
+single rounding. ``"bf16"`` keeps the in-place bf16 all-reduce (RAGTL_BF16_REDUCE=bf16).
 """
 from __future__ import annotations
 
 from typing import List, Optional
+
+import os
 
 import torch
 import torch.distributed as dist
@@ -23,8 +33,10 @@ from .dist import info
 
 
 class GradSync:
-    def __init__(self, flat, bucket_bytes: int = 64 << 20, overlap: bool = True):
+    def __init__(self, flat, bucket_bytes: int = 64 << 20, overlap: bool = True, bf16_reduce: str = None):
         self.flat = flat
+        self.bf16_reduce = bf16_reduce or os.environ.get("RAGTL_BF16_REDUCE", "rs32")
+        assert self.bf16_reduce in ("rs32", "bf16"), self.bf16_reduce
         self.world = info().world
         self.enabled = info().enabled
         self.gloo = self.enabled and dist.get_backend() == "gloo"
@@ -58,6 +70,8 @@ class GradSync:
         self._hooks = []
         self.sync_enabled = True
         self.wait_s = 0.0  # host time blocked in finish() (exposed all-reduce tail), reset by the caller
+        self.comm_bytes = 0  # payload bytes handed to collectives (per rank), reset by the caller
+        self._stage2 = []    # (bf16 slice, fp32 summed shard, gathered fp32-free bf16 buffer) of rs32 buckets
         if self.overlap:
             for p, bi in zip(flat.params, self.param_bucket):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
@@ -75,18 +89,44 @@ class GradSync:
         s, e = self.buckets[bi]
         hs = []
         # one slice per gradient buffer the bucket touches (fp32, or bf16 + fp32 under full-parameter
-        # training: ops.MixedFlatParams); RCCL reduces bf16 in place, 2 B per weight over xGMI
+        # training: ops.MixedFlatParams)
         for t in self.flat.grad_slices(s, e):
-            if t.dtype == torch.bfloat16 and (not t.is_cuda or self.gloo):
-                # gloo (CPU runs, and the one-GPU multi-rank rehearsal): reduce an fp32 copy of a
-                # bf16 slice. RCCL reduces bf16 in place (2 B per weight over xGMI); its ring sums
-                # in bf16, which the full-fine-tuning DP tests bound (docs/DESIGN.md)
-                f = t.float()
-                dist.all_reduce(f)
-                t.copy_(f)
+            if t.dtype == torch.bfloat16 and (self.bf16_reduce == "rs32" or not t.is_cuda or self.gloo):
+                hs.append(self._rs32(t))
             else:
+                self.comm_bytes += t.numel() * t.element_size()
                 hs.append(dist.all_reduce(t, async_op=True))
         self._handles[bi] = hs
+
+    def _rs32(self, t: torch.Tensor):
+        """Stage 1 of the fp32 reduction of a bf16 slice: widen into a padded fp32 buffer and
+        reduce-scatter it (async). Stage 2 (round the shard once, bf16 all-gather) runs in finish()."""
+        w = self.world
+        n = t.numel()
+        shard = (n + w - 1) // w
+        buf = torch.zeros(shard * w, dtype=torch.float32, device=t.device)
+        buf[:n].copy_(t)
+        out = torch.empty(shard, dtype=torch.float32, device=t.device)
+        self.comm_bytes += buf.numel() * 4
+        h = dist.reduce_scatter_tensor(out, buf, async_op=True)
+        self._stage2.append((t, out, h))
+        return _Done()
+
+    def _finish_rs32(self):
+        if not self._stage2:
+            return
+        w = self.world
+        gathers = []
+        for t, out, h in self._stage2:
+            h.wait()
+            shard16 = out.to(torch.bfloat16)  # the ONE rounding of the fp32 sum
+            full = torch.empty(shard16.numel() * w, dtype=torch.bfloat16, device=t.device)
+            self.comm_bytes += full.numel() * 2
+            gathers.append((t, full, dist.all_gather_into_tensor(full, shard16, async_op=True)))
+        for t, full, h in gathers:
+            h.wait()
+            t.copy_(full[:t.numel()])
+        self._stage2 = []
 
     def no_sync(self):
         """Context manager: accumulate gradients locally (micro-batches before the last one)."""
@@ -120,6 +160,7 @@ class GradSync:
         for hs in self._handles:
             for h in hs:
                 h.wait()
+        self._finish_rs32()
         self.flat.div_grads(self.world)
         self.wait_s += time.perf_counter() - t0
         self._handles = [None] * len(self.buckets)
@@ -129,3 +170,10 @@ class GradSync:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+
+class _Done:
+    """Handle of a collective whose completion finish() tracks elsewhere (rs32 stage 2)."""
+
+    def wait(self):
+        return True

@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from ..generation import Generator, SamplingParams
-from .prompt import build_prompt, extract_answer
+from .prompt import build_prompt, extract_answer, encode_prompt
 
 
 @dataclass
@@ -53,12 +53,7 @@ class RagPipeline:
         return self.index.search(q, k or self.top_k)
 
     def _prompt_ids(self, query: str, docs: List[str]) -> List[int]:
-        docs = list(docs)
-        ids = self.tok.encode(build_prompt(query, docs))
-        while len(ids) > self.max_prompt_tokens and docs:
-            docs.pop()
-            ids = self.tok.encode(build_prompt(query, docs))
-        return ids[-self.max_prompt_tokens:]
+        return encode_prompt(self.tok, query, docs, self.max_prompt_tokens)
 
     @torch.no_grad()
     def answer(self, queries: Sequence[str]) -> List[RagAnswer]:

@@ -25,3 +25,18 @@ def fit_docs(query: str, docs: List[str], count_tokens, max_prompt_tokens: int) 
     while docs and count_tokens(build_prompt(query, docs)) > max_prompt_tokens:
         docs.pop()
     return docs
+
+
+def encode_prompt(tokenizer, query: str, docs: Sequence[str], budget: int) -> List[int]:
+    """Token ids of the RAG prompt within ``budget`` tokens: the lowest-ranked documents are
+    dropped first, so the query and the instruction always survive; only a prompt that is still
+    too long with no documents left is cut, from the left. Shared by rollouts, RAG answers and the
+    evaluator."""
+    if isinstance(docs, str):
+        docs = [docs]
+    docs = list(docs)
+    ids = tokenizer.encode(build_prompt(query, docs))
+    while len(ids) > budget and docs:
+        docs.pop()
+        ids = tokenizer.encode(build_prompt(query, docs))
+    return ids[-budget:] if len(ids) > budget else ids

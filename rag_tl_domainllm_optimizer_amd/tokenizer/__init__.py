@@ -51,6 +51,20 @@ def synthetic_words(n: int, seed: int = 1234) -> List[str]:
     return words
 
 
+class BatchEncoding(dict):
+    """dict of tensors with attribute access and ``.to(device)`` (the shape of HF's BatchEncoding
+    that reference-style code unpacks into a model call: ``model(**enc)``)."""
+
+    def __getattr__(self, name):
+        try:
+            return self[name]
+        except KeyError as e:
+            raise AttributeError(name) from e
+
+    def to(self, device):
+        return BatchEncoding({k: (v.to(device) if isinstance(v, torch.Tensor) else v) for k, v in self.items()})
+
+
 class Tokenizer:
     def __init__(self, kind: str, vocab: Dict[str, int], merges=None, specials: Optional[dict] = None,
                  lowercase: bool = False, continuing_prefix: str = "##", add_prefix_space: bool = False,
@@ -100,6 +114,11 @@ class Tokenizer:
     def pad_token(self):
         p = self.specials.get("pad") or self.specials.get("eos")
         return p[0] if p else None
+
+    @pad_token.setter
+    def pad_token(self, tok: str):
+        """``tokenizer.pad_token = tokenizer.eos_token`` (the reference's pad fix, rl.py:143-146)."""
+        self.specials["pad"] = (tok, self.token_to_id(tok))
 
     @property
     def eos_token(self):
@@ -180,10 +199,17 @@ class Tokenizer:
         return out
 
     def __call__(self, texts, padding: bool = True, max_length: Optional[int] = None, add_special_tokens=True,
-                 side: Optional[str] = None, device=None):
+                 side: Optional[str] = None, device=None, return_tensors: Optional[str] = "pt",
+                 truncation: bool = False):
+        """HF-style call (``tokenizer(text, return_tensors="pt").to(device)``, rl.py:36,196,309):
+        a :class:`BatchEncoding` of torch tensors (``input_ids``, ``attention_mask``, plus
+        ``lengths`` / ``start``). ``return_tensors`` other than "pt" is not supported."""
+        if return_tensors not in (None, "pt"):
+            raise ValueError(f"return_tensors={return_tensors!r}: only torch tensors are supported")
         single = isinstance(texts, str)
-        seqs = self.encode_batch([texts] if single else list(texts), add_special_tokens, max_length)
-        return self.pad(seqs, side=side, device=device)
+        seqs = self.encode_batch([texts] if single else list(texts), add_special_tokens,
+                                 max_length if (truncation or max_length) else None)
+        return BatchEncoding(self.pad(seqs, side=side, device=device))
 
     # --------------------------------------------------------------- persistence
     def to_hf_json(self) -> dict:

@@ -147,16 +147,27 @@ def save_rank_rng(prefix: str, rank: int, rng: dict):
 
 
 def load_rank_rng(prefix: str, rank: int):
+    """This rank's saved RNG state. Never another rank's: copying rank 0's streams onto rank r
+    would make dropout masks and sampling draws identical across ranks. When rank r's file is
+    missing (world-size change, crash between the save barriers) the caller gets None plus a
+    warning and keeps its own freshly seeded streams. Rank 0 also reads the single-file layout of
+    older checkpoints (``rng.safetensors`` / ``rng.json``)."""
+    import warnings
+
     from safetensors.torch import load_file
 
     from ..utils.seed import rng_state_unpack
 
     d = f"{prefix}_trainer_state"
-    for r in (rank, 0):
-        f = os.path.join(d, f"rng_rank{r}.safetensors")
+    names = [f"rng_rank{rank}"] + (["rng"] if rank == 0 else [])
+    for n in names:
+        f = os.path.join(d, f"{n}.safetensors")
         if os.path.exists(f):
-            with open(os.path.join(d, f"rng_rank{r}.json")) as fh:
+            with open(os.path.join(d, f"{n}.json")) as fh:
                 return rng_state_unpack(load_file(f), json.load(fh))
+    if os.path.isdir(d):
+        warnings.warn(f"{d}: no RNG state saved for rank {rank}; this rank keeps its own seeded RNG streams",
+                      RuntimeWarning)
     return None
 
 

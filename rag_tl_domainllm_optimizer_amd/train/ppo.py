@@ -34,7 +34,7 @@ from .. import ops
 from ..generation import Generator, SamplingParams
 from ..models import ValueHead
 from ..parallel import GradSync, info as dist_info, reduce_metrics
-from ..rag.prompt import build_prompt, extract_answer
+from ..rag.prompt import build_prompt, encode_prompt, extract_answer
 from ..runtime import PhaseTimer, StreamPair
 from ..utils import MetricsSink, maybe_inject_fault
 from .common import lr_at, score_sequences
@@ -185,18 +185,8 @@ class PPOTrainer:
 
     # ------------------------------------------------------------------ prompts
     def encode_prompts(self, queries: Sequence[str], docs: Sequence[Sequence[str]]) -> List[List[int]]:
-        out = []
-        budget = self.cfg.max_prompt_tokens
-        for q, ds in zip(queries, docs):
-            ids = self.tok.encode(build_prompt(q, ds))
-            if len(ids) > budget:  # drop lowest-ranked docs until the prompt fits (SURVEY 5.7 d)
-                ds = list(ds)
-                while ds and len(ids) > budget:
-                    ds.pop()
-                    ids = self.tok.encode(build_prompt(q, ds))
-                ids = ids[-budget:]
-            out.append(ids)
-        return out
+        # drop lowest-ranked docs until the prompt fits (SURVEY 5.7 d)
+        return [encode_prompt(self.tok, q, ds, self.cfg.max_prompt_tokens) for q, ds in zip(queries, docs)]
 
     # ------------------------------------------------------------------ rollout + reward
     @torch.no_grad()
@@ -420,7 +410,7 @@ class PPOTrainer:
     def trainer_state(self, epoch: int = 0, best: float = -math.inf, batch_in_epoch: int = 0):
         from ..utils import rng_state
 
-        return {"global_step": self.global_step, "epoch": epoch, "batch_in_epoch": batch_in_epoch,
+        return {"kind": "ppo", "global_step": self.global_step, "epoch": epoch, "batch_in_epoch": batch_in_epoch,
                 "best_reward": best, "config": asdict(self.cfg),
                 "kl_coef": self.kl_coef, "rng": rng_state(),
                 # the on-device Philox counter of the rollout sampler: a resumed run continues the

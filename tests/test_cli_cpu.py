@@ -77,3 +77,46 @@ def test_cli_ppo_resume_from_latest(tmp_path, capsys):
     out = capsys.readouterr().out
     assert "Resumed from" in out and "Epoch 2/2" in out and "Epoch 1/2" not in out
     assert (tmp_path / "run" / "epoch_2_trainer_state").is_dir()
+
+
+def test_cli_pipeline_full_finetune_sft(tmp_path):
+    """Full-parameter SFT writes no adapter: the pipeline hands the SFT-trained weights to PPO
+    through the saved HF policy (sft_policy), and the index is built once."""
+    import os
+
+    import torch
+
+    from rag_tl_domainllm_optimizer_amd.models import io as mio
+
+    calls = []
+    real = cli.build_stack
+
+    def counting(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+    cli.build_stack = counting
+    try:
+        tr = cli.main(["pipeline", *_tiny(tmp_path), "--sft.full_finetune=True", "--sft.lr=1e-3"])
+    finally:
+        cli.build_stack = real
+    assert len(calls) == 1
+    run = tmp_path / "run"
+    assert os.path.isdir(run / "sft_policy") and not os.path.isdir(run / "sft_adapter")
+    # the PPO policy started from the SFT weights on disk (PPO then trains LoRA on top of them)
+    sd = mio.read_state_dict(str(run / "sft_policy"))
+    w = sd["model.layers.0.mlp.down_proj.weight"]
+    base = tr.policy.layers[0].down_w.detach().float()
+    torch.testing.assert_close(base, w.float())
+
+
+def test_cli_sft_resume_and_epoch_checkpoints(tmp_path, capsys):
+    args = _tiny(tmp_path) + ["--data.epochs=1", "--sft.save_every=1"]
+    cli.main(["sft", *args])
+    ck = tmp_path / "run" / "sft_ckpt"
+    assert (ck / "epoch_1_adapter").is_dir() and (ck / "best_model_trainer_state").is_dir()
+    cli.main(["sft", *[a for a in args if not a.startswith("--data.epochs")], "--data.epochs=2", "--resume"])
+    out = capsys.readouterr().out
+    assert "[sft] resumed from" in out and "Epoch 2/2" in out and "Epoch 1/2" not in out
+    assert (ck / "epoch_2_trainer_state").is_dir()
+    # a PPO resume in the same run directory must not pick up an SFT checkpoint
+    assert cli.latest_checkpoint(str(tmp_path / "run")) is None

@@ -138,3 +138,51 @@ def test_dp_mixed_precision_grads(tmp_path, bucket_bytes):
         assert torch.equal(g16[48:72], torch.full((24,), 2 * mean_c))
         assert torch.equal(g32[:7], torch.full((7,), 3 * mean_c))
         assert d["buckets"] == (3 if bucket_bytes == 64 else 1)
+
+
+def _bf16_worker(rank, world, port, out_dir, mode):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from rag_tl_domainllm_optimizer_amd import ops, parallel
+    from rag_tl_domainllm_optimizer_amd.parallel import GradSync
+
+    parallel.init(device="cpu")
+    g = torch.Generator().manual_seed(100 + rank)
+    n = 4099  # not a multiple of the world: the padded reduce-scatter tail
+    ps = [torch.nn.Parameter(torch.zeros(n, dtype=torch.bfloat16)), torch.nn.Parameter(torch.zeros(5))]
+    flat = ops.MixedFlatParams(ps)
+    sync = GradSync(flat, bucket_bytes=1 << 12, bf16_reduce=mode)
+    flat.zero_grad()
+    sync.start()
+    local = (torch.randn(n, generator=g) * torch.exp(torch.randn(n, generator=g))).to(torch.bfloat16)
+    (ps[0].float() * local.float()).sum().backward()
+    sync.finish()
+    torch.save({"g": flat.grad16[:n].clone(), "local": local, "bytes": sync.comm_bytes},
+               os.path.join(out_dir, f"bf{rank}.pt"))
+    parallel.barrier()
+    parallel.shutdown()
+
+
+def test_dp_bf16_grads_reduced_in_fp32_world8(tmp_path):
+    """Full fine-tuning at world 8: bf16 gradients are reduce-scattered in fp32 and rounded ONCE
+    (rs32), so the averaged gradient is within one bf16 rounding of the exact mean on every rank —
+    unlike a ring that sums in bf16 (simulated here), which loses ~3 bits at world 8."""
+    world = 8
+    mp.start_processes(_bf16_worker, args=(world, _free_port(), str(tmp_path), "rs32"), nprocs=world,
+                       start_method="spawn", join=True)
+    outs = [torch.load(tmp_path / f"bf{r}.pt") for r in range(world)]
+    exact = sum(o["local"].double() for o in outs) / world
+    got = outs[0]["g"].double()
+    for o in outs[1:]:
+        assert torch.equal(o["g"], outs[0]["g"])  # identical on every rank
+    scale = exact.abs().clamp(min=1e-30)
+    rel = ((got - exact).abs() / scale)
+    assert float(rel.max()) <= 2.0 ** -8 + 1e-12
+    # a bf16 ring: the running sum is rounded to bf16 at every hop
+    ring = outs[0]["local"].clone()
+    for o in outs[1:]:
+        ring = (ring.float() + o["local"].float()).to(torch.bfloat16)
+    ring_rel = ((ring.double() / world - exact).abs() / scale)
+    assert float(rel.mean()) < 0.5 * float(ring_rel.mean())
+    # link payload: fp32 reduce-scatter (4 B) + bf16 all-gather (2 B) per weight (+ fp32 value head)
+    assert outs[0]["bytes"] >= 6 * 4099

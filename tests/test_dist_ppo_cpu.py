@@ -146,3 +146,60 @@ def test_dp_sft_uneven_shards(tmp_path, world, n):
     assert len({x["steps"] for x in r}) == 1 and r[0]["steps"] >= 2
     for x in r[1:]:
         assert torch.equal(x["params"], r[0]["params"])
+
+
+def _sft_resume_worker(rank, world, port, out_dir, mode):
+    _env(rank, world, port)
+    from rag_tl_domainllm_optimizer_amd import models, parallel
+    from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
+    from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
+    from rag_tl_domainllm_optimizer_amd.train.sft import SFTConfig, SFTTrainer
+    from rag_tl_domainllm_optimizer_amd.utils.faults import InjectedFault
+
+    parallel.init(device="cpu", timeout_s=120)
+    cfg = PRESETS["tiny-llama"]
+    tok = Tokenizer.synthetic(cfg.vocab_size, "llama")
+    words = tok.words()
+    ex = [{"prompt": " ".join(words[i:i + 6]), "answer": " ".join(words[50 + i:54 + i])} for i in range(24)]
+
+    def trainer():
+        m = models.CausalLM(cfg, dtype=torch.float32, seed=1)
+        return SFTTrainer(m, tok, SFTConfig(lr=1e-2, lora_r=4, lr_schedule="cosine", warmup_steps=1, total_steps=6,
+                                            batch_size=4))
+    ck = os.path.join(out_dir, f"ck_{mode}")
+    tr = trainer()
+    if mode == "crash":
+        os.environ["RAGTL_FAULT_AT_STEP"] = "5"
+        try:
+            tr.fit(ex, epochs=2, log_every=0, ckpt_dir=ck, save_every=2)
+            raise AssertionError("fault not injected")
+        except InjectedFault:
+            pass
+        del os.environ["RAGTL_FAULT_AT_STEP"]
+        parallel.barrier()
+        tr = trainer()  # a fresh process' state: new model, new optimizer
+        tr.fit(ex, epochs=2, log_every=0, ckpt_dir=ck, save_every=2, resume=True)
+    else:
+        tr.fit(ex, epochs=2, log_every=0, ckpt_dir=ck, save_every=2)
+    params = torch.cat([p.detach().reshape(-1) for p in tr.flat.params])
+    torch.save({"params": params, "step": tr.global_step, "m": tr.opt.state_dict()["exp_avg"].clone()},
+               os.path.join(out_dir, f"sftr_{mode}{rank}.pt"))
+    parallel.barrier()
+    parallel.shutdown()
+
+
+def test_dp_sft_resume_mid_epoch_matches_uninterrupted(tmp_path):
+    """gloo world 2: an SFT run killed at step 5 (mid epoch 2) and resumed from its mid-epoch
+    "latest" checkpoint (adapter, optimizer moments, LR-schedule position, each rank's RNG and
+    place in the epoch) ends with exactly the parameters of the uninterrupted run."""
+    world = 2
+    for mode in ("full", "crash"):
+        mp.start_processes(_sft_resume_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world,
+                           start_method="spawn", join=True)
+    for r in range(world):
+        a = torch.load(tmp_path / f"sftr_full{r}.pt", weights_only=False)
+        b = torch.load(tmp_path / f"sftr_crash{r}.pt", weights_only=False)
+        assert a["step"] == b["step"] == 6
+        assert torch.equal(a["params"], b["params"])
+        assert torch.equal(a["m"], b["m"])
+    assert (tmp_path / "ck_crash" / "latest_trainer_state").is_dir()

@@ -871,3 +871,51 @@ def test_gemv16_no_split_matches_fp32(M, N, K):
         g, u = xn @ w[:F].float().t(), xn @ w[F:].float().t()
         _close(ops.gemm_decode(x, wf, act=ops.ACT_SWIGLU, norm_eps=1e-5, shuf=shuf_f),
                torch.nn.functional.silu(g) * u)
+
+
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 40, 64])
+@pytest.mark.parametrize("N,K", [(512, 256), (6144, 4096), (5120, 13824)])
+@pytest.mark.parametrize("mode", ["plain", "norm_res", "swiglu"])
+def test_gemm_fp8_decode_w8a16(M, N, K, mode):
+    """W8A16 decode GEMMs (config 5): tile-ordered fp8 image on the no-split 16-row kernel (M <= 16)
+    and the fp8 LDS-DMA ring (M > 16), with the in-GEMM RMS norm + residual and SwiGLU pair
+    epilogues, against an fp32 oracle on the dequantised weights."""
+    torch.manual_seed(M * 7 + N + K)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    cache = ops.Fp8Cache()
+    wq, sw = cache.get(w)
+    wd = ops.dequantize_fp8(wq, sw)
+    act = 5 if mode == "swiglu" else 0
+    eps = 1e-5 if mode == "norm_res" else 0.0
+    Nout = N // 2 if act == 5 else N
+    res = torch.randn(M, Nout, device=DEV, dtype=torch.bfloat16) if mode == "norm_res" else None
+    xf = x.float()
+    y = xf @ wd.t()
+    if eps:
+        y = y * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    if act == 5:
+        y = torch.nn.functional.silu(y[:, :N // 2]) * y[:, N // 2:]
+    if res is not None:
+        y = y + res.float()
+    out = ops.gemm_decode(x, w, act=act, residual=res, norm_eps=eps, fp8=cache)
+    _close(out, y)
+    if K % 128 == 0:
+        # the tile-ordered image was built and used; row-major launch of the same product agrees
+        assert "qs" in cache
+        y2 = ops.native().gemm_fp8(x, None, wq, sw, None, act, None, res, eps)
+        _close(y2, y)
+        # refreshing the source rebuilds the image in place (graph-safe address)
+        qs_ptr = cache["qs"].data_ptr()
+        with torch.no_grad():
+            w.mul_(0.5)
+        out2 = ops.gemm_decode(x, w, act=act, residual=res, norm_eps=eps, fp8=cache)
+        assert cache["qs"].data_ptr() == qs_ptr
+        y3 = xf @ ops.dequantize_fp8(*cache.get(w)).t()
+        if eps:
+            y3 = y3 * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+        if act == 5:
+            y3 = torch.nn.functional.silu(y3[:, :N // 2]) * y3[:, N // 2:]
+        if res is not None:
+            y3 = y3 + res.float()
+        _close(out2, y3)
