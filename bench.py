@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--nprobe", type=int, default=16)
     ap.add_argument("--latency-queries", type=int, default=16)
     ap.add_argument("--skip-latency", action="store_true")
+    ap.add_argument("--latency-contexts", default="",
+                    help="long-context RAG answers: comma list of prompt budgets in tokens (e.g. 1024,2048,4096); "
+                         "each retrieves enough documents to fill its budget and reports p50 latency + stages")
     ap.add_argument("--vary-docs", action="store_true",
                     help="1..top-k retrieved docs per query (variable prompt lengths: exercises the varlen "
                          "packed forwards; RAGTL_PACK=0 for the padded comparison)")
@@ -160,11 +163,28 @@ def main():
         torch.cuda.empty_cache()
         log(f"[bench] RAG latency p50={lat['p50_s']:.3f}s p90={lat['p90_s']:.3f}s "
             f"({lat['mean_new_tokens']:.0f} new tokens) stages={lat['stage_mean_s']}")
+    ctx_lat = {}
+    for L in [int(x) for x in args.latency_contexts.split(",") if x]:
+        # ~50 tokens per synthetic document: retrieve enough to fill the budget, the prompt budget
+        # drops the lowest-ranked ones that do not fit
+        k = max(args.top_k_docs, L // 40)
+        rag = RagPipeline(encoder, index, corpus.docs, policy, tok, top_k=k,
+                          sampling=SamplingParams(max_new_tokens=args.new_tokens, temperature=0.7, top_k=50),
+                          max_prompt_tokens=L, max_batch=1, use_graph=not args.no_graph)
+        qs = [it.query for it in corpus.sample_queries(args.latency_queries + 2, seed=98)]
+        st = rag.latency_stats(qs, warmup=2)
+        del rag
+        torch.cuda.empty_cache()
+        ctx_lat[L] = st
+        log(f"[bench] RAG latency @ {L}-token budget: p50={st['p50_s']:.3f}s prompt={st['mean_prompt_tokens']:.0f} "
+            f"tokens, decode {st['stage_mean_s']['decode_s'] / max(st['mean_new_tokens'] - 1, 1) * 1e3:.2f} "
+            f"ms/token, stages={st['stage_mean_s']}")
     log(f"[bench] setup {time.perf_counter() - t_setup:.1f}s")
 
     if args.steps == 0:  # latency-only (profiling) mode
         if di.is_main:
-            print(json.dumps({"p50_rag_latency_s": lat["p50_s"] if lat else None, "rag_stages": lat}), flush=True)
+            print(json.dumps({"p50_rag_latency_s": lat["p50_s"] if lat else None, "rag_stages": lat,
+                              "long_context": ctx_lat}), flush=True)
         parallel.shutdown()
         return
 
@@ -222,6 +242,9 @@ def main():
         "p50_rag_latency_s": lat["p50_s"] if lat else None,
         "p90_rag_latency_s": lat["p90_s"] if lat else None,
         "rag_latency_vs_baseline": (REF_LATENCY_S / lat["p50_s"]) if lat else None,
+        **({"long_context_rag": {str(k): {"p50_s": v["p50_s"], "prompt_tokens": v["mean_prompt_tokens"],
+                                          "stage_mean_s": v["stage_mean_s"]} for k, v in ctx_lat.items()}}
+           if ctx_lat else {}),
         "phase_s_per_step": {k: v / args.steps for k, v in phase.items()},
         # data-parallel diagnostics: gradient payload each rank hands to RCCL per step, and the
         # spread of the per-rank step times (before the closing barrier) in seconds

@@ -22,6 +22,7 @@ int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const vo
 int rt_shuffle_decode_weight(const void*, void*, long, long, hipStream_t);
 int rt_shuffle_decode_weight_fp8(const void*, void*, long, long, hipStream_t);
 void rt_gemm_set_variant(int);
+void rt_gemm_set_wide_split(int);
 void rt_gemm_set_m64_split(int);
 void rt_gemm_set_decode_split(int);
 void rt_gemm_set_decode_depth(int);
@@ -1039,6 +1040,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("shuffle_decode_weight_fp8", &shuffle_decode_weight_fp8,
         "fp8 W [N, K] -> tile-ordered W8A16 decode image (gemm_fp8 w_shuffled=True)", py::arg("q"),
         py::arg("out") = py::none());
+  m.def("gemm_set_wide_split", &rt_gemm_set_wide_split, "tuning: fixed split-K of the wide W8A16 M<=64 kernel (0 = auto)");
   m.def("gemm_set_m64_split", &rt_gemm_set_m64_split, "tuning: fixed split-K of the M<=64 ring kernel (0 = auto)");
   m.def("gemm_set_decode_split", &rt_gemm_set_decode_split, "tuning: fixed split-K of the M<=16 decode kernel (0 = auto)");
   m.def("gemm_set_decode_depth", &rt_gemm_set_decode_depth, "tuning: weight-pipeline depth (2 / 4) of the M<=16 decode kernel (0 = auto)");

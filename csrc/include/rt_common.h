@@ -117,6 +117,40 @@ __device__ __forceinline__ void ds_tr16_frag4(uint32_t a0, uint32_t a1, uint32_t
       : "memory");
 }
 
+// 8 plain 8-B LDS reads at a + {0, 512, ..., 3584} (the fp8 W fragments of the W8A16 LDS-DMA ring:
+// 4 column fragments x 2 MFMA k-steps), issued from asm like the transposed reads above: hipcc
+// otherwise drains every LDS-DMA in flight (s_waitcnt vmcnt(0)) in front of them
+typedef __attribute__((ext_vector_type(2))) unsigned rt_u32x2;
+__device__ __forceinline__ void ds_read_b64_x8_512(uint32_t a, rt_u32x2 (&r)[8]) {
+  asm volatile(
+      "ds_read_b64 %0, %8\n\t"
+      "ds_read_b64 %1, %8 offset:512\n\t"
+      "ds_read_b64 %2, %8 offset:1024\n\t"
+      "ds_read_b64 %3, %8 offset:1536\n\t"
+      "ds_read_b64 %4, %8 offset:2048\n\t"
+      "ds_read_b64 %5, %8 offset:2560\n\t"
+      "ds_read_b64 %6, %8 offset:3072\n\t"
+      "ds_read_b64 %7, %8 offset:3584\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+      : "v"(a)
+      : "memory");
+}
+
+// 4 plain 8-B LDS reads at a + {0, 512, 1024, 1536} (fp8 W fragments of the wide W8A16 kernel:
+// 2 column fragments x 2 MFMA k-steps)
+__device__ __forceinline__ void ds_read_b64_x4_512(uint32_t a, rt_u32x2 (&r)[4]) {
+  asm volatile(
+      "ds_read_b64 %0, %4\n\t"
+      "ds_read_b64 %1, %4 offset:512\n\t"
+      "ds_read_b64 %2, %4 offset:1024\n\t"
+      "ds_read_b64 %3, %4 offset:1536\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+      : "v"(a)
+      : "memory");
+}
+
 // 2 x (2 reads at a_i + {0, O1})
 template <int O1>
 __device__ __forceinline__ void ds_tr16_2x2(uint32_t a0, uint32_t a1, rt_s16x4& r0, rt_s16x4& r1, rt_s16x4& r2,

@@ -26,6 +26,8 @@
 // LDS (once) for dQ = dS·K, which is accumulated with fp32 atomics.
 #include "rt_common.h"
 
+#include <algorithm>
+
 namespace rt {
 
 typedef __attribute__((address_space(3))) void lds_void;  // global_load_lds destination
@@ -787,6 +789,10 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
 // with the prologue's), and the W partial (m, l, O) states merge through LDS in the same launch —
 // no cross-workgroup partition combine, so a layer's attention is one memory round trip plus a
 // workgroup barrier instead of the split kernel's publish / ticket / merge chain.
+// Long caches (a.NP > 1, a.PS keys per partition): B * Hkv * NP workgroups, partition `part`
+// covering keys [part * PS, (part + 1) * PS) of the row; each publishes its merged (m, l, O) with
+// write-through stores and takes a ticket, and the last of the row's NP partitions merges them —
+// at 4k keys one workgroup per (batch, kv head) would stream 2 MB from one CU.
 template <int G, int W>
 __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArgs a) {
   constexpr int D = 128, DS = D / 32, DT = D / 16;
@@ -804,12 +810,17 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
     }
   };
   stamp(0);
-  const int b = blockIdx.x / a.Hkv, hk = blockIdx.x % a.Hkv;
-  const int len = a.attn_len[b];
+  const int NP = W > 1 ? max(a.NP, 1) : 1;
+  const int part = blockIdx.x % NP, bh = blockIdx.x / NP;
+  const int b = bh / a.Hkv, hk = bh % a.Hkv;
+  const int len_row = a.attn_len[b];
   const int s_new = a.slot[b];
-  RT_ASSERT(len <= a.Smax && s_new >= 0 && s_new < a.Smax);
+  RT_ASSERT(len_row <= a.Smax && s_new >= 0 && s_new < a.Smax);
   int kbeg = a.kv_start ? a.kv_start[b] : 0;
-  if (a.window > 0) kbeg = max(kbeg, len - a.window);
+  if (a.window > 0) kbeg = max(kbeg, len_row - a.window);
+  // this workgroup's keys [kbeg, len): the whole row, or partition `part` of it
+  const int len = NP > 1 ? min(len_row, (part + 1) * a.PS) : len_row;
+  if (NP > 1) kbeg = max(kbeg, part * a.PS);
   const int p = a.pos ? a.pos[b] : 0;
   const bf16_t* row = a.qkv + (long)b * a.ldq;
   const bf16_t* kbase = a.kc + ((long)b * a.Hkv + hk) * a.Smax * D;
@@ -1045,6 +1056,7 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
       }
     }
     __syncthreads();
+    float* pp = NP > 1 ? a.part + (long)bh * NP * G * (D + 2) : nullptr;
     for (int e = threadIdx.x; e < G * D; e += 64 * W) {
       const int h = e / D, d = e % D;
       float M = -INFINITY;
@@ -1061,7 +1073,47 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
           O += ost[q][h][d] * f;
         }
       }
-      a.o[(long)b * a.ldo + (long)(hk * G + h) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+      if (NP > 1) {  // publish the unnormalised partial (write-through stores)
+        float* r = pp + ((long)part * G + h) * (D + 2);
+        __hip_atomic_store(r + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == 0) {
+          __hip_atomic_store(r + D, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(r + D + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        a.o[(long)b * a.ldo + (long)(hk * G + h) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+      }
+    }
+    if (NP > 1) {
+      // drained payload -> ticket (handoff-flag); the row's last partition merges all NP records
+      __shared__ int last_flag;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(a.tickets + bh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_flag = old == (unsigned)(NP - 1);
+      }
+      __syncthreads();
+      if (!last_flag) return;
+      for (int e = threadIdx.x; e < G * D; e += 64 * W) {
+        const int h = e / D, d = e % D;
+        float M = -INFINITY, L = 0.f, O = 0.f;
+#pragma unroll 4
+        for (int q = 0; q < NP; ++q) {
+          const float* r = pp + ((long)q * G + h) * (D + 2);
+          const float mq = __hip_atomic_load(r + D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (mq == -INFINITY) continue;  // empty partition: o[] never written
+          const float lq = __hip_atomic_load(r + D + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float oq = __hip_atomic_load(r + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float Mn = fmaxf(M, mq);
+          const float r0 = exp2f(M - Mn), r1 = exp2f(mq - Mn);
+          L = L * r0 + lq * r1;
+          O = O * r0 + oq * r1;
+          M = Mn;
+        }
+        a.o[(long)b * a.ldo + (long)(hk * G + h) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+      }
+      if (threadIdx.x == 0) __hip_atomic_store(a.tickets + bh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     stamp(3);
   }
@@ -1796,13 +1848,20 @@ static int g_dec_qkv_nsplit = 0;
 extern "C" void rt_attn_decode_set_qkv_slabs(const float* p, int nsplit) { g_dec_qkv_slabs = p; g_dec_qkv_nsplit = nsplit; }
 static long long* g_ao_stamps = nullptr;  // debug hook: per-block phase stamps (attn_o and 8-wave kernels)
 extern "C" void rt_attn_o_set_stamps(long long* p) { g_ao_stamps = p; }
-// waves per (batch, kv head) of the small-batch MFMA decode attention; caches up to 1024 slots
-// (<= 8 tiles per wave: the 2-tile register prefetch still covers the memory round trip)
+// waves per (batch, kv head) of the small-batch MFMA decode attention. Caches up to 1024 slots run
+// one workgroup per (batch, kv head) (<= 8 tiles per wave: the 3-tile register prefetch covers the
+// memory round trip); longer caches split the row into partitions of about RT_DECODE_MW_KPP (512)
+// keys, at most the workspace's NP, merged by the last arriving partition.
 constexpr int DEC_MW = 8;
 static bool rt_attn_decode_mw_ok(int B, int Hq, int Hkv, int D, int Smax) {
   static const int use_mw = getenv("RT_DECODE_MW") ? atoi(getenv("RT_DECODE_MW")) : 1;
   const int G = Hkv ? Hq / Hkv : 0;
-  return use_mw && D == 128 && (long)B * Hkv < 256 && Smax <= 1024 && (G == 1 || G == 2 || G == 4 || G == 8);
+  return use_mw && D == 128 && (long)B * Hkv < 256 && (G == 1 || G == 2 || G == 4 || G == 8);
+}
+static int rt_attn_decode_mw_np(int Smax, int np_ws) {
+  static const int kpp = getenv("RT_DECODE_MW_KPP") ? atoi(getenv("RT_DECODE_MW_KPP")) : 512;
+  if (Smax <= 1024 || np_ws <= 1) return 1;
+  return std::max(1, std::min(np_ws, (Smax + kpp - 1) / kpp));
 }
 extern "C" int rt_attn_decode_mfma_ok(int B, int Hq, int Hkv, int D, int NP) {
   static const int use_mfma = getenv("RT_DECODE_MFMA") ? atoi(getenv("RT_DECODE_MFMA")) : 1;
@@ -1844,8 +1903,11 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     return 0;
   }
   // small batch, short caches: 8 waves per (batch, kv head), merged in LDS (RT_DECODE_MW=0 disables)
-  if (rt_attn_decode_mw_ok(B, Hq, Hkv, D, Smax) && !a.qkv_slabs) {
-    dim3 mgrid((unsigned)(B * Hkv)), mblock(64 * DEC_MW);
+  if (rt_attn_decode_mw_ok(B, Hq, Hkv, D, Smax) && !a.qkv_slabs && (NP <= 1 || (part && tickets))) {
+    const int npm = rt_attn_decode_mw_np(Smax, NP);
+    a.NP = npm;
+    a.PS = npm > 1 ? ((Smax + npm - 1) / npm + 15) / 16 * 16 : Smax;
+    dim3 mgrid((unsigned)(B * Hkv * npm)), mblock(64 * DEC_MW);
     switch (G) {
       case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, DEC_MW>), mgrid, mblock, 0, stream, a); break;
       case 2: hipLaunchKernelGGL((attn_decode_mfma_kernel<2, DEC_MW>), mgrid, mblock, 0, stream, a); break;

@@ -1141,18 +1141,24 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
     const char* slot = smem + (i % R64_SLOTS) * R64_SLOT;
     bf16x8 a[2], b[4][2];
     const int ar = wid * 16 + frow;
+    if constexpr (W8) {
+      // fp8 bytes of row frow, k [8c, 8c + 8) = [32 kk + 8 fq, +8) (c = 4 kk + fq): unit 2 kk +
+      // (fq >> 1), half fq & 1 of fragment j's 1-KiB piece -> offsets j * 1024 + kk * 512
+      rt_u32x2 w8[8];
+      ds_read_b64_x8_512(lds_addr(slot + 8192 + ((fq >> 1) * 16 + frow) * 16 + (fq & 1) * 8), w8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) b[j][kk] = fp8x8_to_bf16(w8[2 * j + kk][0], w8[2 * j + kk][1]);
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int c = kk * 4 + fq;
       a[kk] = *(const bf16x8*)(slot + ar * 128 + ((c ^ lds_swz(ar)) << 4));
+      if constexpr (!W8) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int br = j * 16 + frow;
-        if constexpr (W8) {
-          // fp8 bytes of row frow, k [8c, 8c + 8) = [32 kk + 8 fq, +8): unit 2 kk + (fq >> 1), half fq & 1
-          const uint2 w8 = *(const uint2*)(slot + 8192 + j * 1024 + ((2 * kk + (fq >> 1)) * 16 + frow) * 16 + (fq & 1) * 8);
-          b[j][kk] = fp8x8_to_bf16(w8.x, w8.y);
-        } else {
+        for (int j = 0; j < 4; ++j) {
+          const int br = j * 16 + frow;
           b[j][kk] = *(const bf16x8*)(slot + 8192 + br * 128 + ((c ^ lds_swz(br)) << 4));
         }
       }
@@ -1177,6 +1183,235 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
     sq += __shfl_xor(sq, 32, 64);
   }
   m64_finish<OUT_F32, W8>(p, acc, sq, slabs, tickets, split, cg, sp, smem);
+}
+
+// ---------------------------------------------------------------------------------------------
+// W8A16 decode GEMM for 16 < M <= 64 (config-5 rollouts at batch 64): 64 rows x 256 columns
+// ---------------------------------------------------------------------------------------------
+// The 64-column ring above re-reads all of X for every 64 weight columns: at M = 64 that is
+// 2 x the fp8 weight bytes again from L2 (and each of its 4 waves widens the whole fp8 tile).
+// Here a workgroup of 8 waves owns 256 weight rows (16 groups of the tile-ordered fp8 image) x a
+// K range (split-K over workgroups): per 64-deep K-step one 3-slot LDS ring receives X (64 rows x
+// 128 B, one 16-B LDS-DMA per lane) and 16 KiB of fp8 weights (two contiguous 1-KiB image runs
+// per wave). Wave w owns 32 columns (image groups 2w, 2w+1; SwiGLU: the gate group and the
+// matching up group, so silu(g) * u pairs in registers) x all 64 rows: it widens only its own
+// weight bytes (4 ds_read_b64 + 16 cvt per step) and runs 16 MFMAs per step on 4 X fragments.
+// X is read from L2 N / 256 times instead of N / 64. Split-K partials: the write-through slab /
+// ticket hand-off of the kernels above; epilogue = in-GEMM RMS norm (rstd from the X fragments),
+// per-column fp8 scale, bias, activation / SwiGLU, residual.
+constexpr int WD_SLOTS = 3;
+constexpr int WD_SLOT = 8192 + 16384;  // X (64 x 128 B) + 16 fp8 image groups (1 KiB each)
+
+template <bool OUT_F32>
+__global__ __launch_bounds__(512, 2) void gemm_w8_wide_kernel(GemmArgs p, float* __restrict__ slabs,
+                                                              unsigned* __restrict__ tickets, int split) {
+  __shared__ __attribute__((aligned(16))) char smem[WD_SLOTS * WD_SLOT];  // the only __shared__ object
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const int cg = blockIdx.x / split, sp = blockIdx.x % split;
+  const int nk = p.K / 64;
+  const int t0 = (int)((long)sp * nk / split), t1 = (int)((long)(sp + 1) * nk / split);
+  const int nt = t1 - t0;
+  const bool pair = p.act == ACT_SWIGLU;
+  const int F = p.N / 2;
+  const int ngroups = p.N / 16;
+  // image group of this wave's fragment j (0, 1)
+  auto group_of = [&](int j) -> int {
+    if (pair) return j == 0 ? 8 * cg + wid : F / 16 + 8 * cg + wid;
+    return min(16 * cg + 2 * wid + j, ngroups - 1);
+  };
+  const long gstride = (long)(p.K / 128) * 2048;  // bytes per image group
+  const char* wsrc0 = (const char*)p.B + (long)group_of(0) * gstride + lane * 16;
+  const char* wsrc1 = (const char*)p.B + (long)group_of(1) * gstride + lane * 16;
+  const int xr = wid * 8 + (lane >> 3);  // X row this lane stages
+  const int xck = (lane & 7) ^ lds_swz(xr);
+  const bf16_t* xsrc = p.A + (long)min(xr, p.M - 1) * p.lda + xck * 8;
+
+  auto stage = [&](int t) {
+    char* slot = smem + ((t - t0) % WD_SLOTS) * WD_SLOT;
+    __builtin_amdgcn_global_load_lds((const void*)(xsrc + (long)t * 64), (lds_void*)(slot + wid * 1024), 16, 0, 0);
+    const long woff = (long)(t >> 1) * 2048 + (t & 1) * 1024;
+    __builtin_amdgcn_global_load_lds((const void*)(wsrc0 + woff), (lds_void*)(slot + 8192 + (2 * wid) * 1024), 16, 0, 2);
+    __builtin_amdgcn_global_load_lds((const void*)(wsrc1 + woff), (lds_void*)(slot + 8192 + (2 * wid + 1) * 1024), 16, 0, 2);
+  };
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool normed = p.norm_eps > 0.f;
+  float sq[4] = {0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int i = 0; i < WD_SLOTS - 1; ++i)
+    if (i < nt) stage(t0 + i);
+  for (int i = 0; i < nt; ++i) {
+    if (i + 1 < nt) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // step i landed, i + 1 in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (i + WD_SLOTS - 1 < nt) stage(t0 + i + WD_SLOTS - 1);  // the slot every wave finished reading
+    const char* slot = smem + (i % WD_SLOTS) * WD_SLOT;
+    rt_u32x2 w8[4];  // [j * 2 + kk]: row frow, k [32 kk + 8 fq, +8) of group 2 wid + j
+    ds_read_b64_x4_512(lds_addr(slot + 8192 + (2 * wid) * 1024 + ((fq >> 1) * 16 + frow) * 16 + (fq & 1) * 8), w8);
+    bf16x8 b[2][2], a[4][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) b[j][kk] = fp8x8_to_bf16(w8[2 * j + kk][0], w8[2 * j + kk][1]);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = rr * 16 + frow;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + fq;
+        a[rr][kk] = *(const bf16x8*)(slot + row * 128 + ((c ^ lds_swz(row)) << 4));
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[rr][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rr][kk], b[j][kk], acc[rr][j], 0, 0, 0);
+    if (normed) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float f = (float)a[rr][kk][e];
+            sq[rr] += f * f;
+          }
+    }
+  }
+  // row sums of squares: lanes of row 16 rr + frow differ in fq
+  if (normed) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      sq[rr] += __shfl_xor(sq[rr], 16, 64);
+      sq[rr] += __shfl_xor(sq[rr], 32, 64);
+    }
+  }
+  // acc[rr][j][r] = C[row 16 rr + 4 fq + r][column of lane frow in image group group_of(j)]
+  if (split > 1) {
+    constexpr int SLAB = 64 * 256 + 64;
+    float* slab = slabs + ((long)cg * split + sp) * SLAB;
+    const int lc = 32 * wid + frow;  // local column of fragment j: lc + 16 j
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rr * 16 + fq * 4 + r;
+        if (row < p.M) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            __hip_atomic_store(slab + row * 256 + lc + 16 * j, acc[rr][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    if (normed && wid == 0 && fq == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        if (rr * 16 + frow < p.M)
+          __hip_atomic_store(slab + 64 * 256 + rr * 16 + frow, sq[rr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)smem;
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(tickets + cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (old == (unsigned)(split - 1));
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const float* base = slabs + (long)cg * split * SLAB;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rr * 16 + fq * 4 + r;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float t = 0.f;
+          if (row < p.M) {
+#pragma unroll 8
+            for (int s2 = 0; s2 < split; ++s2)
+              t += __hip_atomic_load(base + (long)s2 * SLAB + row * 256 + lc + 16 * j, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+          }
+          acc[rr][j][r] = t;
+        }
+      }
+    if (normed) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        float t = 0.f;
+        if (rr * 16 + frow < p.M) {
+#pragma unroll 8
+          for (int s2 = 0; s2 < split; ++s2)
+            t += __hip_atomic_load(base + (long)s2 * SLAB + 64 * 256 + rr * 16 + frow, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sq[rr] = t;
+      }
+    }
+    if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // ---- epilogue from registers ----
+  float rs[4][4];  // rstd of row 16 rr + 4 fq + r (held by lane frow = 4 fq + r of this wave)
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const float mine = normed ? rsqrtf(sq[rr] / (float)p.K + p.norm_eps) : 1.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rs[rr][r] = normed ? __shfl(mine, fq * 4 + r, 64) : 1.f;
+  }
+  if (pair) {
+    const int col = 16 * (8 * cg + wid) + frow;  // F-column
+    const float sg = p.sb[col], su = p.sb[F + col];
+    const float bg = p.bias ? bf2f(p.bias[col]) : 0.f, bu = p.bias ? bf2f(p.bias[F + col]) : 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rr * 16 + fq * 4 + r;
+        if (row >= p.M) continue;
+        const float gt = acc[rr][0][r] * rs[rr][r] * sg + bg, up = acc[rr][1][r] * rs[rr][r] * su + bu;
+        const float y = gt / (1.f + __expf(-gt)) * up;
+        if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
+        else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
+      }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = 16 * (16 * cg + 2 * wid + j) + frow;
+    if (col >= p.N) continue;
+    const float sc = p.sb[col];
+    const float bv = p.bias ? bf2f(p.bias[col]) : 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rr * 16 + fq * 4 + r;
+        if (row >= p.M) continue;
+        float y = apply_act(acc[rr][j][r] * rs[rr][r] * sc + bv, p.act);
+        if (p.R) y += bf2f(p.R[(long)row * p.ldr + col]);
+        if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
+        else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
+      }
+  }
+}
+
+// split-K of the wide W8A16 kernel: about two workgroups per CU with >= 6 K-steps each
+static int g_wide_split = 0;  // tuning override (rt_gemm_set_wide_split)
+extern "C" void rt_gemm_set_wide_split(int s) { g_wide_split = s; }
+static int wide_split(int N, int K) {
+  if (g_wide_split > 0) return g_wide_split;
+  const int groups = N / 256, nk = K / 64;
+  int split = 1;
+  while (groups * split * 2 <= 512 && nk / (split * 2) >= 6 && split < 16) split *= 2;
+  return split;
 }
 
 // split-K for the ring kernel, from a cold-weight sweep on MI355X (profiles/kernels_m64_split.log,
@@ -1379,6 +1614,11 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
         dim3 grid(pair ? N / 32 : N / 16), block(256);
         if (pair) hipLaunchKernelGGL((gemv16_kernel<false, 4, true, true>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((gemv16_kernel<false, 4, false, true>), grid, block, 0, stream, p);
+      } else if (N % 256 == 0 && g_gemm_variant != 5) {
+        // 256 weight rows per workgroup (X read N / 256 times); RT variant 5 = the 64-column ring
+        const int split = (slabs && tickets) ? fit_split(wide_split(N, K), N / 256, 64 * 256 + 64) : 1;
+        dim3 grid((N / 256) * split), block(512);
+        hipLaunchKernelGGL((gemm_w8_wide_kernel<false>), grid, block, 0, stream, p, slabs, tickets, split);
       } else {
         const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64 + 64) : 1;
         dim3 grid(((N + 63) / 64) * split), block(256);

@@ -217,10 +217,11 @@ def cmd_ppo(cfg, args, policy=None, stack=None):
         avg = sum(rewards) / max(len(rewards), 1)
         if di.is_main:
             print(f"Epoch {ep + 1}/{cfg.data.epochs}: Average Reward = {avg:.4f}")
+        full = cfg.ppo.save_full_policy
         if avg > best:  # rl.py:358-360
             best = avg
-            tr.save_checkpoint(os.path.join(run_dir, "best_model"), ep + 1, best)
-        tr.save_checkpoint(os.path.join(run_dir, f"epoch_{ep + 1}"), ep + 1, best)
+            tr.save_checkpoint(os.path.join(run_dir, "best_model"), ep + 1, best, full_policy=full)
+        tr.save_checkpoint(os.path.join(run_dir, f"epoch_{ep + 1}"), ep + 1, best, full_policy=full)
     return tr
 
 

@@ -151,9 +151,21 @@ class Generator:
 
     @torch.no_grad()
     def generate_async(self, prompts: List[List[int]], params: SamplingParams, pad_id: int = 0,
-                       eos_ids: Sequence[int] = (), early_stop: bool = False) -> "_Pending":
-        """Enqueue prefill + all decode steps on the current stream and return without waiting
-        (unless ``early_stop``, which polls completion every ``sync_every`` steps)."""
+                       eos_ids: Sequence[int] = (), early_stop=False) -> "_Pending":
+        """Enqueue prefill + the decode steps on the current stream and return.
+
+        ``early_stop``:
+          * False   — every decode step is enqueued now (the host never waits);
+          * True    — stop once every row has finished, polling with a blocking read every
+            ``sync_every`` steps (batch-1 answers: the host is idle anyway);
+          * "async" — the same early exit without stalling the GPU: steps are enqueued in chunks
+            of ``sync_every``; after each chunk the "any row active" flag is copied to pinned host
+            memory behind an event, and the host, keeping two chunks queued ahead of the GPU,
+            reads a chunk's flag only when the GPU has already started the next one. The first
+            two chunks are enqueued here, the rest by ``result()`` (so work the caller does
+            between the two calls, e.g. reward scoring, overlaps the decode). Rows are masked
+            after EOS, and the sampler's RNG counter is advanced by the skipped steps, so outputs
+            and later draws are identical to a run without the exit."""
         import time
 
         cfg = self.cfg
@@ -227,28 +239,22 @@ class Generator:
             ev[1].record()
         key = (T, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed, tuple(eos_list), pad_id)
         steps = T - 1
-        if steps > 0:
-            if self.use_graph:
-                if self.runner.needs(key):
-                    # the EOS tensor is created per call: the runner keeps the captured one alive
-                    self.runner.capture(lambda: self._step(params, eos, pad_id), key, keep=(eos,),
-                                        restore=self._state())
-                done = 0
-                while done < steps:
-                    n = min(self.sync_every, steps - done) if early_stop else steps - done
-                    for _ in range(n):
-                        self.runner.replay()
-                    done += n
-                    if early_stop and done < steps and int(self.active.sum().item()) == 0:
-                        break
-            else:
-                for i in range(steps):
-                    self._step(params, eos, pad_id)
-                    if early_stop and (i + 1) % self.sync_every == 0 and int(self.active.sum().item()) == 0:
-                        break
-        if ev:
+        if steps > 0 and self.use_graph and self.runner.needs(key):
+            # the EOS tensor is created per call: the runner keeps the captured one alive
+            self.runner.capture(lambda: self._step(params, eos, pad_id), key, keep=(eos,), restore=self._state())
+        loop = _DecodeLoop(self, steps, params, eos, pad_id, early_stop)
+        loop.run()
+        pend = _Pending(self, B, ids, start, t0, ev, loop)
+        if loop.finished and ev:
             ev[2].record()
-        return _Pending(self, B, ids, start, t0, ev)
+            pend._recorded = True
+        return pend
+
+    def _replay(self, params, eos, pad_id):
+        if self.use_graph:
+            self.runner.replay()
+        else:
+            self._step(params, eos, pad_id)
 
     def _state(self):
         return [self.tok_in, self.kv_len, self.pos, self.attn_len, self.active, self.gen_len, self.step,
@@ -256,16 +262,96 @@ class Generator:
                 self.out_values]
 
 
-class _Pending:
-    """Handle of an enqueued generation; ``result()`` waits and copies the outputs out."""
+class _DecodeLoop:
+    """Enqueues the decode steps of one generation (see ``Generator.generate_async``)."""
 
-    def __init__(self, gen: "Generator", B, ids, start, t0, ev):
+    AHEAD = 2  # chunks kept queued ahead of the GPU in the "async" early-exit mode
+
+    def __init__(self, gen: "Generator", steps: int, params, eos, pad_id, early_stop):
+        self.gen, self.steps, self.params, self.eos, self.pad_id = gen, steps, params, eos, pad_id
+        self.mode = early_stop
+        self.done = 0
+        self.pending = []  # (chunk index, event) of flags not read yet
+        self.stopped = False
+        if early_stop == "async" and steps > 0:
+            dev = gen.device
+            n = (steps + gen.sync_every - 1) // gen.sync_every
+            self.flags_dev = torch.zeros(n, dtype=torch.int32, device=dev)
+            self.flags = torch.zeros(n, dtype=torch.int32, pin_memory=dev.type == "cuda")
+
+    @property
+    def finished(self) -> bool:
+        return self.stopped or self.done >= self.steps
+
+    def _chunk(self, n):
+        g = self.gen
+        for _ in range(n):
+            g._replay(self.params, self.eos, self.pad_id)
+        self.done += n
+
+    def run(self, to_end: bool = False):
+        g = self.gen
+        if self.mode is False:
+            self._chunk(self.steps - self.done)
+            return
+        if self.mode is True:
+            while not self.finished:
+                self._chunk(min(g.sync_every, self.steps - self.done))
+                if self.done < self.steps and int(g.active.sum().item()) == 0:
+                    self._stop()
+            return
+        # "async": keep AHEAD chunks queued; read a chunk's flag once the GPU is past it
+        while not self.finished:
+            if len(self.pending) >= self.AHEAD:
+                c, ev = self.pending.pop(0)
+                if not to_end and not ev.query():
+                    return  # result() continues from here
+                ev.synchronize()
+                if int(self.flags[c]) == 0:
+                    self._stop()
+                    break
+            c = self.done // g.sync_every
+            self._chunk(min(g.sync_every, self.steps - self.done))
+            if self.done < self.steps:
+                self.flags_dev[c:c + 1].copy_(g.active.amax().reshape(1))
+                self.flags[c:c + 1].copy_(self.flags_dev[c:c + 1], non_blocking=True)
+                ev = torch.cuda.Event() if g.device.type == "cuda" else None
+                if ev is not None:
+                    ev.record()
+                    self.pending.append((c, ev))
+                elif int(self.flags[c]) == 0:
+                    self._stop()
+            if not to_end and len(self.pending) >= self.AHEAD:
+                return
+
+    def _stop(self):
+        """Every row has finished: skip the remaining steps, but advance the sampler's RNG counter
+        as if they had run (later generations draw the same numbers either way)."""
+        skipped = self.steps - self.done
+        if skipped > 0:
+            self.gen.rng_offset.add_(skipped)
+        self.stopped = True
+        self.skipped = skipped
+
+
+class _Pending:
+    """Handle of an enqueued generation; ``result()`` finishes enqueuing (async early exit), waits
+    and copies the outputs out."""
+
+    def __init__(self, gen: "Generator", B, ids, start, t0, ev, loop: Optional[_DecodeLoop] = None):
         self.gen, self.B, self.ids, self.start, self.t0, self.ev = gen, B, ids, start, t0, ev
+        self.loop = loop
+        self._recorded = False
 
     def result(self) -> GenerationOutput:
         import time
 
         g, B = self.gen, self.B
+        if self.loop is not None and not self.loop.finished:
+            self.loop.run(to_end=True)
+        if self.ev and not self._recorded:
+            self.ev[2].record()
+            self._recorded = True
         if self.ev:
             self.ev[2].synchronize()
         t_total = time.perf_counter() - self.t0
@@ -273,6 +359,8 @@ class _Pending:
         if self.ev:
             tim["prefill_s"] = self.ev[0].elapsed_time(self.ev[1]) / 1e3
             tim["decode_s"] = self.ev[1].elapsed_time(self.ev[2]) / 1e3
+        if self.loop is not None:
+            tim["decode_steps"] = self.loop.done
         return GenerationOutput(g.out_tokens[:B].clone(), g.gen_len[:B].clone().long(), g.out_logp[:B].clone(),
                                 g.out_values[:B].clone() if g.value_head is not None else None, self.ids,
                                 self.start.to(g.device).long(), tim)

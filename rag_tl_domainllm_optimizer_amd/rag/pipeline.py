@@ -79,7 +79,7 @@ class RagPipeline:
                                      {"retrieve_s": t1 - t0, "prompt_s": t2 - t1, "generate_s": t3 - t2,
                                       "prefill_s": g.timings.get("prefill_s", 0.0),
                                       "decode_s": g.timings.get("decode_s", 0.0),
-                                      "new_tokens": n, "total_s": t4 - t0}))
+                                      "new_tokens": n, "prompt_tokens": len(prompts[b]), "total_s": t4 - t0}))
         return out
 
     def latency_stats(self, queries: Sequence[str], warmup: int = 2) -> dict:
@@ -88,14 +88,16 @@ class RagPipeline:
         for q in queries[:warmup]:
             self.answer([q])
         measured = queries[warmup:] if len(queries) > warmup else queries
-        lat, toks, stages = [], [], {}
+        lat, toks, ptoks, stages = [], [], [], {}
         for q in measured:
             a = self.answer([q])[0]
             lat.append(a.timings["total_s"])
             toks.append(a.timings["new_tokens"])
+            ptoks.append(a.timings["prompt_tokens"])
             for k in ("retrieve_s", "prompt_s", "prefill_s", "decode_s"):
                 stages.setdefault(k, []).append(a.timings[k])
         lat = np.array(lat)
         return {"p50_s": float(np.percentile(lat, 50)), "p90_s": float(np.percentile(lat, 90)),
                 "mean_s": float(lat.mean()), "n": len(lat), "mean_new_tokens": float(np.mean(toks)),
+                "mean_prompt_tokens": float(np.mean(ptoks)),
                 "stage_mean_s": {k: float(np.mean(v)) for k, v in stages.items()}}

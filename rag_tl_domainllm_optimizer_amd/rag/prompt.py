@@ -36,7 +36,19 @@ def encode_prompt(tokenizer, query: str, docs: Sequence[str], budget: int) -> Li
         docs = [docs]
     docs = list(docs)
     ids = tokenizer.encode(build_prompt(query, docs))
-    while len(ids) > budget and docs:
-        docs.pop()
-        ids = tokenizer.encode(build_prompt(query, docs))
-    return ids[-budget:] if len(ids) > budget else ids
+    if len(ids) <= budget or not docs:
+        return ids[-budget:] if len(ids) > budget else ids
+    # the prompt length grows with the number of kept documents: binary search for the most that
+    # fit (a long-context prompt of dozens of retrieved documents costs log2(n) encodes, not n)
+    lo, hi, best = 0, len(docs) - 1, None
+    while lo <= hi:
+        mid = (lo + hi) // 2
+        cand = tokenizer.encode(build_prompt(query, docs[:mid]))
+        if len(cand) <= budget:
+            best, lo = cand, mid + 1
+        else:
+            hi = mid - 1
+    if best is None:  # even the query alone is too long: cut from the left
+        ids = tokenizer.encode(build_prompt(query, []))
+        return ids[-budget:]
+    return best

@@ -78,6 +78,7 @@ class PPOConfig:
     merged_lora_rollout: bool = True  # decode/prefill rollouts on W + sBA (refreshed per update)
     lr_schedule: str = "constant"
     save_every: int = 0              # CLI: mid-epoch "latest" checkpoint every N steps (0 = epoch ends)
+    save_full_policy: bool = True    # epoch / best checkpoints also write the merged HF policy
     bucket_mb: float = 64.0
     warmup_steps: int = 0
     total_steps: int = 0
@@ -215,8 +216,10 @@ class PPOTrainer:
             with self.timer.phase("rollout"):
                 prev = None
                 for lo, hi in bounds:
+                    # "async": the decode stops once every row has emitted EOS (checked behind
+                    # events, two chunks ahead of the GPU; HF generate's stop rule, rl.py:38-44)
                     handle = self.gen.generate_async(prompts[lo:hi], self.sampling, pad_id=self.tok.pad_token_id,
-                                                     eos_ids=[self.tok.eos_token_id])
+                                                     eos_ids=[self.tok.eos_token_id], early_stop="async")
                     if prev is not None:
                         score_chunk(*prev)
                     out = handle.result()

@@ -589,8 +589,10 @@ def test_gemm_256_identity():
                                                         # B * Hkv < 256, D = 128: the 8-wave MFMA kernel (window; G = 2)
                                                         (3, 32, 8, 128, 300, True, 100), (3, 16, 8, 128, 300, True, 0),
                                                         (1, 40, 40, 128, 456, True, 0),  # G = 1 (Llama-2-13B)
-                                                        # D = 128 past 1024 slots at small batch: the split VALU kernel
-                                                        (2, 32, 8, 128, 1500, True, 0),
+                                                        # D = 128 past 1024 slots at small batch: the 8-wave MFMA
+                                                        # kernel over key partitions merged by the last arriver
+                                                        (2, 32, 8, 128, 1500, True, 0), (1, 32, 8, 128, 4096, True, 0),
+                                                        (1, 32, 8, 128, 8200, True, 4096), (2, 40, 40, 128, 2100, True, 0),
                                                         # B * Hkv >= 256: the MFMA kernel (G = 4, 8, 1)
                                                         (40, 32, 8, 128, 300, True, 64), (32, 64, 8, 128, 200, True, 0),
                                                         (16, 16, 16, 128, 97, False, 0)])

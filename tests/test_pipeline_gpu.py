@@ -192,3 +192,86 @@ def test_reward_stream_overlap_matches_serial(monkeypatch):
     a, b = res
     for k in ("reward_mean", "factual_accuracy", "kl_ref", "total_loss"):
         assert abs(a[k] - b[k]) < 1e-5, (k, a[k], b[k])
+
+
+def test_cli_pipeline_config5_fp8_gpu(tmp_path):
+    """BASELINE config 5 through the CLI preset: Llama-2-13B-shaped RAG -> LoRA SFT -> PPO with the
+    fp8 knob on (``model.fp8``): rollout prefill / decode and reference scoring stream e4m3fn
+    weight images (the W8A16 tile-ordered decode GEMVs / ring, W8A8 above 64 rows)."""
+    from rag_tl_domainllm_optimizer_amd import cli
+
+    tr = cli.main(["pipeline", "--preset", "config5_pipeline_llama13b", "--model.encoder=tiny-bert:random",
+                   "--data.synthetic_docs=64", "--data.doc_words=16", "--retrieval.index=flat",
+                   f"--out_dir={tmp_path}", "--data.n_queries=8", "--data.batch_size=8", "--ppo.max_new_tokens=8",
+                   "--ppo.max_prompt_tokens=96", "--ppo.minibatch_size=8", "--sft.batch_size=8",
+                   "--sft.save_full_policy=False", "--ppo.save_full_policy=False"])
+    pol = tr.policy
+    assert pol.cfg.hidden_size == 5120 and pol.cfg.num_layers == 40
+    assert all(layer.fp8_enabled for layer in pol.layers)
+    # the decode path built the tile-ordered fp8 images of the norm-folded projections
+    f8 = pol.layers[0]._fp8
+    assert "qkv_folded" in f8 and "qs" in f8["qkv_folded"]
+    run = tmp_path / "run"
+    lines = [json.loads(x) for x in open(run / "metrics.jsonl")]
+    assert any("reward_mean" in x and math.isfinite(x["total_loss"]) for x in lines)
+    del tr, pol
+    torch.cuda.empty_cache()
+
+
+def test_async_early_exit_gpu():
+    """Rollouts stop once every row has emitted EOS without a blocking poll: forcing EOS at step k
+    (EOS ids = the tokens each row drew at step k) makes the decode time scale with k, and the
+    outputs (and the sampler's Philox counter) equal those of the run that enqueues every step."""
+    from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
+
+    cfg = PRESETS["tiny-mistral"]
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=11)
+    B, T = 16, 160
+    prompts = [list(range(5 + b, 40 + b)) for b in range(B)]
+    sp = SamplingParams(max_new_tokens=T, temperature=0.7, top_k=40, seed=3)
+    g = Generator(m, B, 256, sync_every=8)
+    full = g.generate_async(prompts, sp, pad_id=0, eos_ids=[-1]).result()
+    times = {}
+    for k in (8, 40, 120):
+        eos = sorted({int(t) for t in full.tokens[:, k].tolist()})
+        g.rng_offset.zero_()
+        ref = g.generate_async(prompts, sp, pad_id=0, eos_ids=eos).result()
+        off = int(g.rng_offset)
+        g.rng_offset.zero_()
+        out = g.generate_async(prompts, sp, pad_id=0, eos_ids=eos, early_stop="async").result()
+        assert torch.equal(out.tokens, ref.tokens) and torch.equal(out.logprobs, ref.logprobs)
+        assert int(g.rng_offset) == off
+        assert out.timings["decode_steps"] <= (k // 8 + 3) * 8
+        best = min(g.generate_async(prompts, sp, pad_id=0, eos_ids=eos, early_stop="async").result()
+                   .timings["decode_s"] for _ in range(3))
+        times[k] = best
+    full_t = min(g.generate_async(prompts, sp, pad_id=0, eos_ids=[-1], early_stop="async").result()
+                 .timings["decode_s"] for _ in range(3))
+    assert times[8] < times[40] < times[120] < full_t * 1.05, (times, full_t)
+    assert times[8] < 0.35 * full_t, (times, full_t)
+
+
+def test_gradient_checkpointing_frees_swiglu_activations():
+    """The SwiGLU pre-activation [M, 2F] kept for backward goes through save_for_backward, so
+    non-reentrant activation checkpointing frees it between forward and backward."""
+    cfg = PRESETS["tiny-mistral"]
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=1)
+    m.add_lora(8, 16.0, "all")
+    m.freeze_base()
+    ids = torch.randint(5, cfg.vocab_size, (16, 256), device=DEV)
+
+    def peak(ckpt):
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        h = m(ids, gradient_checkpointing=ckpt)
+        held = torch.cuda.memory_allocated() - base
+        h.float().square().mean().backward()
+        torch.cuda.synchronize()
+        return held
+
+    full = peak(False)
+    ck = peak(True)
+    M, F = 16 * 256, cfg.intermediate_size
+    # without checkpointing every layer keeps at least its [M, 2F] bf16 pre-activation
+    assert full - ck > 0.8 * cfg.num_layers * M * 2 * F * 2, (full, ck)

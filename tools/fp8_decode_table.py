@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--models", default="mistral-7b,llama2-13b")
     ap.add_argument("--ms", default="1,2,4,8,16,24,32,48,64")
     ap.add_argument("--budget-gb", type=float, default=1.2)
-    ap.add_argument("--splits", default="", help="also sweep the fp8 ring's split-K at M > 16 (e.g. 1,2,4,8)")
+    ap.add_argument("--splits", default="", help="also sweep the wide fp8 kernel's split-K at M > 16 (e.g. 1,2,4,8)")
     args = ap.parse_args()
     C = ops.native()
     dev = "cuda"
@@ -80,10 +80,10 @@ def main():
                 if M > 16 and args.splits:
                     sw = {}
                     for sp in [int(v) for v in args.splits.split(",")]:
-                        C.gemm_set_m64_split(sp)
+                        C.gemm_set_wide_split(sp)
                         with torch.no_grad():
                             sw[sp] = round(timeit(fp8, ncopy * 4), 2)
-                    C.gemm_set_m64_split(0)
+                    C.gemm_set_wide_split(0)
                     r["fp8_split_us"] = sw
                 rows.append(r)
                 print(json.dumps(r), flush=True)

@@ -5,7 +5,9 @@ dispatches of each counter and of the dispatch duration, plus derived rates:
   write_TBps  = WRITE_SIZE (KB) / duration
   mfma_util   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs): the fraction of
                 SIMD-cycles the matrix core was busy (GRBM_GUI_ACTIVE sums the 8 XCDs' cycles;
-                MFMA busy cycles are summed over the SIMDs); clock = GRBM_GUI_ACTIVE / 8 / duration
+                MFMA busy cycles are summed over the SIMDs). No clock column: GRBM_GUI_ACTIVE counts
+                over the counter-collection window, which is not the dispatch's Start/End timestamp
+                span (round-2 summaries derived 2.7-4.2 GHz from the two: impossible on MI355X)
   lds_conflict= SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
     python tools/pmc_summary.py file.csv [...]"""
 import collections
@@ -38,8 +40,6 @@ def main():
             if "SQ_VALU_MFMA_BUSY_CYCLES" in med and med.get("GRBM_GUI_ACTIVE"):
                 cyc = med["GRBM_GUI_ACTIVE"] / 8
                 line += f" mfma_util={med['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * cyc):.3f}"
-                if d:
-                    line += f" clock={cyc / d:.2f}GHz"
             if "SQ_LDS_BANK_CONFLICT" in med and med.get("SQ_LDS_IDX_ACTIVE"):
                 line += f" lds_conflict={med['SQ_LDS_BANK_CONFLICT'] / med['SQ_LDS_IDX_ACTIVE']:.3f}"
             print(line)
