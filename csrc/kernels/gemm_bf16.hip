@@ -1199,12 +1199,12 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
 // X is read from L2 N / 256 times instead of N / 64. Split-K partials: the write-through slab /
 // ticket hand-off of the kernels above; epilogue = in-GEMM RMS norm (rstd from the X fragments),
 // per-column fp8 scale, bias, activation / SwiGLU, residual.
-constexpr int WD_SLOTS = 3;
+constexpr int WD_SLOTS = 5;             // 4 K-steps (96 KiB) in flight per workgroup, one workgroup per CU
 constexpr int WD_SLOT = 8192 + 16384;  // X (64 x 128 B) + 16 fp8 image groups (1 KiB each)
+constexpr int WD_SLAB = 64 * 256 + 64;  // split-K partial tile + row sums of squares
 
 template <bool OUT_F32>
-__global__ __launch_bounds__(512, 2) void gemm_w8_wide_kernel(GemmArgs p, float* __restrict__ slabs,
-                                                              unsigned* __restrict__ tickets, int split) {
+__global__ __launch_bounds__(512, 1) void gemm_w8_wide_kernel(GemmArgs p, float* __restrict__ slabs, int split) {
   __shared__ __attribute__((aligned(16))) char smem[WD_SLOTS * WD_SLOT];  // the only __shared__ object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1236,6 +1236,9 @@ __global__ __launch_bounds__(512, 2) void gemm_w8_wide_kernel(GemmArgs p, float*
     __builtin_amdgcn_global_load_lds((const void*)(wsrc1 + woff), (lds_void*)(slot + 8192 + (2 * wid + 1) * 1024), 16, 0, 2);
   };
 
+  // SWAP: the weight fragment is the MFMA's A operand, so acc[rr][j][r] = C[X row 16 rr + frow]
+  // [column 16 g_j + 4 fq + r]: every lane owns 4 CONSECUTIVE output columns of one row (16-B slab
+  // stores / loads, 8-B bf16 stores), and a row's sum of squares is in the lanes of that row
   f32x4 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1246,7 +1249,11 @@ __global__ __launch_bounds__(512, 2) void gemm_w8_wide_kernel(GemmArgs p, float*
   for (int i = 0; i < WD_SLOTS - 1; ++i)
     if (i < nt) stage(t0 + i);
   for (int i = 0; i < nt; ++i) {
-    if (i + 1 < nt) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // step i landed, i + 1 in flight
+    // retire step i (3 LDS-DMAs per lane per step); the later staged steps stay in flight
+    const int ahead = min(WD_SLOTS - 2, nt - 1 - i);
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
     if (i + WD_SLOTS - 1 < nt) stage(t0 + i + WD_SLOTS - 1);  // the slot every wave finished reading
@@ -1273,7 +1280,7 @@ __global__ __launch_bounds__(512, 2) void gemm_w8_wide_kernel(GemmArgs p, float*
       for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[rr][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rr][kk], b[j][kk], acc[rr][j], 0, 0, 0);
+          acc[rr][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][kk], a[rr][kk], acc[rr][j], 0, 0, 0);
     if (normed) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
@@ -1286,7 +1293,7 @@ __global__ __launch_bounds__(512, 2) void gemm_w8_wide_kernel(GemmArgs p, float*
           }
     }
   }
-  // row sums of squares: lanes of row 16 rr + frow differ in fq
+  // row sums of squares: the 4 fq lanes of row 16 rr + frow each hold a quarter
   if (normed) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
@@ -1294,123 +1301,141 @@ __global__ __launch_bounds__(512, 2) void gemm_w8_wide_kernel(GemmArgs p, float*
       sq[rr] += __shfl_xor(sq[rr], 32, 64);
     }
   }
-  // acc[rr][j][r] = C[row 16 rr + 4 fq + r][column of lane frow in image group group_of(j)]
+  const int lc = 32 * wid + 4 * fq;  // local column of fragment j: lc + 16 j
   if (split > 1) {
-    constexpr int SLAB = 64 * 256 + 64;
-    float* slab = slabs + ((long)cg * split + sp) * SLAB;
-    const int lc = 32 * wid + frow;  // local column of fragment j: lc + 16 j
+    // partial tile -> slab (plain 16-B stores); wide_reduce_kernel (the next launch) sums the
+    // splits and runs the epilogue over every (row, 4 columns) in parallel — a last-arriver
+    // reduction would stream split x 64 KiB through ONE workgroup
+    float* slab = slabs + ((long)cg * split + sp) * WD_SLAB;
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = rr * 16 + frow;
+      if (row < p.M) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rr * 16 + fq * 4 + r;
-        if (row < p.M) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            __hip_atomic_store(slab + row * 256 + lc + 16 * j, acc[rr][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        for (int j = 0; j < 2; ++j) *(f32x4*)(slab + row * 256 + lc + 16 * j) = acc[rr][j];
       }
+    }
     if (normed && wid == 0 && fq == 0) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
-        if (rr * 16 + frow < p.M)
-          __hip_atomic_store(slab + 64 * 256 + rr * 16 + frow, sq[rr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (rr * 16 + frow < p.M) slab[64 * 256 + rr * 16 + frow] = sq[rr];
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = (int*)smem;
-    if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(tickets + cg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = (old == (unsigned)(split - 1));
-    }
-    __syncthreads();
-    if (!*flag) return;
-    const float* base = slabs + (long)cg * split * SLAB;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rr * 16 + fq * 4 + r;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          float t = 0.f;
-          if (row < p.M) {
-#pragma unroll 8
-            for (int s2 = 0; s2 < split; ++s2)
-              t += __hip_atomic_load(base + (long)s2 * SLAB + row * 256 + lc + 16 * j, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-          }
-          acc[rr][j][r] = t;
-        }
-      }
-    if (normed) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        float t = 0.f;
-        if (rr * 16 + frow < p.M) {
-#pragma unroll 8
-          for (int s2 = 0; s2 < split; ++s2)
-            t += __hip_atomic_load(base + (long)s2 * SLAB + 64 * 256 + rr * 16 + frow, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        sq[rr] = t;
-      }
-    }
-    if (tid == 0) __hip_atomic_store(tickets + cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
   }
-  // ---- epilogue from registers ----
-  float rs[4][4];  // rstd of row 16 rr + 4 fq + r (held by lane frow = 4 fq + r of this wave)
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const float mine = normed ? rsqrtf(sq[rr] / (float)p.K + p.norm_eps) : 1.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rs[rr][r] = normed ? __shfl(mine, fq * 4 + r, 64) : 1.f;
-  }
+  // ---- epilogue from registers: row 16 rr + frow, 4 consecutive columns per fragment ----
   if (pair) {
-    const int col = 16 * (8 * cg + wid) + frow;  // F-column
-    const float sg = p.sb[col], su = p.sb[F + col];
-    const float bg = p.bias ? bf2f(p.bias[col]) : 0.f, bu = p.bias ? bf2f(p.bias[F + col]) : 0.f;
+    const int col = 16 * (8 * cg + wid) + 4 * fq;  // first of 4 F-columns
+    const float4 sg = *(const float4*)(p.sb + col), su = *(const float4*)(p.sb + F + col);
+    const float sgv[4] = {sg.x, sg.y, sg.z, sg.w}, suv[4] = {su.x, su.y, su.z, su.w};
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = rr * 16 + frow;
+      if (row >= p.M) continue;
+      const float rs = normed ? rsqrtf(sq[rr] / (float)p.K + p.norm_eps) : 1.f;
+      float y[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rr * 16 + fq * 4 + r;
-        if (row >= p.M) continue;
-        const float gt = acc[rr][0][r] * rs[rr][r] * sg + bg, up = acc[rr][1][r] * rs[rr][r] * su + bu;
-        const float y = gt / (1.f + __expf(-gt)) * up;
-        if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
-        else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
+        float gt = acc[rr][0][r] * rs * sgv[r], up = acc[rr][1][r] * rs * suv[r];
+        if (p.bias) { gt += bf2f(p.bias[col + r]); up += bf2f(p.bias[F + col + r]); }
+        y[r] = gt / (1.f + __expf(-gt)) * up;
       }
+      if constexpr (OUT_F32) *(float4*)((float*)p.C + (long)row * p.ldc + col) = make_float4(y[0], y[1], y[2], y[3]);
+      else *(uint2*)((bf16_t*)p.C + (long)row * p.ldc + col) = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+    }
     return;
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int col = 16 * (16 * cg + 2 * wid + j) + frow;
+    const int col = 16 * (16 * cg + 2 * wid + j) + 4 * fq;
     if (col >= p.N) continue;
-    const float sc = p.sb[col];
-    const float bv = p.bias ? bf2f(p.bias[col]) : 0.f;
+    const float4 sc4 = *(const float4*)(p.sb + col);
+    const float scv[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = rr * 16 + frow;
+      if (row >= p.M) continue;
+      const float rs = normed ? rsqrtf(sq[rr] / (float)p.K + p.norm_eps) : 1.f;
+      float res[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.R) {
+        const uint2 rv = *(const uint2*)(p.R + (long)row * p.ldr + col);
+        res[0] = bf2f((bf16_t)(rv.x & 0xffff)); res[1] = bf2f((bf16_t)(rv.x >> 16));
+        res[2] = bf2f((bf16_t)(rv.y & 0xffff)); res[3] = bf2f((bf16_t)(rv.y >> 16));
+      }
+      float y[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = rr * 16 + fq * 4 + r;
-        if (row >= p.M) continue;
-        float y = apply_act(acc[rr][j][r] * rs[rr][r] * sc + bv, p.act);
-        if (p.R) y += bf2f(p.R[(long)row * p.ldr + col]);
-        if constexpr (OUT_F32) ((float*)p.C)[(long)row * p.ldc + col] = y;
-        else ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(y);
+        float v = acc[rr][j][r] * rs * scv[r];
+        if (p.bias) v += bf2f(p.bias[col + r]);
+        y[r] = apply_act(v, p.act) + res[r];
       }
+      if constexpr (OUT_F32) *(float4*)((float*)p.C + (long)row * p.ldc + col) = make_float4(y[0], y[1], y[2], y[3]);
+      else *(uint2*)((bf16_t*)p.C + (long)row * p.ldc + col) = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+    }
   }
 }
 
-// split-K of the wide W8A16 kernel: about two workgroups per CU with >= 6 K-steps each
+// Split-K epilogue of the wide W8A16 kernel: one thread per (row, 4 output columns) sums the
+// split partials (16-B loads), applies the in-GEMM RMS norm (row sums of squares from the slabs),
+// per-column fp8 scales, bias, activation / SwiGLU pair, residual, and stores. Column c of the
+// output lives in slab group c / 256 (SwiGLU: F-column c in group c / 128, gate at local column
+// 32 w + (c % 16), up 16 further, w = (c % 128) / 16).
+template <bool OUT_F32>
+__global__ __launch_bounds__(256) void wide_reduce_kernel(GemmArgs p, const float* __restrict__ slabs, int split) {
+  const bool pair = p.act == ACT_SWIGLU;
+  const int F = p.N / 2;
+  const int ncol4 = (pair ? F : p.N) / 4;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)p.M * ncol4) return;
+  const int row = (int)(e / ncol4), col = (int)(e % ncol4) * 4;
+  const int cg = pair ? col / 128 : col / 256;
+  const int lcol = pair ? 32 * ((col % 128) / 16) + (col % 16) : col % 256;
+  const float* base = slabs + (long)cg * split * WD_SLAB;
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f), u = g;
+  float sq = 0.f;
+  const bool normed = p.norm_eps > 0.f;
+#pragma unroll 8
+  for (int s2 = 0; s2 < split; ++s2) {
+    const float* sl = base + (long)s2 * WD_SLAB;
+    const float4 a = *(const float4*)(sl + row * 256 + lcol);
+    g.x += a.x; g.y += a.y; g.z += a.z; g.w += a.w;
+    if (pair) {
+      const float4 b = *(const float4*)(sl + row * 256 + lcol + 16);
+      u.x += b.x; u.y += b.y; u.z += b.z; u.w += b.w;
+    }
+    if (normed) sq += sl[64 * 256 + row];
+  }
+  const float rs = normed ? rsqrtf(sq / (float)p.K + p.norm_eps) : 1.f;
+  const float gv[4] = {g.x, g.y, g.z, g.w}, uv[4] = {u.x, u.y, u.z, u.w};
+  float y[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (pair) {
+      float gt = gv[r] * rs * p.sb[col + r], up = uv[r] * rs * p.sb[F + col + r];
+      if (p.bias) { gt += bf2f(p.bias[col + r]); up += bf2f(p.bias[F + col + r]); }
+      y[r] = gt / (1.f + __expf(-gt)) * up;
+    } else {
+      float v = gv[r] * rs * p.sb[col + r];
+      if (p.bias) v += bf2f(p.bias[col + r]);
+      y[r] = apply_act(v, p.act);
+      if (p.R) y[r] += bf2f(p.R[(long)row * p.ldr + col + r]);
+    }
+  }
+  if constexpr (OUT_F32) *(float4*)((float*)p.C + (long)row * p.ldc + col) = make_float4(y[0], y[1], y[2], y[3]);
+  else *(uint2*)((bf16_t*)p.C + (long)row * p.ldc + col) = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+}
+
+// split-K of the wide W8A16 kernel (one workgroup per CU, 4 K-steps in flight each): the largest
+// power of two that keeps the grid <= 256 workgroups with >= 8 K-steps each (the partials go
+// through one parallel reduce launch). From the cold-weight sweep (profiles/r3/fp8_decode_table_*,
+// M = 24 .. 64): gate_up 108-112 groups -> 2, qkv 24 / 60 groups -> 8 / 4, o 16-20 -> 8, down
+// (K 13824 / 14336) 16 / 20 groups -> 16 / 8.
 static int g_wide_split = 0;  // tuning override (rt_gemm_set_wide_split)
 extern "C" void rt_gemm_set_wide_split(int s) { g_wide_split = s; }
 static int wide_split(int N, int K) {
   if (g_wide_split > 0) return g_wide_split;
   const int groups = N / 256, nk = K / 64;
   int split = 1;
-  while (groups * split * 2 <= 512 && nk / (split * 2) >= 6 && split < 16) split *= 2;
+  while (groups * split * 2 <= 256 && nk / (split * 2) >= 8 && split < 16) split *= 2;
   return split;
 }
 
@@ -1616,9 +1641,15 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
         else hipLaunchKernelGGL((gemv16_kernel<false, 4, false, true>), grid, block, 0, stream, p);
       } else if (N % 256 == 0 && g_gemm_variant != 5) {
         // 256 weight rows per workgroup (X read N / 256 times); RT variant 5 = the 64-column ring
-        const int split = (slabs && tickets) ? fit_split(wide_split(N, K), N / 256, 64 * 256 + 64) : 1;
+        int split = slabs ? fit_split(wide_split(N, K), N / 256, WD_SLAB) : 1;
+        split = std::min(split, std::max(1, K / 64));
         dim3 grid((N / 256) * split), block(512);
-        hipLaunchKernelGGL((gemm_w8_wide_kernel<false>), grid, block, 0, stream, p, slabs, tickets, split);
+        hipLaunchKernelGGL((gemm_w8_wide_kernel<false>), grid, block, 0, stream, p, slabs, split);
+        if (split > 1) {
+          const long work = (long)M * (pair ? N / 2 : N) / 4;
+          hipLaunchKernelGGL((wide_reduce_kernel<false>), dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream, p,
+                             slabs, split);
+        }
       } else {
         const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64 + 64) : 1;
         dim3 grid(((N + 63) / 64) * split), block(256);

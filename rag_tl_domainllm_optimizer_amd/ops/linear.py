@@ -377,13 +377,21 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
         if on_gpu(x2) and not grad_needed and bias is None and w.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0 \
                 and (x2.shape[0] <= 64 or w.shape[0] % 256 == 0):
             w_eff = lora.merged_weight(w) if use_lora else w
-            if fp8 is not None and x2.shape[0] <= 64:
-                from .fp8 import fp8_supported
+            if fp8 is not None:
+                from .fp8 import fp8_supported, gemm_fp8
 
                 if fp8_supported(w_eff):
-                    shuf = fp8.shuf_ok(w_eff, x2.shape[0], ACT_SWIGLU)
-                    q, sc = fp8.shuf(w_eff) if shuf else fp8.get(w_eff)
-                    y = native().gemm_fp8(x2, None, q, sc, None, ACT_SWIGLU, None, None, 0.0, shuf)
+                    if x2.shape[0] <= 64:
+                        shuf = fp8.shuf_ok(w_eff, x2.shape[0], ACT_SWIGLU)
+                        q, sc = fp8.shuf(w_eff) if shuf else fp8.get(w_eff)
+                        y = native().gemm_fp8(x2, None, q, sc, None, ACT_SWIGLU, None, None, 0.0, shuf)
+                    else:
+                        # prefill / reference scoring: W8A8 [gate | up] on the fp8 MFMA (2x the bf16
+                        # rate), then one SwiGLU pass over the [M, 2F] pre-activation
+                        from .misc import swiglu
+
+                        q, sc = fp8.get(w_eff)
+                        y = swiglu(gemm_fp8(x2, q, sc))
                     return y.reshape(*shp[:-1], w.shape[0] // 2)
             y = gemm(x2, w_eff, None, None, None, ACT_SWIGLU)
             return y.reshape(*shp[:-1], w.shape[0] // 2)
