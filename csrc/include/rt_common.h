@@ -166,6 +166,32 @@ __device__ __forceinline__ void ds_tr16_2x2(uint32_t a0, uint32_t a1, rt_s16x4& 
       : "memory");
 }
 
+// D = A.B + D on a 16x16x32 bf16 MFMA with D tied to AGPRs ("+a") and a "memory" clobber that pins
+// surrounding loads / LDS-DMA issues to their source position (gemm_big.hip's 4-wave kernels).
+// The x86 host pass parses kernel bodies too and has no AGPR constraint: the asm is device-pass only.
+// PAD: lead with `s_nop 1`, the 2 wait states a VALU write of an A/B operand register needs before
+// the MFMA reads it (cdna_hip_programming.md §5.7 item 2: hipcc pads nothing inside asm) — for
+// call sites where hipcc may place a register copy of a fragment right in front of the MFMA.
+typedef __attribute__((ext_vector_type(4))) int rt_i32x4;
+template <bool PAD>
+__device__ __forceinline__ void mfma_16x16x32_bf16_agpr(f32x4& d, const rt_i32x4& a, const rt_i32x4& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (PAD)
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b) : "memory");
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b) : "memory");
+#endif
+}
+
+// Scheduling fence for an AGPR accumulator: the compiler treats the value as redefined here, so
+// reads of it cannot move above this point (it does not know the latency of an asm MFMA and would
+// otherwise read a result that is still in flight) and its initialisation cannot sink below it.
+__device__ __forceinline__ void agpr_fence(f32x4& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+a"(d));
+#endif
+}
+
 __device__ __forceinline__ float bf2f(bf16_t x) {
   return __uint_as_float(((uint32_t)x) << 16);
 }

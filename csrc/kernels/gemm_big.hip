@@ -733,6 +733,327 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   *(uint4*)(C + (long)m * ldc + c0) = pack8(y);
 }
 
+// ---------------------------------------------------------------------------------------------
+// 4-wave NT tile (ROW / ROW) with a large per-wave block: wave (wr, wc) of a 2 x 2 grid owns a
+// (16 WM) x 128 output block = WM x 8 fragments of mfma_f32_16x16x32_bf16; the workgroup tile is
+// (32 WM) x 256. One wave per SIMD, so a wave owns the SIMD's whole register file: the 4 WM x 8
+// fp32 accumulators per lane live in AGPRs (WM = 8: 128 x 128 per wave, the wave shape of the
+// library's MT256x256 4-wave kernels; WM = 6: 96 x 128). LDS bytes read per MAC: 1/(16 WM) + 1/128
+// per k, vs 1/128 + 1/64 for gemm_big_kernel's 128 x 64 wave block.
+// Stages of 64 k through a 2-slot LDS-DMA ring: [rows][128 B] images filled by whole-line LDS-DMA
+// (8 rows x 128 B per instruction; a 64-B-per-row form measured 3.5e7 TA-stalled-by-TC cycles per
+// qkv GEMM, profiles/r3/gemm_w4_pmc_summary.txt), 16-B slot = k-chunk ^ ((row >> 1) & 7) as in
+// gemm_big_kernel (conflict-free ds_read_b128). A stage is computed in two k-halves of 32 with the
+// fragments register double-buffered: half 0 computes while the reads of half 1 go out (the stage
+// is resident: no barrier); half 1 retires stage s+1 (vmcnt), passes the stage's one raw barrier,
+// then issues the LDS-DMA of stage s+2 into the slot just read and the reads of stage s+1's half 0
+// between its MFMAs. Tile order, SwiGLU row pairing, K-extension and epilogues follow
+// gemm_big_kernel.
+template <int WM>
+struct W4Geom {
+  static constexpr int BM = 32 * WM;                 // tile rows
+  static constexpr int A_BYTES = BM * 128;           // A image of one stage (64 k)
+  static constexpr int SLOT = A_BYTES + 256 * 128;   // + B image
+  static constexpr int DMA_A = BM / 32;              // LDS-DMA instructions per lane per stage: A (8 rows x 128 B each)
+  static constexpr int DMA = DMA_A + 8;              // + B
+};
+
+template <int OUT, int EPI, int WM>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(Args p) {
+  using G = W4Geom<WM>;
+  constexpr int BM = G::BM, WROWS = 16 * WM;
+  static_assert(WM % 2 == 0 && G::DMA_A * 32 == BM && (WM - 1) * 8 >= G::DMA + WM + 8 && WM * 8 >= WM + 8, "WM");
+  __shared__ __attribute__((aligned(16))) char smem[2 * G::SLOT];  // the only __shared__ object
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int frow = lane & 15, fq = lane >> 4;
+
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = EPI == E_SWIGLU ? p.N / 256 : (p.N + 255) / 256;
+  const int nwg = tiles_m * tiles_n;
+  if ((int)blockIdx.x >= nwg) return;  // grid / tile-count mismatch: never index past the tile grid
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % gsz);
+  const int tn = (bid % (GROUP_M * tiles_n)) / gsz;
+  const int m0 = tm * BM, n0 = tn * 256;
+  const int Fh = p.N / 2;
+
+  const int ns1 = (p.K + 63) / 64;             // main-K stages (the last may be ragged: zero page)
+  const int ns1f = p.K / 64;                   // full main-K stages
+  const int ns2 = p.A2 ? (p.K2 + 63) / 64 : 0;  // K-extension stages
+  const int ns = ns1 + ns2;
+  const int s_begin = (int)((long)blockIdx.y * ns / p.nsplit);
+  const int s_end = (int)((long)(blockIdx.y + 1) * ns / p.nsplit);
+
+  // LDS-DMA instruction x (A: x = DMA_A wid + j, B: x = 8 wid + j) covers rows 8 x + lane / 8; the
+  // lane's 16-B LDS slot lane % 8 receives k-chunk (lane % 8) ^ ((row >> 1) & 7) = (lane % 8) ^
+  // ((lane >> 4) + 4 (x & 1)) (source-side swizzle, guide rule 21); DMA_A is even, so x & 1 = j & 1
+  auto kc_of = [&](int j) -> int { return (lane & 7) ^ ((lane >> 4) + 4 * (j & 1)); };
+  auto row_of = [&](int op, int j) -> int { return 8 * ((op ? 8 : G::DMA_A) * wid + j) + (lane >> 3); };
+  auto grow_of = [&](int op, int row) -> int {
+    if (op == 0) return min(m0 + row, p.M - 1);
+    if (EPI == E_SWIGLU) return row < 128 ? tn * 128 + row : Fh + tn * 128 + row - 128;
+    return min(n0 + row, p.N - 1);
+  };
+  auto dst_of = [&](char* img, int op, int j) -> char* {
+    return img + (op ? G::A_BYTES : 0) + ((op ? 8 : G::DMA_A) * wid + j) * 1024;
+  };
+  // main-K sources: uniform operand base + 32-bit per-lane byte offset (one VGPR per instruction)
+  uint32_t offa[G::DMA_A], offb[8];
+#pragma unroll
+  for (int j = 0; j < G::DMA_A; ++j)
+    offa[j] = ((uint32_t)grow_of(0, row_of(0, j)) * (uint32_t)p.lda + (uint32_t)(kc_of(j) * 8)) * 2u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    offb[j] = ((uint32_t)grow_of(1, row_of(1, j)) * (uint32_t)p.ldb + (uint32_t)(kc_of(j) * 8)) * 2u;
+  auto dma_main = [&](int s, int k) {  // instruction k (< DMA) of full main stage s
+    char* img = smem + (s & 1) * G::SLOT;
+    if (k < G::DMA_A)
+      __builtin_amdgcn_global_load_lds((const void*)((const char*)p.A + (size_t)s * 128 + offa[k]),
+                                       (lds_void*)dst_of(img, 0, k), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)((const char*)p.B + (size_t)s * 128 + offb[k - G::DMA_A]),
+                                       (lds_void*)dst_of(img, 1, k - G::DMA_A), 16, 0, 0);
+  };
+  auto stage = [&](int s) {  // any stage: ragged main-K tail and K-extension chunks read the zero page
+    if (s < ns1f) {
+#pragma unroll
+      for (int k = 0; k < G::DMA; ++k) dma_main(s, k);
+      return;
+    }
+    char* img = smem + (s & 1) * G::SLOT;
+    const bool ext = s >= ns1;
+    const int k0 = (ext ? s - ns1 : s) * 64;
+    const int klim = ext ? p.K2 : p.K;
+    const bf16_t* zsrc = p.zpage + (lane & 7) * 8;
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      const long ld = ext ? (op ? p.ldb2 : p.lda2) : (op ? p.ldb : p.lda);
+      const bf16_t* base = ext ? (op ? p.B2 : p.A2) : (op ? p.B : p.A);
+#pragma unroll
+      for (int j = 0; j < (op ? 8 : G::DMA_A); ++j) {
+        const int kk = k0 + kc_of(j) * 8;
+        const bf16_t* src = kk < klim ? base + (long)grow_of(op, row_of(op, j)) * ld + kk : zsrc;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst_of(img, op, j), 16, 0, 0);
+      }
+    }
+  };
+
+  // fragment reads, k-half h of a stage: lane (frow, fq) of fragment f reads row 16 f + frow, k-chunk
+  // 4 h + fq, at slot (4 h + fq) ^ ((row >> 1) & 7) = (4 h + fq) ^ ((frow >> 1) & 7)
+  const int rdo0 = frow * 128 + ((fq ^ ((frow >> 1) & 7)) << 4);
+  const int rdo1 = frow * 128 + (((4 + fq) ^ ((frow >> 1) & 7)) << 4);
+  auto rd_a = [&](int s, int h, int i) -> rt_i32x4 {
+    return *(const rt_i32x4*)(smem + (s & 1) * G::SLOT + (wr * WROWS + i * 16) * 128 + (h ? rdo1 : rdo0));
+  };
+  auto rd_b = [&](int s, int h, int j) -> rt_i32x4 {
+    return *(const rt_i32x4*)(smem + (s & 1) * G::SLOT + G::A_BYTES + (wc * 128 + j * 16) * 128 + (h ? rdo1 : rdo0));
+  };
+
+  // SWAP (B fragment as the MFMA's A operand): acc[i][j][r] = C[WROWS wr + 16 i + frow][128 wc + 16 j + 4 fq + r]
+  f32x4 acc[WM][8];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // The MFMAs are issued from asm with the accumulator tied to an AGPR ("+a"): with the builtin,
+  // hipcc selects the untied form for part of the accumulators and shuttles them through VGPRs
+  // (v_accvgpr_read / write / mov around every MFMA of the loop). Its "memory" clobber pins the
+  // LDS-DMA issues and ds_reads interleaved between the MFMAs (one per MFMA, in the MFMA's shadow).
+  // Hazards hipcc cannot see (tools/check_asm_hazards.py audits the ISA): an accumulator is re-used
+  // 8 WM - 1 MFMAs later; fragment VGPRs are rewritten by ds_reads a half-stage after their last
+  // MFMA; a row's first MFMA carries the VALU -> operand pad (s_nop 1) against a register copy at
+  // the row boundary (every MFMA outside the steady state); zero-init -> first MFMA and last MFMA ->
+  // epilogue reads are separated by explicit padding + agpr_fence.
+  auto mma = [&](int i, int j, const rt_i32x4 (&a)[WM], const rt_i32x4 (&b)[8], bool pad) {
+    if (pad) mfma_16x16x32_bf16_agpr<true>(acc[i][j], b[j], a[i]);
+    else mfma_16x16x32_bf16_agpr<false>(acc[i][j], b[j], a[i]);
+  };
+
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) agpr_fence(acc[i][j]);
+  asm volatile("s_nop 4" ::: "memory");  // zero-init (VALU) -> first MFMA srcC
+  if (s_begin < s_end) {
+    stage(s_begin);
+    if (s_begin + 1 < s_end) {
+      stage(s_begin + 1);
+      if (s_begin < ns1f && s_begin + 1 < ns1f) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(G::DMA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    GB_BARRIER();
+    rt_i32x4 a0[WM], b0[8], a1[WM], b1[8];
+#pragma unroll
+    for (int i = 0; i < WM; ++i) a0[i] = rd_a(s_begin, 0, i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b0[j] = rd_b(s_begin, 0, j);
+
+    // one stage s = two k-halves of WM x 8 MFMAs, one LDS-DMA / ds_read issued after an MFMA:
+    //   half 0 (a0/b0): reads of half 1 (-> a1/b1) after MFMAs 0 .. R0-1; lgkmcnt(0) + barrier B1
+    //           (every wave is done with slot s & 1) after MFMA B1-1; LDS-DMA of stage s+2 into it
+    //           after MFMAs B1 .. B1+DMA-1
+    //   half 1 (a1/b1): vmcnt (stage s+1 landed; s+2 may stay in flight) + barrier B2 after MFMA
+    //           B2-1; reads of stage s+1 half 0 (-> a0/b0) after MFMAs B2 .. B2+R0-1, the last 8
+    //           MFMAs cover their latency
+    // so a stage's DMA has ~3 half-stages (~3k MFMA cycles) to land.
+    constexpr int R0 = WM + 8, B1 = R0 + 4, B2 = WM * 8 - R0 - 8;
+    static_assert(B1 + G::DMA <= WM * 8 && B2 > 0, "w4 schedule");
+    auto stage_body = [&](int s, bool fast) {
+      const bool more = s + 1 < s_end, more2 = s + 2 < s_end;
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = i * 8 + j;
+          mma(i, j, a0, b0, !fast || j == 0);
+          if (k < WM) a1[k] = rd_a(s, 1, k);
+          else if (k < R0) b1[k - WM] = rd_b(s, 1, k - WM);
+          if (k == B1 - 1) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            GB_BARRIER();
+          }
+          if (fast && k >= B1 && k < B1 + G::DMA) dma_main(s + 2, k - B1);
+        }
+      if (!fast && more2) stage(s + 2);
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = i * 8 + j;
+          mma(i, j, a1, b1, !fast || j == 0);
+          if (k == B2 - 1) {
+            if (fast || more2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(G::DMA) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            GB_BARRIER();
+          }
+          if (k >= B2 && k < B2 + R0 && (fast || more)) {
+            if (k - B2 < WM) a0[k - B2] = rd_a(s + 1, 0, k - B2);
+            else b0[k - B2 - WM] = rd_b(s + 1, 0, k - B2 - WM);
+          }
+        }
+    };
+    int s = s_begin;
+    const int s_fast = min(s_end, ns1f) - 2;  // stage s + 2 is a full main-K stage (and s + 1 exists)
+    for (; s < s_fast; ++s) stage_body(s, true);
+    for (; s < s_end; ++s) stage_body(s, false);
+  }
+  // last MFMA (8 passes) -> v_accvgpr_read of its result; the fences keep every accumulator read
+  // below the padding
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) agpr_fence(acc[i][j]);
+  __syncthreads();
+
+  // ---- epilogue ----
+  if constexpr (OUT == O_F32) {
+    float* C = (float*)p.C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = n0 + wc * 128 + j * 16 + fq * 4;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias && col < p.N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[col + r]);
+      }
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        const int row = m0 + wr * WROWS + i * 16 + frow;
+        if (row < p.M && col < p.N) {
+          float4 v;
+          v.x = act_fn(acc[i][j][0] + bv[0], EPI);
+          v.y = act_fn(acc[i][j][1] + bv[1], EPI);
+          v.z = act_fn(acc[i][j][2] + bv[2], EPI);
+          v.w = act_fn(acc[i][j][3] + bv[3], EPI);
+          *(float4*)(C + (long)row * p.ldc + col) = v;
+        }
+      }
+    }
+  } else {
+    // bf16 through LDS, one WROWS-row half at a time (the waves with wr == half write it); row
+    // stride 264 elements = 528 B: the 8-B writes of a 32-lane pass cover all 64 banks once, and
+    // 16-B aligned rows for the ds_read_b128 + 16-B global store pass
+    constexpr int LDT = 264;
+    static_assert(WROWS * LDT * 2 <= 2 * G::SLOT, "epilogue tile");
+    bf16_t* tile = (bf16_t*)smem;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      if (wr == hh) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = wc * 128 + j * 16 + fq * 4;
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (EPI != E_SWIGLU && p.bias && n0 + col < p.N) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[n0 + col + r]);
+          }
+#pragma unroll
+          for (int i = 0; i < WM; ++i) {
+            float y[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = EPI == E_SWIGLU ? acc[i][j][r] : act_fn(acc[i][j][r] + bv[r], EPI);
+            *(uint2*)(tile + (i * 16 + frow) * LDT + col) = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+          }
+        }
+      }
+      __syncthreads();
+      if constexpr (EPI == E_SWIGLU) {
+        bf16_t* Cf = (bf16_t*)p.C;
+        const int cc = tid & 15;  // 16-B chunk of the 128-column gate half
+#pragma unroll
+        for (int pass = 0; pass < WROWS / 16; ++pass) {
+          const int row = pass * 16 + (tid >> 4);
+          const int grow = m0 + hh * WROWS + row;
+          if (grow < p.M) {
+            const uint4 g4 = *(const uint4*)(tile + row * LDT + cc * 8);
+            const uint4 u4 = *(const uint4*)(tile + row * LDT + 128 + cc * 8);
+            float g[8], u[8], f[8];
+            unpack8(g4, g);
+            unpack8(u4, u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = g[e] / (1.f + __expf(-g[e])) * u[e];
+            const int fcol = tn * 128 + cc * 8;
+            *(uint4*)(Cf + (long)grow * p.ldc + fcol) = pack8(f);
+            if (p.C2) {
+              *(uint4*)(p.C2 + (long)grow * p.ldc2 + fcol) = g4;
+              *(uint4*)(p.C2 + (long)grow * p.ldc2 + Fh + fcol) = u4;
+            }
+          }
+        }
+      } else {
+        bf16_t* C = (bf16_t*)p.C;
+        const int cc = tid & 31;  // 16-B chunk of the 256-column row
+#pragma unroll
+        for (int pass = 0; pass < WROWS / 8; ++pass) {
+          const int row = pass * 8 + (tid >> 5);
+          const int grow = m0 + hh * WROWS + row, gcol = n0 + cc * 8;
+          if (grow < p.M && gcol < p.N) {
+            uint4 v = *(const uint4*)(tile + row * LDT + cc * 8);
+            if (p.R) {  // residual in fp32 on the bf16-rounded GEMM result (= a separate add kernel)
+              float y[8], r[8];
+              unpack8(v, y);
+              unpack8(*(const uint4*)(p.R + (long)grow * p.ldr + gcol), r);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) y[e] += r[e];
+              v = pack8(y);
+            }
+            *(uint4*)(C + (long)grow * p.ldc + gcol) = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 }  // namespace gb
 }  // namespace rt
 
@@ -754,6 +1075,34 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
     if (key == 10 && bn == 128) hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 128, true>), grid, block, 0, stream, p);
     else if (key == 10) hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 256, true>), grid, block, 0, stream, p);
     else hipLaunchKernelGGL((gemm_big_kernel<KMAJ, KMAJ, O_F32_ATOMIC, E_NONE, 256, true>), grid, block, 0, stream, p);
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
+  if (bn == 4 || bn == 3) {  // 4-wave tiles: bn 3 = 192 x 256 (WM 6), bn 4 = 256 x 256 (WM 8); NT, bf16 / fp32
+    const int bm = bn == 4 ? 256 : 192;
+    const int tn4 = act == E_SWIGLU ? p.N / 256 : (p.N + 255) / 256;  // 256 output columns per tile
+    dim3 g4(((p.M + bm - 1) / bm) * tn4, p.nsplit), b4(256);
+#define W4_LAUNCH(O, E)                                                                       \
+  do {                                                                                        \
+    if (bn == 4) hipLaunchKernelGGL((gemm_w4_kernel<O, E, 8>), g4, b4, 0, stream, p);         \
+    else hipLaunchKernelGGL((gemm_w4_kernel<O, E, 6>), g4, b4, 0, stream, p);                 \
+  } while (0)
+    if (key == 0) {
+      switch (act) {
+        case E_NONE: W4_LAUNCH(O_BF16, E_NONE); break;
+        case E_RELU: W4_LAUNCH(O_BF16, E_RELU); break;
+        case E_GELU: W4_LAUNCH(O_BF16, E_GELU); break;
+        case E_GELU_TANH: W4_LAUNCH(O_BF16, E_GELU_TANH); break;
+        case E_SILU: W4_LAUNCH(O_BF16, E_SILU); break;
+        case E_SWIGLU: W4_LAUNCH(O_BF16, E_SWIGLU); break;
+        default: return -4;
+      }
+    } else if (key == 1 && act == E_NONE) {
+      W4_LAUNCH(O_F32, E_NONE);
+    } else {
+      return -4;
+    }
+#undef W4_LAUNCH
     RT_LAUNCH_CHECK();
     return 0;
   }
@@ -848,9 +1197,12 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   if (nsplit > 1 && out != O_F32_ATOMIC && out != O_F32_SLAB) return -2;
   if (act == E_SWIGLU && (layout_a != ROW || layout_b != ROW || out != O_BF16 || N % 256)) return -3;
   if (act != E_NONE && (layout_a != ROW || layout_b != ROW || out != O_BF16)) return -5;
-  if (bn != 0 && bn != 128 && bn != 256) return -8;
+  if (bn != 0 && bn != 128 && bn != 256 && bn != 4 && bn != 3) return -8;
   const bool can128 = bn128_supported(layout_a, layout_b, act, out);
   if (bn == 128 && !can128) return -8;
+  if ((bn == 4 || bn == 3) && (layout_a != ROW || layout_b != ROW || (out != O_BF16 && out != O_F32) || nsplit != 1 ||
+                  (long)N * ldb * 2 >= (1L << 32) || (long)M * lda * 2 >= (1L << 32)))
+    return -8;
   Args p;
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
   p.A2 = (A2 && B2) ? (const bf16_t*)A2 : nullptr; p.lda2 = lda2;

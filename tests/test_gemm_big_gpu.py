@@ -163,3 +163,40 @@ def test_decode_plan_m256(M, N, K, act):
         ref_ = ref_.to(torch.bfloat16).float()
         ref_ = torch.nn.functional.silu(ref_[:, :N // 2]) * ref_[:, N // 2:]
     _close(y, ref_)
+
+
+# ---- 4-wave tiles (bn 3: 192 x 256, 96 x 128 per wave; bn 4: 256 x 256, 128 x 128 per wave) ----
+@pytest.mark.parametrize("bn", [3, 4])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 520, 224), (77, 136, 4096), (1000, 768, 1024),
+                                   (2900, 1024, 192), (193, 6144, 4096)])
+def test_w4_nt(bn, M, N, K):
+    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
+    ref_nt = a.float() @ w.float().t()
+    _close(ops.gemm_big(a, w, ops.ROW, ops.ROW, bn=bn), ref_nt)
+    _close(ops.gemm_big(a, w, ops.ROW, ops.ROW, out_mode=1, bn=bn), ref_nt, rtol=5e-3, atol=5e-3)
+    r = _r(M, N)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.gemm_big(a, w, ops.ROW, ops.ROW, out=out, residual=r, bn=bn)
+    assert not torch.isnan(out).any()
+    _close(out, ref_nt + r.float())
+
+
+@pytest.mark.parametrize("bn", [3, 4])
+def test_w4_identity_bias_act_lora_swiglu(bn):
+    n = 512
+    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    w = (torch.arange(n * n, device=DEV).reshape(n, n) % 97).to(torch.bfloat16)
+    torch.testing.assert_close(ops.gemm_big(a, w, ops.ROW, ops.ROW, bn=bn).float(), w.float().t())
+    M, K, F, R = 700, 512, 384, 16
+    x, wg = _r(M, K), _r(2 * F, K, s=1 / math.sqrt(K))
+    b = _r(2 * F)
+    for act in (0, 1, 2, 3, 4):
+        want = ops.reference.apply_act(x.float() @ wg.float().t() + b.float(), act)
+        _close(ops.gemm_big(x, wg, ops.ROW, ops.ROW, bias=b, act=act, bn=bn), want)
+    u, ub = _r(M, R), _r(2 * F, R, s=0.1)  # LoRA K-extension with a ragged (K2 = 16) step
+    _close(ops.gemm_big(x, wg, ops.ROW, ops.ROW, u, ub, bn=bn), x.float() @ wg.float().t() + u.float() @ ub.float().t())
+    pre = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    y = ops.gemm_big(x, wg, ops.ROW, ops.ROW, u, ub, act=ops.ACT_SWIGLU, out2=pre, bn=bn)
+    p_ref = (x.float() @ wg.float().t() + u.float() @ ub.float().t()).to(torch.bfloat16)
+    _close(pre, p_ref)
+    _close(y, torch.nn.functional.silu(p_ref[:, :F].float()) * p_ref[:, F:].float())
