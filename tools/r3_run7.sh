@@ -10,3 +10,6 @@ tail -3 gpurun_out/r3/test_w4.log
 timeout -k 10 400 python3 tools/gemm_big_probe.py --M 9632 --shapes qkv,o,gate_up,down \
   --cases nt,w4_192,w4_256,lib_nt,nt_swiglu,w4_192_swiglu,w4_256_swiglu --rounds 5 > gpurun_out/r3/w4_probe.log 2>&1
 cat gpurun_out/r3/w4_probe.log
+timeout -k 10 200 python3 tools/gemm_big_probe.py --M 256 --shapes qkv,o,gate_up,down \
+  --cases nt128,w4_192,w4_256,lib_nt,nt128_swiglu,w4_192_swiglu --rounds 3 > gpurun_out/r3/w4_probe_m256.log 2>&1
+cat gpurun_out/r3/w4_probe_m256.log
