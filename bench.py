@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--mode", default="ppo", choices=["ppo", "sft", "pipeline"])
     ap.add_argument("--fp8", action=argparse.BooleanOptionalAction, default=None,
                     help="fp8 (e4m3fn) weights for no-grad forwards (default: on for --mode pipeline, config 5)")
+    ap.add_argument("--fp8-kv", action=argparse.BooleanOptionalAction, default=None,
+                    help="fp8 (e4m3fn) rollout K/V cache (default: with --fp8)")
     ap.add_argument("--sft-batch", type=int, default=64, help="SFT sequences per GPU per step")
     ap.add_argument("--full-ft", action="store_true",
                     help="PPO over every policy weight (the reference's full-parameter mode: bf16 compute copies "
@@ -90,6 +92,8 @@ def main():
         args.minibatch = 16 if args.mode == "pipeline" else 32
     if args.fp8 is None:
         args.fp8 = args.mode == "pipeline"
+    if args.fp8_kv is None:
+        args.fp8_kv = bool(args.fp8)
 
     from rag_tl_domainllm_optimizer_amd import models, parallel
     from rag_tl_domainllm_optimizer_amd.data import SyntheticCorpus
@@ -330,6 +334,7 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
     # ---- config 5: the SFT-adapted policy continues into PPO (same adapters, fp8 inference) ----
     if args.fp8:
         policy.set_fp8(True)
+    policy.kv_fp8 = bool(args.fp8_kv)
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
                    lora_r=16, lora_alpha=32.0, seed=0)
     ppo = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
@@ -353,7 +358,7 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
             "data": "synthetic (random-init weights, synthetic corpus)",
             "config": {"model": args.model, "global_batch": args.rollout_batch * di.world,
                        "seq_len": args.max_prompt + args.new_tokens, "parallelism": f"dp{di.world}",
-                       "lora_r": 16, "fp8": bool(args.fp8)},
+                       "lora_r": 16, "fp8": bool(args.fp8), "fp8_kv": bool(args.fp8_kv)},
             "sft": res, "ppo_phase_s_per_step": {k: sum(m[k] for m in pm) / len(pm) for k in pm[0]
                                                   if k.startswith("time/")}}
     if di.is_main:

@@ -54,6 +54,8 @@ int rt_attn_decode_fused(const void*, long, void*, void*, int, const int*, const
                          int, float, hipStream_t);
 int rt_attn_decode_fused_ps(int, int);
 void rt_attn_decode_set_qkv_slabs(const float*, int);
+void rt_attn_decode_set_fp8kv(float*, float*, int);
+int rt_kv_store_fp8(const void*, long, void*, void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int rt_attn_decode_mfma_ok(int, int, int, int, int);
 int rt_attn_o_fused(const void*, void*, void*, int, const int*, const int*, const int*, const int*, const float*,
                     const float*, float, int, float*, int, int, int, int, int, float, const void*, long, const void*,
@@ -670,11 +672,54 @@ void attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, const Tens
            "attn_decode");
 }
 
+// fp8 K/V cache (config 5) for the NEXT attn_decode_fused / attn_decode_fused_slabs call: kc / vc
+// are e4m3fn byte caches [B, Hkv, Smax, D] (K rows k-permuted), ksc / vsc fp32 per-slot scales
+// [B, Hkv, SmaxP] (SmaxP >= Smax, a multiple of 16). Only the MFMA decode kernels read it.
+static bool g_fp8kv_pending = false;
+static int64_t g_fp8kv_smaxp = 0;
+void attn_decode_set_fp8kv(Tensor ksc, Tensor vsc) {
+  CHECK_CUDA(ksc); CHECK_F32(ksc); CHECK_F32(vsc);
+  TORCH_CHECK(ksc.dim() == 3 && ksc.is_contiguous() && vsc.is_contiguous() && vsc.sizes() == ksc.sizes(),
+              "attn_decode_set_fp8kv: scales must be contiguous [B, Hkv, SmaxP]");
+  g_fp8kv_smaxp = ksc.size(2);
+  rt_attn_decode_set_fp8kv(ksc.data_ptr<float>(), vsc.data_ptr<float>(), (int)g_fp8kv_smaxp);
+  g_fp8kv_pending = true;
+}
+static void check_cache_dtype(const Tensor& kc, const Tensor& vc, const char* who) {
+  if (g_fp8kv_pending) {
+    g_fp8kv_pending = false;
+    TORCH_CHECK(kc.scalar_type() == at::kByte && vc.scalar_type() == at::kByte, who, ": fp8 scales set for a bf16 cache");
+    TORCH_CHECK(g_fp8kv_smaxp >= kc.size(2) && kc.size(3) == 128, who, ": fp8 cache needs D = 128 and SmaxP >= Smax");
+  } else {
+    CHECK_BF16(kc); CHECK_BF16(vc);
+  }
+}
+static void clear_fp8kv() {
+  g_fp8kv_pending = false;
+  rt_attn_decode_set_fp8kv(nullptr, nullptr, 0);
+}
+
+// Prompt K / V of the rotated qkv rows [B * S] -> fp8 cache slots [0, S) with per-slot scales.
+void kv_store_fp8(const Tensor& qkv, Tensor kc, Tensor vc, Tensor ksc, Tensor vsc, int64_t B, int64_t S, int64_t Hq) {
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_ROWS(qkv); CHECK_F32(ksc); CHECK_F32(vsc);
+  TORCH_CHECK(kc.scalar_type() == at::kByte && vc.scalar_type() == at::kByte && kc.dim() == 4 && kc.is_contiguous() &&
+                  vc.is_contiguous() && vc.sizes() == kc.sizes(), "kv_store_fp8: cache layout");
+  const int64_t Hkv = kc.size(1), Smax = kc.size(2), D = kc.size(3);
+  TORCH_CHECK(kc.size(0) == B && qkv.size(0) == B * S && qkv.size(1) >= (Hq + 2 * Hkv) * D, "kv_store_fp8: shapes");
+  TORCH_CHECK(ksc.dim() == 3 && ksc.size(0) == B && ksc.size(1) == Hkv && ksc.is_contiguous() && vsc.is_contiguous() &&
+                  vsc.sizes() == ksc.sizes(), "kv_store_fp8: scales");
+  check_rc(rt_kv_store_fp8(qkv.data_ptr(), qkv.stride(0), kc.data_ptr(), vc.data_ptr(), ksc.data_ptr<float>(),
+                           vsc.data_ptr<float>(), (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, (int)Smax,
+                           (int)ksc.size(2), cur_stream()),
+           "kv_store_fp8");
+}
+
 void attn_decode_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& slot, const Tensor& attn_len,
                        const optional<Tensor>& kv_start, const optional<Tensor>& pos, const optional<Tensor>& cos,
                        const optional<Tensor>& sin, double sign, int64_t window, double scale, int64_t Hq, Tensor part,
                        Tensor tickets, int64_t PS, Tensor out) {
-  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_ROWS(qkv); CHECK_BF16(kc); CHECK_BF16(vc); CHECK_I32(slot);
+  check_cache_dtype(kc, vc, "attn_decode_fused");
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_ROWS(qkv); CHECK_I32(slot);
   CHECK_I32(attn_len); CHECK_F32(part); CHECK_I32(tickets); CHECK_BF16(out); CHECK_ROWS(out);
   TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes(),
               "attn_decode_fused: cache layout");
@@ -711,14 +756,19 @@ bool attn_decode_fused_slabs(const Tensor& slabs, int64_t nsplit, Tensor kc, Ten
                              const Tensor& attn_len, const optional<Tensor>& kv_start, const optional<Tensor>& pos,
                              const optional<Tensor>& cos, const optional<Tensor>& sin, double sign, int64_t window,
                              double scale, int64_t Hq, Tensor part, Tensor tickets, int64_t PS, Tensor out) {
-  CHECK_CUDA(slabs); CHECK_F32(slabs); CHECK_BF16(kc); CHECK_BF16(vc); CHECK_I32(slot); CHECK_I32(attn_len);
+  const bool fp8kv = g_fp8kv_pending;
+  check_cache_dtype(kc, vc, "attn_decode_fused_slabs");
+  CHECK_CUDA(slabs); CHECK_F32(slabs); CHECK_I32(slot); CHECK_I32(attn_len);
   CHECK_F32(part); CHECK_I32(tickets); CHECK_BF16(out); CHECK_ROWS(out);
   TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes(),
               "attn_decode_fused_slabs: cache layout");
   const int64_t B = kc.size(0), Hkv = kc.size(1), Smax = kc.size(2), D = kc.size(3);
   const int64_t NP = (Smax + PS - 1) / PS, G = Hq / Hkv;
   TORCH_CHECK(G * Hkv == Hq, "attn_decode_fused_slabs: Hq must be a multiple of Hkv");
-  if (!rt_attn_decode_mfma_ok((int)B, (int)Hq, (int)Hkv, (int)D, (int)NP)) return false;
+  if (!rt_attn_decode_mfma_ok((int)B, (int)Hq, (int)Hkv, (int)D, (int)NP)) {
+    if (fp8kv) clear_fp8kv();  // nothing launched: the caller reduces and retries with the scales set again
+    return false;
+  }
   const int64_t W = (Hq + 2 * Hkv) * D;
   TORCH_CHECK(slabs.is_contiguous() && slabs.numel() >= nsplit * B * W && nsplit >= 1, "attn_decode_fused_slabs: slabs");
   TORCH_CHECK(out.size(0) == B && slot.numel() == B && attn_len.numel() == B && out.size(1) >= Hq * D,
@@ -1047,6 +1097,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
   m.def("attn_decode_fused_slabs", &attn_decode_fused_slabs, "decode attention with the qkv split-K reduce fused");
+  m.def("attn_decode_set_fp8kv", &attn_decode_set_fp8kv, "fp8 K/V cache scales for the next decode attention call");
+  m.def("kv_store_fp8", &kv_store_fp8, "prompt K/V -> fp8 cache (per-slot scales)");
   m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");
   m.def("quant_fp8", &quant_fp8, "per-row absmax e4m3fn quantisation -> (uint8 [R,C], scale fp32 [R])");
   m.def("gemm_big", &gemm_big, "token-parallel GEMM family (NT / NN / TN, LoRA K-extension, split-K, SwiGLU)",

@@ -48,6 +48,13 @@ __device__ __forceinline__ uint4 load_nt16(const void* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// 8-B non-temporal load (fp8 K/V cache rows: read once per decode step)
+__device__ __forceinline__ uint2 load_nt8(const void* p) {
+  typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+  const u32x2_t v = __builtin_nontemporal_load((const u32x2_t*)p);
+  return make_uint2(v.x, v.y);
+}
+
 // ---- transposed LDS reads that do not drain LDS-DMA ----
 // hipcc places `s_waitcnt vmcnt(0)` in front of every __builtin_amdgcn_ds_read_tr16_b64 while a
 // global_load_lds is in flight (the intrinsic carries no alias information, so every pending
@@ -224,6 +231,26 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   v.z = pack2bf(f[4], f[5]);
   v.w = pack2bf(f[6], f[7]);
   return v;
+}
+
+// 8 OCP e4m3fn bytes (lo = bytes 0-3, hi = 4-7) -> 8 bf16 (exact: every e4m3fn value is a bf16)
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16(unsigned lo, unsigned hi) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+  const bf16x2_t a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.f, false);
+  const bf16x2_t b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.f, true);
+  const bf16x2_t c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.f, false);
+  const bf16x2_t d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.f, true);
+  return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+// 8 floats * inv -> 8 OCP e4m3fn bytes (round to nearest even; |x * inv| <= 448 by the caller's scale)
+__device__ __forceinline__ uint2 f32x8_to_fp8(const float* v, float inv) {
+  unsigned lo = 0, hi = 0;
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, lo, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, lo, true);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, hi, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, hi, true);
+  return make_uint2(lo, hi);
 }
 
 // Sum of `ns` fp32 split-K slabs of 8 consecutive floats (slab q at p + q * stride), added in

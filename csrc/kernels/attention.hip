@@ -27,6 +27,7 @@
 #include "rt_common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace rt {
 
@@ -480,6 +481,10 @@ struct DecodeFusedArgs {
   const float* qkv_slabs; int qkv_nsplit; long qkv_sstride;
   int kv_nt;                        // MFMA kernel: non-temporal K/V cache loads (each read once per step)
   long long* stamps;                // debug (W > 1 kernel): [blocks * W][8] s_memrealtime phase stamps, or null
+  // fp8 K/V cache (config 5, MFMA kernels only): kc / vc hold OCP e4m3fn bytes, one fp32 scale per
+  // (batch, kv head, slot) in ksc / vsc [B, Hkv, SmaxP]; K rows are stored k-permuted (element
+  // 32 s + 8 g + e at byte 32 g + 8 s + e: one lane's four MFMA K chunks are 32 contiguous bytes)
+  float* ksc; float* vsc; int SmaxP;
 };
 
 template <int D>
@@ -793,7 +798,7 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
 // covering keys [part * PS, (part + 1) * PS) of the row; each publishes its merged (m, l, O) with
 // write-through stores and takes a ticket, and the last of the row's NP partitions merges them —
 // at 4k keys one workgroup per (batch, kv head) would stream 2 MB from one CU.
-template <int G, int W>
+template <int G, int W, bool KV8 = false>
 __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArgs a) {
   constexpr int D = 128, DS = D / 32, DT = D / 16;
   __shared__ __attribute__((aligned(16))) char vimg_all[W][32 * D * 2];  // per wave; rows 16..31 stay zero
@@ -825,15 +830,35 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
   const bf16_t* row = a.qkv + (long)b * a.ldq;
   const bf16_t* kbase = a.kc + ((long)b * a.Hkv + hk) * a.Smax * D;
   const bf16_t* vbase = a.vc + ((long)b * a.Hkv + hk) * a.Smax * D;
+  // fp8 cache: byte rows of D, scales per slot
+  const unsigned char* kbase8 = (const unsigned char*)a.kc + ((long)b * a.Hkv + hk) * a.Smax * D;
+  const unsigned char* vbase8 = (const unsigned char*)a.vc + ((long)b * a.Hkv + hk) * a.Smax * D;
+  const float* ksb = KV8 ? a.ksc + ((long)b * a.Hkv + hk) * a.SmaxP : nullptr;
+  const float* vsb = KV8 ? a.vsc + ((long)b * a.Hkv + hk) * a.SmaxP : nullptr;
 
   // tile of 16 keys from c0 (32 registers per set: two sets keep every wave of a batch-256 layer
   // resident, 3 per SIMD): K fragments k[s] = K[c0 + r16][32 s + 8 g ..] (A operand of S^T);
   // V pieces v[i] = V[c0 + 4 i + g][8 r16 ..] (4 whole rows per load instruction).
   // Keys past len - 1 re-read slot len - 1 (masked).
-  struct Tile { uint4 k[DS]; uint4 v[4]; };
+  // fp8 tile (KV8): the lane's 32 K bytes (k-permuted row), 4 x 8 V bytes, and the scales of the
+  // 4 keys c0 + 4 g + i whose scores the lane holds (S^T rows) — 24 registers instead of 32
+  struct Tile16 { uint4 k[DS]; uint4 v[4]; };
+  struct Tile8 { uint4 k8[2]; uint2 v8[4]; float ks[4], vs[4]; };
+  typedef typename std::conditional<KV8, Tile8, Tile16>::type Tile;
   auto load = [&](Tile& T, int c0) {
     const long keyk = min(c0 + r16, len - 1);
-    if (a.kv_nt) {
+    if constexpr (KV8) {
+      T.k8[0] = load_nt16(kbase8 + keyk * D + 32 * g);
+      T.k8[1] = load_nt16(kbase8 + keyk * D + 32 * g + 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) T.v8[i] = load_nt8(vbase8 + (long)min(c0 + 4 * i + g, len - 1) * D + 8 * r16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = min(c0 + 4 * g + i, len - 1);
+        T.ks[i] = ksb[key];
+        T.vs[i] = vsb[key];
+      }
+    } else if (a.kv_nt) {
 #pragma unroll
       for (int s2 = 0; s2 < DS; ++s2) T.k[s2] = load_nt16(kbase + keyk * D + 32 * s2 + 8 * g);
 #pragma unroll
@@ -850,9 +875,12 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
   };
   Tile ta, tb, tc;
   const int cfirst = kbeg + 16 * w, cstep = 16 * W;  // this wave's tiles: cfirst + j * cstep
+  // fp8 tiles carry half the bytes: the single-wave kernel keeps THREE in flight (12 KiB per wave;
+  // a fourth register set would cost the second wave per SIMD)
+  constexpr bool DEEP8 = KV8 && W == 1;
   if (cfirst < len) load(ta, cfirst);
-  if (W > 1 && cfirst + cstep < len) load(tb, cfirst + cstep);
-  if (W > 1 && cfirst + 2 * cstep < len) load(tc, cfirst + 2 * cstep);
+  if ((W > 1 || DEEP8) && cfirst + cstep < len) load(tb, cfirst + cstep);
+  if ((W > 1 || DEEP8) && cfirst + 2 * cstep < len) load(tc, cfirst + 2 * cstep);
 
   // ---- q / k_new / v_new and the rotary tables, all loads at once. D = 128: chunk 4 s + g's
   // rotary partner (chunk ^ 8) is the lane's own chunk 4 (s ^ 2) + g, its table offset
@@ -921,15 +949,63 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
     knew[s2] = rope8(kraw[s2], kraw[s2 ^ 2], cq[s2 & 1], sq[s2 & 1], s2 < 2);
   }
   stamp(1);  // q / k_new / v_new / tables and the first tiles landed, RoPE done
+  // fp8 cache: quantise k_new / v_new per (token, kv head) (absmax / 448); this step attends over
+  // the quantised values too (knew / vxq hold them widened back to bf16, sk / sv their scales), so
+  // the step sees exactly what later steps read from the cache
+  uint4 vxq = vx;
+  float sk_new = 1.f, sv_new = 1.f;
+  uint2 kq[DS], vq = make_uint2(0, 0);
+  if constexpr (KV8) {
+    float amk = 0.f, amv = 0.f, f[8];
+#pragma unroll
+    for (int s2 = 0; s2 < DS; ++s2) {
+      unpack8(knew[s2], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amk = fmaxf(amk, fabsf(f[e]));
+    }
+    amk = fmaxf(amk, __shfl_xor(amk, 16, 64));  // lane group g holds chunks 4 s + g
+    amk = fmaxf(amk, __shfl_xor(amk, 32, 64));
+    unpack8(vx, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) amv = fmaxf(amv, fabsf(f[e]));
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) amv = fmaxf(amv, __shfl_xor(amv, o2, 64));  // chunk r16
+    sk_new = amk > 0.f ? amk / 448.f : 1.f;
+    sv_new = amv > 0.f ? amv / 448.f : 1.f;
+    const float ik = 1.f / sk_new, iv = 1.f / sv_new;
+#pragma unroll
+    for (int s2 = 0; s2 < DS; ++s2) {
+      unpack8(knew[s2], f);
+      kq[s2] = f32x8_to_fp8(f, ik);
+      knew[s2] = __builtin_bit_cast(uint4, fp8x8_to_bf16(kq[s2].x, kq[s2].y));
+    }
+    unpack8(vx, f);
+    vq = f32x8_to_fp8(f, iv);
+    vxq = __builtin_bit_cast(uint4, fp8x8_to_bf16(vq.x, vq.y));
+  }
   // cache append: lane (g, 0) stores its 4 k chunks 4 s + g, lane group 1 the v chunks (wave 0)
   if (has_new && w == 0) {
-    bf16_t* kdst = a.kc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
-    bf16_t* vdst = a.vc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
-    if (r16 == 0) {
+    if constexpr (KV8) {
+      unsigned char* kdst = (unsigned char*)a.kc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
+      unsigned char* vdst = (unsigned char*)a.vc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
+      if (r16 == 0) {  // k-permuted: chunks 4 s + g at bytes 32 g + 8 s
+        *(uint4*)(kdst + 32 * g) = make_uint4(kq[0].x, kq[0].y, kq[1].x, kq[1].y);
+        *(uint4*)(kdst + 32 * g + 16) = make_uint4(kq[2].x, kq[2].y, kq[3].x, kq[3].y);
+      }
+      if (g == 1) *(uint2*)(vdst + r16 * 8) = vq;
+      if (lane == 0) {
+        a.ksc[((long)b * a.Hkv + hk) * a.SmaxP + s_new] = sk_new;
+        a.vsc[((long)b * a.Hkv + hk) * a.SmaxP + s_new] = sv_new;
+      }
+    } else {
+      bf16_t* kdst = a.kc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
+      bf16_t* vdst = a.vc + (((long)b * a.Hkv + hk) * a.Smax + s_new) * D;
+      if (r16 == 0) {
 #pragma unroll
-      for (int s2 = 0; s2 < DS; ++s2) *(uint4*)(kdst + (4 * s2 + g) * 8) = knew[s2];
+        for (int s2 = 0; s2 < DS; ++s2) *(uint4*)(kdst + (4 * s2 + g) * 8) = knew[s2];
+      }
+      if (g == 1) *(uint4*)(vdst + r16 * 8) = vx;
     }
-    if (g == 1) *(uint4*)(vdst + r16 * 8) = vx;
   }
 
   f32x4 o[DT];
@@ -941,28 +1017,55 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
   for (int i = 0; i < 4; ++i) *(uint4*)(vimg + v_off<D>(16 + 4 * i + g, r16)) = make_uint4(0, 0, 0, 0);
 
   auto consume = [&](Tile& T, int c0) {
+    // bf16 K fragments / V pieces of the tile (fp8: widened, unscaled e4m3 values; the per-key
+    // scales go on the scores and on P)
+    uint4 kf[DS], vf[4];
+    float ks[4] = {1.f, 1.f, 1.f, 1.f}, vs[4] = {1.f, 1.f, 1.f, 1.f};
+    if constexpr (KV8) {
+#pragma unroll
+      for (int s2 = 0; s2 < DS; ++s2) {
+        const uint4& q = T.k8[s2 >> 1];
+        kf[s2] = __builtin_bit_cast(uint4, (s2 & 1) ? fp8x8_to_bf16(q.z, q.w) : fp8x8_to_bf16(q.x, q.y));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        vf[i] = __builtin_bit_cast(uint4, fp8x8_to_bf16(T.v8[i].x, T.v8[i].y));
+        ks[i] = T.ks[i];
+        vs[i] = T.vs[i];
+      }
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < DS; ++s2) kf[s2] = T.k[s2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) vf[i] = T.v[i];
+    }
     if (has_new && s_new >= c0 && s_new < c0 + 16) {
       if (min(c0 + r16, len - 1) == s_new) {
 #pragma unroll
-        for (int s2 = 0; s2 < DS; ++s2) T.k[s2] = knew[s2];
+        for (int s2 = 0; s2 < DS; ++s2) kf[s2] = knew[s2];
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (min(c0 + 4 * i + g, len - 1) == s_new) T.v[i] = vx;
+      for (int i = 0; i < 4; ++i) {
+        if (min(c0 + 4 * i + g, len - 1) == s_new) vf[i] = vxq;
+        if (KV8 && c0 + 4 * g + i == s_new) {  // this step's own scales (the prefetched ones may be stale)
+          ks[i] = sk_new;
+          vs[i] = sv_new;
+        }
+      }
     }
     // V image rows 0..15 (the previous tile's transposed reads precede these writes in this
     // wave's LDS queue)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *(uint4*)(vimg + v_off<D>(4 * i + g, r16)) = T.v[i];
+    for (int i = 0; i < 4; ++i) *(uint4*)(vimg + v_off<D>(4 * i + g, r16)) = vf[i];
     // S^T: lane holds the scores of keys c0 + 4 g + i for head r16
     f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s2 = 0; s2 < DS; ++s2)
-      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, T.k[s2]), qf[s2], st, 0, 0, 0);
+      st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf[s2]), qf[s2], st, 0, 0, 0);
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float x = c0 + 4 * g + i < len ? st[i] * a.scale_log2 : -INFINITY;
+      const float x = c0 + 4 * g + i < len ? st[i] * (KV8 ? ks[i] * a.scale_log2 : a.scale_log2) : -INFINITY;
       st[i] = x;
       mx = fmaxf(mx, x);
     }
@@ -975,15 +1078,16 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float pv = exp2f(st[i] - mn);
-      st[i] = pv;
+      st[i] = KV8 ? pv * vs[i] : pv;  // fp8: the V scale of key c0 + 4 g + i rides on P
       rs += pv;
     }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
-    // O rows are heads 4 g + i: their factors live in lanes 4 g + i
+    // O rows are heads 4 g + i: their factors live in lanes 4 g + i. Only rows < G are ever
+    // stored or merged (an O row depends on its own P row only), so G < 4 rescales G rows
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < (G < 4 ? G : 4); ++i) {
       const float al = __shfl(alpha, 4 * g + i, 64);
 #pragma unroll
       for (int c = 0; c < DT; ++c) o[c][i] *= al;
@@ -1000,7 +1104,7 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
     }
   };
 
-  if constexpr (W == 1) {
+  if constexpr (W == 1 && !DEEP8) {
     for (int c0 = cfirst; c0 < len; c0 += 2 * cstep) {
       if (c0 + cstep < len) load(tb, c0 + cstep);
       consume(ta, c0);
@@ -1869,6 +1973,59 @@ extern "C" int rt_attn_decode_mfma_ok(int B, int Hq, int Hkv, int D, int NP) {
   return use_mfma && NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
 }
 
+// fp8 K/V cache for the NEXT rt_attn_decode_fused call (set by the binding; one launch only):
+// kc / vc are then e4m3fn byte caches with per-slot scales ksc / vsc [B, Hkv, SmaxP]
+static float* g_dec_ksc = nullptr;
+static float* g_dec_vsc = nullptr;
+static int g_dec_smaxp = 0;
+extern "C" void rt_attn_decode_set_fp8kv(float* ksc, float* vsc, int SmaxP) {
+  g_dec_ksc = ksc; g_dec_vsc = vsc; g_dec_smaxp = SmaxP;
+}
+
+// Prompt K / V (rows [b * S + s] of the rotated qkv) -> fp8 cache slots [0, S): one 16-lane group
+// per (token, kv head, K | V), 8 elements per lane, absmax over the head row by shuffles. K rows
+// are written k-permuted (chunk c = 4 s + g at byte 32 g + 8 s), as attn_decode_mfma_kernel<KV8>
+// reads them. D = 128.
+__global__ __launch_bounds__(256) void kv_store_fp8_kernel(const bf16_t* __restrict__ qkv, long ldq,
+                                                           unsigned char* __restrict__ kc, unsigned char* __restrict__ vc,
+                                                           float* __restrict__ ksc, float* __restrict__ vsc, int B, int S,
+                                                           int Hq, int Hkv, int Smax, int SmaxP) {
+  constexpr int D = 128;
+  const long gid = (long)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int c = threadIdx.x & 15;
+  if (gid >= (long)B * S * Hkv * 2) return;  // whole 16-lane groups
+  const int kv = (int)(gid & 1);
+  const long t = gid >> 1;
+  const int hk = (int)(t % Hkv);
+  const long row = t / Hkv;
+  const int b = (int)(row / S), s = (int)(row % S);
+  float f[8];
+  unpack8(*(const uint4*)(qkv + row * ldq + (long)(Hq + kv * Hkv + hk) * D + 8 * c), f);
+  float am = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(f[e]));
+#pragma unroll
+  for (int o2 = 1; o2 < 16; o2 <<= 1) am = fmaxf(am, __shfl_xor(am, o2, 16));
+  const float sc = am > 0.f ? am / 448.f : 1.f;
+  const uint2 q = f32x8_to_fp8(f, 1.f / sc);
+  const long base = (((long)b * Hkv + hk) * Smax + s) * D;
+  if (kv == 0) *(uint2*)(kc + base + 32 * (c & 3) + 8 * (c >> 2)) = q;
+  else *(uint2*)(vc + base + 8 * c) = q;
+  if (c == 0) (kv == 0 ? ksc : vsc)[((long)b * Hkv + hk) * SmaxP + s] = sc;
+}
+
+extern "C" int rt_kv_store_fp8(const void* qkv, long ldq, void* kc, void* vc, float* ksc, float* vsc, int B, int S,
+                               int Hq, int Hkv, int D, int Smax, int SmaxP, hipStream_t stream) {
+  if ((long)B * S == 0) return 0;
+  if (D != 128 || S > Smax || SmaxP < Smax || ldq % 8) return -1;
+  const long groups = (long)B * S * Hkv * 2;
+  hipLaunchKernelGGL(kv_store_fp8_kernel, dim3((unsigned)((groups + 15) / 16)), dim3(256), 0, stream,
+                     (const bf16_t*)qkv, ldq, (unsigned char*)kc, (unsigned char*)vc, ksc, vsc, B, S, Hq, Hkv, Smax,
+                     SmaxP);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* vc, int Smax, const int* slot,
                                     const int* attn_len, const int* kv_start, const int* pos, const float* cosT,
                                     const float* sinT, float sign, int window, float* part, unsigned* tickets, int NP,
@@ -1886,9 +2043,42 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   static const int kv_nt_env = getenv("RT_ATTN_KV_NT") ? atoi(getenv("RT_ATTN_KV_NT")) : 1;
   a.kv_nt = kv_nt_env;
   a.stamps = g_ao_stamps;
+  a.ksc = g_dec_ksc; a.vsc = g_dec_vsc; a.SmaxP = g_dec_smaxp;
+  const bool kv8 = g_dec_ksc != nullptr;
+  g_dec_ksc = g_dec_vsc = nullptr;  // one launch only
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -1;
+  if (kv8) {
+    // fp8 cache: the MFMA kernels only (large batch: one workgroup per (batch, kv head); small
+    // batch: 8 waves per (batch, kv head), partitions for long caches)
+    if (D != 128 || a.SmaxP < Smax || (G != 1 && G != 2 && G != 4 && G != 8)) return -3;
+    // RT_DECODE_FP8_MW=1: the 8-wave kernel at every batch (A/B hook)
+    static const int fp8_mw = getenv("RT_DECODE_FP8_MW") ? atoi(getenv("RT_DECODE_FP8_MW")) : 0;
+    if (!fp8_mw && rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
+      dim3 mgrid((unsigned)(B * Hkv)), mblock(64);
+      switch (G) {
+        case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, 1, true>), mgrid, mblock, 0, stream, a); break;
+        case 2: hipLaunchKernelGGL((attn_decode_mfma_kernel<2, 1, true>), mgrid, mblock, 0, stream, a); break;
+        case 4: hipLaunchKernelGGL((attn_decode_mfma_kernel<4, 1, true>), mgrid, mblock, 0, stream, a); break;
+        default: hipLaunchKernelGGL((attn_decode_mfma_kernel<8, 1, true>), mgrid, mblock, 0, stream, a); break;
+      }
+    } else {
+      if (NP > 1 && !(part && tickets)) return -3;
+      const int npm = rt_attn_decode_mw_np(Smax, NP);
+      a.NP = npm;
+      a.PS = npm > 1 ? ((Smax + npm - 1) / npm + 15) / 16 * 16 : Smax;
+      dim3 mgrid((unsigned)(B * Hkv * npm)), mblock(64 * DEC_MW);
+      switch (G) {
+        case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, DEC_MW, true>), mgrid, mblock, 0, stream, a); break;
+        case 2: hipLaunchKernelGGL((attn_decode_mfma_kernel<2, DEC_MW, true>), mgrid, mblock, 0, stream, a); break;
+        case 4: hipLaunchKernelGGL((attn_decode_mfma_kernel<4, DEC_MW, true>), mgrid, mblock, 0, stream, a); break;
+        default: hipLaunchKernelGGL((attn_decode_mfma_kernel<8, DEC_MW, true>), mgrid, mblock, 0, stream, a); break;
+      }
+    }
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
   // large batch, one partition per (batch, kv head): the MFMA kernel (RT_DECODE_MFMA=0 disables)
   if (rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
     dim3 mgrid((unsigned)(B * Hkv)), mblock(64);

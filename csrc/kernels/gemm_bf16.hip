@@ -551,15 +551,6 @@ __device__ __forceinline__ void dg_load(DGRegs<MT>& r, const char* const* wrow, 
   }
 }
 
-__device__ __forceinline__ bf16x8 fp8x8_to_bf16(unsigned lo, unsigned hi) {
-  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
-  const bf16x2_t a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.f, false);
-  const bf16x2_t b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(lo, 1.f, true);
-  const bf16x2_t c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.f, false);
-  const bf16x2_t d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(hi, 1.f, true);
-  return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
-}
-
 template <int MT, bool W8>
 __device__ __forceinline__ void dg_mma(const DGRegs<MT>& r, f32x4 (&acc)[MT][4]) {
   bf16x8 w0[4], w1[4];

@@ -125,6 +125,9 @@ def _apply_fp8(cfg, policy):
     if policy is not None and getattr(cfg.model, "fp8", False) and hasattr(policy, "set_fp8"):
         if next(policy.parameters()).is_cuda:
             policy.set_fp8(True)
+    if policy is not None and getattr(cfg.model, "fp8_kv", False) and hasattr(policy, "kv_fp8"):
+        if next(policy.parameters()).is_cuda:
+            policy.kv_fp8 = True  # generators built on the policy keep an e4m3fn K/V cache
     return policy
 
 

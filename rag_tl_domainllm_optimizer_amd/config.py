@@ -29,6 +29,9 @@ class ModelSection:
     # fp8 (OCP e4m3fn) weight images for every no-grad policy forward: rollout prefill / decode,
     # reference scoring, RAG answers (config 5). Training forwards keep the bf16 weights.
     fp8: bool = False
+    # fp8 (e4m3fn, per-slot scales) K/V cache for rollout / RAG-answer generation (config 5): half
+    # the bytes the decode attention streams
+    fp8_kv: bool = False
 
 
 @dataclass
@@ -83,7 +86,7 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     "config4_ppo_mistral7b": {"model.policy": "mistral-7b:random", "ppo.lora_r": 16, "data.batch_size": 64},
     # 5: Llama-2-13B full pipeline (RAG -> LoRA SFT -> PPO) on 8 GPUs
     "config5_pipeline_llama13b": {"model.policy": "llama2-13b:random", "sft.lora_r": 16, "ppo.lora_r": 16,
-                                  "model.fp8": True},
+                                  "model.fp8": True, "model.fp8_kv": True},
 }
 
 

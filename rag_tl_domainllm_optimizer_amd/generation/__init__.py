@@ -53,22 +53,43 @@ class GenerationOutput:
 
 
 class KVCache:
-    def __init__(self, num_layers, B, Hkv, Smax, D, device, dtype=torch.bfloat16):
+    """Static K/V cache [L, B, Hkv, Smax, D]. ``fp8``: e4m3fn bytes (K rows k-permuted) plus one
+    fp32 scale per (layer, row, kv head, slot) in ``ks`` / ``vs`` [L, B, Hkv, SmaxP] (SmaxP = Smax
+    rounded up to 16; zero-initialised so never-written slots scale to 0) — config 5's rollout
+    cache, half the bytes the decode attention streams (``ops.kv_store_fp8``)."""
+
+    def __init__(self, num_layers, B, Hkv, Smax, D, device, dtype=torch.bfloat16, fp8: bool = False):
         alloc = torch.empty if torch.device(device).type == "cuda" else torch.zeros
-        self.k = alloc(num_layers, B, Hkv, Smax, D, device=device, dtype=dtype)
-        self.v = alloc(num_layers, B, Hkv, Smax, D, device=device, dtype=dtype)
+        self.fp8 = fp8
+        cdt = torch.uint8 if fp8 else dtype
+        self.k = alloc(num_layers, B, Hkv, Smax, D, device=device, dtype=cdt)
+        self.v = alloc(num_layers, B, Hkv, Smax, D, device=device, dtype=cdt)
+        self.ks = self.vs = None
+        if fp8:
+            if D != ops.FP8_KV_D:
+                raise ValueError(f"fp8 KV cache needs head_dim {ops.FP8_KV_D}, got {D}")
+            smaxp = (Smax + 15) // 16 * 16
+            self.ks = torch.zeros(num_layers, B, Hkv, smaxp, device=device, dtype=torch.float32)
+            self.vs = torch.zeros(num_layers, B, Hkv, smaxp, device=device, dtype=torch.float32)
         self.B, self.Smax = B, Smax
+
+    def scales(self, layer: int):
+        """(k_scale, v_scale) of one layer, or (None, None) for a bf16 cache"""
+        return (self.ks[layer], self.vs[layer]) if self.fp8 else (None, None)
 
     @property
     def nbytes(self):
-        return 2 * self.k.numel() * self.k.element_size()
+        n = 2 * self.k.numel() * self.k.element_size()
+        if self.fp8:
+            n += 2 * self.ks.numel() * 4
+        return n
 
 
 class Generator:
     """Owns the cache and captured graph for one (model, max_batch, max_seq) configuration."""
 
     def __init__(self, model, max_batch: int, max_seq: int, device=None, use_graph: bool = True,
-                 value_head=None, sync_every: int = 16):
+                 value_head=None, sync_every: int = 16, kv_fp8: Optional[bool] = None):
         self.model = model
         cfg = model.cfg
         self.cfg = cfg
@@ -77,8 +98,11 @@ class Generator:
         self.use_graph = use_graph and self.device.type == "cuda"
         self.value_head = value_head
         self.sync_every = sync_every
+        # fp8 K/V cache (config 5): the model's setting unless given; GPU MFMA decode kernels only
+        # (head_dim 128), the CPU path runs the quantise / dequantise reference
+        kv_fp8 = getattr(model, "kv_fp8", False) if kv_fp8 is None else kv_fp8
         self.cache = KVCache(cfg.num_layers, max_batch, cfg.num_kv_heads, max_seq, cfg.head_dim, self.device,
-                             model.dtype)
+                             model.dtype, fp8=bool(kv_fp8))
         dev = self.device
         B = max_batch
         self.workspace = ops.decode_workspace(B, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, max_seq, dev) \
@@ -372,6 +396,13 @@ class _SubCache:
     def __init__(self, cache: KVCache, B: int):
         self.k = [cache.k[l, :B] for l in range(cache.k.shape[0])]
         self.v = [cache.v[l, :B] for l in range(cache.v.shape[0])]
+        self.fp8 = cache.fp8
+        if cache.fp8:
+            self.ks = [cache.ks[l, :B] for l in range(cache.ks.shape[0])]
+            self.vs = [cache.vs[l, :B] for l in range(cache.vs.shape[0])]
+
+    def scales(self, layer: int):
+        return (self.ks[layer], self.vs[layer]) if self.fp8 else (None, None)
 
 
 def generate_text(model, tokenizer, prompts: List[str], params: SamplingParams, generator: Optional[Generator] = None,

@@ -193,6 +193,8 @@ class CausalLM(nn.Module):
         # default: measured 26.4 vs 25.0 us per layer for the two-kernel path (docs/DESIGN.md,
         # profiles/kernels_attn_o_fused_rejected.log); RAGTL_ATTN_O=1 turns it on
         self.fused_attn_o = os.environ.get("RAGTL_ATTN_O", "0") == "1"
+        # fp8 (e4m3fn) K/V cache for generators built on this model (config 5, ``model.fp8_kv``)
+        self.kv_fp8 = False
         if init:
             self.reset_parameters(seed)
 
@@ -334,8 +336,14 @@ class CausalLM(nn.Module):
             qkv, residual = layer.attn_in(x, residual)
             if idx is not None:
                 qkv = ops.scatter_rows(qkv, idx, inv, B * S)
-            ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S,
-                          k_cache=cache.k[li], v_cache=cache.v[li], slot_base=None)
+            if getattr(cache, "fp8", False):
+                # fp8 cache: rotate in place, then quantise the prompt K / V rows into it
+                ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S)
+                k_sc, v_sc = cache.scales(li)
+                ops.kv_store_fp8(qkv, cache.k[li], cache.v[li], k_sc, v_sc, B, S, cfg.num_heads)
+            else:
+                ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S,
+                              k_cache=cache.k[li], v_cache=cache.v[li], slot_base=None)
             o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
                                         cfg.sliding_window, kv_start=ks)
             if li == len(self.layers) - 1:
@@ -362,27 +370,31 @@ class CausalLM(nn.Module):
         if (self.fused_decode and cfg.arch != "opt" and x.is_cuda and x.shape[0] <= max_b
                 and not torch.is_grad_enabled()):
             h = x
+            kv8 = getattr(cache, "fp8", False)
             for li, layer in enumerate(self.layers):
                 def attend(qkv, li=li):
+                    ks, vs = cache.scales(li) if kv8 else (None, None)
                     return ops.decode_step_attention(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads,
                                                      pos, cos, sin, kv_start, cfg.sliding_window,
-                                                     workspace=workspace)
+                                                     workspace=workspace, k_scale=ks, v_scale=vs)
 
                 def attend_o(qkv, w_o, res, li=li):
                     return ops.decode_step_attention_o(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads,
                                                        w_o, res, pos, cos, sin, kv_start, cfg.sliding_window,
                                                        workspace=workspace)
-                h = layer.decode_fused(h, attend, attend_o if self.fused_attn_o else None)
+                h = layer.decode_fused(h, attend, attend_o if (self.fused_attn_o and not kv8) else None)
             y, _ = ops.rms_norm(h, self.norm_w, cfg.norm_eps)
             return y
         residual = None
         # batch > 64: split-K GEMM partials flow unreduced into the attention prologue and the norms
         defer = x.is_cuda and x.shape[0] > 64 and self.defer_splitk
+        kv8 = getattr(cache, "fp8", False)
         for li, layer in enumerate(self.layers):
             qkv, residual = layer.attn_in(x, residual, defer)
             # one fused kernel: RoPE(q, k_new) + cache append + split-K attention + combine
+            ks, vs = cache.scales(li) if kv8 else (None, None)
             o = ops.decode_step_attention(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads, pos, cos, sin,
-                                          kv_start, cfg.sliding_window, workspace=workspace)
+                                          kv_start, cfg.sliding_window, workspace=workspace, k_scale=ks, v_scale=vs)
             x, residual = layer.mlp(o, residual, defer)
         return self.final_norm(x, residual)
 

@@ -255,27 +255,103 @@ def decode_workspace(B, Hq, Hkv, D, Smax, device, PS=None):
     return DecodeWorkspace((part, PS, tickets, sync))
 
 
+# ----------------------------------------------------------------------------- fp8 K/V cache
+# Config 5 keeps the rollout KV cache in OCP e4m3fn with one fp32 scale per
+# (batch row, kv head, slot): absmax / 448 of the rotated head row. K rows are stored
+# k-permuted so that one lane of the MFMA decode kernel reads its four 8-element K chunks as 32
+# contiguous bytes: element d = 32 s + 8 g + e lives at byte 32 g + 8 s + e (D = 128). V rows are
+# stored in order. Half the cache bytes of bf16: the decode attention of the 13B MHA model is a
+# pure K/V stream (csrc/kernels/attention.hip, attn_decode_mfma_kernel<KV8>).
+FP8_KV_D = 128
+
+
+def fp8_kv_perm(D: int = FP8_KV_D) -> torch.Tensor:
+    """byte position of element d in a stored K row."""
+    d = torch.arange(D)
+    return 32 * ((d % 32) // 8) + 8 * (d // 32) + d % 8
+
+
+def kv_quantize_rows(x: torch.Tensor, permute: bool):
+    """[..., D] -> (e4m3fn bytes [..., D] (k-permuted if ``permute``), fp32 scales [...]) — the
+    same rounding as the kernels (scale = amax / 448, x / scale rounded to nearest even)."""
+    xf = x.float()
+    amax = xf.abs().amax(-1)
+    sc = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    q = (xf * (1.0 / sc)[..., None]).to(torch.float8_e4m3fn).view(torch.uint8)
+    if permute:
+        out = torch.empty_like(q)
+        out[..., fp8_kv_perm(x.shape[-1]).to(q.device)] = q
+        q = out
+    return q, sc
+
+
+def kv_dequantize(q: torch.Tensor, sc: torch.Tensor, permute: bool) -> torch.Tensor:
+    """inverse of ``kv_quantize_rows`` -> fp32 [..., D]"""
+    if permute:
+        q = q[..., fp8_kv_perm(q.shape[-1]).to(q.device)]
+    return q.view(torch.float8_e4m3fn).float() * sc[..., None]
+
+
+def kv_store_fp8(qkv: torch.Tensor, k_cache, v_cache, k_scale, v_scale, B: int, S: int, Hq: int):
+    """rotated prompt rows qkv [B*S, ...] -> fp8 cache slots [0, S) of [B, Hkv, Smax, D] (+ scales)."""
+    _, Hkv, Smax, D = k_cache.shape
+    if on_gpu(qkv):
+        native().kv_store_fp8(qkv, k_cache, v_cache, k_scale, v_scale, B, S, Hq)
+        return
+    k = qkv[:, Hq * D:(Hq + Hkv) * D].reshape(B, S, Hkv, D).transpose(1, 2)
+    v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(B, S, Hkv, D).transpose(1, 2)
+    kq, ks = kv_quantize_rows(k, True)
+    vq, vs = kv_quantize_rows(v, False)
+    k_cache[:, :, :S] = kq
+    v_cache[:, :, :S] = vq
+    k_scale[:, :, :S] = ks
+    v_scale[:, :, :S] = vs
+
+
+def _decode_step_fp8kv_cpu(qkv, k_cache, v_cache, k_scale, v_scale, slot, attn_len, Hq, pos, cos, sin, kv_start,
+                           window, scale, out, sign):
+    B, Hkv, Smax, D = k_cache.shape
+    q = rope_qkv_(qkv.clone(), pos, cos, sin, Hq, Hkv, D, S=1, sign=sign)
+    kq, ks = kv_quantize_rows(q[:, Hq * D:(Hq + Hkv) * D].reshape(B, Hkv, D), True)
+    vq, vs = kv_quantize_rows(q[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(B, Hkv, D), False)
+    for b in range(B):
+        s = int(slot[b])
+        k_cache[b, :, s], v_cache[b, :, s] = kq[b], vq[b]
+        k_scale[b, :, s], v_scale[b, :, s] = ks[b], vs[b]
+    kd = kv_dequantize(k_cache, k_scale[..., :Smax], True).to(qkv.dtype)
+    vd = kv_dequantize(v_cache, v_scale[..., :Smax], False).to(qkv.dtype)
+    return decode_attention(q, kd, vd, attn_len, Hq, kv_start, window, scale, out=out)
+
+
 def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, cos=None, sin=None, kv_start=None,
-                          window=0, scale=None, workspace=None, out=None, sign: float = 1.0):
+                          window=0, scale=None, workspace=None, out=None, sign: float = 1.0, k_scale=None,
+                          v_scale=None):
     """One decode step of a layer, fused: rotate q / k_new (if ``cos`` is given), append k_new and
     v_new at cache slot ``slot[b]``, attend over ``attn_len[b]`` keys -> [B, Hq*D].
-    ``qkv`` [B, (Hq + 2 Hkv) D] is left unrotated (the fused kernel rotates in registers)."""
+    ``qkv`` [B, (Hq + 2 Hkv) D] is left unrotated (the fused kernel rotates in registers).
+    ``k_scale`` / ``v_scale`` [B, Hkv, SmaxP]: the caches are fp8 (uint8) — see ``kv_store_fp8``."""
     from .linear import SplitK
 
     B, Hkv, Smax, D = k_cache.shape
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    fp8kv = k_scale is not None
     if isinstance(qkv, SplitK):
         # the qkv GEMM's split-K partials: summed in the MFMA kernel's prologue when it applies
         if workspace is None or len(workspace) < 3:
             workspace = decode_workspace(B, Hq, Hkv, D, Smax, k_cache.device)
         if out is None:
             out = torch.empty(B, Hq * D, dtype=qkv.dtype, device=qkv.device)
+        if fp8kv:
+            native().attn_decode_set_fp8kv(k_scale, v_scale)
         if native().attn_decode_fused_slabs(qkv.slabs, qkv.nsplit, k_cache, v_cache, slot, attn_len, kv_start, pos,
                                             cos, sin, sign, window, scale, Hq, workspace[0], workspace[2],
                                             workspace[1], out):
             return out
         qkv = qkv.reduce()
     if not on_gpu(qkv):
+        if fp8kv:
+            return _decode_step_fp8kv_cpu(qkv, k_cache, v_cache, k_scale, v_scale, slot, attn_len, Hq, pos, cos, sin,
+                                          kv_start, window, scale, out, sign)
         q = rope_qkv_(qkv.clone(), pos, cos, sin, Hq, Hkv, D, S=1, k_cache=k_cache, v_cache=v_cache,
                       slot_base=slot, sign=sign)
         return decode_attention(q, k_cache, v_cache, attn_len, Hq, kv_start, window, scale, out=out)
@@ -284,6 +360,8 @@ def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, c
     part, PS, tickets = workspace[0], workspace[1], workspace[2]
     if out is None:
         out = torch.empty(B, Hq * D, dtype=qkv.dtype, device=qkv.device)
+    if fp8kv:
+        native().attn_decode_set_fp8kv(k_scale, v_scale)
     native().attn_decode_fused(qkv, k_cache, v_cache, slot, attn_len, kv_start, pos, cos, sin, sign, window, scale,
                                Hq, part, tickets, PS, out)
     return out

@@ -921,3 +921,95 @@ def test_gemm_fp8_decode_w8a16(M, N, K, mode):
         if res is not None:
             y3 = y3 + res.float()
         _close(out2, y3)
+
+
+# ------------------------------------------------------------------ fp8 K/V cache (config 5)
+def test_kv_store_fp8_matches_cpu_reference():
+    torch.manual_seed(11)
+    B, S, Hq, Hkv, D, Smax = 3, 37, 8, 4, 128, 50
+    W = (Hq + 2 * Hkv) * D
+    qkv = (torch.randn(B * S, W, device=DEV) * torch.logspace(-2, 1, B * S, device=DEV)[:, None]).to(torch.bfloat16)
+    kc = torch.zeros(B, Hkv, Smax, D, device=DEV, dtype=torch.uint8)
+    vc = torch.zeros_like(kc)
+    ks = torch.zeros(B, Hkv, 64, device=DEV)
+    vs = torch.zeros_like(ks)
+    ops.kv_store_fp8(qkv, kc, vc, ks, vs, B, S, Hq)
+    kc2, vc2, ks2, vs2 = kc.cpu().zero_(), vc.cpu().zero_(), ks.cpu().zero_(), vs.cpu().zero_()
+    ops.kv_store_fp8(qkv.cpu(), kc2, vc2, ks2, vs2, B, S, Hq)
+    torch.testing.assert_close(ks.cpu(), ks2, rtol=1e-6, atol=0)
+    torch.testing.assert_close(vs.cpu(), vs2, rtol=1e-6, atol=0)
+    for a, b in ((kc.cpu(), kc2), (vc.cpu(), vc2)):
+        diff = a != b
+        assert diff.float().mean().item() < 5e-3  # reciprocal-scale rounding boundary cases only
+        assert ((a.int() - b.int()).abs()[diff] <= 1).all()
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,Smax,window", [(64, 40, 40, 456, 0),   # Llama-2-13B rollout: MFMA, G = 1
+                                                  (40, 32, 8, 300, 64),   # MFMA, G = 4, sliding window
+                                                  (1, 40, 40, 456, 0),    # batch-1 8-wave kernel
+                                                  (3, 16, 8, 300, 0),     # 8-wave, G = 2
+                                                  (2, 32, 8, 1500, 0)])   # 8-wave over key partitions
+def test_decode_step_fused_fp8kv(B, Hq, Hkv, Smax, window):
+    """fp8 cache decode step (RoPE + quantised append + attention over e4m3 K/V with per-slot
+    scales) == fp32 attention over the dequantised cache, and the appended bytes / scales equal the
+    reference quantisation of the rotated k_new / v_new."""
+    torch.manual_seed(B + Smax)
+    D = 128
+    W = (Hq + 2 * Hkv) * D
+    S = Smax - 40
+    smaxp = (Smax + 15) // 16 * 16
+    prompt = torch.randn(B * S, W, device=DEV, dtype=torch.bfloat16)
+    kc = torch.zeros(B, Hkv, Smax, D, device=DEV, dtype=torch.uint8)
+    vc = torch.zeros_like(kc)
+    ks = torch.zeros(B, Hkv, smaxp, device=DEV)
+    vs = torch.zeros_like(ks)
+    ops.kv_store_fp8(prompt, kc, vc, ks, vs, B, S, Hq)
+    kv_start = torch.randint(0, 8, (B,), device=DEV, dtype=torch.int32)
+    slot = torch.randint(S, Smax - 4, (B,), device=DEV, dtype=torch.int32)
+    attn_len = slot + 1
+    pos = (slot - kv_start).to(torch.int32)
+    cos, sin = ref.rope_tables(D, 4096, 10000.0, DEV)
+    ws = ops.decode_workspace(B, Hq, Hkv, D, Smax, DEV)
+    for it in range(2):
+        qkv = torch.randn(B, W, device=DEV, dtype=torch.bfloat16)
+        out = ops.decode_step_attention(qkv, kc, vc, slot, attn_len, Hq, pos, cos, sin, kv_start, window,
+                                        workspace=ws, k_scale=ks, v_scale=vs)
+        q = ops.rope_qkv_(qkv.clone(), pos, cos, sin, Hq, Hkv, D, S=1)
+        kq, ksn = ops.kv_quantize_rows(q[:, Hq * D:(Hq + Hkv) * D].reshape(B, Hkv, D), True)
+        vq, vsn = ops.kv_quantize_rows(q[:, (Hq + Hkv) * D:].reshape(B, Hkv, D), False)
+        bi = torch.arange(B, device=DEV)
+        torch.testing.assert_close(ks[bi, :, slot.long()], ksn, rtol=1e-6, atol=0)
+        torch.testing.assert_close(vs[bi, :, slot.long()], vsn, rtol=1e-6, atol=0)
+        assert (kc[bi, :, slot.long()].int() - kq.int()).abs().max().item() <= 1
+        assert (vc[bi, :, slot.long()].int() - vq.int()).abs().max().item() <= 1
+        kd = ops.kv_dequantize(kc, ks[..., :Smax], True)
+        vd = ops.kv_dequantize(vc, vs[..., :Smax], False)
+        o_ref = ref.decode_attention(q.float(), kd, vd, attn_len, Hq, kv_start, window, 1.0 / math.sqrt(D))
+        assert torch.isfinite(out).all()
+        _close(out, o_ref)
+    assert int(ws.tickets.abs().sum()) == 0
+
+
+def test_generation_fp8kv_matches_teacher_forcing():
+    """Generation on an fp8 K/V cache: the behaviour log-probs stay close to a full-precision
+    teacher-forced rescoring of the same tokens (head_dim 128 model)."""
+    import dataclasses
+
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
+    from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
+    from rag_tl_domainllm_optimizer_amd.train.common import score_sequences
+
+    cfg = dataclasses.replace(PRESETS["tiny-llama"], hidden_size=512, num_heads=4, num_kv_heads=2, head_dim=128,
+                              intermediate_size=1024, name="tiny-llama-d128")
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=4)
+    prompts = [[5, 9, 33, 41, 7, 8, 9, 10], [12, 300, 4], list(range(20, 90))]
+    p = SamplingParams(max_new_tokens=16, temperature=0.7, top_k=0, seed=5)
+    gen = Generator(m, 3, 128, DEV, kv_fp8=True)
+    assert gen.cache.fp8 and gen.cache.k.dtype == torch.uint8
+    out = gen.generate(prompts, p, pad_id=0, eos_ids=[-1])
+    with torch.no_grad():
+        lp, _, _, _ = score_sequences(m, out.prompt_ids, out.prompt_start, out.tokens, out.lengths, 1 / 0.7)
+    d = (lp - out.logprobs).abs()
+    assert torch.isfinite(out.logprobs).all()
+    assert d.mean().item() < 0.1 and d.max().item() < 0.6, (d.mean().item(), d.max().item())

@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--new", type=int, default=64)
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--no-lora", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="fp8 weight images (config 5)")
+    ap.add_argument("--fp8-kv", action="store_true", help="fp8 K/V cache (config 5)")
     ap.add_argument("--depths", default="0", help="M<=16 GEMM weight-pipeline depths to A/B (0 = auto)")
     a = ap.parse_args()
     from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
@@ -27,10 +29,12 @@ def main():
     m = build_model(a.model, device=dev, dtype=torch.bfloat16, seed=0, fast_init=True)
     if not a.no_lora:
         m.add_lora(16, 32.0, "all")
+    if a.fp8:
+        m.set_fp8(True)
     g = torch.Generator().manual_seed(0)
     prompts = [torch.randint(5, m.cfg.vocab_size, (a.prompt - (i % 7) * 3,), generator=g).tolist()
                for i in range(a.batch)]
-    gen = Generator(m, a.batch, a.prompt + a.new + 8, dev)
+    gen = Generator(m, a.batch, a.prompt + a.new + 8, dev, kv_fp8=a.fp8_kv)
     sp = SamplingParams(max_new_tokens=a.new, temperature=0.7, top_k=50)
     from rag_tl_domainllm_optimizer_amd import ops
 
