@@ -76,12 +76,16 @@ class DecoderLayer(nn.Module):
             return None
         return self._fp8.setdefault(name, ops.Fp8Cache())
 
-    def _shuf(self, name, m: int):
-        """ShufCache of a decode projection at batch ``m`` <= 16 (bf16 weights; fp8 streams its
-        own e4m3 image)."""
-        if not shuffle_enabled(m) or self.fp8_enabled:
-            return None
-        return self._shufc.setdefault(name, ops.ShufCache())
+    def _dec_caches(self, f8name: str, shufname: str, w: torch.Tensor, m: int):
+        """(Fp8Cache, ShufCache) for one decode projection at batch ``m``: the fp8 image except
+        where the bf16 GEMV is faster — 2 <= m <= 16 on projections of <= 2^24 weights (Mistral
+        o_proj), where the fp8 16-row GEMV reads twice its weight bytes of activations per row
+        group (profiles/r3/fp8_decode_table_v6.log: o 8.1-8.8 us bf16 vs 10.1-10.9 us fp8)."""
+        if self.fp8_enabled and not (2 <= m <= 16 and w.numel() <= (1 << 24)):
+            return self._f8(f8name), None
+        if not shuffle_enabled(m):
+            return None, None
+        return None, self._shufc.setdefault(shufname, ops.ShufCache())
 
     # ---------------------------------------------------------------- fused decode step (M <= 64)
     def _w_eff(self, wname: str, gname: str):
@@ -119,17 +123,20 @@ class DecoderLayer(nn.Module):
         eps = cfg.norm_eps
         m = h.shape[0]
         wq = self._fold.setdefault("qkv", ops.FoldCache()).get(self._w_eff("qkv_w", "qkv"), self.ln1_w)
-        qkv = ops.gemm_decode(h, wq, norm_eps=eps, fp8=self._f8("qkv_folded"), shuf=self._shuf("qkv", m))
+        f8, sh = self._dec_caches("qkv_folded", "qkv", wq, m)
+        qkv = ops.gemm_decode(h, wq, norm_eps=eps, fp8=f8, shuf=sh)
         wo = self._w_eff("o_w", "o")
-        h_new = attend_o(qkv, wo, h) if (attend_o is not None and self._f8("o") is None) else None
+        f8, sh = self._dec_caches("o", "o", wo, m)
+        h_new = attend_o(qkv, wo, h) if (attend_o is not None and f8 is None) else None
         if h_new is None:
-            h_new = ops.gemm_decode(attend(qkv), wo, residual=h, fp8=self._f8("o"), shuf=self._shuf("o", m))
+            h_new = ops.gemm_decode(attend(qkv), wo, residual=h, fp8=f8, shuf=sh)
         h = h_new
         wgu = self._fold.setdefault("gate_up", ops.FoldCache()).get(self._w_eff("gate_up_w", "gate_up"), self.ln2_w)
-        f = ops.gemm_decode(h, wgu, act=ops.ACT_SWIGLU, norm_eps=eps, fp8=self._f8("gate_up_folded"),
-                            shuf=self._shuf("gate_up", m))
-        return ops.gemm_decode(f, self._w_eff("down_w", "down"), residual=h, fp8=self._f8("down"),
-                               shuf=self._shuf("down", m))
+        f8, sh = self._dec_caches("gate_up_folded", "gate_up", wgu, m)
+        f = ops.gemm_decode(h, wgu, act=ops.ACT_SWIGLU, norm_eps=eps, fp8=f8, shuf=sh)
+        wd = self._w_eff("down_w", "down")
+        f8, sh = self._dec_caches("down", "down", wd, m)
+        return ops.gemm_decode(f, wd, residual=h, fp8=f8, shuf=sh)
 
     def attn_in(self, x, residual, defer: bool = False):
         """``defer`` (no-grad decode, batch > 64): the qkv GEMM may return unreduced split-K
