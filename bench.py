@@ -71,7 +71,10 @@ def main():
                          "packed forwards; RAGTL_PACK=0 for the padded comparison)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--mode", default="ppo", choices=["ppo", "sft", "pipeline"])
+    ap.add_argument("--mode", default="ppo", choices=["ppo", "sft", "pipeline", "serve"])
+    ap.add_argument("--serve-concurrency", default="1,4,16",
+                    help="--mode serve: closed-loop client counts (one engine, max batch = the largest)")
+    ap.add_argument("--serve-requests", type=int, default=64, help="--mode serve: answers per concurrency level")
     ap.add_argument("--fp8", action=argparse.BooleanOptionalAction, default=None,
                     help="fp8 (e4m3fn) weights for no-grad forwards (default: on for --mode pipeline, config 5)")
     ap.add_argument("--fp8-kv", action=argparse.BooleanOptionalAction, default=None,
@@ -135,6 +138,8 @@ def main():
 
     if args.mode in ("sft", "pipeline"):
         return run_sft_pipeline(args, di, policy, tok, encoder, corpus, index)
+    if args.mode == "serve":
+        return run_serve(args, di, policy, tok, encoder, corpus, index)
 
     # ---- PPO trainer ----
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
@@ -288,6 +293,67 @@ def _timed(di, fn, steps):
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=di.device)
     parallel.all_reduce_(el, "max")
     return float(el), out
+
+
+def run_serve(args, di, policy, tok, encoder, corpus, index):
+    """RAG answer serving with dynamic request batching (serve.BatchingEngine): closed-loop clients
+    at each concurrency level; answers/s, generated tokens/s and per-request latency percentiles."""
+    import threading
+
+    import numpy as np
+
+    from rag_tl_domainllm_optimizer_amd import parallel
+    from rag_tl_domainllm_optimizer_amd.generation import SamplingParams
+    from rag_tl_domainllm_optimizer_amd.rag import RagPipeline
+    from rag_tl_domainllm_optimizer_amd.serve import BatchingEngine
+
+    levels = [int(c) for c in args.serve_concurrency.split(",") if c]
+    if args.fp8:
+        policy.set_fp8(True)
+    policy.kv_fp8 = bool(args.fp8_kv)
+    rag = RagPipeline(encoder, index, corpus.docs, policy, tok, top_k=args.top_k_docs,
+                      sampling=SamplingParams(max_new_tokens=args.new_tokens, temperature=0.7, top_k=50),
+                      max_prompt_tokens=args.max_prompt, max_batch=max(levels), use_graph=not args.no_graph)
+    qs = [it.query for it in corpus.sample_queries(args.serve_requests * len(levels) + 32, seed=17)]
+    rows = []
+    with BatchingEngine(rag, max_wait_s=0.004) as eng:
+        eng.answer_many(qs[:32])  # warm-up: graph capture at the batch sizes the levels produce
+        for li, c in enumerate(levels):
+            mine = qs[32 + li * args.serve_requests: 32 + (li + 1) * args.serve_requests]
+            lat, ntok, bsz = [], [], []
+            lock = threading.Lock()
+
+            def client(part):
+                for q in part:
+                    a = eng.answer(q, timeout=600)
+                    with lock:
+                        lat.append(a.timings["total_s"])
+                        ntok.append(a.timings["new_tokens"])
+                        bsz.append(a.timings["batch_size"])
+
+            ts = [threading.Thread(target=client, args=(mine[i::c],)) for i in range(c)]
+            t0 = time.perf_counter()
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            el = time.perf_counter() - t0
+            la = np.array(lat)
+            rows.append({"concurrency": c, "answers_per_s": len(lat) / el, "tokens_per_s": float(sum(ntok)) / el,
+                         "p50_latency_s": float(np.percentile(la, 50)), "p90_latency_s": float(np.percentile(la, 90)),
+                         "mean_batch": float(np.mean(bsz)), "requests": len(lat)})
+            log(f"[bench] serve c={c}: {rows[-1]['answers_per_s']:.2f} answers/s {rows[-1]['tokens_per_s']:.0f} tok/s "
+                f"p50 {rows[-1]['p50_latency_s']:.3f}s p90 {rows[-1]['p90_latency_s']:.3f}s batch {rows[-1]['mean_batch']:.1f}")
+    best = max(rows, key=lambda r: r["tokens_per_s"])
+    res = {"metric": "RAG answer serving tokens/sec (dynamic batching), " + args.model, "value": best["tokens_per_s"],
+           "unit": "tokens/s", "n_gpus": di.world, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "fp8-e4m3fn" if args.fp8 else "bf16", "data": "synthetic (random-init weights, synthetic corpus)",
+           "config": {"model": args.model, "new_tokens": args.new_tokens, "index": f"ivf{args.nlist}/nprobe{args.nprobe}",
+                      "top_k_docs": args.top_k_docs, "max_batch": max(levels)},
+           "levels": rows}
+    if di.is_main:
+        print(json.dumps(res), flush=True)
+    parallel.shutdown()
 
 
 def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):

@@ -56,13 +56,18 @@ class RagPipeline:
         return encode_prompt(self.tok, query, docs, self.max_prompt_tokens)
 
     @torch.no_grad()
-    def answer(self, queries: Sequence[str]) -> List[RagAnswer]:
+    def answer(self, queries: Sequence[str], top_ks: Optional[Sequence[Optional[int]]] = None) -> List[RagAnswer]:
+        """Answers in batches of ``max_batch`` (one retrieval, one prefill, one graph-replayed
+        decode per batch). ``top_ks``: per-query document counts (None = the pipeline's top_k):
+        the batch retrieves the largest and each row keeps its own prefix."""
         out: List[RagAnswer] = []
         for s in range(0, len(queries), self.max_batch):
             qs = list(queries[s:s + self.max_batch])
+            ks = [(k or self.top_k) for k in (top_ks[s:s + self.max_batch] if top_ks else [None] * len(qs))]
             t0 = time.perf_counter()
-            scores, ids = self.retrieve(qs)
-            ids_l = ids.tolist()
+            scores, ids = self.retrieve(qs, max(ks))
+            ids_l = [row[:k] for row, k in zip(ids.tolist(), ks)]
+            scores = [row[:k] for row, k in zip(scores.tolist(), ks)]
             self._sync()
             t1 = time.perf_counter()
             docs = [[self.docs[i] for i in row if i >= 0] for row in ids_l]
@@ -75,7 +80,7 @@ class RagPipeline:
                 n = int(g.lengths[b])
                 text = extract_answer(self.tok.decode(g.tokens[b, :n].tolist()))
                 t4 = time.perf_counter()
-                out.append(RagAnswer(q, text, ids_l[b], docs[b], scores[b].tolist(),
+                out.append(RagAnswer(q, text, ids_l[b], docs[b], scores[b],
                                      {"retrieve_s": t1 - t0, "prompt_s": t2 - t1, "generate_s": t3 - t2,
                                       "prefill_s": g.timings.get("prefill_s", 0.0),
                                       "decode_s": g.timings.get("decode_s", 0.0),

@@ -1,15 +1,25 @@
-"""Minimal HTTP answer service (the README's optional frontend, README.md:9,31: Streamlit / Gradio
-are not installed; FastAPI + uvicorn are). POST /answer {"query": "...", "top_k": 3} ->
-{"answer", "doc_ids", "docs", "scores", "timings"}; GET /health."""
+"""HTTP answer service (the README's optional frontend, README.md:9,31: Streamlit / Gradio are not
+installed; FastAPI + uvicorn are). POST /answer {"query": "...", "top_k": 3} ->
+{"answer", "doc_ids", "docs", "scores", "timings"}; GET /health; GET /stats.
+
+Concurrent requests are batched dynamically (``serve.batching.BatchingEngine``): the async handler
+awaits a future while one worker thread answers up to ``max_batch`` queued queries per batched
+retrieve + prefill + graph-replayed decode."""
 
 from typing import Optional
 
+from .batching import BatchingEngine  # noqa: F401
 
-def create_app(pipeline):
+
+def create_app(pipeline, max_wait_s: float = 0.004):
+    import asyncio
+
     from fastapi import FastAPI
     from pydantic import BaseModel
 
+    engine = BatchingEngine(pipeline, max_wait_s=max_wait_s)
     app = FastAPI(title="rag-tl-domainllm-optimizer-amd")
+    app.state.engine = engine
 
     class Query(BaseModel):
         query: str
@@ -17,19 +27,25 @@ def create_app(pipeline):
 
     @app.get("/health")
     def health():
-        return {"status": "ok", "docs": len(pipeline.docs)}
+        return {"status": "ok", "docs": len(pipeline.docs), "max_batch": engine.max_batch}
+
+    @app.get("/stats")
+    def stats():
+        return dict(engine.stats)
 
     @app.post("/answer")
-    def answer(q: Query):
-        if q.top_k:
-            pipeline.top_k = q.top_k
-        a = pipeline.answer([q.query])[0]
+    async def answer(q: Query):
+        a = await asyncio.wrap_future(engine.submit(q.query, q.top_k))
         return {"answer": a.answer, "doc_ids": a.doc_ids, "docs": a.docs, "scores": a.scores, "timings": a.timings}
+
+    @app.on_event("shutdown")
+    def _shutdown():
+        engine.close()
 
     return app
 
 
-def serve(cfg, host: str = "127.0.0.1", port: int = 8000):
+def serve(cfg, host: str = "127.0.0.1", port: int = 8000, max_batch: int = 16, max_wait_s: float = 0.004):
     import uvicorn
 
     from ..cli import build_stack
@@ -42,5 +58,5 @@ def serve(cfg, host: str = "127.0.0.1", port: int = 8000):
     sp = SamplingParams(max_new_tokens=cfg.ppo.max_new_tokens, temperature=cfg.eval.temperature,
                         do_sample=cfg.eval.do_sample, top_k=cfg.eval.top_k)
     rag = RagPipeline(st["encoder"], st["index"], st["docs"], st["policy"], st["tokenizer"], cfg.retrieval.top_k, sp,
-                      cfg.ppo.max_prompt_tokens)
-    uvicorn.run(create_app(rag), host=host, port=port)
+                      cfg.ppo.max_prompt_tokens, max_batch=max_batch)
+    uvicorn.run(create_app(rag, max_wait_s), host=host, port=port)

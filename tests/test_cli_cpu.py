@@ -58,8 +58,9 @@ def test_serve_app():
     class FakePipe:
         docs = ["a", "b"]
         top_k = 2
+        max_batch = 4
 
-        def answer(self, qs):
+        def answer(self, qs, top_ks=None):
             from rag_tl_domainllm_optimizer_amd.rag import RagAnswer
 
             return [RagAnswer(q, "ans", [0], ["a"], [1.0], {"total_s": 0.1}) for q in qs]
@@ -68,6 +69,7 @@ def test_serve_app():
     assert c.get("/health").json()["docs"] == 2
     r = c.post("/answer", json={"query": "q"}).json()
     assert r["answer"] == "ans" and r["doc_ids"] == [0]
+    assert r["timings"]["batch_size"] == 1 and c.get("/stats").json()["requests"] == 1
 
 
 def test_cli_ppo_resume_from_latest(tmp_path, capsys):

@@ -1,0 +1,103 @@
+"""Dynamic request batching in front of the RAG pipeline (serve.batching.BatchingEngine)."""
+import threading
+import time
+
+import pytest
+import torch
+
+from rag_tl_domainllm_optimizer_amd.rag import RagAnswer
+from rag_tl_domainllm_optimizer_amd.serve.batching import BatchingEngine
+
+
+class RecordingPipe:
+    """Stands in for RagPipeline: records every batch, answers "<query>|k=<top_k>"."""
+    docs = ["d0", "d1", "d2"]
+    top_k = 2
+
+    def __init__(self, max_batch=8, delay=0.02, fail_on=None):
+        self.max_batch, self.delay, self.fail_on = max_batch, delay, fail_on
+        self.batches = []
+
+    def answer(self, qs, top_ks=None):
+        self.batches.append(list(qs))
+        time.sleep(self.delay)
+        if self.fail_on and self.fail_on in qs:
+            raise ValueError("boom")
+        ks = top_ks or [None] * len(qs)
+        return [RagAnswer(q, f"{q}|k={k or self.top_k}", [0], ["d0"], [1.0], {"total_s": self.delay})
+                for q, k in zip(qs, ks)]
+
+
+def test_concurrent_requests_are_batched_and_routed():
+    pipe = RecordingPipe(max_batch=8, delay=0.05)
+    with BatchingEngine(pipe, max_wait_s=0.02) as eng:
+        res = {}
+
+        def client(i):
+            res[i] = eng.answer(f"q{i}", top_k=(i % 3) or None, timeout=10)
+
+        ts = [threading.Thread(target=client, args=(i,)) for i in range(20)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert sorted(res) == list(range(20))
+    for i, a in res.items():  # every caller gets its own answer, with its own top_k
+        assert a.query == f"q{i}" and a.answer == f"q{i}|k={(i % 3) or 2}"
+        assert a.timings["queue_s"] >= 0 and 1 <= a.timings["batch_size"] <= 8
+    assert all(len(b) <= 8 for b in pipe.batches)
+    assert len(pipe.batches) < 20  # 20 concurrent requests did not run one by one
+    assert eng.stats["requests"] == 20 and eng.stats["max_batch_seen"] > 1
+
+
+def test_batch_error_reaches_every_caller_and_engine_survives():
+    pipe = RecordingPipe(max_batch=4, delay=0.0, fail_on="bad")
+    with BatchingEngine(pipe, max_wait_s=0.05) as eng:
+        f1, f2 = eng.submit("bad"), eng.submit("ok1")
+        for f in (f1, f2):
+            with pytest.raises(ValueError):
+                f.result(10)
+        assert eng.answer("ok2", timeout=10).answer == "ok2|k=2"
+
+
+def test_close_fails_queued_requests_and_rejects_new_ones():
+    pipe = RecordingPipe(max_batch=1, delay=0.2)
+    eng = BatchingEngine(pipe, max_wait_s=0.0)
+    futs = [eng.submit(f"q{i}") for i in range(4)]
+    time.sleep(0.05)
+    eng.close()
+    done = [f for f in futs if f.done() and f.exception() is None]
+    assert len(done) >= 1  # the running batch finished
+    for f in futs:
+        assert f.done()
+    with pytest.raises(RuntimeError):
+        eng.submit("late")
+
+
+def test_engine_over_real_pipeline_cpu():
+    """Tiny models on the CPU: answers through the engine equal a direct batched call."""
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.generation import SamplingParams
+    from rag_tl_domainllm_optimizer_amd.rag import RagPipeline
+    from rag_tl_domainllm_optimizer_amd.retrieval import Encoder, FlatIndex
+    from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
+
+    torch.manual_seed(0)
+    pol = models.CausalLM(models.resolve_preset("tiny-llama"), device="cpu", dtype=torch.float32, seed=1)
+    enc_m = models.build_model("tiny-bert", device="cpu", dtype=torch.float32, seed=2).eval()
+    tok = Tokenizer.synthetic(pol.cfg.vocab_size, pol.cfg.arch)
+    enc = Encoder(enc_m, Tokenizer.synthetic(enc_m.cfg.vocab_size, enc_m.cfg.arch), max_length=32)
+    words = tok.words()
+    docs = [" ".join(words[(7 * i + j) % len(words)] for j in range(12)) for i in range(30)]
+    index = FlatIndex(enc.dim, "ip", "cpu")
+    index.add(enc.encode(docs))
+    pipe = RagPipeline(enc, index, docs, pol, tok, top_k=2,
+                       sampling=SamplingParams(max_new_tokens=4, do_sample=False), max_prompt_tokens=96,
+                       max_batch=4, use_graph=False)
+    qs = [f"{words[i]} {words[i + 3]}" for i in range(4)]
+    direct = pipe.answer(qs)
+    with BatchingEngine(pipe, max_wait_s=0.2) as eng:
+        futs = [eng.submit(q) for q in qs]
+        got = [f.result(60) for f in futs]
+    assert [a.answer for a in got] == [a.answer for a in direct]
+    assert [a.doc_ids for a in got] == [a.doc_ids for a in direct]
