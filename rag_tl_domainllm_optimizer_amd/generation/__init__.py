@@ -52,6 +52,43 @@ class GenerationOutput:
     timings: dict = field(default_factory=dict)
 
 
+class _GraphSet:
+    """Captured decode steps by key (sampling parameters, output width, row bucket): replaying a
+    generator at another batch bucket switches graphs instead of recapturing. Least recently used
+    graphs beyond ``max_graphs`` are dropped; ``reset()`` drops all (e.g. when the output buffers
+    they captured are reallocated). Same interface as ``runtime.GraphRunner``."""
+
+    def __init__(self, max_graphs: int = 8):
+        from collections import OrderedDict
+
+        self.graphs = OrderedDict()
+        self.cur = None
+        self.max_graphs = max_graphs
+
+    def needs(self, key) -> bool:
+        r = self.graphs.get(key)
+        if r is None:
+            return True
+        self.graphs.move_to_end(key)
+        self.cur = r
+        return False
+
+    def capture(self, fn, key=None, keep=(), restore=()):
+        r = GraphRunner()
+        r.capture(fn, key, keep, restore)
+        self.graphs[key] = r
+        self.cur = r
+        while len(self.graphs) > self.max_graphs:
+            self.graphs.popitem(last=False)
+
+    def replay(self):
+        self.cur.replay()
+
+    def reset(self):
+        self.graphs.clear()
+        self.cur = None
+
+
 class KVCache:
     """Static K/V cache [L, B, Hkv, Smax, D]. ``fp8``: e4m3fn bytes (K rows k-permuted) plus one
     fp32 scale per (layer, row, kv head, slot) in ``ks`` / ``vs`` [L, B, Hkv, SmaxP] (SmaxP = Smax
@@ -121,28 +158,41 @@ class Generator:
         self.sampled_lp = torch.zeros(B, dtype=torch.float32, device=dev)
         self.values = torch.zeros(B, dtype=torch.float32, device=dev)
         self.out_tokens = None
-        self.runner = GraphRunner()  # captured decode step (runtime.GraphRunner, shared graph pool)
+        self.runner = _GraphSet()  # captured decode steps (runtime.GraphRunner each, shared graph pool)
 
     # ------------------------------------------------------------------ one decode step (device only)
+    def _bucket(self, B: int) -> int:
+        """Rows a decode step runs for a batch of B: the next power of two (capped at max_batch).
+        A serving generator sized for 16 or 64 users then decodes one answer at the batch-1 cost;
+        each bucket has its own captured graph (the rows past B stay inactive)."""
+        nb = 1
+        while nb < B:
+            nb *= 2
+        return min(nb, self.max_batch)
+
     def _step(self, params: SamplingParams, eos_ids: torch.Tensor, pad_id: int):
         # attn_len = kv_len + 1 and pos = kv_len - kv_start were set by the previous bookkeeping
         # (decode_update on the GPU, _update_cpu on the CPU) — no elementwise launches here
-        h = self.model.decode(self.tok_in, self.pos, self.kv_len, self.attn_len, self.kv_start, self.cache,
-                              self.workspace)
+        nb = self._nb
+        cache = self.cache if nb == self.max_batch else _SubCache(self.cache, nb)
+        h = self.model.decode(self.tok_in[:nb], self.pos[:nb], self.kv_len[:nb], self.attn_len[:nb],
+                              self.kv_start[:nb], cache, self.workspace)
         self._emit(h, params, eos_ids, pad_id)
 
     def _emit(self, h, params: SamplingParams, eos_ids, pad_id):
+        nb = h.shape[0]  # the step's row bucket (first nb rows of every state tensor)
         logits = self.model.logits(h)
         ops.sample(logits, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed,
-                   self.rng_offset, self.active, self.sampled, self.sampled_lp)
+                   self.rng_offset, self.active[:nb], self.sampled[:nb], self.sampled_lp[:nb])
         if self.value_head is not None:
-            self.values.copy_(self.value_head(h))
+            self.values[:nb].copy_(self.value_head(h))
         if h.is_cuda:
-            ops.native().decode_update(self.sampled, self.out_tokens, self.out_logp, self.sampled_lp,
-                                       self.out_values if self.value_head is not None else None,
-                                       self.values if self.value_head is not None else None, self.active,
-                                       self.kv_len, self.pos, self.tok_in, self.gen_len, self.step, self.rng_offset,
-                                       eos_ids, pad_id, self.attn_len, self.kv_start)
+            vh = self.value_head is not None
+            ops.native().decode_update(self.sampled[:nb], self.out_tokens[:nb], self.out_logp[:nb],
+                                       self.sampled_lp[:nb], self.out_values[:nb] if vh else None,
+                                       self.values[:nb] if vh else None, self.active[:nb], self.kv_len[:nb],
+                                       self.pos[:nb], self.tok_in[:nb], self.gen_len[:nb], self.step,
+                                       self.rng_offset, eos_ids, pad_id, self.attn_len[:nb], self.kv_start[:nb])
         else:
             self._update_cpu(eos_ids, pad_id)
 
@@ -253,7 +303,8 @@ class Generator:
             self.model.prefill(ids, self.kv_start[:B], sub)
         if hasattr(self.model, "refresh_decode_weights"):
             self.model.refresh_decode_weights()  # merged / folded / fp8 images used by graph replays
-        h = torch.zeros(MB, cfg.hidden_size, dtype=h_last.dtype, device=dev)
+        self._nb = self._bucket(B)
+        h = torch.zeros(self._nb, cfg.hidden_size, dtype=h_last.dtype, device=dev)
         h[:B] = h_last
         # the first sampled token is not in the cache yet: the bookkeeping kernel advances kv_len
         # to S, so the first decode step writes it at slot S
@@ -261,7 +312,8 @@ class Generator:
         self._emit(h, params, eos, pad_id)
         if ev:
             ev[1].record()
-        key = (T, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed, tuple(eos_list), pad_id)
+        key = (T, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed, tuple(eos_list), pad_id,
+               self._nb)
         steps = T - 1
         if steps > 0 and self.use_graph and self.runner.needs(key):
             # the EOS tensor is created per call: the runner keeps the captured one alive
