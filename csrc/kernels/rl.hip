@@ -109,12 +109,16 @@ __global__ void decode_update_kernel(const long* __restrict__ tok, long* __restr
   if (b < B) {
     const bool act = active[b] != 0;
     long t = tok[b];
-    if (act && s < max_new) {
-      out_tokens[(long)b * max_new + s] = t;
-      if (out_logp) out_logp[(long)b * max_new + s] = logp[b];
-      if (out_values && values) out_values[(long)b * max_new + s] = values[b];
-      gen_len[b] = (int)s + 1;
-      bool fin = (s + 1 >= max_new);
+    // the row's own output position: equal to the step counter for every active row of a static
+    // batch (rows start together and never reactivate); rows admitted mid-flight by continuous
+    // batching start at 0
+    const int sr = gen_len[b];
+    if (act && sr < max_new) {
+      out_tokens[(long)b * max_new + sr] = t;
+      if (out_logp) out_logp[(long)b * max_new + sr] = logp[b];
+      if (out_values && values) out_values[(long)b * max_new + sr] = values[b];
+      gen_len[b] = sr + 1;
+      bool fin = (sr + 1 >= max_new);
       for (int e = 0; e < n_eos; ++e) fin = fin || (t == eos_ids[e]);
       if (fin) active[b] = 0;
       kv_len[b] += 1;

@@ -179,38 +179,49 @@ class Generator:
                               self.kv_start[:nb], cache, self.workspace)
         self._emit(h, params, eos_ids, pad_id)
 
-    def _emit(self, h, params: SamplingParams, eos_ids, pad_id):
-        nb = h.shape[0]  # the step's row bucket (first nb rows of every state tensor)
+    def _emit(self, h, params: SamplingParams, eos_ids, pad_id, r0: int = 0):
+        """Sample from the hidden states of rows [r0, r0 + len(h)) and run the bookkeeping for them
+        (the decode step's row bucket, or one row admitted by continuous batching)."""
+        r1 = r0 + h.shape[0]
         logits = self.model.logits(h)
         ops.sample(logits, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed,
-                   self.rng_offset, self.active[:nb], self.sampled[:nb], self.sampled_lp[:nb])
+                   self.rng_offset, self.active[r0:r1], self.sampled[r0:r1], self.sampled_lp[r0:r1])
         if self.value_head is not None:
-            self.values[:nb].copy_(self.value_head(h))
+            self.values[r0:r1].copy_(self.value_head(h))
         if h.is_cuda:
             vh = self.value_head is not None
-            ops.native().decode_update(self.sampled[:nb], self.out_tokens[:nb], self.out_logp[:nb],
-                                       self.sampled_lp[:nb], self.out_values[:nb] if vh else None,
-                                       self.values[:nb] if vh else None, self.active[:nb], self.kv_len[:nb],
-                                       self.pos[:nb], self.tok_in[:nb], self.gen_len[:nb], self.step,
-                                       self.rng_offset, eos_ids, pad_id, self.attn_len[:nb], self.kv_start[:nb])
+            ops.native().decode_update(self.sampled[r0:r1], self.out_tokens[r0:r1], self.out_logp[r0:r1],
+                                       self.sampled_lp[r0:r1], self.out_values[r0:r1] if vh else None,
+                                       self.values[r0:r1] if vh else None, self.active[r0:r1],
+                                       self.kv_len[r0:r1], self.pos[r0:r1], self.tok_in[r0:r1],
+                                       self.gen_len[r0:r1], self.step, self.rng_offset, eos_ids, pad_id,
+                                       self.attn_len[r0:r1], self.kv_start[r0:r1])
         else:
-            self._update_cpu(eos_ids, pad_id)
+            self._update_cpu(eos_ids, pad_id, r0, r1)
 
-    def _update_cpu(self, eos_ids, pad_id):
-        s = int(self.step.item())
+    def _update_cpu(self, eos_ids, pad_id, r0: int = 0, r1: Optional[int] = None):
+        """CPU twin of decode_update_kernel over rows [r0, r1): each active row writes at its own
+        output position gen_len[b] (the step counter for a static batch)."""
+        r1 = self.max_batch if r1 is None else r1
         T = self.out_tokens.shape[1]
-        act = self.active.bool()
-        if s < T:
-            self.out_tokens[act, s] = self.sampled[act]
-            self.out_logp[act, s] = self.sampled_lp[act]
+        act = self.active[r0:r1].bool()
+        gl = self.gen_len[r0:r1]
+        act = act & (gl < T)
+        rows = torch.nonzero(act).flatten()
+        if rows.numel():
+            idx = gl[rows].long()
+            samp = self.sampled[r0:r1]
+            self.out_tokens[r0 + rows, idx] = samp[rows]
+            self.out_logp[r0 + rows, idx] = self.sampled_lp[r0:r1][rows]
             if self.value_head is not None:
-                self.out_values[act, s] = self.values[act]
-            self.gen_len[act] = s + 1
-            fin = torch.isin(self.sampled, eos_ids) | torch.full_like(act, s + 1 >= T)
-            self.kv_len[act] += 1
-            self.pos[act] += 1
-            self.tok_in.copy_(torch.where(act, self.sampled, torch.full_like(self.sampled, pad_id)))
-            self.active[act & fin] = 0
+                self.out_values[r0 + rows, idx] = self.values[r0:r1][rows]
+            fin = torch.isin(samp, eos_ids) | (gl + 1 >= T)
+            gl[act] += 1
+            self.kv_len[r0:r1][act] += 1
+            self.tok_in[r0:r1].copy_(torch.where(act, samp, torch.full_like(samp, pad_id)))
+            self.active[r0:r1][act & fin] = 0
+        else:
+            self.tok_in[r0:r1].fill_(pad_id)
         self.step += 1
         self.rng_offset += 1
         torch.add(self.kv_len, 1, out=self.attn_len)
@@ -312,12 +323,9 @@ class Generator:
         self._emit(h, params, eos, pad_id)
         if ev:
             ev[1].record()
-        key = (T, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed, tuple(eos_list), pad_id,
-               self._nb)
         steps = T - 1
-        if steps > 0 and self.use_graph and self.runner.needs(key):
-            # the EOS tensor is created per call: the runner keeps the captured one alive
-            self.runner.capture(lambda: self._step(params, eos, pad_id), key, keep=(eos,), restore=self._state())
+        if steps > 0:
+            self._ensure_graph(params, eos, eos_list, pad_id, T)
         loop = _DecodeLoop(self, steps, params, eos, pad_id, early_stop)
         loop.run()
         pend = _Pending(self, B, ids, start, t0, ev, loop)
@@ -325,6 +333,14 @@ class Generator:
             ev[2].record()
             pend._recorded = True
         return pend
+
+    def _ensure_graph(self, params, eos, eos_list, pad_id, T):
+        """The captured decode step for (sampling parameters, output width, row bucket)."""
+        key = (T, params.inv_temp, params.top_k, params.top_p, params.greedy, params.seed, tuple(eos_list), pad_id,
+               self._nb)
+        if self.use_graph and self.runner.needs(key):
+            # the EOS tensor is created per call: the runner keeps the captured one alive
+            self.runner.capture(lambda: self._step(params, eos, pad_id), key, keep=(eos,), restore=self._state())
 
     def _replay(self, params, eos, pad_id):
         if self.use_graph:
@@ -471,3 +487,155 @@ def generate_text(model, tokenizer, prompts: List[str], params: SamplingParams, 
         n = int(out.lengths[b])
         res.append(tokenizer.decode(out.tokens[b, :n].tolist()))
     return res
+
+
+class _RowCache:
+    """View of batch rows [b, b + n) of a KVCache (prefill of admitted requests)."""
+
+    def __init__(self, cache: KVCache, b: int, n: int = 1):
+        self.k = [cache.k[l, b:b + n] for l in range(cache.k.shape[0])]
+        self.v = [cache.v[l, b:b + n] for l in range(cache.v.shape[0])]
+        self.fp8 = cache.fp8
+        if cache.fp8:
+            self.ks = [cache.ks[l, b:b + n] for l in range(cache.ks.shape[0])]
+            self.vs = [cache.vs[l, b:b + n] for l in range(cache.vs.shape[0])]
+
+    def scales(self, layer: int):
+        return (self.ks[layer], self.vs[layer]) if self.fp8 else (None, None)
+
+
+@dataclass
+class FinishedRow:
+    tag: object
+    tokens: List[int]
+    logprobs: List[float]
+    prompt_len: int
+    steps_waited: int
+
+
+class ContinuousBatcher:
+    """Iteration-level (continuous) batching over one Generator's static cache and captured decode
+    step: a request is admitted into a free batch row between decode steps — its prompt is
+    prefilled into that row alone (``_RowCache``), its first token sampled from the prefill — and
+    the graph-replayed decode step then advances every active row at once; each row writes at its
+    own output position (``decode_update_kernel`` indexes by the row's generated length) and
+    leaves the batch when it emits EOS or reaches ``max_new_tokens``, freeing the row for the next
+    request. Rows are independent: other rows' K/V, positions and attention lengths are untouched
+    by an admission. One sampling configuration per batcher; the decode step runs the
+    power-of-two bucket of rows that covers the active ones (inactive rows in it are masked).
+
+    Usage: ``admit(prompt_ids, tag)`` while ``free_rows()``; ``step(n)``; ``collect()`` returns the
+    rows that finished (a host read of the per-row flags once per call)."""
+
+    def __init__(self, gen: Generator, params: SamplingParams, pad_id: int = 0, eos_ids: Sequence[int] = ()):
+        self.gen, self.params, self.pad_id = gen, params, pad_id
+        g = gen
+        dev, MB, T = g.device, g.max_batch, params.max_new_tokens
+        self.T = T
+        self.eos_list = list(eos_ids) or [g.cfg.eos_token_id]
+        self.eos = torch.tensor(self.eos_list, dtype=torch.long, device=dev)
+        g.active.zero_()
+        g.gen_len.zero_()
+        g.step.zero_()
+        g.kv_start.zero_()
+        g.kv_len.zero_()
+        g.tok_in.fill_(pad_id)
+        if g.out_tokens is None or g.out_tokens.shape[1] != T:
+            g.out_tokens = torch.full((MB, T), pad_id, dtype=torch.long, device=dev)
+            g.out_logp = torch.zeros(MB, T, dtype=torch.float32, device=dev)
+            g.out_values = torch.zeros(MB, T, dtype=torch.float32, device=dev)
+            g.runner.reset()
+        g._nb = 1
+        self._prev_merged = g.model.set_lora_merged(True) if hasattr(g.model, "set_lora_merged") else None
+        if hasattr(g.model, "refresh_decode_weights"):
+            g.model.refresh_decode_weights()
+        if T > 1:
+            g._ensure_graph(params, self.eos, self.eos_list, pad_id, T)  # captured while no row is active
+        self.rows = {}  # row -> (tag, prompt_len, steps at admission)
+        self.free = list(range(MB))
+        self.steps = 0
+
+    def close(self):
+        if self._prev_merged is not None:
+            self.gen.model.set_lora_merged(self._prev_merged)
+            self._prev_merged = None
+
+    def free_rows(self) -> int:
+        return len(self.free)
+
+    def active_rows(self) -> int:
+        return len(self.rows)
+
+    @torch.no_grad()
+    def admit(self, prompt: List[int], tag=None) -> int:
+        return self.admit_many([prompt], [tag])[0]
+
+    @torch.no_grad()
+    def admit_many(self, prompts: List[List[int]], tags=None) -> List[int]:
+        """Admit len(prompts) <= free_rows() requests. The lowest free rows are taken and every run
+        of consecutive rows is prefilled as ONE left-padded batch into its cache rows."""
+        g = self.gen
+        tags = list(tags) if tags is not None else [None] * len(prompts)
+        if len(prompts) > len(self.free):
+            raise ValueError(f"{len(prompts)} requests for {len(self.free)} free rows")
+        for p in prompts:
+            if len(p) < 1 or len(p) + self.T > g.max_seq:
+                raise ValueError(f"prompt of {len(p)} tokens + {self.T} new exceeds the cache ({g.max_seq})")
+        self.free.sort()
+        rows, self.free = self.free[:len(prompts)], self.free[len(prompts):]
+        i = 0
+        while i < len(rows):
+            j = i + 1
+            while j < len(rows) and rows[j] == rows[j - 1] + 1:
+                j += 1
+            b0, n = rows[i], j - i
+            grp = prompts[i:j]
+            S = max(len(p) for p in grp)
+            ids = torch.full((n, S), self.pad_id, dtype=torch.long)
+            start = torch.zeros(n, dtype=torch.int32)
+            for r, p in enumerate(grp):
+                ids[r, S - len(p):] = torch.tensor(p, dtype=torch.long)
+                start[r] = S - len(p)
+            g.kv_start[b0:b0 + n].copy_(start.to(g.device, non_blocking=True))
+            h_last = g.model.prefill(ids.to(g.device, non_blocking=True), g.kv_start[b0:b0 + n],
+                                     _RowCache(g.cache, b0, n))
+            g.kv_len[b0:b0 + n].fill_(S - 1)  # the first bookkeeping advances them to S
+            g.gen_len[b0:b0 + n].zero_()
+            g.active[b0:b0 + n].fill_(1)
+            g._emit(h_last, self.params, self.eos, self.pad_id, r0=b0)
+            for r in range(n):
+                self.rows[b0 + r] = (tags[i + r], len(grp[r]), self.steps)
+            i = j
+        return rows
+
+    def step(self, n: int = 1):
+        """n decode steps over the power-of-two bucket of rows covering every active row (rows are
+        handed out lowest-first, so the active set stays compact); one captured graph per bucket."""
+        g = self.gen
+        nb = g._bucket(max(self.rows) + 1 if self.rows else 1)
+        if nb != g._nb:
+            g._nb = nb
+            if self.T > 1:
+                g._ensure_graph(self.params, self.eos, self.eos_list, self.pad_id, self.T)
+        for _ in range(n):
+            g._replay(self.params, self.eos, self.pad_id)
+        self.steps += n
+
+    def collect(self) -> List[FinishedRow]:
+        """Rows that have finished since the last call (their outputs copied to the host)."""
+        if not self.rows:
+            return []
+        g = self.gen
+        act = g.active.cpu()
+        done = [b for b in self.rows if not bool(act[b])]
+        out = []
+        if done:
+            idx = torch.tensor(done, device=g.device)
+            lens = g.gen_len.index_select(0, idx).cpu().tolist()
+            toks = g.out_tokens.index_select(0, idx).cpu()
+            lps = g.out_logp.index_select(0, idx).cpu()
+            for b, n, t, lp in zip(done, lens, toks, lps):
+                tag, S, s0 = self.rows.pop(b)
+                out.append(FinishedRow(tag, t[:n].tolist(), lp[:n].tolist(), S, self.steps - s0))
+                self.free.append(b)
+        return out

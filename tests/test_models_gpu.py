@@ -379,3 +379,34 @@ def test_side_stream_is_high_priority():
     sp = StreamPair(DEV)
     lo, hi = torch.cuda.Stream.priority_range()
     assert sp.side.priority == hi and hi < lo
+
+
+def test_continuous_batching_gpu_matches_teacher_forcing():
+    """Requests admitted into a running graph-replayed decode batch: every row's behaviour
+    log-probs equal a teacher-forced rescoring of its own prompt + tokens (rows independent)."""
+    from rag_tl_domainllm_optimizer_amd.generation import ContinuousBatcher
+    from rag_tl_domainllm_optimizer_amd.train.common import score_sequences
+
+    cfg = PRESETS["tiny-mistral"]
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=4)
+    p = SamplingParams(max_new_tokens=10, temperature=0.7, top_k=0, seed=5)
+    prompts = [[5, 9, 33, 41, 7, 8, 9, 10], [12, 300, 4], list(range(20, 60)), [7, 7, 7, 7], list(range(100, 130))]
+    cb = ContinuousBatcher(Generator(m, 2, 96, DEV), p, pad_id=0, eos_ids=[-1])
+    pending, got = list(enumerate(prompts)), {}
+    while pending or cb.active_rows():
+        if pending and cb.free_rows():
+            i, pr = pending.pop(0)
+            cb.admit(pr, i)
+        cb.step(3)
+        for f in cb.collect():
+            got[f.tag] = f
+    cb.close()
+    for i, pr in enumerate(prompts):
+        f = got[i]
+        assert len(f.tokens) == 10
+        ids = torch.tensor([pr], device=DEV)
+        resp = torch.tensor([f.tokens], device=DEV)
+        with torch.no_grad():
+            lp, _, _, _ = score_sequences(m, ids, torch.zeros(1, dtype=torch.long, device=DEV), resp,
+                                          torch.tensor([10], device=DEV), 1 / 0.7)
+        torch.testing.assert_close(lp[0].cpu(), torch.tensor(f.logprobs), rtol=0.0, atol=0.08)

@@ -101,3 +101,84 @@ def test_engine_over_real_pipeline_cpu():
         got = [f.result(60) for f in futs]
     assert [a.answer for a in got] == [a.answer for a in direct]
     assert [a.doc_ids for a in got] == [a.doc_ids for a in direct]
+
+
+def _tiny_pipe(max_batch=2, new=5):
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.generation import SamplingParams
+    from rag_tl_domainllm_optimizer_amd.rag import RagPipeline
+    from rag_tl_domainllm_optimizer_amd.retrieval import Encoder, FlatIndex
+    from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
+
+    pol = models.CausalLM(models.resolve_preset("tiny-llama"), device="cpu", dtype=torch.float32, seed=1)
+    enc_m = models.build_model("tiny-bert", device="cpu", dtype=torch.float32, seed=2).eval()
+    tok = Tokenizer.synthetic(pol.cfg.vocab_size, pol.cfg.arch)
+    enc = Encoder(enc_m, Tokenizer.synthetic(enc_m.cfg.vocab_size, enc_m.cfg.arch), max_length=32)
+    words = tok.words()
+    docs = [" ".join(words[(7 * i + j) % len(words)] for j in range(12)) for i in range(30)]
+    index = FlatIndex(enc.dim, "ip", "cpu")
+    index.add(enc.encode(docs))
+    pipe = RagPipeline(enc, index, docs, pol, tok, top_k=2, sampling=SamplingParams(max_new_tokens=new, do_sample=False),
+                       max_prompt_tokens=96, max_batch=max_batch, use_graph=False)
+    return pipe, words
+
+
+def test_continuous_batcher_matches_one_at_a_time_greedy():
+    """Rows admitted into a running batch (2 rows, 4 requests, staggered) decode exactly what a
+    batch-1 generation of the same prompt does."""
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.generation import ContinuousBatcher, Generator, SamplingParams
+
+    m = models.CausalLM(models.resolve_preset("tiny-llama"), device="cpu", dtype=torch.float32, seed=3)
+    p = SamplingParams(max_new_tokens=6, do_sample=False)
+    prompts = [[5, 9, 33, 41, 7], [12, 300, 4, 8, 9, 10, 11], [20, 21, 22], [100, 200, 300, 400]]
+    ref = [Generator(m, 1, 64, "cpu", use_graph=False).generate([pr], p, pad_id=0, eos_ids=[-1]).tokens[0].tolist()
+           for pr in prompts]
+    cb = ContinuousBatcher(Generator(m, 2, 64, "cpu", use_graph=False), p, pad_id=0, eos_ids=[-1])
+    pending, got, admitted_at = list(enumerate(prompts)), {}, {}
+    while pending or cb.active_rows():
+        if pending and cb.free_rows():  # one admission per step: rows join a batch in flight
+            i, pr = pending.pop(0)
+            cb.admit(pr, i)
+            admitted_at[i] = cb.steps
+        cb.step(1)
+        for f in cb.collect():
+            got[f.tag] = f.tokens
+    assert [got[i] for i in range(4)] == ref
+    assert admitted_at[1] > admitted_at[0]  # the second request joined after the first had started
+    cb.close()
+
+
+def test_continuous_engine_answers_like_direct_pipeline():
+    from rag_tl_domainllm_optimizer_amd.serve import ContinuousEngine
+
+    pipe, words = _tiny_pipe(max_batch=2)
+    qs = [f"{words[i]} {words[i + 3]}" for i in range(5)]
+    direct = [pipe.answer([q])[0] for q in qs]  # one at a time
+    with ContinuousEngine(pipe, chunk=2) as eng:
+        futs = [eng.submit(q) for q in qs]
+        got = [f.result(120) for f in futs]
+        assert eng.stats["finished"] == 5 and eng.stats["max_active"] <= 2
+    assert [a.answer for a in got] == [a.answer for a in direct]
+    assert [a.doc_ids for a in got] == [a.doc_ids for a in direct]
+    assert all(a.timings["new_tokens"] == 5 and a.timings["queue_s"] >= 0 for a in got)
+
+
+def test_continuous_admit_many_batches_consecutive_rows():
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.generation import ContinuousBatcher, Generator, SamplingParams
+
+    m = models.CausalLM(models.resolve_preset("tiny-llama"), device="cpu", dtype=torch.float32, seed=3)
+    p = SamplingParams(max_new_tokens=5, do_sample=False)
+    prompts = [[5, 9, 33, 41, 7], [12, 300, 4], [20, 21, 22, 23, 24, 25, 26], [100, 200]]
+    ref = [Generator(m, 1, 64, "cpu", use_graph=False).generate([pr], p, pad_id=0, eos_ids=[-1]).tokens[0].tolist()
+           for pr in prompts]
+    cb = ContinuousBatcher(Generator(m, 4, 64, "cpu", use_graph=False), p, pad_id=0, eos_ids=[-1])
+    rows = cb.admit_many(prompts, list(range(4)))  # one left-padded prefill over rows 0..3
+    assert rows == [0, 1, 2, 3]
+    got = {}
+    while cb.active_rows():
+        cb.step(2)
+        for f in cb.collect():
+            got[f.tag] = f.tokens
+    assert [got[i] for i in range(4)] == ref
