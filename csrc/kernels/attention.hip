@@ -769,6 +769,258 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(DecodeFusedArgs 
 }
 
 // ---------------------------------------------------------------------------------------------
+// fp8-cache decode step for MHA (G = 1: Llama-2-13B, config 5) on the VALU
+// ---------------------------------------------------------------------------------------------
+// With one query head per kv head the MFMA form above computes 16 query rows of which 15 are
+// empty, and its fp8 variant moves only 3.6 TB/s (profiles/r3/dec13b_b64_fp8kv_kernels.txt).
+// Here one wave owns one (batch, head) and walks 16-key tiles, four in flight:
+//   * QK: lane (g, r) dots key c0 + r over elements {32 s + 8 g + e} — the 32 contiguous bytes of
+//     the k-permuted fp8 row at byte 32 g — against its 32 q values (fp32 registers, pre-scaled
+//     by softmax scale * log2 e); the 4 lane groups' partials meet by two shuffles;
+//   * online softmax over the tile's 16 scores (lanes r: 4 shuffles each for max and sum);
+//   * PV: lane (g, r) accumulates dims [8 r, 8 r + 8) over keys c0 + 4 i + g (i < 4): 8 V bytes per
+//     key, P (with the key's V scale folded in) broadcast from lane 4 i + g.
+// The 4 groups' O partials meet once, after the last tile. No LDS and no MFMA. The new token is
+// rotated, quantised and appended as in attn_decode_mfma_kernel<KV8> (same bytes, same scales),
+// and this step attends over the quantised values.
+typedef __attribute__((ext_vector_type(2))) float rt_f32x2;
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_decode_g1_fp8_kernel(DecodeFusedArgs a) {
+  constexpr int D = 128;
+  // NW waves per (batch, head), tiles dealt round-robin, merged through LDS: NW times the waves of
+  // one-wave-per-row, so the last round of a 2560-row batch (2 waves per SIMD resident) is a
+  // fraction of a row, not a whole one
+  __shared__ float mrg[NW][2 + D];
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  const int w = (int)(threadIdx.x >> 6);
+  const int bh = blockIdx.x;
+  const int b = bh / a.Hkv, hk = bh % a.Hkv;
+  const int len = a.attn_len[b];
+  const int s_new = a.slot[b];
+  RT_ASSERT(len <= a.Smax && s_new >= 0 && s_new < a.Smax);
+  int kbeg = a.kv_start ? a.kv_start[b] : 0;
+  if (a.window > 0) kbeg = max(kbeg, len - a.window);
+  const int p = a.pos ? a.pos[b] : 0;
+  const bf16_t* row = a.qkv + (long)b * a.ldq;
+  const unsigned char* kbase = (const unsigned char*)a.kc + (long)bh * a.Smax * D;
+  const unsigned char* vbase = (const unsigned char*)a.vc + (long)bh * a.Smax * D;
+  const float* ksb = a.ksc + (long)bh * a.SmaxP;
+  const float* vsb = a.vsc + (long)bh * a.SmaxP;
+
+  struct Tile { uint4 k0, k1; uint2 v[4]; float ks, vs; };
+  auto load = [&](Tile& T, int c0) {
+    const long key = min(c0 + r, len - 1);
+    T.k0 = load_nt16(kbase + key * D + 32 * g);
+    T.k1 = load_nt16(kbase + key * D + 32 * g + 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) T.v[i] = load_nt8(vbase + (long)min(c0 + 4 * i + g, len - 1) * D + 8 * r);
+    T.ks = ksb[key];
+    T.vs = vsb[key];
+  };
+  Tile ta, tb, tc, td;
+  constexpr int ST = 16 * NW;      // key stride between one wave's tiles
+  const int cf = kbeg + 16 * w;  // this wave's tiles: cf + ST j
+  if (cf < len) load(ta, cf);
+  if (cf + ST < len) load(tb, cf + ST);
+  if (cf + 2 * ST < len) load(tc, cf + 2 * ST);
+  if (cf + 3 * ST < len) load(td, cf + 3 * ST);
+
+  // ---- q / k_new / v_new (+ RoPE): lane group g holds chunks 4 s + g of q and k, chunk r of v
+  const bool rot = a.cosT != nullptr;
+  const bf16_t* qrow = row + (long)hk * D;
+  const bf16_t* krow = row + (long)(a.Hq + hk) * D;
+  const bf16_t* vrow = row + (long)(a.Hq + a.Hkv + hk) * D;
+  uint4 qraw[4], kraw[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    qraw[s2] = *(const uint4*)(qrow + (4 * s2 + g) * 8);
+    kraw[s2] = *(const uint4*)(krow + (4 * s2 + g) * 8);
+  }
+  const uint4 vx = *(const uint4*)(vrow + r * 8);
+  float4 cq[2][2], sq[2][2];
+  {
+    const float* ct = rot ? a.cosT + (long)p * (D / 2) : (const float*)row;
+    const float* stb = rot ? a.sinT + (long)p * (D / 2) : (const float*)row;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int j0 = (4 * par + g) * 8;
+      cq[par][0] = *(const float4*)(ct + j0); cq[par][1] = *(const float4*)(ct + j0 + 4);
+      sq[par][0] = *(const float4*)(stb + j0); sq[par][1] = *(const float4*)(stb + j0 + 4);
+    }
+  }
+  auto rope8 = [&](const uint4& xv, const uint4& yv, const float4 (&c)[2], const float4 (&sn)[2], bool lo) -> uint4 {
+    if (!rot) return xv;
+    float x[8], y[8], o8[8];
+    unpack8(xv, x);
+    unpack8(yv, y);
+    const float cs[8] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w};
+    const float sv[8] = {sn[0].x, sn[0].y, sn[0].z, sn[0].w, sn[1].x, sn[1].y, sn[1].z, sn[1].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float t = a.sign * sv[e];
+      o8[e] = fmaf(x[e], cs[e], lo ? -(y[e] * t) : y[e] * t);  // = rope_qkv_kernel's rounding
+    }
+    return pack8(o8);
+  };
+  float q[32];  // element 32 s + 8 g + e at q[8 s + e], times scale * log2 e
+  uint4 knew[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    float f[8];
+    unpack8(rope8(qraw[s2], qraw[s2 ^ 2], cq[s2 & 1], sq[s2 & 1], s2 < 2), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[8 * s2 + e] = f[e] * a.scale_log2;
+    knew[s2] = rope8(kraw[s2], kraw[s2 ^ 2], cq[s2 & 1], sq[s2 & 1], s2 < 2);
+  }
+  // quantise k_new / v_new (absmax / 448 per head row), as attn_decode_mfma_kernel<KV8>
+  uint2 kq[4], vq;
+  float sk_new, sv_new;
+  {
+    float amk = 0.f, amv = 0.f, f[8];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      unpack8(knew[s2], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amk = fmaxf(amk, fabsf(f[e]));
+    }
+    amk = fmaxf(amk, __shfl_xor(amk, 16, 64));
+    amk = fmaxf(amk, __shfl_xor(amk, 32, 64));
+    unpack8(vx, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) amv = fmaxf(amv, fabsf(f[e]));
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) amv = fmaxf(amv, __shfl_xor(amv, o2, 64));
+    sk_new = amk > 0.f ? amk / 448.f : 1.f;
+    sv_new = amv > 0.f ? amv / 448.f : 1.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      unpack8(knew[s2], f);
+      kq[s2] = f32x8_to_fp8(f, 1.f / sk_new);
+    }
+    unpack8(vx, f);
+    vq = f32x8_to_fp8(f, 1.f / sv_new);
+  }
+  const bool has_new = s_new >= kbeg && s_new < len;
+  if (has_new && w == 0) {
+    unsigned char* kdst = (unsigned char*)a.kc + ((long)bh * a.Smax + s_new) * D;
+    unsigned char* vdst = (unsigned char*)a.vc + ((long)bh * a.Smax + s_new) * D;
+    if (r == 0) {
+      *(uint4*)(kdst + 32 * g) = make_uint4(kq[0].x, kq[0].y, kq[1].x, kq[1].y);
+      *(uint4*)(kdst + 32 * g + 16) = make_uint4(kq[2].x, kq[2].y, kq[3].x, kq[3].y);
+    }
+    if (g == 1) *(uint2*)(vdst + r * 8) = vq;
+    if (lane == 0) {
+      a.ksc[(long)bh * a.SmaxP + s_new] = sk_new;
+      a.vsc[(long)bh * a.SmaxP + s_new] = sv_new;
+    }
+  }
+
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  auto consume = [&](const Tile& T, int c0) {
+    unsigned kw[8] = {T.k0.x, T.k0.y, T.k0.z, T.k0.w, T.k1.x, T.k1.y, T.k1.z, T.k1.w};
+    uint2 vv[4] = {T.v[0], T.v[1], T.v[2], T.v[3]};
+    float ks = T.ks, vs = T.vs;
+    if (has_new && s_new >= c0 && s_new < c0 + 16) {  // this step's own bytes and scales
+      if (min(c0 + r, len - 1) == s_new) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) { kw[2 * s2] = kq[s2].x; kw[2 * s2 + 1] = kq[s2].y; }
+        ks = sk_new;
+        vs = sv_new;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (min(c0 + 4 * i + g, len - 1) == s_new) vv[i] = vq;
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < 8; ++w2) {
+      const rt_f32x2 lo = __builtin_amdgcn_cvt_pk_f32_fp8(kw[w2], false);
+      const rt_f32x2 hi = __builtin_amdgcn_cvt_pk_f32_fp8(kw[w2], true);
+      dot = fmaf(q[4 * w2], lo.x, dot);
+      dot = fmaf(q[4 * w2 + 1], lo.y, dot);
+      dot = fmaf(q[4 * w2 + 2], hi.x, dot);
+      dot = fmaf(q[4 * w2 + 3], hi.y, dot);
+    }
+    dot += __shfl_xor(dot, 16, 64);
+    dot += __shfl_xor(dot, 32, 64);
+    const float sc = c0 + r < len ? dot * ks : -INFINITY;
+    float mx = sc;
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+    const float mn = fmaxf(m, mx);  // finite: every tile holds >= 1 valid key
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    const float pk = exp2f(sc - mn);
+    float rs = pk;
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) rs += __shfl_xor(rs, o2, 64);
+    l = l * alpha + rs;
+    const float pv = pk * vs;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] *= alpha;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float pp = __shfl(pv, 4 * i + g, 64);  // P' of key c0 + 4 i + g (lane r = 4 i + g)
+      const rt_f32x2 v0 = __builtin_amdgcn_cvt_pk_f32_fp8(vv[i].x, false), v1 = __builtin_amdgcn_cvt_pk_f32_fp8(vv[i].x, true);
+      const rt_f32x2 v2 = __builtin_amdgcn_cvt_pk_f32_fp8(vv[i].y, false), v3 = __builtin_amdgcn_cvt_pk_f32_fp8(vv[i].y, true);
+      o[0] = fmaf(pp, v0.x, o[0]); o[1] = fmaf(pp, v0.y, o[1]);
+      o[2] = fmaf(pp, v1.x, o[2]); o[3] = fmaf(pp, v1.y, o[3]);
+      o[4] = fmaf(pp, v2.x, o[4]); o[5] = fmaf(pp, v2.y, o[5]);
+      o[6] = fmaf(pp, v3.x, o[6]); o[7] = fmaf(pp, v3.y, o[7]);
+    }
+  };
+  for (int c0 = cf; c0 < len; c0 += 4 * ST) {
+    consume(ta, c0);
+    if (c0 + 4 * ST < len) load(ta, c0 + 4 * ST);
+    if (c0 + ST < len) {
+      consume(tb, c0 + ST);
+      if (c0 + 5 * ST < len) load(tb, c0 + 5 * ST);
+    }
+    if (c0 + 2 * ST < len) {
+      consume(tc, c0 + 2 * ST);
+      if (c0 + 6 * ST < len) load(tc, c0 + 6 * ST);
+    }
+    if (c0 + 3 * ST < len) {
+      consume(td, c0 + 3 * ST);
+      if (c0 + 7 * ST < len) load(td, c0 + 7 * ST);
+    }
+  }
+  // the 4 lane groups hold disjoint key subsets of the same 8 dims
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  // merge the waves' (m, l, O) (m = -inf, l = 0 for a wave without tiles)
+  if (lane == 0) { mrg[w][0] = m; mrg[w][1] = l; }
+  if (g == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mrg[w][2 + 8 * r + e] = o[e];
+  }
+  __syncthreads();
+  if (w == 0 && g == 0) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int q2 = 0; q2 < NW; ++q2) M = fmaxf(M, mrg[q2][0]);
+    float L = 0.f, y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int q2 = 0; q2 < NW; ++q2) {
+        const float f = exp2f(mrg[q2][0] - M);  // 0 for a wave without tiles
+        L += mrg[q2][1] * f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] += mrg[q2][2 + 8 * r + e] * f;
+      }
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] *= inv;
+    *(uint4*)(a.o + (long)b * a.ldo + (long)hk * D + 8 * r) = pack8(y);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Fused decode step on MFMA (large batch: B * Hkv >= 256, one partition per (batch, kv head))
 // ---------------------------------------------------------------------------------------------
 // At batch 256 the decode attention of a layer streams ~250 MB of K/V (256 x 8 kv-heads x ~240
@@ -2055,6 +2307,17 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     if (D != 128 || a.SmaxP < Smax || (G != 1 && G != 2 && G != 4 && G != 8)) return -3;
     // RT_DECODE_FP8_MW=1: the 8-wave kernel at every batch (A/B hook)
     static const int fp8_mw = getenv("RT_DECODE_FP8_MW") ? atoi(getenv("RT_DECODE_FP8_MW")) : 0;
+    // MHA at large batch: the VALU kernel (RT_DECODE_G1_VALU=0: the MFMA form)
+    static const int g1_valu = getenv("RT_DECODE_G1_VALU") ? atoi(getenv("RT_DECODE_G1_VALU")) : 1;
+    if (!fp8_mw && g1_valu && G == 1 && !a.qkv_slabs && rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
+      // waves per row (A/B hook RT_DECODE_G1_NW = 1, 2, 4; default 2)
+      static const int g1_nw = getenv("RT_DECODE_G1_NW") ? atoi(getenv("RT_DECODE_G1_NW")) : 2;
+      if (g1_nw == 4) hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<4>, dim3((unsigned)(B * Hkv)), dim3(256), 0, stream, a);
+      else if (g1_nw == 1) hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<1>, dim3((unsigned)(B * Hkv)), dim3(64), 0, stream, a);
+      else hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<2>, dim3((unsigned)(B * Hkv)), dim3(128), 0, stream, a);
+      RT_LAUNCH_CHECK();
+      return 0;
+    }
     if (!fp8_mw && rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
       dim3 mgrid((unsigned)(B * Hkv)), mblock(64);
       switch (G) {
