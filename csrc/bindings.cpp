@@ -450,7 +450,9 @@ Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, c
   }
   if (bias.has_value() && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N); }
   const bool pair = act == 5;  // SwiGLU pair mode (W8A16 skinny only)
-  if (pair) TORCH_CHECK(a_bf16 && N % 64 == 0, "gemm_fp8: SwiGLU pair mode needs bf16 activations, N % 64 == 0");
+  if (pair)
+    TORCH_CHECK(a_bf16 ? N % 64 == 0 : N % 256 == 0,
+                "gemm_fp8: SwiGLU pair mode needs N % 64 == 0 (W8A16) / N % 256 == 0 (W8A8)");
   const int64_t Nout = pair ? N / 2 : N;
   Tensor c = (out.has_value() && out->defined()) ? *out : at::empty({M, Nout}, a.options().dtype(at::kBFloat16));
   TORCH_CHECK(c.size(0) == M && c.size(1) == Nout && c.stride(1) == 1 && c.scalar_type() == at::kBFloat16, "gemm_fp8: out");

@@ -1600,6 +1600,9 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   return 0;
 }
 
+extern "C" int rt_gemm_big_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*,
+                               long, int, int, int, int, hipStream_t);
+
 // fp8 GEMMs: C[M,N] (bf16) = act( (A_q B_q^T) * sa[row] * sb[col] + bias ), A_q / B_q OCP e4m3fn.
 //  * M > 64 : W8A8, 256x256 8-phase kernel on MX-scaled mfma_16x16x128_f8f6f4 (2x the bf16 rate)
 //  * M <= 64: W8A16 (A = bf16 activations, sa ignored): half the weight bytes.
@@ -1662,7 +1665,13 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
       }
     }
   } else {
+    // W8A8 (M > 64): the gemm_big schedule with the MX fp8 MFMA (RT_GEMM_FP8_256=1: the older
+    // 256x256 8-phase kernel, kept for A/B); SwiGLU pairs [gate; up] in its epilogue
     if (K % 128 || N % 8) return -1;
+    static const int use256 = getenv("RT_GEMM_FP8_256") ? atoi(getenv("RT_GEMM_FP8_256")) : 0;
+    if (!use256 && lda % 16 == 0 && ldb % 16 == 0 && ldc % 8 == 0 && (act == 0 || (act == ACT_SWIGLU && N % 256 == 0)))
+      return rt_gemm_big_fp8(A, lda, sa, B, ldb, sb, bias, C, ldc, M, N, K, act == ACT_SWIGLU ? 5 : 0, stream);
+    if (act == ACT_SWIGLU) return -2;
     const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
     hipLaunchKernelGGL((gemm_256_kernel<false, true>), dim3(tiles), dim3(512), 0, stream, p);
   }

@@ -33,6 +33,8 @@
 // Reduction tails (K % 64 != 0) and the K-extension read a zero page for out-of-range k.
 #include "rt_common.h"
 
+#include <algorithm>
+
 namespace rt {
 
 namespace gb {
@@ -67,6 +69,11 @@ struct Args {
   int nsplit;                     // split-K factor (gridDim.y)
   const bf16_t* zpage;            // >= 128 zero bytes
   int b_nt;                       // B (weight) stream read once per launch: non-temporal LDS-DMA
+  // F8 (W8A8, config 5): A / B are OCP e4m3fn bytes viewed as bf16 pairs (K and the strides in
+  // 2-byte units), one MX-scaled 16x16x128 MFMA per fragment pair and K-step; C = acc * sa[row] *
+  // sb[weight row] before bias / activation / SwiGLU
+  const float* sa;
+  const float* sb;
 };
 
 __device__ __forceinline__ int row_swz(int row) { return (row >> 1) & 7; }
@@ -111,9 +118,10 @@ __device__ __forceinline__ void wait_granules(int n) {
 // each wave owns 2 B fragments instead of 4 (columns 64 (wc >> 1) + 16 (wc & 1) + 32 s): used for
 // M = 256 decode GEMMs (twice the workgroups, no split-K on the widest weights) and for the last,
 // partial wave of tiles of a large GEMM (rt_gemm_big_planned).
-template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false>
+template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false, bool F8 = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   static_assert(BN == 256 || BN == 128, "BN");
+  static_assert(!F8 || (LA == ROW && LB == ROW && OUT == O_BF16), "F8: NT with a bf16 output only");
   constexpr int NB = BN / 128;  // B fragments per wave and B sub-block; LDS-DMA instructions per B granule
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];  // the only __shared__ object
 
@@ -333,6 +341,13 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                      \
     __builtin_amdgcn_sched_barrier(0);                                                      \
     __builtin_amdgcn_s_setprio(1);                                                          \
+    if constexpr (F8) {                                                                     \
+      /* the 32 bytes of a lane are the same two 16-B chunks of A and B rows: one k pairing */ \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                         \
+        _Pragma("unroll") for (int j = 0; j < NB; ++j)                                      \
+          acc[(SA) * 4 + i][(SB) * NB + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4( \
+              FB[j], fa[i], acc[(SA) * 4 + i][(SB) * NB + j], 0, 0, 0, 127, 0, 127);        \
+    } else {                                                                                \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                           \
       _Pragma("unroll") for (int j = 0; j < NB; ++j)                                        \
         _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                    \
@@ -341,6 +356,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
                                                         acc[(SA) * 4 + i][(SB) * NB + j], 0, 0, 0) \
               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(half(fa[i], kk), half(FB[j], kk),   \
                                                         acc[(SA) * 4 + i][(SB) * NB + j], 0, 0, 0); \
+    }                                                                                       \
     __builtin_amdgcn_s_setprio(0);                                                          \
     GB_BARRIER();                                                                           \
   } while (0)
@@ -464,11 +480,19 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     constexpr int LDT = BN + 4;
     bf16_t* tile = (bf16_t*)smem;
     float bcol[2 * NB][4];
+    float scol[2 * NB][4];  // F8: per-output-channel weight scale of the lane's columns
 #pragma unroll
     for (int j = 0; j < 2 * NB; ++j) {
       const int col = n0 + col_of(j) + fq * 4;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bcol[j][r] = (EPI != E_SWIGLU && p.bias && col < p.N) ? bf2f(p.bias[col + r]) : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        bcol[j][r] = (EPI != E_SWIGLU && p.bias && col < p.N) ? bf2f(p.bias[col + r]) : 0.f;
+        if constexpr (F8) {
+          const int c = col_of(j) + fq * 4 + r;  // tile column -> weight row
+          const int wrow = EPI == E_SWIGLU ? (c < HALF ? tn * HALF + c : Fh + tn * HALF + c - HALF) : min(n0 + c, p.N - 1);
+          scol[j][r] = p.sb[wrow];
+        }
+      }
     }
     auto ld16 = [&](int row, int c8) -> uint4 {  // 8 bf16 at tile[row][8 c8], 8-B aligned
       const uint2 lo = *(const uint2*)(tile + row * LDT + c8 * 8);
@@ -479,15 +503,21 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     for (int hh = 0; hh < 2; ++hh) {
       if (wr == hh) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i) {
+          // F8: per-token activation scale of this fragment row (x the column's weight scale)
+          const float srow = F8 ? p.sa[min(m0 + hh * 128 + i * 16 + frow, p.M - 1)] : 1.f;
 #pragma unroll
           for (int j = 0; j < 2 * NB; ++j) {
             const int row = i * 16 + frow, col = col_of(j) + fq * 4;
             float y[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) y[r] = EPI == E_SWIGLU ? acc[i][j][r] : act_fn(acc[i][j][r] + bcol[j][r], EPI);
+            for (int r = 0; r < 4; ++r) {
+              const float v = F8 ? acc[i][j][r] * (srow * scol[j][r]) : acc[i][j][r];
+              y[r] = EPI == E_SWIGLU ? v : act_fn(v + bcol[j][r], EPI);
+            }
             *(uint2*)(tile + row * LDT + col) = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
           }
+        }
       }
       __syncthreads();
       if constexpr (EPI == E_SWIGLU) {
@@ -1246,6 +1276,63 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   if (p.C2) q.C2 = p.C2 + r0 * ldc2;
   if (p.R) q.R = p.R + r0 * ldr;
   return launch_gemm_big(q, layout_a, layout_b, act, out, 128, stream);
+}
+
+// W8A8 on the gemm_big schedule (config 5 prefill / reference scoring): A [M, K] e4m3fn with
+// per-row scales sa, B [N, K] e4m3fn with per-row scales sb, C = act(A B^T * sa sb^T + bias) bf16
+// (E_SWIGLU: B = [gate; up], C [M, N / 2]). The fp8 rows are the bf16 kernel's operands at half
+// the K (the same 128-B LDS rows, one 16x16x128 MX MFMA per 64-bf16 K-step at twice the bf16
+// rate), with the same wave planner: 256x256 tiles, the last partial wave on 256x128.
+extern "C" int rt_gemm_big_fp8(const void* A, long lda, const float* sa, const void* B, long ldb, const float* sb,
+                               const void* bias, void* C, long ldc, int M, int N, int K, int act,
+                               hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 128 || lda % 16 || ldb % 16 || ldc % 8 || (act != E_NONE && act != E_SWIGLU)) return -1;
+  if (act == E_SWIGLU && N % 256) return -3;
+  Args p{};
+  p.A = (const bf16_t*)A; p.lda = lda / 2; p.B = (const bf16_t*)B; p.ldb = ldb / 2;
+  p.A2 = nullptr; p.B2 = nullptr; p.K2 = 0;
+  p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = nullptr; p.ldc2 = 0; p.R = nullptr; p.ldr = 0;
+  p.M = M; p.N = N; p.K = K / 2; p.act = act; p.nsplit = 1; p.zpage = (const bf16_t*)A; p.b_nt = 0;
+  p.sa = sa; p.sb = sb;
+  const int tiles_m = (M + 255) / 256;
+  const int tn256 = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
+  const int tn128 = act == E_SWIGLU ? N / 128 : (N + 127) / 128;
+  const long cus = (long)num_cus();
+  int m1 = tiles_m;
+  float best = 1e30f;
+  for (int m = tiles_m; m >= 0; --m) {
+    const long w256 = ((long)m * tn256 + cus - 1) / cus, w128 = ((long)(tiles_m - m) * tn128 + cus - 1) / cus;
+    const float cost = (float)w256 + bn128_cost() * (float)w128;
+    if (cost < best - 1e-3f) { best = cost; m1 = m; }
+  }
+  auto launch = [&](const Args& q, int bn) {
+    const int tn = bn == 256 ? (act == E_SWIGLU ? q.N / 256 : (q.N + 255) / 256) : (act == E_SWIGLU ? q.N / 128 : (q.N + 127) / 128);
+    dim3 grid(((q.M + 255) / 256) * tn, 1), block(512);
+    if (bn == 256) {
+      if (act == E_SWIGLU) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_SWIGLU, 256, false, true>), grid, block, 0, stream, q);
+      else hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_NONE, 256, false, true>), grid, block, 0, stream, q);
+    } else {
+      if (act == E_SWIGLU) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_SWIGLU, 128, false, true>), grid, block, 0, stream, q);
+      else hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_NONE, 128, false, true>), grid, block, 0, stream, q);
+    }
+  };
+  if (m1 > 0) {
+    Args q = p;
+    q.M = std::min(M, m1 * 256);
+    launch(q, 256);
+  }
+  if (m1 < tiles_m) {
+    const long r0 = (long)m1 * 256;
+    Args q = p;
+    q.M = M - (int)r0;
+    q.A = p.A + r0 * p.lda;
+    q.sa = sa + r0;
+    q.C = (char*)C + r0 * ldc * 2;
+    launch(q, 128);
+  }
+  RT_LAUNCH_CHECK();
+  return 0;
 }
 
 extern "C" int rt_gemm_splitk_reduce(const float* slabs, int nsplit, int M, int N, const void* bias, int act,

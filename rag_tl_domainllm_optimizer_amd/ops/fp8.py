@@ -38,7 +38,8 @@ def dequantize_fp8(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
 
 
 def gemm_fp8(x: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor, bias=None, act=0, out=None) -> torch.Tensor:
-    """y = act(x W^T + b) with W given as fp8 (wq, sw). W8A16 for M <= 64, W8A8 above."""
+    """y = act(x W^T + b) with W given as fp8 (wq, sw). W8A16 for M <= 64, W8A8 above (the
+    gemm_big schedule on the MX fp8 MFMA). ``act`` 5 = SwiGLU over W = [gate; up] -> [M, N / 2]."""
     M, K = x.shape
     if on_gpu(x):
         C = native()
@@ -50,7 +51,11 @@ def gemm_fp8(x: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor, bias=None, act
     y = xf @ dequantize_fp8(wq, sw).t()
     if bias is not None:
         y = y + bias.float()
-    y = ref.apply_act(y, act).to(x.dtype)
+    if act == 5:  # SwiGLU pair: weight rows [gate; up]
+        F = y.shape[1] // 2
+        y = (torch.nn.functional.silu(y[:, :F]) * y[:, F:]).to(x.dtype)
+    else:
+        y = ref.apply_act(y, act).to(x.dtype)
     if out is not None:
         out.copy_(y)
         return out

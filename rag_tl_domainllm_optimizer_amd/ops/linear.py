@@ -387,11 +387,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
                         y = native().gemm_fp8(x2, None, q, sc, None, ACT_SWIGLU, None, None, 0.0, shuf)
                     else:
                         # prefill / reference scoring: W8A8 [gate | up] on the fp8 MFMA (2x the bf16
-                        # rate), then one SwiGLU pass over the [M, 2F] pre-activation
-                        from .misc import swiglu
-
+                        # rate) with SwiGLU paired in the GEMM epilogue
                         q, sc = fp8.get(w_eff)
-                        y = swiglu(gemm_fp8(x2, q, sc))
+                        y = gemm_fp8(x2, q, sc, act=ACT_SWIGLU)
                     return y.reshape(*shp[:-1], w.shape[0] // 2)
             y = gemm(x2, w_eff, None, None, None, ACT_SWIGLU)
             return y.reshape(*shp[:-1], w.shape[0] // 2)

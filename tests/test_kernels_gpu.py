@@ -1013,3 +1013,20 @@ def test_generation_fp8kv_matches_teacher_forcing():
     d = (lp - out.logprobs).abs()
     assert torch.isfinite(out.logprobs).all()
     assert d.mean().item() < 0.1 and d.max().item() < 0.6, (d.mean().item(), d.max().item())
+
+
+@pytest.mark.parametrize("M,F,K", [(300, 512, 256), (2048, 1024, 512), (777, 2304, 384)])
+def test_gemm_fp8_w8a8_swiglu_fused(M, F, K):
+    """W8A8 [gate; up] with SwiGLU in the gemm_big fp8 epilogue == silu(g) * u over the
+    dequantised operands (and the plain W8A8 product for every planner split)."""
+    torch.manual_seed(M)
+    w = (torch.randn(2 * F, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    wq, sw = ops.quantize_fp8(w)
+    xq, sx = ops.quantize_fp8(x)
+    xd, wd = ops.dequantize_fp8(xq, sx), ops.dequantize_fp8(wq, sw)
+    y = ops.native().gemm_fp8(xq, sx, wq, sw, None, 5, None)
+    assert y.shape == (M, F)
+    g, u = xd @ wd[:F].t(), xd @ wd[F:].t()
+    _close(y, torch.nn.functional.silu(g) * u)
+    _close(ops.native().gemm_fp8(xq, sx, wq, sw, None, 0, None), xd @ wd.t())

@@ -1,0 +1,58 @@
+"""W8A8 GEMM (M > 64) timing on the prefill / reference-scoring shapes: the gemm_big fp8 schedule
+(default) or the older 256x256 8-phase kernel (RT_GEMM_FP8_256=1), plus the fused SwiGLU form.
+
+    python tools/fp8_w8a8_probe.py [--M 7168 20480]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from rag_tl_domainllm_optimizer_amd import ops  # noqa: E402
+
+SHAPES = {"mistral-7b": [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336)],
+          "llama2-13b": [("qkv", 15360, 5120), ("o", 5120, 5120), ("gate_up", 27648, 5120), ("down", 5120, 13824)]}
+
+
+def timeit(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, nargs="+", default=[7168, 20480])
+    a = ap.parse_args()
+    C = ops.native()
+    tag = "gemm_256" if os.environ.get("RT_GEMM_FP8_256") == "1" else "gemm_big"
+    for model, shapes in SHAPES.items():
+        for M in a.M:
+            for name, N, K in shapes:
+                x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+                w = (torch.randn(N, K, device="cuda") / math.sqrt(K)).to(torch.bfloat16)
+                wq, sw = ops.quantize_fp8(w)
+                xq, sx = ops.quantize_fp8(x)
+                t = timeit(lambda: C.gemm_fp8(xq, sx, wq, sw))
+                r = {"kernel": tag, "model": model, "name": name, "M": M, "N": N, "K": K, "us": round(t, 1),
+                     "pflops": round(2 * M * N * K / t / 1e9, 3)}
+                if name == "gate_up" and tag == "gemm_big":
+                    r["swiglu_fused_us"] = round(timeit(lambda: C.gemm_fp8(xq, sx, wq, sw, None, 5)), 1)
+                print(json.dumps(r), flush=True)
+                del x, w, wq, xq
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
