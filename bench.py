@@ -81,6 +81,8 @@ def main():
                     help="fp8 (e4m3fn) weights for no-grad forwards (default: on for --mode pipeline, config 5)")
     ap.add_argument("--fp8-kv", action=argparse.BooleanOptionalAction, default=None,
                     help="fp8 (e4m3fn) rollout K/V cache (default: with --fp8)")
+    ap.add_argument("--fp8-train", action=argparse.BooleanOptionalAction, default=None,
+                    help="W8A8 frozen-base product in LoRA training forwards (default: with --fp8)")
     ap.add_argument("--sft-batch", type=int, default=64, help="SFT sequences per GPU per step")
     ap.add_argument("--full-ft", action="store_true",
                     help="PPO over every policy weight (the reference's full-parameter mode: bf16 compute copies "
@@ -99,6 +101,8 @@ def main():
         args.fp8 = args.mode == "pipeline"
     if args.fp8_kv is None:
         args.fp8_kv = bool(args.fp8)
+    if args.fp8_train is None:
+        args.fp8_train = bool(args.fp8)
 
     from rag_tl_domainllm_optimizer_amd import models, parallel
     from rag_tl_domainllm_optimizer_amd.data import SyntheticCorpus
@@ -401,9 +405,10 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
             print(json.dumps(res), flush=True)
         parallel.shutdown()
         return
-    # ---- config 5: the SFT-adapted policy continues into PPO (same adapters, fp8 inference) ----
+    # ---- config 5: the SFT-adapted policy continues into PPO (same adapters, fp8 inference and,
+    # with --fp8-train, fp8 frozen-base forwards in the update) ----
     if args.fp8:
-        policy.set_fp8(True)
+        policy.set_fp8(True, train=args.fp8_train)
     policy.kv_fp8 = bool(args.fp8_kv)
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
                    lora_r=16, lora_alpha=32.0, seed=0)
@@ -424,11 +429,13 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
     res2 = {"metric": "RAG -> LoRA SFT -> PPO pipeline, " + args.model, "value": toks / el2, "unit": "tokens/s",
             "n_gpus": di.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el2 / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp8-e4m3fn inference / bf16 training" if args.fp8 else "bf16",
+            "dtype": ("fp8-e4m3fn inference + frozen-base training forwards / bf16 adapters and backward"
+                      if args.fp8_train else "fp8-e4m3fn inference / bf16 training") if args.fp8 else "bf16",
             "data": "synthetic (random-init weights, synthetic corpus)",
             "config": {"model": args.model, "global_batch": args.rollout_batch * di.world,
                        "seq_len": args.max_prompt + args.new_tokens, "parallelism": f"dp{di.world}",
-                       "lora_r": 16, "fp8": bool(args.fp8), "fp8_kv": bool(args.fp8_kv)},
+                       "lora_r": 16, "fp8": bool(args.fp8), "fp8_kv": bool(args.fp8_kv),
+                       "fp8_train": bool(args.fp8 and args.fp8_train)},
             "sft": res, "ppo_phase_s_per_step": {k: sum(m[k] for m in pm) / len(pm) for k in pm[0]
                                                   if k.startswith("time/")}}
     if di.is_main:

@@ -32,6 +32,8 @@ int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, lon
 int rt_gemm_small(int, int, const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
                   hipStream_t);
 int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
+int rt_gemm_big_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int,
+                    int, int, int, const void*, long, const void*, long, int, void*, long, const void*, hipStream_t);
 int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
                 int, int, int, float*, unsigned*, const void*, long, float, int, hipStream_t);
 int rt_quant_fp8_rows(const void*, long, void*, long, float*, long, int, hipStream_t);
@@ -426,6 +428,38 @@ std::vector<Tensor> quant_fp8(const Tensor& x) {
                              (int)x.size(1), cur_stream()),
            "quant_fp8");
   return {q, s};
+}
+
+// W8A8 forward of a LoRA-adapted frozen projection (config 5 training, M > 64): xq [M, K] e4m3fn
+// with per-token scales sx, wq [N, K] with per-channel scales sw, plus the bf16 K-extension
+// u8 [M, Rp] · ub8 [N, Rp]^T (pre-divided by sx / sw by the caller) on the same accumulators.
+// act 5 = SwiGLU over [gate; up] (out [M, N / 2], optional pre-activation out2 [M, N]).
+Tensor gemm_fp8_lora(const Tensor& xq, const Tensor& sx, const Tensor& wq, const Tensor& sw, const Tensor& u8,
+                     const Tensor& ub8, int64_t act, const optional<Tensor>& out2) {
+  CHECK_CUDA(xq); CHECK_F32(sx); CHECK_F32(sw); CHECK_BF16(u8); CHECK_BF16(ub8);
+  TORCH_CHECK(xq.scalar_type() == at::kByte && wq.scalar_type() == at::kByte, "gemm_fp8_lora: e4m3fn operands");
+  CHECK_ROWS(xq); CHECK_ROWS(wq); CHECK_ROWS(u8); CHECK_ROWS(ub8);
+  const int64_t M = xq.size(0), K = xq.size(1), N = wq.size(0), Rp = u8.size(1);
+  TORCH_CHECK(wq.size(1) == K && sx.numel() == M && sw.numel() == N && u8.size(0) == M && ub8.size(0) == N &&
+                  ub8.size(1) == Rp && Rp % 8 == 0, "gemm_fp8_lora: shapes");
+  TORCH_CHECK(act == 0 || act == 5, "gemm_fp8_lora: act 0 or SwiGLU");
+  const int64_t Nout = act == 5 ? N / 2 : N;
+  Tensor c = at::empty({M, Nout}, xq.options().dtype(at::kBFloat16));
+  void* c2 = nullptr;
+  long ldc2 = 0;
+  if (out2.has_value() && out2->defined()) {
+    TORCH_CHECK(act == 5 && out2->scalar_type() == at::kBFloat16 && out2->size(0) == M && out2->size(1) == N &&
+                    out2->stride(1) == 1, "gemm_fp8_lora: out2 is the [M, N] SwiGLU pre-activation");
+    c2 = out2->data_ptr();
+    ldc2 = out2->stride(0);
+  }
+  if (M == 0) return c;
+  check_rc(rt_gemm_big_fp8(xq.data_ptr(), xq.stride(0), sx.data_ptr<float>(), wq.data_ptr(), wq.stride(0),
+                           sw.data_ptr<float>(), nullptr, c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K, (int)act,
+                           u8.data_ptr(), u8.stride(0), ub8.data_ptr(), ub8.stride(0), (int)Rp, c2, ldc2,
+                           zero_page(u8).data_ptr(), cur_stream()),
+           "gemm_fp8_lora");
+  return c;
 }
 
 Tensor gemm_fp8(const Tensor& a, const optional<Tensor>& sa, const Tensor& wq, const Tensor& sw,
@@ -1099,6 +1133,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
   m.def("attn_decode_fused_slabs", &attn_decode_fused_slabs, "decode attention with the qkv split-K reduce fused");
+  m.def("gemm_fp8_lora", &gemm_fp8_lora, "W8A8 GEMM + bf16 LoRA K-extension (config-5 training forward)");
   m.def("attn_decode_set_fp8kv", &attn_decode_set_fp8kv, "fp8 K/V cache scales for the next decode attention call");
   m.def("kv_store_fp8", &kv_store_fp8, "prompt K/V -> fp8 cache (per-slot scales)");
   m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");

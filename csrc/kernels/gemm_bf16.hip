@@ -1601,7 +1601,8 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
 }
 
 extern "C" int rt_gemm_big_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*,
-                               long, int, int, int, int, hipStream_t);
+                               long, int, int, int, int, const void*, long, const void*, long, int, void*, long,
+                               const void*, hipStream_t);
 
 // fp8 GEMMs: C[M,N] (bf16) = act( (A_q B_q^T) * sa[row] * sb[col] + bias ), A_q / B_q OCP e4m3fn.
 //  * M > 64 : W8A8, 256x256 8-phase kernel on MX-scaled mfma_16x16x128_f8f6f4 (2x the bf16 rate)
@@ -1670,7 +1671,8 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
     if (K % 128 || N % 8) return -1;
     static const int use256 = getenv("RT_GEMM_FP8_256") ? atoi(getenv("RT_GEMM_FP8_256")) : 0;
     if (!use256 && lda % 16 == 0 && ldb % 16 == 0 && ldc % 8 == 0 && (act == 0 || (act == ACT_SWIGLU && N % 256 == 0)))
-      return rt_gemm_big_fp8(A, lda, sa, B, ldb, sb, bias, C, ldc, M, N, K, act == ACT_SWIGLU ? 5 : 0, stream);
+      return rt_gemm_big_fp8(A, lda, sa, B, ldb, sb, bias, C, ldc, M, N, K, act == ACT_SWIGLU ? 5 : 0, nullptr, 0,
+                             nullptr, 0, 0, nullptr, 0, nullptr, stream);
     if (act == ACT_SWIGLU) return -2;
     const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
     hipLaunchKernelGGL((gemm_256_kernel<false, true>), dim3(tiles), dim3(512), 0, stream, p);

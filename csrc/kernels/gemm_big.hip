@@ -335,13 +335,15 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   // 4 CONSECUTIVE output columns of one row (16-B fp32 / 8-B bf16 epilogue stores instead of
   // 2-4-B scattered ones). The atomic form keeps C (16 consecutive columns per 16 lanes per row).
   constexpr bool SWAP = OUT != O_F32_ATOMIC;
-#define GB_MMA(SA, SB, FB)                                                                   \
+#define GB_MMA(SA, SB, FB) GB_MMA_X(SA, SB, FB, false)
+  // EXT (F8 only): a K-extension step (LoRA, bf16 operands) inside an fp8 GEMM -> bf16 MFMAs
+#define GB_MMA_X(SA, SB, FB, EXT)                                                            \
   do {                                                                                      \
     GB_BARRIER();                                                                           \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                      \
     __builtin_amdgcn_sched_barrier(0);                                                      \
     __builtin_amdgcn_s_setprio(1);                                                          \
-    if constexpr (F8) {                                                                     \
+    if (F8 && !(EXT)) {                                                                     \
       /* the 32 bytes of a lane are the same two 16-B chunks of A and B rows: one k pairing */ \
       _Pragma("unroll") for (int i = 0; i < 4; ++i)                                         \
         _Pragma("unroll") for (int j = 0; j < NB; ++j)                                      \
@@ -406,29 +408,31 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     for (; t < t_end; ++t) {
       const int buf = t & 1;
       const bool n1 = t + 1 < t_end, n2 = t + 2 < t_end;
+      const bool ext = F8 && t >= nk1;  // fp8 GEMM: the LoRA K-extension steps are bf16
       // p1: quadrant a0 x b0; stage b1(t+1); retire b1(t) (issued after it: a1(t), a0 / b0 / b1 (t+1))
       read_a(buf, 0);
       read_b(buf, 0, fb0);
       if (n1) stage(3, t + 1);
       wait_granules<BN>(n1 ? 4 : 1);
-      GB_MMA(0, 0, fb0);
+      GB_MMA_X(0, 0, fb0, ext);
       // p2: a0 x b1; stage a1(t+1); retire a1(t)
       read_b(buf, 1, fb1);
       if (n1) stage(1, t + 1);
       wait_granules<BN>(n1 ? 4 : 0);
-      GB_MMA(0, 1, fb1);
+      GB_MMA_X(0, 1, fb1, ext);
       // p3: a1 x b1; stage a0(t+2)
       read_a(buf, 1);
       if (n2) stage(0, t + 2);
-      GB_MMA(1, 1, fb1);
+      GB_MMA_X(1, 1, fb1, ext);
       // p4: a1 x b0; stage b0(t+2); retire a0 / b0 of t+1 (after them: b1 / a1 (t+1), a0 / b0 (t+2))
       if (n2) stage(2, t + 2);
       if (n1) wait_granules<BN>(n2 ? 4 : 2);
-      GB_MMA(1, 0, fb0);
+      GB_MMA_X(1, 0, fb0, ext);
     }
     if (wr == 0) GB_BARRIER();
   }
 #undef GB_MMA
+#undef GB_MMA_X
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -1283,17 +1287,22 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
 // (E_SWIGLU: B = [gate; up], C [M, N / 2]). The fp8 rows are the bf16 kernel's operands at half
 // the K (the same 128-B LDS rows, one 16x16x128 MX MFMA per 64-bf16 K-step at twice the bf16
 // rate), with the same wave planner: 256x256 tiles, the last partial wave on 256x128.
+// A2 [M, K2] / B2 [N, K2] (bf16, optional): a K-extension (LoRA U / UB) run on bf16 MFMAs into
+// the same accumulators — the caller pre-divides them by sa / sb so the epilogue scaling leaves
+// A2 B2^T as it is. C2 (E_SWIGLU, optional): the bf16 [gate | up] pre-activation, as gemm_big.
 extern "C" int rt_gemm_big_fp8(const void* A, long lda, const float* sa, const void* B, long ldb, const float* sb,
                                const void* bias, void* C, long ldc, int M, int N, int K, int act,
-                               hipStream_t stream) {
+                               const void* A2, long lda2, const void* B2, long ldb2, int K2, void* C2, long ldc2,
+                               const void* zpage, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 128 || lda % 16 || ldb % 16 || ldc % 8 || (act != E_NONE && act != E_SWIGLU)) return -1;
   if (act == E_SWIGLU && N % 256) return -3;
+  if ((A2 || B2) && (!A2 || !B2 || K2 % 8 || !zpage)) return -4;
   Args p{};
   p.A = (const bf16_t*)A; p.lda = lda / 2; p.B = (const bf16_t*)B; p.ldb = ldb / 2;
-  p.A2 = nullptr; p.B2 = nullptr; p.K2 = 0;
-  p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = nullptr; p.ldc2 = 0; p.R = nullptr; p.ldr = 0;
-  p.M = M; p.N = N; p.K = K / 2; p.act = act; p.nsplit = 1; p.zpage = (const bf16_t*)A; p.b_nt = 0;
+  p.A2 = (const bf16_t*)A2; p.lda2 = lda2; p.B2 = (const bf16_t*)B2; p.ldb2 = ldb2; p.K2 = A2 ? K2 : 0;
+  p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = (bf16_t*)C2; p.ldc2 = ldc2; p.R = nullptr; p.ldr = 0;
+  p.M = M; p.N = N; p.K = K / 2; p.act = act; p.nsplit = 1; p.zpage = (const bf16_t*)(zpage ? zpage : A); p.b_nt = 0;
   p.sa = sa; p.sb = sb;
   const int tiles_m = (M + 255) / 256;
   const int tn256 = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
@@ -1327,8 +1336,10 @@ extern "C" int rt_gemm_big_fp8(const void* A, long lda, const float* sa, const v
     Args q = p;
     q.M = M - (int)r0;
     q.A = p.A + r0 * p.lda;
+    if (p.A2) q.A2 = p.A2 + r0 * p.lda2;
     q.sa = sa + r0;
     q.C = (char*)C + r0 * ldc * 2;
+    if (p.C2) q.C2 = p.C2 + r0 * p.ldc2;
     launch(q, 128);
   }
   RT_LAUNCH_CHECK();

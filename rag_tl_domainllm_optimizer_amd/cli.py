@@ -124,7 +124,7 @@ def _apply_fp8(cfg, policy):
     """config 5: fp8 e4m3fn weight images for the no-grad forwards (``model.fp8``)."""
     if policy is not None and getattr(cfg.model, "fp8", False) and hasattr(policy, "set_fp8"):
         if next(policy.parameters()).is_cuda:
-            policy.set_fp8(True)
+            policy.set_fp8(True, train=getattr(cfg.model, "fp8_train", False))
     if policy is not None and getattr(cfg.model, "fp8_kv", False) and hasattr(policy, "kv_fp8"):
         if next(policy.parameters()).is_cuda:
             policy.kv_fp8 = True  # generators built on the policy keep an e4m3fn K/V cache

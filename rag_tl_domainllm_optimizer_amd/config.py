@@ -32,6 +32,9 @@ class ModelSection:
     # fp8 (e4m3fn, per-slot scales) K/V cache for rollout / RAG-answer generation (config 5): half
     # the bytes the decode attention streams
     fp8_kv: bool = False
+    # with fp8: the frozen base product of LoRA training forwards on the fp8 MFMA too (adapter
+    # term and backward stay bf16; loss parity checked in tests/test_kernels_gpu.py)
+    fp8_train: bool = False
 
 
 @dataclass
@@ -86,7 +89,7 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     "config4_ppo_mistral7b": {"model.policy": "mistral-7b:random", "ppo.lora_r": 16, "data.batch_size": 64},
     # 5: Llama-2-13B full pipeline (RAG -> LoRA SFT -> PPO) on 8 GPUs
     "config5_pipeline_llama13b": {"model.policy": "llama2-13b:random", "sft.lora_r": 16, "ppo.lora_r": 16,
-                                  "model.fp8": True, "model.fp8_kv": True},
+                                  "model.fp8": True, "model.fp8_kv": True, "model.fp8_train": True},
 }
 
 

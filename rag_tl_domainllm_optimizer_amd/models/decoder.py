@@ -57,6 +57,7 @@ class DecoderLayer(nn.Module):
         self.lora_enabled = True
         # fp8 inference images of the projection weights (CausalLM.set_fp8)
         self.fp8_enabled = False
+        self.fp8_train = False  # W8A8 frozen-base product in LoRA training forwards (config 5)
         self._fp8: Dict[str, ops.Fp8Cache] = {}
         # norm-folded weights of the fused decode path (Llama/Mistral)
         self._fold: Dict[str, ops.FoldCache] = {}
@@ -74,7 +75,9 @@ class DecoderLayer(nn.Module):
     def _f8(self, name):
         if not self.fp8_enabled:
             return None
-        return self._fp8.setdefault(name, ops.Fp8Cache())
+        c = self._fp8.setdefault(name, ops.Fp8Cache())
+        c.train = self.fp8_train  # config 5: W8A8 training forwards of the frozen base too
+        return c
 
     def _dec_caches(self, f8name: str, shufname: str, w: torch.Tensor, m: int):
         """(Fp8Cache, ShufCache) for one decode projection at batch ``m``: the fp8 image except
@@ -439,13 +442,16 @@ class CausalLM(nn.Module):
         if self._head_shuf is not None:
             self._head_shuf.get(self.head_weight)
 
-    def set_fp8(self, on: bool = True):
+    def set_fp8(self, on: bool = True, train: Optional[bool] = None):
         """fp8 (e4m3fn) weights for no-grad forwards (prefill, decode, reference scoring):
-        W8A8 MX-MFMA GEMMs for M > 64, W8A16 weight streaming for decode. Training forwards
-        (autograd) keep the bf16 weights. Returns the previous setting."""
+        W8A8 MX-MFMA GEMMs for M > 64, W8A16 weight streaming for decode. ``train``: the frozen
+        base product of LoRA training forwards runs W8A8 as well (the adapter term and every
+        backward GEMM stay bf16); None keeps the current setting. Returns the previous ``on``."""
         prev = any(layer.fp8_enabled for layer in self.layers)
         for layer in self.layers:
             layer.fp8_enabled = on
+            if train is not None:
+                layer.fp8_train = bool(train) and on
         return prev
 
     def refresh_lora(self):

@@ -69,7 +69,19 @@ def fp8_supported(w: torch.Tensor) -> bool:
 class Fp8Cache(dict):
     """fp8 image of one weight, refreshed in place when the source tensor changes (address or
     in-place version, e.g. a re-merged LoRA weight) so graph-captured decode steps stay valid.
-    ``shuf`` adds the tile-ordered decode image (built on first use, then kept in step)."""
+    ``shuf`` adds the tile-ordered decode image (built on first use, then kept in step).
+    ``train`` (config 5, ``model.fp8_train``): training forwards of the frozen base run W8A8 too,
+    from ``train_cache()`` — a second image of the UNMERGED base weight, so rollouts (merged
+    weights) and updates (base weights) do not re-quantise each other's image every step."""
+
+    train = False
+
+    def train_cache(self) -> "Fp8Cache":
+        tc = getattr(self, "_train_cache", None)
+        if tc is None:
+            tc = Fp8Cache()
+            self._train_cache = tc
+        return tc
 
     @torch.no_grad()
     def get(self, w: torch.Tensor):

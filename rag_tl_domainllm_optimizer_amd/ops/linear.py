@@ -263,9 +263,19 @@ def _dropout_mask(x: torch.Tensor, p: float) -> torch.Tensor:
     return (keep / (1.0 - p)).to(x.dtype)
 
 
+def _fp8_train_ok(f8, x2, w, bias, act, lora) -> bool:
+    """The config-5 fp8 training forward applies: a frozen base weight under LoRA (no dropout),
+    W8A8-compatible shapes, no bias, plain or SwiGLU epilogue, M > 64, on the GPU."""
+    if f8 is None or lora is None or lora.dropout > 0 or bias is not None or not on_gpu(x2) or x2.shape[0] <= 64:
+        return False
+    from .fp8 import fp8_supported
+
+    return fp8_supported(w) and x2.shape[1] % 128 == 0 and (act == 0 or (act == ACT_SWIGLU and w.shape[0] % 256 == 0))
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], *lora_params):
+    def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], f8, *lora_params):
         u = ub = xd = None
         mask = None
         if lora is not None:
@@ -279,7 +289,22 @@ class _LinearFn(torch.autograd.Function):
         ctx.lora = lora
         ctx.has_bias = bias is not None
         pre = None
-        if act == ACT_SWIGLU:
+        if _fp8_train_ok(f8, x2, w, bias, act, lora):
+            # config 5: the frozen base product on the fp8 MFMA (W8A8: per-token x, per-channel W
+            # scales), the adapter term as a bf16 K-extension of the same accumulators — its
+            # operands pre-divided by the scales the epilogue applies. The backward stays bf16.
+            from .fp8 import quantize_fp8
+
+            wq, sw = f8.get(w)
+            xq, sx = quantize_fp8(x2)
+            u8 = (u.float() / sx[:, None]).to(x2.dtype)
+            ub8 = (ub.float() / sw[:, None]).to(x2.dtype)
+            if act == ACT_SWIGLU:
+                pre = torch.empty(x2.shape[0], w.shape[0], dtype=x2.dtype, device=x2.device)
+                y = native().gemm_fp8_lora(xq, sx, wq, sw, u8, ub8, ACT_SWIGLU, pre)
+            else:
+                y = native().gemm_fp8_lora(xq, sx, wq, sw, u8, ub8, 0, None)
+        elif act == ACT_SWIGLU:
             # w = [gate; up]: ONE GEMM writes silu(g) * u and the [M, 2F] pre-activation (kept for
             # the SwiGLU backward) from its epilogue — no separate SwiGLU pass over the activations
             pre = torch.empty(x2.shape[0], w.shape[0], dtype=x2.dtype, device=x2.device)
@@ -345,7 +370,7 @@ class _LinearFn(torch.autograd.Function):
                 lora_grads.append((ga_all[r0:r0 + ri] * s).to(a.dtype))
                 lora_grads.append(gb_all[c0:c0 + ni, r0:r0 + ri].to(b.dtype))
             # parameter order in forward(*lora_params) is a0, b0, a1, b1, ...
-        return (dx, dw, db, None, None, *lora_grads)
+        return (dx, dw, db, None, None, None, *lora_grads)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional[LoRAGroup] = None, fp8=None):
@@ -365,14 +390,15 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
     if act_id == ACT_SWIGLU:
         # SwiGLU is the GEMM epilogue. no-grad: skinny kernels for decode, gemm_big otherwise;
         # training (_LinearFn): gemm_big also writes the [gate | up] pre-activation for backward
-        if on_gpu(x2) and grad_needed and bias is None and fp8 is None and w.shape[0] % 256 == 0 \
+        if on_gpu(x2) and grad_needed and bias is None and w.shape[0] % 256 == 0 \
                 and x2.shape[1] % 8 == 0 and x2.shape[0] > 64 and w.dtype == torch.bfloat16 \
                 and not (use_lora and lora.use_merged):
             params = []
             if use_lora:
                 for a, b in zip(lora.a, lora.b):
                     params += [a, b]
-            y = _LinearFn.apply(x2, w, None, ACT_SWIGLU, lora if use_lora else None, *params)
+            f8 = fp8.train_cache() if (fp8 is not None and fp8.train) else None
+            y = _LinearFn.apply(x2, w, None, ACT_SWIGLU, lora if use_lora else None, f8, *params)
             return y.reshape(*shp[:-1], w.shape[0] // 2)
         if on_gpu(x2) and not grad_needed and bias is None and w.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0 \
                 and (x2.shape[0] <= 64 or w.shape[0] % 256 == 0):
@@ -419,7 +445,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
         if use_lora:
             for a, b in zip(lora.a, lora.b):
                 params += [a, b]
-        y = _LinearFn.apply(x2, w, bias, act_id, lora if use_lora else None, *params)
+        f8 = fp8.train_cache() if (fp8 is not None and fp8.train) else None
+        y = _LinearFn.apply(x2, w, bias, act_id, lora if use_lora else None, f8, *params)
     return y.reshape(*shp[:-1], w.shape[0])
 
 

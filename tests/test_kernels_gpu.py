@@ -1030,3 +1030,38 @@ def test_gemm_fp8_w8a8_swiglu_fused(M, F, K):
     g, u = xd @ wd[:F].t(), xd @ wd[F:].t()
     _close(y, torch.nn.functional.silu(g) * u)
     _close(ops.native().gemm_fp8(xq, sx, wq, sw, None, 0, None), xd @ wd.t())
+
+
+def test_fp8_training_forward_loss_parity():
+    """config 5 ``model.fp8_train``: the frozen base product of LoRA training forwards on W8A8
+    (adapter as a bf16 K-extension, bf16 backward) keeps the loss and the adapter gradients of
+    the bf16 forward (tiny Llama, 2 x 120 tokens: every projection takes the fp8 path)."""
+    from rag_tl_domainllm_optimizer_amd import models
+
+    cfg = models.resolve_preset("tiny-llama")
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=7)
+    m.add_lora(8, 16.0, "all")
+    m.freeze_base()
+    for p in m.lora_parameters():  # non-zero B so the adapter term matters
+        p.data.normal_(0, 0.05)
+    m.refresh_lora()
+    ids = torch.randint(3, cfg.vocab_size, (2, 120), device=DEV)
+
+    def run():
+        for p in m.lora_parameters():
+            p.grad = None
+        logits = m(ids).float().view(ids.shape[0], ids.shape[1], -1)
+        loss = torch.nn.functional.cross_entropy(logits[:, :-1].reshape(-1, logits.shape[-1]), ids[:, 1:].reshape(-1))
+        loss.backward()
+        return loss.item(), torch.cat([p.grad.flatten().float() for p in m.lora_parameters()])
+
+    l16, g16 = run()
+    m.set_fp8(True, train=True)
+    try:
+        l8, g8 = run()
+        assert "q" in m.layers[0]._fp8["qkv"].train_cache(), "fp8 training forward did not run"
+    finally:
+        m.set_fp8(False, train=False)
+    assert abs(l8 - l16) <= 0.02 * abs(l16), (l8, l16)
+    cos = torch.nn.functional.cosine_similarity(g8, g16, dim=0).item()
+    assert cos > 0.98, cos
