@@ -380,6 +380,9 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
     sft = SFTTrainer(policy, tok, SFTConfig(batch_size=args.sft_batch, lora_r=16, max_seq=args.max_prompt + 64,
                                             warmup_steps=0, lr_schedule="constant"))
     B = args.sft_batch
+    sft_f8 = bool(args.mode == "pipeline" and args.fp8 and args.fp8_train)
+    if sft_f8:  # config 5: the SFT stage's frozen-base forwards on W8A8 as well
+        policy.set_fp8(True, train=True)
     for w in range(args.warmup):
         m = sft.step(ex[w * B:(w + 1) * B])
         log(f"[bench] sft warmup {w}: {m['step_time_s']:.2f}s loss={m['loss']:.3f}")
@@ -395,7 +398,8 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
     sft_tok = sum(seq_tok) * di.world
     res = {"metric": "RAFT LoRA SFT tokens/sec (node), " + args.model, "value": sft_tok / el, "unit": "tokens/s",
            "n_gpus": di.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "fp8-e4m3fn frozen-base forwards / bf16 adapters and backward" if sft_f8 else "bf16",
            "data": "synthetic (random-init weights, synthetic corpus)",
            "config": {"model": args.model, "global_batch": B * di.world, "seq_len": args.max_prompt + 64,
                       "parallelism": f"dp{di.world}", "lora_r": 16, "raft_distractors": 3},

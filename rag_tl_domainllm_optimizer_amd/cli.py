@@ -161,6 +161,8 @@ def cmd_sft(cfg, args, stack=None):
     run_dir = os.path.join(cfg.out_dir, cfg.name)
     sink = MetricsSink(run_dir if di.is_main else None, config=C.to_dict(cfg), use_wandb=cfg.use_wandb)
     tr = SFTTrainer(st["policy"], st["tokenizer"], cfg.sft, sink)
+    if getattr(cfg.model, "fp8_train", False):
+        _apply_fp8(cfg, st["policy"])  # config 5: frozen-base SFT forwards on W8A8 too
     # best / per-epoch / mid-epoch checkpoints (rl.py:357-363) in their own directory; --resume
     # continues from the most advanced of them
     hist = tr.fit(examples, epochs=cfg.data.epochs, ckpt_dir=os.path.join(run_dir, "sft_ckpt"),

@@ -266,7 +266,8 @@ def _dropout_mask(x: torch.Tensor, p: float) -> torch.Tensor:
 def _fp8_train_ok(f8, x2, w, bias, act, lora) -> bool:
     """The config-5 fp8 training forward applies: a frozen base weight under LoRA (no dropout),
     W8A8-compatible shapes, no bias, plain or SwiGLU epilogue, M > 64, on the GPU."""
-    if f8 is None or lora is None or lora.dropout > 0 or bias is not None or not on_gpu(x2) or x2.shape[0] <= 64:
+    if f8 is None or lora is None or lora.dropout > 0 or bias is not None or w.requires_grad or not on_gpu(x2) \
+            or x2.shape[0] <= 64:
         return False
     from .fp8 import fp8_supported
 

@@ -1050,7 +1050,7 @@ def test_fp8_training_forward_loss_parity():
     def run():
         for p in m.lora_parameters():
             p.grad = None
-        logits = m(ids).float().view(ids.shape[0], ids.shape[1], -1)
+        logits = m.logits(m(ids)).float().view(ids.shape[0], ids.shape[1], -1)
         loss = torch.nn.functional.cross_entropy(logits[:, :-1].reshape(-1, logits.shape[-1]), ids[:, 1:].reshape(-1))
         loss.backward()
         return loss.item(), torch.cat([p.grad.flatten().float() for p in m.lora_parameters()])
