@@ -203,3 +203,33 @@ def test_dp_sft_resume_mid_epoch_matches_uninterrupted(tmp_path):
         assert torch.equal(a["params"], b["params"])
         assert torch.equal(a["m"], b["m"])
     assert (tmp_path / "ck_crash" / "latest_trainer_state").is_dir()
+
+
+def _cli_pipeline_worker(rank, world, port, out_dir):
+    _env(rank, world, port)
+    from rag_tl_domainllm_optimizer_amd import cli, parallel
+
+    args = ["pipeline", "--model.policy=tiny-llama:random", "--model.encoder=tiny-bert:random",
+            "--data.synthetic_docs=64", "--data.doc_words=16", "--retrieval.index=flat", f"--out_dir={out_dir}",
+            "--data.n_queries=16", "--data.batch_size=4", "--ppo.max_new_tokens=6", "--ppo.max_prompt_tokens=96",
+            "--ppo.minibatch_size=2", "--sft.batch_size=2", "--sft.lora_r=4", "--ppo.lora_r=4"]
+    tr = cli.main(args)
+    torch.save({"params": torch.cat([p.detach().reshape(-1) for p in tr.flat.params]), "step": tr.global_step},
+               os.path.join(out_dir, f"pipe{rank}.pt"))
+    parallel.barrier()
+    parallel.shutdown()
+
+
+def test_dp_cli_pipeline_world2(tmp_path):
+    """Config 5 (`cli pipeline`: index -> RAFT LoRA SFT -> adapter on disk -> PPO) at world 2: the
+    SFT adapter rank 0 writes is what both ranks reload, both ranks run the same number of PPO steps
+    and end with identical trainable parameters, and the run directory holds every stage's output."""
+    world = 2
+    mp.start_processes(_cli_pipeline_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    r = [torch.load(tmp_path / f"pipe{i}.pt", weights_only=True) for i in range(world)]
+    assert r[0]["step"] == r[1]["step"] > 0
+    assert torch.equal(r[0]["params"], r[1]["params"])
+    run = tmp_path / "run"
+    assert os.path.isdir(run / "sft_adapter") and os.path.isdir(run / "best_model_adapter")
+    assert os.path.exists(run / "metrics.jsonl")
