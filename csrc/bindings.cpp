@@ -77,6 +77,7 @@ int rt_grad_sumsq_mixed(const void*, long, const float*, long, float*, int, hipS
 int rt_adamw_mixed(float*, const void*, long, const float*, float*, float*, void*, long, float, float, float, float,
                    float, int, float, const float*, int, float*, int*, hipStream_t);
 int rt_pool_norm(const void*, const int*, int, int, int, int, float*, hipStream_t);
+int rt_scatter_scaled(const long*, int, long, hipStream_t);
 int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*, hipStream_t);
 int rt_segment_mean(const float*, int, const long*, const int*, int, int, float*, hipStream_t);
 int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const int*, const void*, const long*, const float*,
@@ -945,6 +946,16 @@ void adamw(Tensor p, const Tensor& g, Tensor m, Tensor v, const optional<Tensor>
            "adamw");
 }
 
+// Batched scaled fp32 -> bf16 scatter (LoRA compute images): tab int64 [n, 7] on the device =
+// {src, src_ld, dst, dst_ld, rows, cols, fp32 scale bits}; max_elems = max rows * cols.
+void scatter_scaled(const Tensor& tab, int64_t max_elems) {
+  CHECK_CUDA(tab);
+  TORCH_CHECK(tab.scalar_type() == at::kLong && tab.dim() == 2 && tab.size(1) == 7 && tab.is_contiguous(),
+              "scatter_scaled: table must be contiguous int64 [n, 7]");
+  check_rc(rt_scatter_scaled((const long*)tab.data_ptr<int64_t>(), (int)tab.size(0), (long)max_elems, cur_stream()),
+           "scatter_scaled");
+}
+
 // Full-parameter training of a bf16 model (ops.MixedFlatParams): bf16 gradients g16 of the first
 // n16 elements + fp32 gradients g32 of the fp32 tail; fp32 master p and moments over all n; the bf16
 // compute copy p16 of the first n16 elements is rewritten in the same pass.
@@ -1169,6 +1180,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("logprob_bwd", &logprob_bwd);
   m.def("sample", &sample);
   m.def("adamw", &adamw);
+  m.def("scatter_scaled", &scatter_scaled, "batched scaled fp32 -> bf16 strided scatter (LoRA images)");
   m.def("adamw_mixed", &adamw_mixed);
   m.def("grad_norm", &grad_norm);
   m.def("pool_norm", &pool_norm);

@@ -173,3 +173,35 @@ extern "C" int rt_adamw_mixed(float* p, const void* g16, long n16, const float* 
   RT_LAUNCH_CHECK();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Batched scaled scatter fp32 -> bf16 (LoRA compute images after an optimizer step): entry e of
+// the int64 table [n, 7] = {src, src_ld, dst, dst_ld, rows, cols, bit pattern of the fp32 scale}
+// writes dst[r * dst_ld + c] = bf16(src[r * src_ld + c] * scale). One launch rebuilds every
+// adapter's A_pad (scaled A rows) and UB (B blocks at their column / rank offsets) of a model,
+// instead of two torch copies (plus a scale) per adapter. blockIdx.y = entry.
+namespace rt {
+__global__ __launch_bounds__(256) void scatter_scaled_kernel(const long* __restrict__ tab) {
+  const long* t = tab + (long)blockIdx.y * 7;
+  const float* src = (const float*)t[0];
+  bf16_t* dst = (bf16_t*)t[2];
+  const long sld = t[1], dld = t[3], rows = t[4], cols = t[5];
+  const float scale = __int_as_float((int)t[6]);
+  const long n = rows * cols;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long r = e / cols, c = e - r * cols;
+    dst[r * dld + c] = f2bf(src[r * sld + c] * scale);
+  }
+}
+}  // namespace rt
+
+extern "C" int rt_scatter_scaled(const long* tab, int n, long max_elems, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (n > 65535) return -1;
+  long bx = (max_elems + 255) / 256;
+  if (bx > 64) bx = 64;
+  if (bx < 1) bx = 1;
+  hipLaunchKernelGGL(scatter_scaled_kernel, dim3((unsigned)bx, (unsigned)n), dim3(256), 0, stream, tab);
+  RT_LAUNCH_CHECK();
+  return 0;
+}

@@ -455,9 +455,13 @@ class CausalLM(nn.Module):
         return prev
 
     def refresh_lora(self):
-        for layer in self.layers:
-            for g in layer.lora.values():
-                g.refresh(dtype=self.dtype)
+        """Rebuild every adapter's bf16 compute images after an optimizer step: one native launch
+        for the whole model on the GPU (``ops.refresh_lora_batched``), per-group copies otherwise."""
+        groups = [g for layer in self.layers for g in layer.lora.values()]
+        if ops.refresh_lora_batched(groups, self.dtype):
+            return
+        for g in groups:
+            g.refresh(dtype=self.dtype)
 
     def freeze_base(self):
         for n, p in self.named_parameters():

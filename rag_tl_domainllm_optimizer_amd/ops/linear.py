@@ -133,15 +133,16 @@ def gemm_nn(dy: torch.Tensor, w: torch.Tensor, du=None, a_pad=None) -> torch.Ten
     return gemm_big(dy, w, ROW, KMAJ, du, a_pad)
 
 
-def gemm_tn(a: torch.Tensor, b: torch.Tensor, nsplit: int = 0, out=None) -> torch.Tensor:
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, nsplit: int = 0, out=None, zeroed: bool = False) -> torch.Tensor:
     """a^T b in fp32 (weight / LoRA gradients): a [T, P], b [T, Q] -> [P, Q]; the token reduction
     is split over ``nsplit`` workgroup rows (0 = fill the chip) with fp32 atomic accumulation.
-    Narrow outputs (a LoRA rank side of 64) run on the 64x64-tile kernel, wide ones on gemm_big."""
+    Narrow outputs (a LoRA rank side of 64) run on the 64x64-tile kernel, wide ones on gemm_big.
+    ``zeroed``: ``out`` is already zero (one fill shared by several products)."""
     T, P = a.shape
     Q = b.shape[1]
     if out is None:
         out = torch.zeros(P, Q, dtype=torch.float32, device=a.device)
-    else:
+    elif not zeroed:
         out.zero_()
     if not on_gpu(a):
         out.add_(a.float().t() @ b.float())
@@ -234,7 +235,52 @@ class LoRAGroup:
         return self.merged
 
 
-def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0) -> torch.Tensor:
+_SCATTER_TABLES: dict = {}
+
+
+def refresh_lora_batched(groups: List["LoRAGroup"], dtype=torch.bfloat16) -> bool:
+    """Rebuild the bf16 compute images (``a_pad`` = scaled A rows, ``ub`` = B blocks) of many LoRA
+    groups in ONE native launch (``scatter_scaled``) instead of ``LoRAGroup.refresh``'s two torch
+    copies and a scale per adapter — after every optimizer step that was ~7 x 3 launches per layer.
+    The descriptor table (device int64) is cached per set of buffer addresses. Returns False when
+    the groups are not fp32-parameter / bf16-image GPU groups (the caller refreshes eagerly)."""
+    import struct
+
+    if not groups or dtype != torch.bfloat16 or not on_gpu(groups[0].a[0]):
+        return False
+    rows, key = [], []
+    for g in groups:
+        K = g.a[0].shape[1]
+        if g.a_pad is None or g.a_pad.shape != (g.rp, K) or g.a_pad.dtype != dtype or g.a_pad.device != g.a[0].device:
+            g.refresh(dtype=dtype)  # allocates the images (and fills them this once)
+        if not g.r0:
+            r = 0
+            for a in g.a:
+                g.r0.append(r)
+                r += a.shape[0]
+        rp = g.ub.shape[1]
+        for a, b, r0, c0, sc in zip(g.a, g.b, g.r0, g.col0, g.scale):
+            if a.dtype != torch.float32 or b.dtype != torch.float32 or a.stride(1) != 1 or b.stride(1) != 1:
+                return False
+            ri, ni = a.shape[0], b.shape[0]
+            bits = struct.unpack("<i", struct.pack("<f", float(sc)))[0]
+            rows.append((a.data_ptr(), a.stride(0), g.a_pad.data_ptr() + 2 * r0 * g.a_pad.stride(0),
+                         g.a_pad.stride(0), ri, K, bits))
+            rows.append((b.data_ptr(), b.stride(0), g.ub.data_ptr() + 2 * (c0 * rp + r0), rp, ni, ri,
+                         struct.unpack("<i", struct.pack("<f", 1.0))[0]))
+        g.merged_dirty = True
+    key = (groups[0].a[0].device, tuple(rows))
+    ent = _SCATTER_TABLES.get(key)
+    if ent is None:
+        if len(_SCATTER_TABLES) > 8:
+            _SCATTER_TABLES.clear()
+        tab = torch.tensor(rows, dtype=torch.int64).to(groups[0].a[0].device)
+        ent = _SCATTER_TABLES[key] = (tab, max(r[4] * r[5] for r in rows))
+    native().scatter_scaled(ent[0], ent[1])
+    return True
+
+
+def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0, zero32=None) -> torch.Tensor:
     """a [M, K] (ROW) times a narrow operand b (ROW [R, K] or KMAJ [K, R]; R = padded LoRA rank) ->
     [M, R] bf16 on the 64x64-tile kernel (U = X A_pad^T forward, dU = dY UB backward). One
     workgroup per 64 tokens leaves most CUs idle at a few thousand tokens (151 workgroups at 9632
@@ -252,7 +298,8 @@ def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0) -> torch
     ns = nsplit or auto
     if ns == 1:
         return native().gemm_small(a, b, ROW, lb, 0, 1)
-    out = torch.zeros(M, R, dtype=torch.float32, device=a.device)
+    # ``zero32``: a caller-provided zeroed fp32 [M, R] accumulator (shared fill)
+    out = zero32 if zero32 is not None else torch.zeros(M, R, dtype=torch.float32, device=a.device)
     native().gemm_small(a, b, ROW, lb, 2, ns, out)
     return out.to(a.dtype)
 
@@ -343,7 +390,16 @@ class _LinearFn(torch.autograd.Function):
         needs = ctx.needs_input_grad
         dx = dw = db = None
         gpu = on_gpu(dy)
-        du = _narrow(dy, lora.ub, KMAJ) if lora is not None else None  # [M, Rp] = dL/dU
+        ws = None
+        if lora is not None and gpu:
+            # one zero fill for the three fp32 accumulators of the adapter products: dU [M, Rp]
+            # (split-K over N), dA_all [Rp, K], dB_all [N, Rp]
+            Mr, Kr, Nr, Rp = dy.shape[0], x2.shape[1], dy.shape[1], lora.ub.shape[1]
+            ws = torch.zeros(Mr * Rp + Rp * Kr + Nr * Rp, dtype=torch.float32, device=dy.device)
+            du32 = ws[:Mr * Rp].view(Mr, Rp)
+            ga_out = ws[Mr * Rp:Mr * Rp + Rp * Kr].view(Rp, Kr)
+            gb_out = ws[Mr * Rp + Rp * Kr:].view(Nr, Rp)
+        du = _narrow(dy, lora.ub, KMAJ, zero32=du32 if ws is not None else None) if lora is not None else None
         if needs[0]:
             if lora is not None and mask is None:
                 # dX = dY W + dU A_pad in ONE NN GEMM (the adapter term as K-extension steps)
@@ -364,11 +420,15 @@ class _LinearFn(torch.autograd.Function):
             # accumulate): dA_all = dU^T drop(X) [Rp, K]; dB_all = dY^T U [N, Rp] (adapter i uses
             # its diagonal block)
             xd = x2 * mask if mask is not None else x2
-            ga_all = gemm_tn(du, xd)
-            gb_all = gemm_tn(dy, u)
+            ga_all = gemm_tn(du, xd, out=ga_out, zeroed=True) if ws is not None else gemm_tn(du, xd)
+            gb_all = gemm_tn(dy, u, out=gb_out, zeroed=True) if ws is not None else gemm_tn(dy, u)
+            one_scale = len(set(lora.scale)) == 1
+            if one_scale:
+                ga_all.mul_(lora.scale[0])  # one launch for every adapter of the projection
             for a, b, r0, c0, s in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
                 ri, ni = a.shape[0], b.shape[0]
-                lora_grads.append((ga_all[r0:r0 + ri] * s).to(a.dtype))
+                ga = ga_all[r0:r0 + ri]
+                lora_grads.append((ga if one_scale else ga * s).to(a.dtype))
                 lora_grads.append(gb_all[c0:c0 + ni, r0:r0 + ri].to(b.dtype))
             # parameter order in forward(*lora_params) is a0, b0, a1, b1, ...
         return (dx, dw, db, None, None, None, *lora_grads)

@@ -87,6 +87,53 @@ def test_linear_lora_autograd(M):
         _close(p.grad, pr.grad, rtol=3e-2, atol=3e-2)
 
 
+def test_linear_lora_mixed_scales_grads():
+    """Adapters of one projection with different scales: dA_i = s_i dU_i^T X per adapter (the shared
+    zero-filled accumulators and the one-launch scale apply only when the scales agree)."""
+    torch.manual_seed(3)
+    M, K, N, r = 200, 256, 192, 8
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.nn.Parameter((torch.randn(N, K, device=DEV) / 16).to(torch.bfloat16), requires_grad=False)
+    ps = [torch.nn.Parameter(torch.randn(*shp, device=DEV) * 0.05) for shp in ((r, K), (N // 2, r), (r, K), (N // 2, r))]
+    grp = ops.LoRAGroup(["q", "v"], [ps[0], ps[2]], [ps[1], ps[3]], [0, N // 2], [2.0, 0.5], N)
+    y = ops.linear(x, w, lora=grp)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    pr = [p.detach().clone().requires_grad_(True) for p in ps]
+    xr = x.float()
+    yr = xr @ w.float().t() + torch.cat([2.0 * (xr @ pr[0].t()) @ pr[1].t(), 0.5 * (xr @ pr[2].t()) @ pr[3].t()], 1)
+    (yr * g.float()).sum().backward()
+    for p, q in zip(ps, pr):
+        _close(p.grad, q.grad, rtol=3e-2, atol=3e-2)
+
+
+def test_refresh_lora_batched_matches_per_group():
+    """One-launch rebuild of every group's bf16 images (scaled A rows, B blocks) is bitwise the
+    per-group torch refresh."""
+    torch.manual_seed(4)
+    groups, ref_imgs = [], []
+    for N, K, ranks, scales in ((192, 256, (8, 8), (2.0, 0.5)), (512, 384, (16,), (2.0,)), (96, 128, (4, 4, 4), (1.0,) * 3)):
+        n_each = N // len(ranks)
+        a = [torch.nn.Parameter(torch.randn(r, K, device=DEV)) for r in ranks]
+        b = [torch.nn.Parameter(torch.randn(n_each, r, device=DEV)) for r in ranks]
+        grp = ops.LoRAGroup([f"p{i}" for i in range(len(ranks))], a, b, [i * n_each for i in range(len(ranks))],
+                            list(scales), N)
+        grp.refresh()
+        with torch.no_grad():
+            for p in a + b:
+                p.mul_(1.7).add_(0.1)  # an "optimizer step"
+        groups.append(grp)
+    for grp in groups:
+        g2 = ops.LoRAGroup(grp.names, grp.a, grp.b, grp.col0, grp.scale, grp.n_out)
+        g2.refresh()
+        ref_imgs.append((g2.a_pad.clone(), g2.ub.clone()))
+    assert ops.refresh_lora_batched(groups, torch.bfloat16)
+    torch.cuda.synchronize()
+    for grp, (ap, ub) in zip(groups, ref_imgs):
+        assert torch.equal(grp.a_pad, ap) and torch.equal(grp.ub, ub)
+        assert grp.merged_dirty
+
+
 @pytest.mark.parametrize("M,N,K", [(96, 16384, 256), (300, 512, 8192)])
 def test_linear_lora_deep(M, N, K):
     """Deep shapes: a 16384-wide output (deep dX reduction in the NN GEMM) and an 8192-deep K
