@@ -30,7 +30,7 @@ int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, lon
                 const void*, void*, long, void*, long, const void*, long, int, int, int, int, int, int, const void*,
                 int, hipStream_t);
 int rt_gemm_small(int, int, const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
-                  hipStream_t);
+                  int, hipStream_t);
 int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
 int rt_gemm_big_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int,
                     int, int, int, const void*, long, const void*, long, int, void*, long, const void*, hipStream_t);
@@ -352,8 +352,10 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
 
 // 64x64-tile GEMM for narrow products (LoRA U / dU / dA / dB): same operand layouts as gemm_big;
 // out_mode 0 bf16 / 1 fp32 / 2 fp32 atomic accumulate into `out` (split-K over `nsplit`).
+// bm: 64 (64x64 tiles) or 128 (128x64 tiles: the narrow B image staged once per 128 A rows).
 Tensor gemm_small(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layout_b, int64_t out_mode,
-                  int64_t nsplit, optional<Tensor> out) {
+                  int64_t nsplit, optional<Tensor> out, int64_t bm) {
+  TORCH_CHECK(bm == 64 || bm == 128, "gemm_small: bm must be 64 or 128");
   CHECK_CUDA(a); CHECK_CUDA(b); CHECK_BF16(a); CHECK_BF16(b); CHECK_ROWS(a); CHECK_ROWS(b);
   CHECK_ALIGN16(a); CHECK_ALIGN16(b);
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_small: row strides must be multiples of 8");
@@ -372,7 +374,7 @@ Tensor gemm_small(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t la
   if (M == 0 || N == 0) return c;
   check_rc(rt_gemm_small((int)layout_a, (int)layout_b, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                          c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K, (int)out_mode, (int)nsplit,
-                         zero_page(a).data_ptr(), cur_stream()),
+                         zero_page(a).data_ptr(), (int)bm, cur_stream()),
            "gemm_small");
   return c;
 }
@@ -1159,7 +1161,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("bn") = 256);
   m.def("gemm_small", &gemm_small, "64x64-tile GEMM for narrow (LoRA) products", py::arg("a"), py::arg("b"),
         py::arg("layout_a"), py::arg("layout_b"), py::arg("out_mode") = 0, py::arg("nsplit") = 1,
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("bm") = 64);
   m.def("gemm_fp8", &gemm_fp8, "fp8 GEMM: W8A8 (MX MFMA 256x256) or W8A16 (skinny, M <= 64)", py::arg("a"),
         py::arg("sa") = py::none(), py::arg("wq"), py::arg("sw"), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("norm_eps") = 0.0,

@@ -584,23 +584,32 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
 // 4 waves (2 x 2, 32 x 32 each = 2 x 2 fragments), K-step 64 through a 3-slot LDS-DMA ring
 // (one slot issued, one landing, one read; counted vmcnt + raw s_barrier), several workgroups per
 // CU for latency hiding. Split-K over blockIdx.y with fp32 atomics for the token reductions.
-constexpr int SM_SLOT = 2 * 64 * 128;  // A + B images of one K-step (8 KiB each)
+// BM = 128: 128 x 64 tiles (4 waves stacked along M, 32 x 64 each = 2 x 4 fragments) for the
+// products whose WIDE operand is A (dB = dY^T U, dU = dY UB, U = X A_pad^T): the narrow B image is
+// then staged once per 128 rows of A instead of once per 64 (1.5x instead of 2x the A bytes
+// through L2 -> LDS).
 constexpr int SM_SLOTS = 3;
 
-template <int LA, int LB, int OUT>
+template <int LA, int LB, int OUT, int BM = 64>
 __global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
+  static_assert(BM == 64 || BM == 128, "gemm_small: BM");
+  constexpr int SM_A = BM * 128, SM_SLOT = SM_A + 64 * 128;  // A + B images of one K-step
+  constexpr int WN = BM == 64 ? 2 : 1;                       // waves along N
+  constexpr int NJ = 4 / WN;                                 // B fragments per wave (wave = 32 x 16 NJ)
+  constexpr int NIA = BM / 32;                               // LDS-DMA instructions per wave for A
   __shared__ __attribute__((aligned(16))) char smem[SM_SLOTS * SM_SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid / WN, wc = wid % WN;
   const int frow = lane & 15, fq = lane >> 4;
   const int tiles_n = (p.N + 63) / 64;
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
-  const int m0 = tm * 64, n0 = tn * 64;
+  const int m0 = tm * BM, n0 = tn * 64;
   const int nk = (p.K + 63) / 64;
   const int t_begin = (int)((long)blockIdx.y * nk / p.nsplit), t_end = (int)((long)(blockIdx.y + 1) * nk / p.nsplit);
 
-  // instruction j (0, 1) of this wave for operand op: ROW 8 rows x 128 B; KMAJ 16 k-rows x 64 B
+  // instruction j of this wave for operand op (NIA for A, 2 for B): ROW 8 rows x 128 B; KMAJ 16
+  // k-rows x 64 B (blocks of 32 m / n columns)
   auto stage = [&](int t) {
     char* slot = smem + ((t - t_begin) % SM_SLOTS) * SM_SLOT;
     const int k0 = t * 64;
@@ -610,24 +619,25 @@ __global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
       const long ld = op ? p.ldb : p.lda;
       const int lim = op ? p.N : p.M;
       const int mn0 = op ? n0 : m0;
+      const int ni = op ? 2 : NIA;
+      char* img = slot + (op ? SM_A : 0);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int o = wid * 2 + j;
+      for (int j = 0; j < (op ? 2 : NIA); ++j) {
+        const int o = wid * ni + j;
         if ((op ? LB : LA) == ROW) {
           const int row = o * 8 + (lane >> 3);
           const int kc = (lane & 7) ^ row_swz(row);
           const int gr = min(mn0 + row, lim - 1);
           const int kk = k0 + kc * 8;
           const bf16_t* src = kk < p.K ? base + (long)gr * ld + kk : p.zpage + (lane & 7) * 8;
-          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(slot + op * 8192 + o * 1024), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(img + o * 1024), 16, 0, 0);
         } else {
           const int blk = o >> 2, kr0 = (o & 3) * 16;
           const int kr = kr0 + (lane >> 2);
           const int ch = (lane & 3) ^ kmaj_swz(kr);
           const int col = min(mn0 + blk * 32 + ch * 8, lim - 8);
           const bf16_t* src = (k0 + kr) < p.K ? base + (long)(k0 + kr) * ld + col : p.zpage + (lane & 3) * 8;
-          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(slot + op * 8192 + blk * 4096 + kr0 * 64),
-                                           16, 0, 0);
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(img + blk * 4096 + kr0 * 64), 16, 0, 0);
         }
       }
     }
@@ -656,24 +666,28 @@ __global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
                   : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (t_begin < t_end) {
     stage(t_begin);
     if (t_begin + 1 < t_end) stage(t_begin + 1);
     for (int t = t_begin; t < t_end; ++t) {
-      // retire step t (4 DMA instructions per lane per step); step t+1 may stay in flight
-      if (t + 1 < t_end) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // retire step t (NIA + 2 DMA instructions per lane per step); step t+1 may stay in flight
+      if (t + 1 < t_end) {
+        if constexpr (BM == 64) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       asm volatile("s_barrier" ::: "memory");
       // refill the slot read in iteration t-1 (every wave passed the barrier above after reading it)
       if (t + 2 < t_end) stage(t + 2);
       const char* slot = smem + ((t - t_begin) % SM_SLOTS) * SM_SLOT;
-      i32x8 fa[2], fb[2];
+      i32x8 fa[2], fb[NJ];
       // KMAJ fragments by inline-asm transposed reads (the builtin drains the LDS-DMA ring)
       if constexpr (LA == ROW) {
 #pragma unroll
@@ -686,19 +700,23 @@ __global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
       }
       if constexpr (LB == ROW) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = rd_row(slot + 8192, wc * 32 + j * 16 + frow);
+        for (int j = 0; j < NJ; ++j) fb[j] = rd_row(slot + SM_A, wc * 32 + j * 16 + frow);
       } else {
-        rt_s16x4 v[8];
-        ds_tr16_frag2<256, 2048, 2304>(kmaj_addr(slot + 8192, wc * 32), kmaj_addr(slot + 8192, wc * 32 + 16), v);
-        fb[0] = frag_of(v);
-        fb[1] = frag_of(v + 4);
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj += 2) {
+          rt_s16x4 v[8];
+          ds_tr16_frag2<256, 2048, 2304>(kmaj_addr(slot + SM_A, wc * 32 + jj * 16),
+                                         kmaj_addr(slot + SM_A, wc * 32 + jj * 16 + 16), v);
+          fb[jj] = frag_of(v);
+          fb[jj + 1] = frag_of(v + 4);
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(half(fa[i], kk), half(fb[j], kk), acc[i][j], 0, 0, 0);
@@ -706,7 +724,7 @@ __global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
   }
   // lane holds C[m0 + 32 wr + 16 i + 4 fq + r][n0 + 32 wc + 16 j + frow]
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int col = n0 + wc * 32 + j * 16 + frow;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1359,7 +1377,7 @@ extern "C" int rt_gemm_splitk_reduce(const float* slabs, int nsplit, int M, int 
 
 // 64x64-tile GEMM (narrow LoRA products). out: 0 bf16, 1 fp32 store, 2 fp32 atomic add (split-K).
 extern "C" int rt_gemm_small(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb, void* C,
-                             long ldc, int M, int N, int K, int out, int nsplit, const void* zpage,
+                             long ldc, int M, int N, int K, int out, int nsplit, const void* zpage, int bm,
                              hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (!zpage || ((layout_a == ROW || layout_b == ROW) && K % 8)) return -1;
@@ -1369,9 +1387,14 @@ extern "C" int rt_gemm_small(int layout_a, int layout_b, const void* A, long lda
   Args p{};
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
   p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
-  dim3 grid(((M + 63) / 64) * ((N + 63) / 64), nsplit), block(256);
+  if (bm != 64 && bm != 128) return -5;
+  dim3 grid(((M + bm - 1) / bm) * ((N + 63) / 64), nsplit), block(256);
   const int key = layout_a * 100 + layout_b * 10 + out;
-#define GS_LAUNCH(LA, LB, O) hipLaunchKernelGGL((gemm_small_kernel<LA, LB, O>), grid, block, 0, stream, p)
+#define GS_LAUNCH(LA, LB, O)                                                                   \
+  do {                                                                                         \
+    if (bm == 128) hipLaunchKernelGGL((gemm_small_kernel<LA, LB, O, 128>), grid, block, 0, stream, p); \
+    else hipLaunchKernelGGL((gemm_small_kernel<LA, LB, O, 64>), grid, block, 0, stream, p);          \
+  } while (0)
   switch (key) {
     case 0: GS_LAUNCH(ROW, ROW, O_BF16); break;
     case 1: GS_LAUNCH(ROW, ROW, O_F32); break;

@@ -148,9 +148,12 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, nsplit: int = 0, out=None, zeroed:
         out.add_(a.float().t() @ b.float())
         return out
     if min(P, Q) <= 128:
-        tiles = ((P + 63) // 64) * ((Q + 63) // 64)
+        # 128x64 tiles when the wide side is A and very wide (dB of gate_up, P = 28672: 152 -> 121
+        # us at 9632 tokens, profiles/r3/small_bm_probe.log); narrower products lose parallelism
+        bm = 128 if P >= 16384 else 64
+        tiles = ((P + bm - 1) // bm) * ((Q + 63) // 64)
         ns = nsplit or max(1, min(T // 256, (1024 + tiles - 1) // tiles))
-        return native().gemm_small(a, b, KMAJ, KMAJ, 2, ns, out)
+        return native().gemm_small(a, b, KMAJ, KMAJ, 2, ns, out, bm)
     tiles = ((P + 255) // 256) * ((Q + 255) // 256)
     ns = nsplit or max(1, min(64, 256 // max(tiles, 1), T // 512))
     return gemm_big(a, b, KMAJ, KMAJ, out_mode=2, nsplit=ns, out=out)
@@ -291,16 +294,18 @@ def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0, zero32=N
         return (a.float() @ B).to(a.dtype)
     M, K = a.shape
     R = b.shape[0] if lb == ROW else b.shape[1]
-    tiles = ((M + 63) // 64) * ((R + 63) // 64)
+    # 128x64 tiles over the deepest reductions (dU of gate_up, K = 28672: 125 -> 116 us)
+    bm = 128 if K >= 24576 else 64
+    tiles = ((M + bm - 1) // bm) * ((R + 63) // 64)
     # (measured at 9632 tokens: dU 383 -> 172 us at K = 28672; U at K = 4096 is already at 3.2 TB/s
     # unsplit and only pays the fp32 pass, profiles/lora_narrow_r2.log)
     auto = 1 if (lb == ROW and K <= 4096) else max(1, min(K // 512, (768 + tiles - 1) // tiles))
     ns = nsplit or auto
     if ns == 1:
-        return native().gemm_small(a, b, ROW, lb, 0, 1)
+        return native().gemm_small(a, b, ROW, lb, 0, 1, None, bm)
     # ``zero32``: a caller-provided zeroed fp32 [M, R] accumulator (shared fill)
     out = zero32 if zero32 is not None else torch.zeros(M, R, dtype=torch.float32, device=a.device)
-    native().gemm_small(a, b, ROW, lb, 2, ns, out)
+    native().gemm_small(a, b, ROW, lb, 2, ns, out, bm)
     return out.to(a.dtype)
 
 

@@ -120,6 +120,30 @@ def test_small_tile_narrow(M, K, R):
     _close(ops.gemm_tn(x, t), x.float().t() @ t.float(), rtol=5e-3, atol=5e-3)
 
 
+@pytest.mark.parametrize("bm", [64, 128])
+@pytest.mark.parametrize("M,K,R", [(300, 4096, 64), (1000, 1024, 64), (77, 520, 128), (200, 192, 64)])
+def test_small_tile_bm(M, K, R, bm):
+    """64x64 and 128x64 tiles of the narrow-product kernel, every layout it serves, bf16 / fp32 /
+    split-K atomic outputs, partial tiles along M and K."""
+    nat = ops.native()
+    x, a = _r(M, K), _r(R, K, s=1 / math.sqrt(K))
+    _close(nat.gemm_small(x, a, ops.ROW, ops.ROW, 0, 1, None, bm), x.float() @ a.float().t())
+    ub = _r(K, R, s=1 / math.sqrt(K))
+    _close(nat.gemm_small(x, ub, ops.ROW, ops.KMAJ, 0, 1, None, bm), x.float() @ ub.float())
+    acc = torch.zeros(M, R, device=DEV)
+    nat.gemm_small(x, ub, ops.ROW, ops.KMAJ, 2, 3, acc, bm)
+    _close(acc, x.float() @ ub.float(), rtol=5e-3, atol=5e-3)
+    t = _r(M, R)  # TN: [K, R] = x^T t and [R, K] = t^T x, token reduction split 4 ways
+    out = torch.zeros(K, R, device=DEV)
+    nat.gemm_small(x, t, ops.KMAJ, ops.KMAJ, 2, 4, out, bm)
+    _close(out, x.float().t() @ t.float(), rtol=5e-3, atol=5e-3)
+    out2 = torch.zeros(R, K, device=DEV)
+    nat.gemm_small(t, x, ops.KMAJ, ops.KMAJ, 2, 4, out2, bm)
+    _close(out2, t.float().t() @ x.float(), rtol=5e-3, atol=5e-3)
+    o32 = nat.gemm_small(x, a, ops.ROW, ops.ROW, 1, 1, None, bm)
+    _close(o32, x.float() @ a.float().t(), rtol=5e-3, atol=5e-3)
+
+
 # ---- 256x128 tiles (decode at M <= 512, last partial wave of large GEMMs) and the wave planner ----
 @pytest.mark.parametrize("bn", [128, 256, 0])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 512), (300, 520, 200), (77, 136, 4096), (2900, 1024, 192)])
