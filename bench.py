@@ -14,6 +14,9 @@ value = generated rollout tokens summed over ranks / max-over-ranks wall time of
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N --steps K --warmup W
+``python bench.py --gpus N`` with N > 1 and no torchrun environment starts the N ranks itself
+(torch.distributed.run as a child process, parallel/launch.py) and exits with their status;
+RAGTL_DIST_BACKEND=gloo rehearses N ranks on one GPU.
 
 Secondary modes (not the headline; each prints its own JSON line):
   --mode sft       BASELINE config 3: RAFT-style LoRA r=16 SFT with distractor docs, tokens/s
@@ -104,6 +107,18 @@ def main():
     if args.fp8_train is None:
         args.fp8_train = bool(args.fp8)
 
+    # --gpus N without a torchrun environment: start N ranks (one process per GPU) as a child
+    # torch.distributed.run BEFORE anything touches the GPU, relay rank 0's JSON line and exit with
+    # the ranks' status (non-zero if any rank fails or the reported world is not N)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        from rag_tl_domainllm_optimizer_amd.parallel.launch import self_launch
+
+        sys.exit(self_launch(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}: refusing to report a "
+              f"mislabelled scaling point", file=sys.stderr, flush=True)
+        sys.exit(2)
+
     from rag_tl_domainllm_optimizer_amd import models, parallel
     from rag_tl_domainllm_optimizer_amd.data import SyntheticCorpus
     from rag_tl_domainllm_optimizer_amd.generation import SamplingParams
@@ -116,10 +131,14 @@ def main():
 
     di = parallel.init()
     dev = di.device
-    if args.gpus != di.world:
-        log(f"[bench] warning: --gpus {args.gpus} but {di.world} rank(s); launch one process per GPU "
-            f"(python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py ...)")
+    assert di.world == args.gpus, (di.world, args.gpus)
     assert dev.type == "cuda", "bench.py needs a GPU"
+    # one-shot collective probe (outside every timed region): the bus bandwidth a 168 MiB fp32
+    # all-reduce (the LoRA gradient payload) reaches on this job's process group (RCCL over xGMI)
+    ar_probe = parallel.allreduce_bandwidth() if di.world > 1 else None
+    if ar_probe:
+        log(f"[bench] all-reduce probe ({ar_probe['backend']}, world {di.world}): {ar_probe['bytes'] / 1e6:.0f} MB in "
+            f"{ar_probe['time_s'] * 1e3:.2f} ms, bus {ar_probe['busbw_GBps']:.1f} GB/s")
     torch.manual_seed(1234)
     t_setup = time.perf_counter()
 
@@ -143,7 +162,7 @@ def main():
     log(f"[bench] indexed {len(corpus)} docs (IVF nlist={index.nlist}) in {time.perf_counter() - t0:.1f}s")
 
     if args.mode in ("sft", "pipeline"):
-        return run_sft_pipeline(args, di, policy, tok, encoder, corpus, index)
+        return run_sft_pipeline(args, di, policy, tok, encoder, corpus, index, ar_probe)
     if args.mode == "serve":
         return run_serve(args, di, policy, tok, encoder, corpus, index)
 
@@ -265,6 +284,7 @@ def main():
         # spread of the per-rank step times (before the closing barrier) in seconds
         "allreduce_bytes_per_step": comm_bytes,
         "rank_step_s": spread,
+        "allreduce_probe": ar_probe,
     }
     if di.is_main:
         print(json.dumps(res), flush=True)
@@ -288,6 +308,8 @@ def rank_spread(step_s: float, dev) -> dict:
 
 
 def _timed(di, fn, steps):
+    """Run ``fn`` ``steps`` times between barriers + device syncs; returns (max-over-ranks wall
+    seconds, outputs, per-rank step-time spread)."""
     from rag_tl_domainllm_optimizer_amd import parallel
 
     parallel.barrier()
@@ -295,10 +317,11 @@ def _timed(di, fn, steps):
     t0 = time.perf_counter()
     out = [fn(i) for i in range(steps)]
     torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0
     parallel.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=di.device)
     parallel.all_reduce_(el, "max")
-    return float(el), out
+    return float(el), out, rank_spread(t_local / max(steps, 1), di.device)
 
 
 def run_serve(args, di, policy, tok, encoder, corpus, index):
@@ -364,7 +387,7 @@ def run_serve(args, di, policy, tok, encoder, corpus, index):
     parallel.shutdown()
 
 
-def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
+def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index, ar_probe=None):
     """config 3 (--mode sft) and config 5 (--mode pipeline) on synthetic data / random weights."""
     import random
 
@@ -394,7 +417,9 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
         seq_tok.append(int((ids.shape[1] - start).sum()))
         return sft.step(batch)
 
-    el, ms = _timed(di, sft_step, args.steps)
+    sft.sync.comm_bytes = 0
+    el, ms, sft_spread = _timed(di, sft_step, args.steps)
+    sft_bytes = sft.sync.comm_bytes / max(args.steps, 1)
     sft_tok = sum(seq_tok) * di.world
     res = {"metric": "RAFT LoRA SFT tokens/sec (node), " + args.model, "value": sft_tok / el, "unit": "tokens/s",
            "n_gpus": di.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
@@ -403,7 +428,9 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
            "data": "synthetic (random-init weights, synthetic corpus)",
            "config": {"model": args.model, "global_batch": B * di.world, "seq_len": args.max_prompt + 64,
                       "parallelism": f"dp{di.world}", "lora_r": 16, "raft_distractors": 3},
-           "final_loss": ms[-1]["loss"] if ms else None}
+           "final_loss": ms[-1]["loss"] if ms else None,
+           "world": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
+           "allreduce_bytes_per_step": sft_bytes, "rank_step_s": sft_spread, "allreduce_probe": ar_probe}
     if args.mode == "sft":
         if di.is_main:
             print(json.dumps(res), flush=True)
@@ -428,7 +455,9 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
     for w in range(args.warmup):
         ppo.step(make_batch())
     # retrieval (query encode + IVF search) inside the timed region, as in the headline mode
-    el2, pm = _timed(di, lambda i: ppo.step(make_batch()), args.steps)
+    ppo.sync.comm_bytes = 0
+    el2, pm, ppo_spread = _timed(di, lambda i: ppo.step(make_batch()), args.steps)
+    ppo_bytes = ppo.sync.comm_bytes / max(args.steps, 1)
     toks = sum(m["rollout_tokens"] for m in pm) * di.world
     res2 = {"metric": "RAG -> LoRA SFT -> PPO pipeline, " + args.model, "value": toks / el2, "unit": "tokens/s",
             "n_gpus": di.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el2 / args.steps * 1e3,
@@ -441,7 +470,9 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index):
                        "lora_r": 16, "fp8": bool(args.fp8), "fp8_kv": bool(args.fp8_kv),
                        "fp8_train": bool(args.fp8 and args.fp8_train)},
             "sft": res, "ppo_phase_s_per_step": {k: sum(m[k] for m in pm) / len(pm) for k in pm[0]
-                                                  if k.startswith("time/")}}
+                                                  if k.startswith("time/")},
+            "world": res["world"], "allreduce_bytes_per_step": ppo_bytes, "rank_step_s": ppo_spread,
+            "allreduce_probe": ar_probe}
     if di.is_main:
         print(json.dumps(res2), flush=True)
     parallel.shutdown()

@@ -230,24 +230,127 @@ def cmd_ppo(cfg, args, policy=None, stack=None):
     return tr
 
 
+# the reference's comparison columns (rl.py:446-453), in its order
+REF_MODEL_NAMES = ("Base Model", "RAG Model", "RL-finetuned Model", "Transfer-learned Model")
+
+
+def is_adapter_dir(path: str) -> bool:
+    return os.path.isfile(os.path.join(path, "adapter_config.json"))
+
+
+def _adapter_view(policy, path: Optional[str]):
+    """``prepare`` hook: the shared base policy with the PEFT adapter at ``path`` loaded and enabled,
+    or with its adapters disabled (the base model) when ``path`` is None."""
+    from .models import load_adapter
+
+    def prepare():
+        if path is None:
+            if hasattr(policy, "set_lora_enabled"):
+                policy.set_lora_enabled(False)
+            return
+        load_adapter(policy, path)
+        policy.set_lora_enabled(True)
+    return prepare
+
+
+def _held_out_records(cfg, st, n: int):
+    """Evaluation queries disjoint from the training sample of ``_records`` (another seed) with
+    their retrieved documents; the configured training file when one is given."""
+    if cfg.data.train_path or n <= 0:
+        return _records(cfg, st, n)[:n] if n > 0 else []
+    corpus, index, enc = st["corpus"], st["index"], st["encoder"]
+    items = corpus.sample_queries(n, seed=cfg.model.seed + 1013)
+    _, ids = index.search(enc.encode([it.query for it in items]), cfg.retrieval.top_k)
+    return [{"query": it.query, "retrieved_docs": [st["docs"][i] for i in row if i >= 0],
+             "ground_truth": it.ground_truth} for it, row in zip(items, ids.tolist())]
+
+
+def write_comparison(report, run_dir: str, is_main: bool = True) -> str:
+    out = os.path.join(run_dir, "model_comparison_results.csv")
+    if is_main:
+        os.makedirs(run_dir, exist_ok=True)
+        report.to_csv(out)  # rl.py:525
+        print("Model Comparison Report:")  # rl.py:521
+        print(report)
+    return out
+
+
 def cmd_eval(cfg, args):
+    """The reference's ``compare_models`` (rl.py:444-463) from the CLI: "Base Model" (bare query),
+    "RAG Model" (base + retrieved documents), then each ``--checkpoint`` — a PEFT adapter directory
+    (loaded into the base policy) or a full HF model directory. Checkpoints take the reference's
+    remaining names in its argument order (RL-finetuned, then Transfer-learned) unless given as
+    ``--checkpoint "Name=path"``."""
     from .eval import Evaluator
     from .models import build_model
     from .rewards import RewardModel
 
     di = _device()
     st = build_stack(cfg, di.device)
-    recs = _records(cfg, st, min(cfg.data.n_queries, 64))
+    recs = _held_out_records(cfg, st, min(cfg.data.n_queries, 64))
     ev = Evaluator(RewardModel(st["encoder"], cfg.reward), cfg.eval)
-    models = {"Base Model": (st["policy"], st["tokenizer"])}
-    for p in args.checkpoint or []:
-        models[os.path.basename(p.rstrip("/"))] = (build_model(p, device=di.device), st["tokenizer"])
+    base, tok = st["policy"], st["tokenizer"]
+    models = {"Base Model": (base, tok, {"include_docs": False, "prepare": _adapter_view(base, None)}),
+              "RAG Model": (base, tok, {"include_docs": True, "prepare": _adapter_view(base, None)})}
+    free_names = list(REF_MODEL_NAMES[2:])
+    for spec in args.checkpoint or []:
+        name, sep, path = spec.partition("=")
+        if not sep:
+            name, path = (free_names.pop(0) if free_names else os.path.basename(spec.rstrip("/"))), spec
+        elif name in free_names:
+            free_names.remove(name)
+        if is_adapter_dir(path):
+            models[name] = (base, tok, {"include_docs": True, "prepare": _adapter_view(base, path)})
+        else:
+            models[name] = (build_model(path, device=di.device), tok, {"include_docs": True})
     report = ev.compare_models(models, recs)
-    out = os.path.join(cfg.out_dir, cfg.name, "model_comparison_results.csv")
-    os.makedirs(os.path.dirname(out), exist_ok=True)
-    report.to_csv(out)
-    print("Model Comparison Report:")
-    print(report)
+    write_comparison(report, os.path.join(cfg.out_dir, cfg.name), di.is_main)
+    return report
+
+
+def compare_pipeline_models(cfg, st, policy, run_dir: str, is_main: bool = True):
+    """End of ``cli pipeline``: the reference's model comparison (rl.py:444-463, 491-525) over one
+    shared set of base weights — "Base Model" (adapters off, bare query), "RAG Model" (adapters
+    off, retrieved documents in the prompt), "RL-finetuned Model" (the PPO ``best_model`` adapter),
+    "Transfer-learned Model" (the SFT adapter) — written to model_comparison_results.csv. The
+    policy's live adapter values are restored afterwards (the PPO trainer keeps using them)."""
+    from .eval import Evaluator
+    from .rewards import RewardModel
+
+    n = int(getattr(cfg.eval, "compare_items", 0))
+    if n <= 0:
+        return None
+    recs = _held_out_records(cfg, st, n)
+    tok = st["tokenizer"]
+    lora = list(policy.lora_parameters()) if hasattr(policy, "lora_parameters") else []
+    saved = [p.detach().clone() for p in lora]
+    rl_dir = os.path.join(run_dir, "best_model_adapter")
+    sft_dir = os.path.join(run_dir, "sft_adapter")
+    if not lora:  # full fine-tuning: the base weights themselves were trained; only the result is left
+        report = Evaluator(RewardModel(st["encoder"], cfg.reward), cfg.eval).compare_models(
+            {"RL-finetuned Model": (policy, tok, {"include_docs": True})}, recs)
+        write_comparison(report, run_dir, is_main)
+        return report
+    models = {"Base Model": (policy, tok, {"include_docs": False, "prepare": _adapter_view(policy, None)}),
+              "RAG Model": (policy, tok, {"include_docs": True, "prepare": _adapter_view(policy, None)})}
+    if is_adapter_dir(rl_dir):
+        models["RL-finetuned Model"] = (policy, tok, {"include_docs": True, "prepare": _adapter_view(policy, rl_dir)})
+    if is_adapter_dir(sft_dir):
+        models["Transfer-learned Model"] = (policy, tok, {"include_docs": True,
+                                                          "prepare": _adapter_view(policy, sft_dir)})
+    ev = Evaluator(RewardModel(st["encoder"], cfg.reward), cfg.eval)
+    try:
+        report = ev.compare_models(models, recs)
+    finally:
+        with torch.no_grad():
+            for p, v in zip(lora, saved):
+                p.copy_(v)
+        if hasattr(policy, "set_lora_enabled"):
+            policy.set_lora_enabled(True)
+        if lora and hasattr(policy, "refresh_lora"):
+            policy.refresh_lora()
+    write_comparison(report, run_dir, is_main)
+    return report
 
 
 def cmd_pipeline(cfg, args):
@@ -262,6 +365,7 @@ def cmd_pipeline(cfg, args):
     tr, st = cmd_sft(cfg, args)
     run_dir = os.path.join(cfg.out_dir, cfg.name)
     policy = tr.model
+    tr.close()  # the SFT GradSync's post-accumulate hooks on the LoRA parameters go with it
     del tr
     if cfg.sft.full_finetune:
         mio.load_hf_state_dict(policy, mio.read_state_dict(os.path.join(run_dir, "sft_policy")))
@@ -270,7 +374,11 @@ def cmd_pipeline(cfg, args):
         load_adapter(policy, os.path.join(run_dir, "sft_adapter"))
     if policy.embed.is_cuda:
         torch.cuda.empty_cache()
-    return cmd_ppo(cfg, args, policy=policy, stack=st)
+    ppo = cmd_ppo(cfg, args, policy=policy, stack=st)
+    from . import parallel
+
+    compare_pipeline_models(cfg, st, policy, run_dir, parallel.info().is_main)
+    return ppo
 
 
 def cmd_serve(cfg, args):
@@ -286,17 +394,15 @@ def cmd_bench(cfg, args, rest):
 
 
 def cmd_launch(args, rest):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.nproc}",
-           "--master-addr", "127.0.0.1", f"--master-port={args.port}", "-m", "rag_tl_domainllm_optimizer_amd", *rest]
+    from .parallel.launch import launch_env, torchrun_cmd
+
+    cmd = torchrun_cmd(args.nproc, ["-m", "rag_tl_domainllm_optimizer_amd", *rest], args.port)
     # the caller's environment (NCCL_* / RCCL_* / HSA_* tuning) passes through to every rank;
     # --env KEY=VALUE adds or overrides entries (e.g. --env NCCL_MIN_NCHANNELS=32)
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    for kv in args.env or []:
-        k, sep, v = kv.partition("=")
-        if not sep or not k:
-            raise SystemExit(f"launch: --env expects KEY=VALUE, got {kv!r}")
-        env[k] = v
+    try:
+        env = launch_env(args.env or [])
+    except ValueError as e:
+        raise SystemExit(f"launch: {e}")
     sys.exit(subprocess.run(cmd, env=env).returncode)
 
 

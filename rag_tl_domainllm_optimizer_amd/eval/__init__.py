@@ -9,6 +9,7 @@ Fixed vs the reference: the RAG prompt includes the retrieved docum
 """
 from __future__ import annotations
 
+import dataclasses
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -32,6 +33,9 @@ class EvalConfig:
     include_docs: bool = True
     batch_size: int = 16
     seed: int = 0
+    # ``cli pipeline`` ends with the reference's model comparison (rl.py:444-463, 491-525) over this
+    # many held-out queries (0 disables it)
+    compare_items: int = 32
 
 
 class Evaluator:
@@ -40,8 +44,10 @@ class Evaluator:
         self.cfg = cfg or EvalConfig()
 
     @torch.no_grad()
-    def generate(self, model, tokenizer, items: Sequence[dict]) -> List[str]:
+    def generate(self, model, tokenizer, items: Sequence[dict], include_docs: Optional[bool] = None) -> List[str]:
         c = self.cfg
+        if include_docs is not None and include_docs != c.include_docs:
+            c = dataclasses.replace(c, include_docs=include_docs)
         prompts = []
         # the prompt keeps room for the answer: documents are dropped lowest-ranked first (as in
         # the rollouts) instead of cutting "Query: ..." off the front
@@ -66,7 +72,8 @@ class Evaluator:
                 out_txt.append(extract_answer(tokenizer.decode(o.tokens[b, :n].tolist())))
         return out_txt
 
-    def evaluate_model(self, model, tokenizer, test_data: Sequence[dict]) -> Dict[str, float]:
+    def evaluate_model(self, model, tokenizer, test_data: Sequence[dict],
+                       include_docs: Optional[bool] = None) -> Dict[str, float]:
         """Under data parallelism each rank scores its shard (items rank::world); the per-item
         scores are all-gathered (object all-gather) so every rank returns the same
         means over the whole test set."""
@@ -75,7 +82,7 @@ class Evaluator:
         di = info()
         full = list(test_data)
         test_data = full[di.rank::di.world] if di.world > 1 else full
-        responses = self.generate(model, tokenizer, test_data) if test_data else []
+        responses = self.generate(model, tokenizer, test_data, include_docs) if test_data else []
         res = {k: [] for k in METRIC_KEYS}
         for it, resp in zip(test_data, responses):
             gt = it.get("ground_truth")
@@ -99,10 +106,18 @@ class Evaluator:
         return {k: float(np.mean(v)) for k, v in res.items() if v}
 
     def compare_models(self, models: Dict[str, tuple], test_data: Sequence[dict]):
+        """``models``: name -> (model, tokenizer) or (model, tokenizer, opts) with opts
+        ``include_docs`` (per-model prompt mode: the reference's "Base Model" answers the bare
+        query, the "RAG Model" sees the retrieved documents) and ``prepare`` (a callable run right
+        before that model is evaluated, e.g. loading an adapter into a shared base)."""
         import pandas as pd
 
         comparison = {}
-        for name, (model, tok) in models.items():
+        for name, spec in models.items():
+            model, tok = spec[0], spec[1]
+            opts = spec[2] if len(spec) > 2 else {}
+            if opts.get("prepare") is not None:
+                opts["prepare"]()
             print(f"Evaluating {name}...")
-            comparison[name] = self.evaluate_model(model, tok, test_data)
+            comparison[name] = self.evaluate_model(model, tok, test_data, opts.get("include_docs"))
         return pd.DataFrame(comparison)

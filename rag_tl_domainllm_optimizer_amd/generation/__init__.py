@@ -435,12 +435,22 @@ class _Pending:
         self.loop = loop
         self._recorded = False
 
+    @torch.no_grad()
     def result(self) -> GenerationOutput:
         import time
 
         g, B = self.gen, self.B
         if self.loop is not None and not self.loop.finished:
-            self.loop.run(to_end=True)
+            # the remaining steps run under the same conditions the loop started with: no autograd,
+            # adapters merged (generate_async restored the caller's mode on return; the eager
+            # non-graph path would otherwise decode with unmerged adapters)
+            m = g.model
+            prev = m.set_lora_merged(True) if hasattr(m, "set_lora_merged") else None
+            try:
+                self.loop.run(to_end=True)
+            finally:
+                if prev is not None:
+                    m.set_lora_merged(prev)
         if self.ev and not self._recorded:
             self.ev[2].record()
             self._recorded = True
@@ -583,6 +593,20 @@ class ContinuousBatcher:
                 raise ValueError(f"prompt of {len(p)} tokens + {self.T} new exceeds the cache ({g.max_seq})")
         self.free.sort()
         rows, self.free = self.free[:len(prompts)], self.free[len(prompts):]
+        try:
+            self._admit_runs(rows, prompts, tags)
+        except BaseException:
+            # all-or-nothing: rows of this call that were already prefilled leave the batch again
+            # (inactive, back on the free list), so the caller can fail every request it passed
+            for b in rows:
+                self.rows.pop(b, None)
+            g.active[torch.tensor(rows, device=g.device)] = 0
+            self.free = sorted(self.free + rows)
+            raise
+        return rows
+
+    def _admit_runs(self, rows, prompts, tags):
+        g = self.gen
         i = 0
         while i < len(rows):
             j = i + 1
@@ -606,7 +630,6 @@ class ContinuousBatcher:
             for r in range(n):
                 self.rows[b0 + r] = (tags[i + r], len(grp[r]), self.steps)
             i = j
-        return rows
 
     def step(self, n: int = 1):
         """n decode steps over the power-of-two bucket of rows covering every active row (rows are

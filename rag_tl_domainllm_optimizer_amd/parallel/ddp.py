@@ -18,7 +18,9 @@ world 8). Mode ``"rs32"`` (default): the slice is widened to an fp32 staging buf
 reduce-scattered in fp32 (overlapped with backward, (N-1)/N x 4 B per weight), each rank rounds its
 summed shard to bf16 once, and a bf16 all-gather ((N-1)/N x 2 B) completes it in ``finish()`` —
 6 B of link traffic per weight against 4 B for a bf16 all-reduce and 8 B for an fp32 one, with a
-single rounding. ``"bf16"`` keeps the in-place bf16 all-reduce (RAGTL_BF16_REDUCE=bf16).
+single rounding. ``"bf16"`` keeps the in-place bf16 all-reduce (RAGTL_BF16_REDUCE=bf16). Memory: each
+bucket in flight holds a padded fp32 staging copy plus its fp32 shard (~(1 + 1/N) x 4 B per weight
+of the bucket); at most ``rs32_inflight`` (default 2, RAGTL_RS32_INFLIGHT) are alive at once.
 """
 from __future__ import annotations
 
@@ -71,7 +73,13 @@ class GradSync:
         self.sync_enabled = True
         self.wait_s = 0.0  # host time blocked in finish() (exposed all-reduce tail), reset by the caller
         self.comm_bytes = 0  # payload bytes handed to collectives (per rank), reset by the caller
-        self._stage2 = []    # (bf16 slice, fp32 summed shard, gathered fp32-free bf16 buffer) of rs32 buckets
+        self._stage1 = []    # rs32 buckets in flight: (bf16 slice, fp32 shard out, handle, fp32 staging buffer)
+        self._stage2 = []    # rs32 buckets reduced and rounded: (bf16 slice, bf16 summed shard)
+        # at most this many fp32 staging buffers stay alive: launching another first retires the
+        # oldest (wait, round its shard to bf16, drop both fp32 buffers), so full-parameter DP holds
+        # ~2 buckets of fp32 staging at the end of backward instead of 2x the whole bf16 gradient
+        # (~28 GB for a 7B model)
+        self.rs32_inflight = max(1, int(os.environ.get("RAGTL_RS32_INFLIGHT", "2")))
         if self.overlap:
             for p, bi in zip(flat.params, self.param_bucket):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
@@ -101,6 +109,8 @@ class GradSync:
     def _rs32(self, t: torch.Tensor):
         """Stage 1 of the fp32 reduction of a bf16 slice: widen into a padded fp32 buffer and
         reduce-scatter it (async). Stage 2 (round the shard once, bf16 all-gather) runs in finish()."""
+        while len(self._stage1) >= self.rs32_inflight:
+            self._retire_oldest()
         w = self.world
         n = t.numel()
         shard = (n + w - 1) // w
@@ -109,17 +119,22 @@ class GradSync:
         out = torch.empty(shard, dtype=torch.float32, device=t.device)
         self.comm_bytes += buf.numel() * 4
         h = dist.reduce_scatter_tensor(out, buf, async_op=True)
-        self._stage2.append((t, out, h))
+        self._stage1.append((t, out, h, buf))
         return _Done()
 
+    def _retire_oldest(self):
+        t, out, h, _buf = self._stage1.pop(0)
+        h.wait()  # on RCCL a stream dependency, not a host wait
+        self._stage2.append((t, out.to(torch.bfloat16)))  # the ONE rounding of the fp32 sum
+
     def _finish_rs32(self):
+        while self._stage1:
+            self._retire_oldest()
         if not self._stage2:
             return
         w = self.world
         gathers = []
-        for t, out, h in self._stage2:
-            h.wait()
-            shard16 = out.to(torch.bfloat16)  # the ONE rounding of the fp32 sum
+        for t, shard16 in self._stage2:
             full = torch.empty(shard16.numel() * w, dtype=torch.bfloat16, device=t.device)
             self.comm_bytes += full.numel() * 2
             gathers.append((t, full, dist.all_gather_into_tensor(full, shard16, async_op=True)))

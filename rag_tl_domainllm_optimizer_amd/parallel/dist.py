@@ -128,6 +128,39 @@ def all_gather_object(obj):
     return out
 
 
+def allreduce_bandwidth(nbytes: int = 168 << 20, iters: int = 5, warmup: int = 2) -> Optional[dict]:
+    """One-shot all-reduce probe on the job's process group: an fp32 tensor of ``nbytes`` (default
+    168 MiB, the Mistral-7B LoRA r=16 all-linear gradient payload) summed ``iters``
+    times after ``warmup``. Returns the mean time and the algorithm / bus bandwidth (bus = algbw x
+    2(N-1)/N, the bytes each rank's links carry in a ring all-reduce); None without a group. On
+    RCCL this is the xGMI figure the scaling curve rests on; over gloo it measures the host path."""
+    if not _INFO.enabled:
+        return None
+    import time
+
+    n = max(1, nbytes // 4)
+    dev = _INFO.device
+    t = torch.ones(n, dtype=torch.float32, device=dev)
+    on_gpu = dev.type == "cuda"
+    for _ in range(warmup):
+        dist.all_reduce(t)
+    if on_gpu:
+        torch.cuda.synchronize(dev)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(t)
+    if on_gpu:
+        torch.cuda.synchronize(dev)
+    el = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    sec = float(el)
+    w = _INFO.world
+    algbw = n * 4 / sec
+    return {"bytes": n * 4, "time_s": sec, "algbw_GBps": algbw / 1e9, "busbw_GBps": algbw * 2 * (w - 1) / w / 1e9,
+            "backend": _INFO.backend, "world": w}
+
+
 def shutdown():
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -32,6 +32,8 @@ class ContinuousEngine:
         self.chunk = max(1, chunk)
         self._q: "queue.Queue" = queue.Queue()
         self._closed = False
+        self._dead: Optional[BaseException] = None  # the error that ended the worker, if any
+        self._lock = threading.Lock()  # submit's closed-check + put vs the worker's final drain
         self.stats = {"admitted": 0, "finished": 0, "steps": 0, "max_active": 0}
         self._ready = threading.Event()
         self._init_error = None
@@ -43,11 +45,18 @@ class ContinuousEngine:
 
     # ---------------------------------------------------------------- client side
     def submit(self, query: str, top_k: Optional[int] = None) -> cf.Future:
-        if self._closed:
-            raise RuntimeError("ContinuousEngine is closed")
-        fut: cf.Future = cf.Future()
-        self._q.put((query, top_k, fut, time.perf_counter()))
+        with self._lock:
+            if self._closed:
+                if self._dead is not None:
+                    raise RuntimeError(f"ContinuousEngine worker failed: {self._dead!r}") from self._dead
+                raise RuntimeError("ContinuousEngine is closed")
+            fut: cf.Future = cf.Future()
+            self._q.put((query, top_k, fut, time.perf_counter()))
         return fut
+
+    @property
+    def alive(self) -> bool:
+        return not self._closed and self._worker.is_alive()
 
     def answer(self, query: str, top_k: Optional[int] = None, timeout: Optional[float] = None) -> RagAnswer:
         return self.submit(query, top_k).result(timeout)
@@ -57,10 +66,11 @@ class ContinuousEngine:
         return [f.result(timeout) for f in futs]
 
     def close(self, timeout: Optional[float] = 60.0):
-        if not self._closed:
-            self._closed = True
+        with self._lock:
+            was_open, self._closed = not self._closed, True
+        if was_open:
             self._q.put(None)
-            self._worker.join(timeout)
+        self._worker.join(timeout)
 
     def __enter__(self):
         return self
@@ -110,6 +120,8 @@ class ContinuousEngine:
         now = time.perf_counter()
         for r in rows:
             m = r.tag
+            if m["fut"].done():  # failed or cancelled elsewhere: nothing to deliver
+                continue
             text = extract_answer(p.tok.decode(r.tokens))
             tim = {"queue_s": m["t_admit"] - m["t_submit"], "retrieve_s": m["retrieve_s"],
                    "total_s": now - m["t_submit"], "new_tokens": len(r.tokens), "prompt_tokens": r.prompt_len,
@@ -153,16 +165,25 @@ class ContinuousEngine:
                     self.stats["steps"] += self.chunk
                     self._finish(cb.collect())
         except BaseException as e:  # noqa: BLE001 - in-flight callers get the error
+            self._dead = e
             for b, (meta, _, _) in list(cb.rows.items()):
                 if not meta["fut"].done():
                     meta["fut"].set_exception(e)
             cb.rows.clear()
         finally:
+            # the worker is gone for good: later submits raise instead of queueing futures nothing
+            # would resolve, and whatever is queued now fails
+            with self._lock:
+                self._closed = True
+                pending = []
+                while True:
+                    try:
+                        pending.append(self._q.get_nowait())
+                    except queue.Empty:
+                        break
             cb.close()
-            while True:
-                try:
-                    item = self._q.get_nowait()
-                except queue.Empty:
-                    break
+            err = RuntimeError(f"ContinuousEngine worker failed: {self._dead!r}" if self._dead is not None
+                               else "ContinuousEngine closed")
+            for item in pending:
                 if item is not None and item[2].set_running_or_notify_cancel():
-                    item[2].set_exception(RuntimeError("ContinuousEngine closed"))
+                    item[2].set_exception(err)

@@ -148,8 +148,19 @@ class SFTTrainer:
         if not c.full_finetune:
             self.model.refresh_lora()
         self.global_step += 1
-        self._pending.append((tot_loss / len(mbs), self.opt.last_norm, float(tot_tok), lr, t0))
+        # last_norm is rewritten in place by every optimizer step: queue a snapshot (a device copy,
+        # no sync), or every queued step would report the norm of the last one
+        norm = self.opt.last_norm
+        norm = norm.detach().clone() if torch.is_tensor(norm) else float(norm)
+        self._pending.append((tot_loss / len(mbs), norm, float(tot_tok), lr, t0))
         return self.collect()[-1] if sync else None
+
+    def close(self):
+        """Detach from the policy: remove the gradient-sync hooks on its parameters (a policy handed
+        on to PPO must not fire this trainer's all-reduces on stale buffers) and drop the optimizer
+        state. Idempotent."""
+        self.sync.remove()
+        self._pending = []
 
     def collect(self) -> List[dict]:
         """Metrics of every queued step: ONE device->host copy for all of them, then the rank

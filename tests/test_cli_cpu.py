@@ -48,6 +48,32 @@ def test_cli_pipeline_sft_then_ppo(tmp_path):
     run = tmp_path / "run"
     assert os.path.isdir(run / "sft_adapter") and os.path.isdir(run / "best_model_adapter")
     assert os.path.exists(run / "metrics.jsonl")
+    # the reference's comparison report (rl.py:444-463, 521-525): four models, seven metric keys
+    import pandas as pd
+
+    from rag_tl_domainllm_optimizer_amd.eval import METRIC_KEYS
+
+    rep = pd.read_csv(run / "model_comparison_results.csv", index_col=0)
+    assert list(rep.columns) == ["Base Model", "RAG Model", "RL-finetuned Model", "Transfer-learned Model"]
+    assert sorted(rep.index) == sorted(METRIC_KEYS)
+    assert rep.notna().all().all()
+
+
+def test_cli_eval_adapter_checkpoints(tmp_path, capsys):
+    """cmd_eval takes PEFT adapter directories (loaded into the base policy) and names the columns
+    after the reference's models."""
+    import pandas as pd
+
+    cli.main(["pipeline", *_tiny(tmp_path)])
+    run = tmp_path / "run"
+    rep = cli.main(["eval", *_tiny(tmp_path), "--checkpoint", str(run / "best_model_adapter"),
+                    "--checkpoint", f"Transfer-learned Model={run / 'sft_adapter'}"])
+    assert list(rep.columns) == ["Base Model", "RAG Model", "RL-finetuned Model", "Transfer-learned Model"]
+    assert "Model Comparison Report:" in capsys.readouterr().out
+    # different adapters give different answers than the base on at least one metric
+    assert not rep["Base Model"].equals(rep["RL-finetuned Model"]) or not rep["RAG Model"].equals(
+        rep["Transfer-learned Model"])
+    assert (pd.read_csv(run / "model_comparison_results.csv", index_col=0).shape[1]) == 4
 
 
 def test_serve_app():

@@ -186,3 +186,31 @@ def test_dp_bf16_grads_reduced_in_fp32_world8(tmp_path):
     assert float(rel.mean()) < 0.5 * float(ring_rel.mean())
     # link payload: fp32 reduce-scatter (4 B) + bf16 all-gather (2 B) per weight (+ fp32 value head)
     assert outs[0]["bytes"] >= 6 * 4099
+
+
+def test_sft_fit_reports_each_steps_grad_norm():
+    """fit() queues up to log_every steps before one D2H copy; every queued step must report ITS
+    gradient norm (a snapshot), equal to a run that syncs after every step."""
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
+    from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
+    from rag_tl_domainllm_optimizer_amd.train.sft import SFTConfig, SFTTrainer
+
+    cfg = PRESETS["tiny-llama"]
+    tok = Tokenizer.synthetic(cfg.vocab_size, "llama")
+    ex = _examples(tok, 16)
+
+    def trainer():
+        m = models.CausalLM(cfg, dtype=torch.float32, seed=1)
+        return SFTTrainer(m, tok, SFTConfig(lr=3e-2, lora_r=4, lr_schedule="constant", warmup_steps=0, batch_size=2,
+                                            seed=3))
+
+    a = trainer()
+    queued = a.fit(ex, epochs=1, shuffle=False, log_every=4)
+    b = trainer()
+    synced = [b.step(ex[k * 2:(k + 1) * 2]) for k in range(8)]
+    na = [m["grad_norm"] for m in queued]
+    nb = [m["grad_norm"] for m in synced]
+    assert len(na) == 8
+    assert len(set(round(x, 6) for x in na)) > 1  # not one repeated value
+    torch.testing.assert_close(torch.tensor(na), torch.tensor(nb), rtol=1e-5, atol=1e-7)

@@ -214,8 +214,11 @@ def _cli_pipeline_worker(rank, world, port, out_dir):
             "--data.n_queries=16", "--data.batch_size=4", "--ppo.max_new_tokens=6", "--ppo.max_prompt_tokens=96",
             "--ppo.minibatch_size=2", "--sft.batch_size=2", "--sft.lora_r=4", "--ppo.lora_r=4"]
     tr = cli.main(args)
-    torch.save({"params": torch.cat([p.detach().reshape(-1) for p in tr.flat.params]), "step": tr.global_step},
-               os.path.join(out_dir, f"pipe{rank}.pt"))
+    # post-accumulate-grad hooks per trainable parameter: PPO's GradSync only (the SFT trainer's
+    # were removed when the policy was handed over)
+    nhooks = [len(getattr(p, "_post_accumulate_grad_hooks", None) or {}) for p in tr.flat.params]
+    torch.save({"params": torch.cat([p.detach().reshape(-1) for p in tr.flat.params]), "step": tr.global_step,
+                "hooks": nhooks}, os.path.join(out_dir, f"pipe{rank}.pt"))
     parallel.barrier()
     parallel.shutdown()
 
@@ -230,6 +233,7 @@ def test_dp_cli_pipeline_world2(tmp_path):
     r = [torch.load(tmp_path / f"pipe{i}.pt", weights_only=True) for i in range(world)]
     assert r[0]["step"] == r[1]["step"] > 0
     assert torch.equal(r[0]["params"], r[1]["params"])
+    assert all(set(x["hooks"]) == {1} for x in r), [x["hooks"] for x in r]
     run = tmp_path / "run"
     assert os.path.isdir(run / "sft_adapter") and os.path.isdir(run / "best_model_adapter")
     assert os.path.exists(run / "metrics.jsonl")

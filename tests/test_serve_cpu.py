@@ -182,3 +182,59 @@ def test_continuous_admit_many_batches_consecutive_rows():
         for f in cb.collect():
             got[f.tag] = f.tokens
     assert [got[i] for i in range(4)] == ref
+
+
+def test_continuous_admit_many_rolls_back_on_failure():
+    """A prefill failure in the second run of rows releases the first run's rows too (no row keeps
+    decoding for a request whose future the engine is about to fail)."""
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.generation import ContinuousBatcher, Generator, SamplingParams
+
+    m = models.CausalLM(models.resolve_preset("tiny-llama"), device="cpu", dtype=torch.float32, seed=3)
+    p = SamplingParams(max_new_tokens=4, do_sample=False)
+    cb = ContinuousBatcher(Generator(m, 4, 64, "cpu", use_graph=False), p, pad_id=0, eos_ids=[-1])
+    cb.admit([5, 6, 7], "held")  # row 0
+    cb.free = [1, 3]  # row 2 withheld: the next admission is two runs of rows, [1] and [3]
+    calls = {"n": 0}
+    orig = m.prefill
+
+    def flaky(*a, **k):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            raise RuntimeError("boom")
+        return orig(*a, **k)
+
+    m.prefill = flaky
+    with pytest.raises(RuntimeError, match="boom"):
+        cb.admit_many([[9, 10], [11, 12, 13]], ["a", "b"])
+    m.prefill = orig
+    assert set(cb.rows) == {0} and sorted(cb.free) == [1, 3]
+    assert int(cb.gen.active[1]) == 0 and int(cb.gen.active[3]) == 0
+    cb.close()
+
+
+def test_continuous_engine_worker_failure_fails_closed():
+    """If the worker loop dies, in-flight and queued requests fail and later submits raise instead of
+    returning futures nothing would ever resolve."""
+    from rag_tl_domainllm_optimizer_amd.generation import ContinuousBatcher
+    from rag_tl_domainllm_optimizer_amd.serve import ContinuousEngine
+
+    pipe, words = _tiny_pipe(max_batch=2)
+    orig_step = ContinuousBatcher.step
+
+    def bad_step(self, n=1):
+        raise RuntimeError("gpu went away")
+
+    ContinuousBatcher.step = bad_step
+    try:
+        eng = ContinuousEngine(pipe, chunk=2)
+        fut = eng.submit(f"{words[0]} {words[3]}")
+        with pytest.raises(RuntimeError, match="gpu went away"):
+            fut.result(60)
+        eng._worker.join(30)
+        assert not eng.alive
+        with pytest.raises(RuntimeError, match="worker failed"):
+            eng.submit("another")
+        eng.close()
+    finally:
+        ContinuousBatcher.step = orig_step
