@@ -15,20 +15,16 @@
 #include "host/tokenizer.h"
 #include "host/ivf_host.h"
 #include "rt_workspace.h"
+#include "rt_tuning.h"
 
 extern "C" {
 int rt_gemm_nt(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*, void*,
                long, int, int, int, int, int, float*, unsigned*, const void*, long, float, int, hipStream_t);
 int rt_shuffle_decode_weight(const void*, void*, long, long, hipStream_t);
 int rt_shuffle_decode_weight_fp8(const void*, void*, long, long, hipStream_t);
-void rt_gemm_set_variant(int);
-void rt_gemm_set_wide_split(int);
-void rt_gemm_set_m64_split(int);
-void rt_gemm_set_decode_split(int);
-void rt_gemm_set_decode_depth(int);
 int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, long, const void*, long, int,
                 const void*, void*, long, void*, long, const void*, long, int, int, int, int, int, int, const void*,
-                int, hipStream_t);
+                int, float*, unsigned*, hipStream_t);
 int rt_gemm_small(int, int, const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
                   int, hipStream_t);
 int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
@@ -53,15 +49,13 @@ int rt_attn_decode(const void*, long, const void*, const void*, int, const int*,
                    void*, long, int, int, int, int, float, hipStream_t);
 int rt_attn_decode_fused(const void*, long, void*, void*, int, const int*, const int*, const int*, const int*,
                          const float*, const float*, float, int, float*, unsigned*, int, int, void*, long, int, int, int,
-                         int, float, hipStream_t);
+                         int, float, const float*, int, float*, float*, int, long long*, hipStream_t);
 int rt_attn_decode_fused_ps(int, int);
-void rt_attn_decode_set_qkv_slabs(const float*, int);
-void rt_attn_decode_set_fp8kv(float*, float*, int);
 int rt_kv_store_fp8(const void*, long, void*, void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int rt_attn_decode_mfma_ok(int, int, int, int, int);
 int rt_attn_o_fused(const void*, void*, void*, int, const int*, const int*, const int*, const int*, const float*,
                     const float*, float, int, float*, int, int, int, int, int, float, const void*, long, const void*,
-                    void*, int, unsigned*, int*, hipStream_t);
+                    void*, int, unsigned*, int*, long long*, hipStream_t);
 int rt_attn_bwd(const void*, long, const void*, long, const void*, long, const void*, long, const void*, long,
                 const float*, float*, float*, void*, long, void*, long, void*, long, const int*, int, int, int, int,
                 int, int, int, float, hipStream_t);
@@ -86,8 +80,6 @@ int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const int*, 
 int rt_gae(const float*, const float*, const float*, int, int, float, float, float*, float*, hipStream_t);
 int rt_ppo_advantages(const float*, const float*, const float*, const float*, const int*, int, int, float, float, float,
                       int, float, float*, float*, float*, float*, hipStream_t);
-void rt_attn_decode_set_nk(int nk);
-void rt_attn_o_set_stamps(long long* p);
 int rt_ppo_loss(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
                 const float*, long, float, float, float, float, float*, float*, float*, float*, hipStream_t);
 int rt_decode_update(const long*, long*, int, float*, const float*, float*, const float*, uint8_t*, int*, int*, long*,
@@ -98,6 +90,65 @@ namespace {
 
 using at::Tensor;
 using c10::optional;
+
+// ---- rt::Tuning <-> dict (csrc/include/rt_tuning.h) ----
+struct TuningField {
+  const char* name;
+  int rt::Tuning::*i;
+  float rt::Tuning::*f;
+};
+static const TuningField kTuningFields[] = {
+    {"decode_mw", &rt::Tuning::decode_mw, nullptr},
+    {"decode_mw_kpp", &rt::Tuning::decode_mw_kpp, nullptr},
+    {"decode_mfma", &rt::Tuning::decode_mfma, nullptr},
+    {"attn_kv_nt", &rt::Tuning::attn_kv_nt, nullptr},
+    {"decode_fp8_mw", &rt::Tuning::decode_fp8_mw, nullptr},
+    {"decode_g1_valu", &rt::Tuning::decode_g1_valu, nullptr},
+    {"decode_g1_nw", &rt::Tuning::decode_g1_nw, nullptr},
+    {"decode_nk", &rt::Tuning::decode_nk, nullptr},
+    {"attn_bwd_atomic_dq", &rt::Tuning::attn_bwd_atomic_dq, nullptr},
+    {"gemm_variant", &rt::Tuning::gemm_variant, nullptr},
+    {"gemv16", &rt::Tuning::gemv16, nullptr},
+    {"gemv16_maxm", &rt::Tuning::gemv16_maxm, nullptr},
+    {"gemv16_depth", &rt::Tuning::gemv16_depth, nullptr},
+    {"decode_split", &rt::Tuning::decode_split, nullptr},
+    {"decode_depth", &rt::Tuning::decode_depth, nullptr},
+    {"m64_split", &rt::Tuning::m64_split, nullptr},
+    {"wide_split", &rt::Tuning::wide_split, nullptr},
+    {"gemm_fp8_256", &rt::Tuning::gemm_fp8_256, nullptr},
+    {"gemm_tr_builtin", &rt::Tuning::gemm_tr_builtin, nullptr},
+    {"gemm_b_nt", &rt::Tuning::gemm_b_nt, nullptr},
+    {"gemm_bn128_cost", nullptr, &rt::Tuning::gemm_bn128_cost},
+    {"gemm_streamk", &rt::Tuning::gemm_streamk, nullptr},
+};
+
+py::dict get_tuning() {
+  py::dict d;
+  const rt::Tuning& t = rt::tuning();
+  for (const auto& f : kTuningFields) {
+    if (f.i) d[f.name] = t.*(f.i);
+    else d[f.name] = t.*(f.f);
+  }
+  return d;
+}
+
+void set_tuning(const py::dict& d) {
+  rt::Tuning t = rt::tuning();
+  for (auto kv : d) {
+    const std::string k = py::str(kv.first);
+    bool found = false;
+    for (const auto& f : kTuningFields) {
+      if (k == f.name) {
+        if (f.i) t.*(f.i) = kv.second.cast<int>();
+        else t.*(f.f) = kv.second.cast<float>();
+        found = true;
+        break;
+      }
+    }
+    TORCH_CHECK(found, "set_tuning: unknown field '", k, "'");
+  }
+  rt_set_tuning(&t);
+}
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
@@ -142,6 +193,40 @@ DecodeWS& decode_ws(const Tensor& like, hipStream_t st) {
   w->tickets = at::zeros({RT_SPLITK_TICKETS}, like.options().dtype(at::kInt));
   (*map)[key] = w;
   return *w;
+}
+
+// Stream-K workspace of the token-parallel GEMM (gemm_big.hip): 2 partial slots of 256 x 256 fp32
+// per unit (one unit per CU) and one self-resetting ticket per tail tile, one per (device, stream)
+// like DecodeWS. Allocated on first use (128 MiB at 256 CUs), never freed. An empty struct when the
+// stream-K tail is switched off (tuning gemm_streamk = 0).
+struct StreamKWS {
+  Tensor part, tickets;
+};
+static std::mutex g_skws_mu;
+static std::unordered_map<uint64_t, StreamKWS*>* g_skws_map = new std::unordered_map<uint64_t, StreamKWS*>();
+const StreamKWS& streamk_ws(const Tensor& like, hipStream_t st) {
+  static const StreamKWS none;
+  if (!rt::tuning().gemm_streamk) return none;
+  std::lock_guard<std::mutex> g(g_skws_mu);
+  const uint64_t key = (uint64_t)like.get_device() << 56 ^ (uint64_t)(uintptr_t)st;
+  auto it = g_skws_map->find(key);
+  if (it != g_skws_map->end()) return *it->second;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  auto* w = new StreamKWS();
+  w->part = at::empty({(int64_t)2 * cus * 256 * 256}, like.options().dtype(at::kFloat));
+  w->tickets = at::zeros({(int64_t)cus}, like.options().dtype(at::kInt));
+  (*g_skws_map)[key] = w;
+  return *w;
+}
+
+// diagnostics: stream-K tickets not back at zero (every launch leaves them at zero)
+int64_t streamk_dirty_tickets() {
+  std::lock_guard<std::mutex> g(g_skws_mu);
+  int64_t n = 0;
+  for (auto& kv : *g_skws_map) n += (kv.second->tickets.ne(0)).sum().item<int64_t>();
+  return n;
 }
 
 // diagnostics: per decode workspace, the number of arrival tickets not back at zero (every
@@ -340,12 +425,14 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
     CHECK_ALIGN16(*residual);
   }
   if (M == 0 || N == 0) return c;
+  const StreamKWS& sk = streamk_ws(a, cur_stream());
   check_rc(rt_gemm_big((int)layout_a, (int)layout_b, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                        ext ? a2->data_ptr() : nullptr, ext ? a2->stride(0) : 0, ext ? b2->data_ptr() : nullptr,
                        ext ? b2->stride(0) : 0, (int)K2, opt_ptr(bias), c.data_ptr(), c.stride(0), c2, ldc2,
                        has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, (int)M,
                        (int)N, (int)K, (int)act, (int)out_mode, (int)nsplit, zero_page(a).data_ptr(), (int)bn,
-                       cur_stream()),
+                       sk.part.defined() ? sk.part.data_ptr<float>() : nullptr,
+                       sk.tickets.defined() ? (unsigned*)sk.tickets.data_ptr<int>() : nullptr, cur_stream()),
            "gemm_big");
   return c;
 }
@@ -411,7 +498,7 @@ Tensor gemm_splitk(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor slab
   if (M == 0) return c;
   check_rc(rt_gemm_big(0, 0, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), nullptr, 0, nullptr, 0, 0,
                        nullptr, slabs.data_ptr(), N, nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, 0, 3,
-                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, cur_stream()),
+                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, nullptr, nullptr, cur_stream()),
            "gemm_splitk");
   check_rc(rt_gemm_splitk_reduce(slabs.data_ptr<float>(), (int)nsplit, (int)M, (int)N, opt_ptr(bias), (int)act,
                                  has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, c.data_ptr(),
@@ -580,7 +667,7 @@ void gemm_splitk_raw(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor sl
   if (M == 0) return;
   check_rc(rt_gemm_big(0, 0, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), nullptr, 0, nullptr, 0, 0,
                        nullptr, slabs.data_ptr(), N, nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, 0, 3,
-                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, cur_stream()),
+                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, nullptr, nullptr, cur_stream()),
            "gemm_splitk_raw");
 }
 
@@ -711,31 +798,33 @@ void attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, const Tens
            "attn_decode");
 }
 
-// fp8 K/V cache (config 5) for the NEXT attn_decode_fused / attn_decode_fused_slabs call: kc / vc
-// are e4m3fn byte caches [B, Hkv, Smax, D] (K rows k-permuted), ksc / vsc fp32 per-slot scales
-// [B, Hkv, SmaxP] (SmaxP >= Smax, a multiple of 16). Only the MFMA decode kernels read it.
-static bool g_fp8kv_pending = false;
-static int64_t g_fp8kv_smaxp = 0;
-void attn_decode_set_fp8kv(Tensor ksc, Tensor vsc) {
-  CHECK_CUDA(ksc); CHECK_F32(ksc); CHECK_F32(vsc);
-  TORCH_CHECK(ksc.dim() == 3 && ksc.is_contiguous() && vsc.is_contiguous() && vsc.sizes() == ksc.sizes(),
-              "attn_decode_set_fp8kv: scales must be contiguous [B, Hkv, SmaxP]");
-  g_fp8kv_smaxp = ksc.size(2);
-  rt_attn_decode_set_fp8kv(ksc.data_ptr<float>(), vsc.data_ptr<float>(), (int)g_fp8kv_smaxp);
-  g_fp8kv_pending = true;
-}
-static void check_cache_dtype(const Tensor& kc, const Tensor& vc, const char* who) {
-  if (g_fp8kv_pending) {
-    g_fp8kv_pending = false;
-    TORCH_CHECK(kc.scalar_type() == at::kByte && vc.scalar_type() == at::kByte, who, ": fp8 scales set for a bf16 cache");
-    TORCH_CHECK(g_fp8kv_smaxp >= kc.size(2) && kc.size(3) == 128, who, ": fp8 cache needs D = 128 and SmaxP >= Smax");
-  } else {
+// fp8 K/V cache (config 5): kc / vc are e4m3fn byte caches [B, Hkv, Smax, D] (K rows k-permuted)
+// with fp32 per-slot scales ksc / vsc [B, Hkv, SmaxP] (SmaxP >= Smax, a multiple of 16), passed to
+// the decode call itself. Only the MFMA decode kernels read them.
+struct KvScales {
+  float* k = nullptr;
+  float* v = nullptr;
+  int smaxp = 0;
+};
+static KvScales check_cache(const Tensor& kc, const Tensor& vc, const optional<Tensor>& ksc,
+                            const optional<Tensor>& vsc, const char* who) {
+  KvScales r;
+  const bool fp8 = ksc.has_value() && ksc->defined();
+  TORCH_CHECK(fp8 == (vsc.has_value() && vsc->defined()), who, ": k and v scales go together");
+  if (!fp8) {
     CHECK_BF16(kc); CHECK_BF16(vc);
+    return r;
   }
-}
-static void clear_fp8kv() {
-  g_fp8kv_pending = false;
-  rt_attn_decode_set_fp8kv(nullptr, nullptr, 0);
+  CHECK_CUDA(*ksc); CHECK_F32(*ksc); CHECK_F32(*vsc);
+  TORCH_CHECK(ksc->dim() == 3 && ksc->is_contiguous() && vsc->is_contiguous() && vsc->sizes() == ksc->sizes(),
+              who, ": scales must be contiguous [B, Hkv, SmaxP]");
+  TORCH_CHECK(kc.scalar_type() == at::kByte && vc.scalar_type() == at::kByte, who, ": fp8 scales for a bf16 cache");
+  TORCH_CHECK(ksc->size(2) >= kc.size(2) && kc.size(3) == 128, who, ": fp8 cache needs D = 128 and SmaxP >= Smax");
+  TORCH_CHECK(ksc->size(0) == kc.size(0) && ksc->size(1) == kc.size(1), who, ": scale shape");
+  r.k = ksc->data_ptr<float>();
+  r.v = vsc->data_ptr<float>();
+  r.smaxp = (int)ksc->size(2);
+  return r;
 }
 
 // Prompt K / V of the rotated qkv rows [B * S] -> fp8 cache slots [0, S) with per-slot scales.
@@ -756,8 +845,9 @@ void kv_store_fp8(const Tensor& qkv, Tensor kc, Tensor vc, Tensor ksc, Tensor vs
 void attn_decode_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& slot, const Tensor& attn_len,
                        const optional<Tensor>& kv_start, const optional<Tensor>& pos, const optional<Tensor>& cos,
                        const optional<Tensor>& sin, double sign, int64_t window, double scale, int64_t Hq, Tensor part,
-                       Tensor tickets, int64_t PS, Tensor out) {
-  check_cache_dtype(kc, vc, "attn_decode_fused");
+                       Tensor tickets, int64_t PS, Tensor out, const optional<Tensor>& ksc,
+                       const optional<Tensor>& vsc, const optional<Tensor>& stamps) {
+  const KvScales sc = check_cache(kc, vc, ksc, vsc, "attn_decode_fused");
   CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_ROWS(qkv); CHECK_I32(slot);
   CHECK_I32(attn_len); CHECK_F32(part); CHECK_I32(tickets); CHECK_BF16(out); CHECK_ROWS(out);
   TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes(),
@@ -784,6 +874,8 @@ void attn_decode_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& sl
                                 rot ? sin->data_ptr<float>() : nullptr, (float)sign, (int)window,
                                 part.data_ptr<float>(), (unsigned*)tickets.data_ptr<int>(), (int)NP, (int)PS,
                                 out.data_ptr(), out.stride(0), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
+                                nullptr, 0, sc.k, sc.v, sc.smaxp,
+                                stamps.has_value() && stamps->defined() ? (long long*)stamps->data_ptr() : nullptr,
                                 cur_stream()),
            "attn_decode_fused");
 }
@@ -794,9 +886,9 @@ void attn_decode_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& sl
 bool attn_decode_fused_slabs(const Tensor& slabs, int64_t nsplit, Tensor kc, Tensor vc, const Tensor& slot,
                              const Tensor& attn_len, const optional<Tensor>& kv_start, const optional<Tensor>& pos,
                              const optional<Tensor>& cos, const optional<Tensor>& sin, double sign, int64_t window,
-                             double scale, int64_t Hq, Tensor part, Tensor tickets, int64_t PS, Tensor out) {
-  const bool fp8kv = g_fp8kv_pending;
-  check_cache_dtype(kc, vc, "attn_decode_fused_slabs");
+                             double scale, int64_t Hq, Tensor part, Tensor tickets, int64_t PS, Tensor out,
+                             const optional<Tensor>& ksc, const optional<Tensor>& vsc) {
+  const KvScales sc = check_cache(kc, vc, ksc, vsc, "attn_decode_fused_slabs");
   CHECK_CUDA(slabs); CHECK_F32(slabs); CHECK_I32(slot); CHECK_I32(attn_len);
   CHECK_F32(part); CHECK_I32(tickets); CHECK_BF16(out); CHECK_ROWS(out);
   TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes(),
@@ -804,10 +896,7 @@ bool attn_decode_fused_slabs(const Tensor& slabs, int64_t nsplit, Tensor kc, Ten
   const int64_t B = kc.size(0), Hkv = kc.size(1), Smax = kc.size(2), D = kc.size(3);
   const int64_t NP = (Smax + PS - 1) / PS, G = Hq / Hkv;
   TORCH_CHECK(G * Hkv == Hq, "attn_decode_fused_slabs: Hq must be a multiple of Hkv");
-  if (!rt_attn_decode_mfma_ok((int)B, (int)Hq, (int)Hkv, (int)D, (int)NP)) {
-    if (fp8kv) clear_fp8kv();  // nothing launched: the caller reduces and retries with the scales set again
-    return false;
-  }
+  if (!rt_attn_decode_mfma_ok((int)B, (int)Hq, (int)Hkv, (int)D, (int)NP)) return false;  // caller reduces first
   const int64_t W = (Hq + 2 * Hkv) * D;
   TORCH_CHECK(slabs.is_contiguous() && slabs.numel() >= nsplit * B * W && nsplit >= 1, "attn_decode_fused_slabs: slabs");
   TORCH_CHECK(out.size(0) == B && slot.numel() == B && attn_len.numel() == B && out.size(1) >= Hq * D,
@@ -821,14 +910,13 @@ bool attn_decode_fused_slabs(const Tensor& slabs, int64_t nsplit, Tensor kc, Ten
     TORCH_CHECK(cos->size(-1) == D / 2 && cos->is_contiguous() && sin->is_contiguous(), "attn_decode_fused_slabs: tables");
   }
   if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
-  rt_attn_decode_set_qkv_slabs(slabs.data_ptr<float>(), (int)nsplit);
   check_rc(rt_attn_decode_fused(slabs.data_ptr(), W, kc.data_ptr(), vc.data_ptr(), (int)Smax, slot.data_ptr<int>(),
                                 attn_len.data_ptr<int>(), (const int*)opt_ptr(kv_start),
                                 rot ? pos->data_ptr<int>() : nullptr, rot ? cos->data_ptr<float>() : nullptr,
                                 rot ? sin->data_ptr<float>() : nullptr, (float)sign, (int)window,
                                 part.data_ptr<float>(), (unsigned*)tickets.data_ptr<int>(), (int)NP, (int)PS,
                                 out.data_ptr(), out.stride(0), (int)B, (int)Hq, (int)Hkv, (int)D, (float)scale,
-                                cur_stream()),
+                                slabs.data_ptr<float>(), (int)nsplit, sc.k, sc.v, sc.smaxp, nullptr, cur_stream()),
            "attn_decode_fused_slabs");
   return true;
 }
@@ -838,7 +926,8 @@ bool attn_decode_fused_slabs(const Tensor& slabs, int64_t nsplit, Tensor kc, Ten
 bool attn_o_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& slot, const Tensor& attn_len,
                   const optional<Tensor>& kv_start, const optional<Tensor>& pos, const optional<Tensor>& cos,
                   const optional<Tensor>& sin, double sign, int64_t window, double scale, int64_t Hq, Tensor part,
-                  int64_t PS, const Tensor& w, const Tensor& residual, Tensor out, Tensor sync, Tensor err) {
+                  int64_t PS, const Tensor& w, const Tensor& residual, Tensor out, Tensor sync, Tensor err,
+                  const optional<Tensor>& stamps) {
   CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_BF16(kc); CHECK_BF16(vc); CHECK_I32(slot); CHECK_I32(attn_len);
   CHECK_F32(part); CHECK_BF16(w); CHECK_ROWS(w); CHECK_ALIGN16(w); CHECK_BF16(residual); CHECK_BF16(out);
   CHECK_I32(sync); CHECK_I32(err);
@@ -865,7 +954,9 @@ bool attn_o_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& slot, c
                                  rot ? sin->data_ptr<float>() : nullptr, (float)sign, (int)window,
                                  part.data_ptr<float>(), (int)NP, (int)PS, (int)Hq, (int)Hkv, (int)D, (float)scale,
                                  w.data_ptr(), w.stride(0), residual.data_ptr(), out.data_ptr(), (int)H,
-                                 (unsigned*)sync.data_ptr<int>(), err.data_ptr<int>(), cur_stream());
+                                 (unsigned*)sync.data_ptr<int>(), err.data_ptr<int>(),
+                                 stamps.has_value() && stamps->defined() ? (long long*)stamps->data_ptr() : nullptr,
+                                 cur_stream());
   return rc == 0;
 }
 
@@ -875,8 +966,8 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   CHECK_CUDA(q); CHECK_ROWS(q); CHECK_ROWS(k); CHECK_ROWS(v); CHECK_ROWS(o); CHECK_ROWS(dout);
   CHECK_ROWS(dq); CHECK_ROWS(dk); CHECK_ROWS(dv); CHECK_F32(lse);
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
-  // fp32 dQ accumulator: only the atomic form (RT_ATTN_BWD_ATOMIC_DQ=1) uses it
-  static const bool atomic_dq = getenv("RT_ATTN_BWD_ATOMIC_DQ") && atoi(getenv("RT_ATTN_BWD_ATOMIC_DQ"));
+  // fp32 dQ accumulator: only the atomic form (tuning attn_bwd_atomic_dq) uses it
+  const bool atomic_dq = rt::tuning().attn_bwd_atomic_dq != 0;
   auto dq32 = at::empty({atomic_dq ? B * S : 1, atomic_dq ? Hq * D : 1}, q.options().dtype(at::kFloat));
   if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
   check_rc(rt_attn_bwd(q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0), o.data_ptr(),
@@ -1139,15 +1230,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("shuffle_decode_weight_fp8", &shuffle_decode_weight_fp8,
         "fp8 W [N, K] -> tile-ordered W8A16 decode image (gemm_fp8 w_shuffled=True)", py::arg("q"),
         py::arg("out") = py::none());
-  m.def("gemm_set_wide_split", &rt_gemm_set_wide_split, "tuning: fixed split-K of the wide W8A16 M<=64 kernel (0 = auto)");
-  m.def("gemm_set_m64_split", &rt_gemm_set_m64_split, "tuning: fixed split-K of the M<=64 ring kernel (0 = auto)");
-  m.def("gemm_set_decode_split", &rt_gemm_set_decode_split, "tuning: fixed split-K of the M<=16 decode kernel (0 = auto)");
-  m.def("gemm_set_decode_depth", &rt_gemm_set_decode_depth, "tuning: weight-pipeline depth (2 / 4) of the M<=16 decode kernel (0 = auto)");
-  m.def("gemm_set_variant", &rt_gemm_set_variant, "0 auto, 1 force 128x128 tile, 2 force 256x256 (M > 64)");
-  m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine");
-  m.def("attn_decode_fused_slabs", &attn_decode_fused_slabs, "decode attention with the qkv split-K reduce fused");
+  m.def("streamk_dirty_tickets", &streamk_dirty_tickets, "stream-K tickets not back at zero (diagnostic)");
+  m.def("get_tuning", &get_tuning, "the launchers' kernel-selection knobs (rt::Tuning) as a dict");
+  m.def("set_tuning", &set_tuning, "update rt::Tuning fields from a dict (unknown keys raise)");
+  m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine",
+        py::arg("qkv"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("attn_len"), py::arg("kv_start"),
+        py::arg("pos"), py::arg("cos"), py::arg("sin"), py::arg("sign"), py::arg("window"), py::arg("scale"),
+        py::arg("Hq"), py::arg("part"), py::arg("tickets"), py::arg("PS"), py::arg("out"),
+        py::arg("k_scale") = py::none(), py::arg("v_scale") = py::none(), py::arg("stamps") = py::none());
+  m.def("attn_decode_fused_slabs", &attn_decode_fused_slabs, "decode attention with the qkv split-K reduce fused",
+        py::arg("slabs"), py::arg("nsplit"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("attn_len"),
+        py::arg("kv_start"), py::arg("pos"), py::arg("cos"), py::arg("sin"), py::arg("sign"), py::arg("window"),
+        py::arg("scale"), py::arg("Hq"), py::arg("part"), py::arg("tickets"), py::arg("PS"), py::arg("out"),
+        py::arg("k_scale") = py::none(), py::arg("v_scale") = py::none());
   m.def("gemm_fp8_lora", &gemm_fp8_lora, "W8A8 GEMM + bf16 LoRA K-extension (config-5 training forward)");
-  m.def("attn_decode_set_fp8kv", &attn_decode_set_fp8kv, "fp8 K/V cache scales for the next decode attention call");
   m.def("kv_store_fp8", &kv_store_fp8, "prompt K/V -> fp8 cache (per-slot scales)");
   m.def("attn_decode_fused_ps", &rt_attn_decode_fused_ps, "keys per partition of the fused decode kernel");
   m.def("quant_fp8", &quant_fp8, "per-row absmax e4m3fn quantisation -> (uint8 [R,C], scale fp32 [R])");
@@ -1189,11 +1285,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk", &topk);
   m.def("ivf_scan", &ivf_scan);
   m.def("segment_mean", &segment_mean, "k-means update: per-segment mean of sorted rows (+ L2 normalise)");
-  m.def("attn_decode_set_nk", &rt_attn_decode_set_nk, "fused decode attention: keys per lane per chunk (0 = default 4)");
-  m.def("attn_o_set_stamps", [](optional<Tensor> t) {
-    rt_attn_o_set_stamps(t.has_value() && t->defined() ? (long long*)t->data_ptr() : nullptr);
-  }, "debug: int64 [NB, 8] buffer receiving per-block s_memrealtime phase stamps of attn_o_fused (None = off)");
-  m.def("attn_o_fused", &attn_o_fused, "batch-1 decode: attention + o_proj + residual in one launch (false = unsupported)");
+  m.def("attn_o_fused", &attn_o_fused, "batch-1 decode: attention + o_proj + residual in one launch (false = unsupported)",
+        py::arg("qkv"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("attn_len"), py::arg("kv_start"),
+        py::arg("pos"), py::arg("cos"), py::arg("sin"), py::arg("sign"), py::arg("window"), py::arg("scale"),
+        py::arg("Hq"), py::arg("part"), py::arg("PS"), py::arg("w"), py::arg("residual"), py::arg("out"),
+        py::arg("sync"), py::arg("err"), py::arg("stamps") = py::none());
   m.def("gae", &gae);
   m.def("ppo_advantages", &ppo_advantages, "token KL rewards + GAE + advantage whitening in one launch");
   m.def("ppo_loss", &ppo_loss, "fused token-level PPO loss: {stats[6], dlp, dv, dent}");

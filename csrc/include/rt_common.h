@@ -3,6 +3,7 @@
 // Everything here is written for wave64: lane ids are threadIdx.x & 63, cross-lane
 // reductions walk offsets 32..1, block sizes are multiples of 64.
 #pragma once
+#include "rt_tuning.h"
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>

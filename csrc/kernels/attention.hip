@@ -1058,7 +1058,7 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
   const int lane = threadIdx.x & 63, g = lane >> 4, r16 = lane & 15;
   const int w = W > 1 ? (int)(threadIdx.x >> 6) : 0;
   char* vimg = vimg_all[w];
-  // debug phase stamps (a.stamps set by rt_attn_o_set_stamps): every load drained first
+  // debug phase stamps (a.stamps: the launch's stamps argument): every load drained first
   auto stamp = [&](int k) {
     if (W > 1 && a.stamps) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -2195,43 +2195,23 @@ extern "C" int rt_attn_decode(const void* q, long ldq, const void* kc, const voi
 // keys per chunk of the fused kernel: 4 waves x (64 / (D/8)) keys per step x NK (= 4)
 extern "C" int rt_attn_decode_fused_ps(int D, int nk) { return 4 * (64 / (D / 8)) * nk; }
 
-// keys per lane per chunk (bytes in flight per block); 0 = default 4. Tuning hook.
-static int g_dec_nk = 0;
-extern "C" void rt_attn_decode_set_nk(int nk) { g_dec_nk = nk; }
-// qkv given as split-K slabs for the NEXT rt_attn_decode_fused call (set by the binding)
-static const float* g_dec_qkv_slabs = nullptr;
-static int g_dec_qkv_nsplit = 0;
-extern "C" void rt_attn_decode_set_qkv_slabs(const float* p, int nsplit) { g_dec_qkv_slabs = p; g_dec_qkv_nsplit = nsplit; }
-static long long* g_ao_stamps = nullptr;  // debug hook: per-block phase stamps (attn_o and 8-wave kernels)
-extern "C" void rt_attn_o_set_stamps(long long* p) { g_ao_stamps = p; }
 // waves per (batch, kv head) of the small-batch MFMA decode attention. Caches up to 1024 slots run
 // one workgroup per (batch, kv head) (<= 8 tiles per wave: the 3-tile register prefetch covers the
 // memory round trip); longer caches split the row into partitions of about RT_DECODE_MW_KPP (512)
 // keys, at most the workspace's NP, merged by the last arriving partition.
 constexpr int DEC_MW = 8;
 static bool rt_attn_decode_mw_ok(int B, int Hq, int Hkv, int D, int Smax) {
-  static const int use_mw = getenv("RT_DECODE_MW") ? atoi(getenv("RT_DECODE_MW")) : 1;
   const int G = Hkv ? Hq / Hkv : 0;
-  return use_mw && D == 128 && (long)B * Hkv < 256 && (G == 1 || G == 2 || G == 4 || G == 8);
+  return tuning().decode_mw && D == 128 && (long)B * Hkv < 256 && (G == 1 || G == 2 || G == 4 || G == 8);
 }
 static int rt_attn_decode_mw_np(int Smax, int np_ws) {
-  static const int kpp = getenv("RT_DECODE_MW_KPP") ? atoi(getenv("RT_DECODE_MW_KPP")) : 512;
+  const int kpp = std::max(16, tuning().decode_mw_kpp);
   if (Smax <= 1024 || np_ws <= 1) return 1;
   return std::max(1, std::min(np_ws, (Smax + kpp - 1) / kpp));
 }
 extern "C" int rt_attn_decode_mfma_ok(int B, int Hq, int Hkv, int D, int NP) {
-  static const int use_mfma = getenv("RT_DECODE_MFMA") ? atoi(getenv("RT_DECODE_MFMA")) : 1;
   const int G = Hkv ? Hq / Hkv : 0;
-  return use_mfma && NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
-}
-
-// fp8 K/V cache for the NEXT rt_attn_decode_fused call (set by the binding; one launch only):
-// kc / vc are then e4m3fn byte caches with per-slot scales ksc / vsc [B, Hkv, SmaxP]
-static float* g_dec_ksc = nullptr;
-static float* g_dec_vsc = nullptr;
-static int g_dec_smaxp = 0;
-extern "C" void rt_attn_decode_set_fp8kv(float* ksc, float* vsc, int SmaxP) {
-  g_dec_ksc = ksc; g_dec_vsc = vsc; g_dec_smaxp = SmaxP;
+  return tuning().decode_mfma && NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
 }
 
 // Prompt K / V (rows [b * S + s] of the rotated qkv) -> fp8 cache slots [0, S): one 16-lane group
@@ -2282,22 +2262,25 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
                                     const int* attn_len, const int* kv_start, const int* pos, const float* cosT,
                                     const float* sinT, float sign, int window, float* part, unsigned* tickets, int NP,
                                     int PS, void* o, long ldo, int B, int Hq, int Hkv, int D, float scale,
-                                    hipStream_t stream) {
+                                    const float* qkv_slabs, int qkv_nsplit, float* ksc, float* vsc, int SmaxP,
+                                    long long* stamps, hipStream_t stream) {
+  // qkv_slabs: q | k | v given as the qkv GEMM's qkv_nsplit fp32 split-K slabs [nsplit, B, ldq]
+  // (summed in the MFMA kernel's prologue; qkv is then unused). ksc / vsc: the caches kc / vc are
+  // e4m3fn bytes with per-slot fp32 scales [B, Hkv, SmaxP]. stamps: debug phase stamps or null.
   DecodeFusedArgs a;
   a.qkv = (const bf16_t*)qkv; a.ldq = ldq; a.kc = (bf16_t*)kc; a.vc = (bf16_t*)vc; a.Smax = Smax;
   a.slot = slot; a.attn_len = attn_len; a.kv_start = kv_start; a.pos = pos; a.cosT = cosT; a.sinT = sinT;
   a.sign = sign; a.window = window; a.part = part; a.tickets = tickets; a.o = (bf16_t*)o; a.ldo = ldo;
   a.B = B; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
-  a.qkv_slabs = g_dec_qkv_slabs; a.qkv_nsplit = g_dec_qkv_nsplit; a.qkv_sstride = (long)B * ldq;
-  g_dec_qkv_slabs = nullptr;  // one launch only
+  a.qkv_slabs = qkv_slabs; a.qkv_nsplit = qkv_slabs ? qkv_nsplit : 0; a.qkv_sstride = (long)B * ldq;
   // K/V cache bytes are read once per decode step: non-temporal loads (batch 256: 56 -> 50 us per
-  // layer, profiles/decode_nt_ab.log); RT_ATTN_KV_NT=0 for A/B runs
-  static const int kv_nt_env = getenv("RT_ATTN_KV_NT") ? atoi(getenv("RT_ATTN_KV_NT")) : 1;
-  a.kv_nt = kv_nt_env;
-  a.stamps = g_ao_stamps;
-  a.ksc = g_dec_ksc; a.vsc = g_dec_vsc; a.SmaxP = g_dec_smaxp;
-  const bool kv8 = g_dec_ksc != nullptr;
-  g_dec_ksc = g_dec_vsc = nullptr;  // one launch only
+  // layer, profiles/decode_nt_ab.log); tuning attn_kv_nt = 0 for A/B runs
+  const Tuning& tu = tuning();
+  a.kv_nt = tu.attn_kv_nt;
+  a.stamps = stamps;
+  a.ksc = ksc; a.vsc = vsc; a.SmaxP = ksc ? SmaxP : 0;
+  const bool kv8 = ksc != nullptr;
+  if (kv8 && !vsc) return -3;
   if (B == 0) return 0;
   const int G = Hq / Hkv;
   if (G * Hkv != Hq) return -1;
@@ -2305,13 +2288,11 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     // fp8 cache: the MFMA kernels only (large batch: one workgroup per (batch, kv head); small
     // batch: 8 waves per (batch, kv head), partitions for long caches)
     if (D != 128 || a.SmaxP < Smax || (G != 1 && G != 2 && G != 4 && G != 8)) return -3;
-    // RT_DECODE_FP8_MW=1: the 8-wave kernel at every batch (A/B hook)
-    static const int fp8_mw = getenv("RT_DECODE_FP8_MW") ? atoi(getenv("RT_DECODE_FP8_MW")) : 0;
-    // MHA at large batch: the VALU kernel (RT_DECODE_G1_VALU=0: the MFMA form)
-    static const int g1_valu = getenv("RT_DECODE_G1_VALU") ? atoi(getenv("RT_DECODE_G1_VALU")) : 1;
-    if (!fp8_mw && g1_valu && G == 1 && !a.qkv_slabs && rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
-      // waves per row (A/B hook RT_DECODE_G1_NW = 1, 2, 4; default 2)
-      static const int g1_nw = getenv("RT_DECODE_G1_NW") ? atoi(getenv("RT_DECODE_G1_NW")) : 2;
+    // tuning decode_fp8_mw = 1: the 8-wave kernel at every batch (A/B)
+    const int fp8_mw = tu.decode_fp8_mw;
+    // MHA at large batch: the VALU kernel (decode_g1_valu = 0: the MFMA form)
+    if (!fp8_mw && tu.decode_g1_valu && G == 1 && !a.qkv_slabs && rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
+      const int g1_nw = tu.decode_g1_nw;  // waves per row (1, 2, 4; default 2)
       if (g1_nw == 4) hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<4>, dim3((unsigned)(B * Hkv)), dim3(256), 0, stream, a);
       else if (g1_nw == 1) hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<1>, dim3((unsigned)(B * Hkv)), dim3(64), 0, stream, a);
       else hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<2>, dim3((unsigned)(B * Hkv)), dim3(128), 0, stream, a);
@@ -2371,7 +2352,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     return 0;
   }
   if (a.qkv_slabs) return -2;  // the slab form exists only in the MFMA kernel (caller reduces first)
-  const int nk = g_dec_nk > 0 ? g_dec_nk : 4;  // keys per lane per chunk; PS must be a multiple of the chunk
+  const int nk = tu.decode_nk > 0 ? tu.decode_nk : 4;  // keys per lane per chunk; PS must be a multiple of the chunk
   if (PS % (4 * (64 / (D / 8)) * nk) != 0) return -1;
   dim3 grid(NP, Hkv, B), block(256);
 #define DF_CASE(DD, GG, NN)                                                                   \
@@ -2403,8 +2384,8 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
   const long rows_per_block = 4L * (64 / (D / 8));
   dim3 pgrid((unsigned)((rows + rows_per_block - 1) / rows_per_block)), grid((S + 63) / 64, Hkv, B);
   // dQ: a separate kernel per 64-query block (default) or fp32 atomics from the key-block kernel
-  // (RT_ATTN_BWD_ATOMIC_DQ=1, the round-1 form)
-  static const bool atomic_dq = getenv("RT_ATTN_BWD_ATOMIC_DQ") && atoi(getenv("RT_ATTN_BWD_ATOMIC_DQ"));
+  // (tuning attn_bwd_atomic_dq = 1, the round-1 form)
+  const bool atomic_dq = tuning().attn_bwd_atomic_dq != 0;
   if (D != 64 && D != 128) return -1;
   if (atomic_dq) RT_HIP_CHECK(hipMemsetAsync(dq_f32, 0, (size_t)B * S * Hq * D * sizeof(float), stream));
   dim3 qgrid((S + 63) / 64, Hq, B);
@@ -2435,7 +2416,7 @@ extern "C" int rt_attn_o_fused(const void* qkv, void* kc, void* vc, int Smax, co
                                const int* kv_start, const int* pos, const float* cosT, const float* sinT, float sign,
                                int window, float* part, int NP, int PS, int Hq, int Hkv, int D, float scale,
                                const void* w, long ldw, const void* res, void* out, int H, unsigned* sync, int* err,
-                               hipStream_t stream) {
+                               long long* stamps, hipStream_t stream) {
   AttnOArgs g;
   DecodeFusedArgs& a = g.at;
   a.qkv = (const bf16_t*)qkv; a.ldq = 0; a.kc = (bf16_t*)kc; a.vc = (bf16_t*)vc; a.Smax = Smax;
@@ -2444,7 +2425,7 @@ extern "C" int rt_attn_o_fused(const void* qkv, void* kc, void* vc, int Smax, co
   a.B = 1; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
   a.qkv_slabs = nullptr; a.qkv_nsplit = 0; a.qkv_sstride = 0; a.kv_nt = 0; a.stamps = nullptr;
   g.w = (const bf16_t*)w; g.ldw = ldw; g.res = (const bf16_t*)res; g.out = (bf16_t*)out; g.H = H;
-  g.sync = sync; g.err = err; g.stamps = g_ao_stamps;
+  g.sync = sync; g.err = err; g.stamps = stamps;
   const int G = Hq / Hkv;
   const int nk = 4;
   if (G * Hkv != Hq || Hq * D != AO_K || H % AO_ROWS != 0 || (ldw % 8) != 0) return -1;

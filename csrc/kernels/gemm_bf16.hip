@@ -1420,10 +1420,8 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(GemmArgs p, const floa
 // through one parallel reduce launch). From the cold-weight sweep (profiles/r3/fp8_decode_table_*,
 // M = 24 .. 64): gate_up 108-112 groups -> 2, qkv 24 / 60 groups -> 8 / 4, o 16-20 -> 8, down
 // (K 13824 / 14336) 16 / 20 groups -> 16 / 8.
-static int g_wide_split = 0;  // tuning override (rt_gemm_set_wide_split)
-extern "C" void rt_gemm_set_wide_split(int s) { g_wide_split = s; }
 static int wide_split(int N, int K) {
-  if (g_wide_split > 0) return g_wide_split;
+  if (tuning().wide_split > 0) return tuning().wide_split;
   const int groups = N / 256, nk = K / 64;
   int split = 1;
   while (groups * split * 2 <= 256 && nk / (split * 2) >= 8 && split < 16) split *= 2;
@@ -1433,10 +1431,9 @@ static int wide_split(int N, int K) {
 // split-K for the ring kernel, from a cold-weight sweep on MI355X (profiles/kernels_m64_split.log,
 // M = 64): wide outputs (>= 256 column groups) stream best unsplit, long K / narrow N want 8-way
 // split, mid shapes 2-way.
-static int g_m64_split = 0;  // 0 = heuristic below; tuning override (rt_gemm_set_m64_split)
 
 static int m64_split(int N, int K) {
-  if (g_m64_split > 0) return g_m64_split;
+  if (tuning().m64_split > 0) return tuning().m64_split;
   const int groups = (N + 63) / 64, nk = K / 64;
   int split;
   if (groups >= 256) split = 1;
@@ -1451,13 +1448,12 @@ static int m64_split(int N, int K) {
 // groups: gate_up, lm_head) stream best unsplit — a second round of workgroups costs more than it
 // hides; narrower ones split until ~2 workgroups per CU are resident, keeping >= 2 k-chunks per wave
 // (M = 1: qkv 16.5 -> 13.7 us, o 11.8 -> 10.9, down 29.4 -> 28.4 at split 8 vs 4).
-static int g_decode_split = 0;  // 0 = heuristic below; tuning override (rt_gemm_set_decode_split)
 
 // Tile-ordered (shuffled) weights stream best with ~8 blocks per column group at every width
 // (gate_up 52.0 -> 43.2 us, lm_head 52.2 -> 47.7 at split 8 vs unsplit row-major; qkv / o / down
 // as the row-major heuristic), keeping >= 2 k-chunks per wave (profiles/kernels_decode_depth_shuffle.log).
 static int decode_split_shuf(int K) {
-  if (g_decode_split > 0) return g_decode_split;
+  if (tuning().decode_split > 0) return tuning().decode_split;
   const int nc = K / 64;
   int split = 8;
   while (split > 1 && nc / (4 * split) < 2) split >>= 1;
@@ -1465,7 +1461,7 @@ static int decode_split_shuf(int K) {
 }
 
 static int decode_split(int N, int K) {
-  if (g_decode_split > 0) return g_decode_split;
+  if (tuning().decode_split > 0) return tuning().decode_split;
   const int groups = (N + DG_COLS - 1) / DG_COLS;
   const int nc = K / 64;
   if (groups >= 256) return 1;
@@ -1487,28 +1483,22 @@ static int fit_split(int split, int groups, long slab_floats) {
 }
 
 // 0 = automatic, 1 = force the 128x128 tile kernel, 2 = force the 256x256 kernel (M > 64)
-static int g_gemm_variant = 0;
-extern "C" void rt_gemm_set_variant(int v) { g_gemm_variant = v; }
-extern "C" void rt_gemm_set_m64_split(int s) { g_m64_split = s; }
-extern "C" void rt_gemm_set_decode_split(int s) { g_decode_split = s; }
 
 // register sets of the M <= 16 kernel's weight pipeline (DEPTH - 1 k-chunks in flight per wave).
 // 4 sets cost ~85 VGPRs at MT = 1 (occupancy 3 -> 2 blocks per CU; MT = 2 would spill) and
 // measured no faster even on the unsplit wide GEMMs (gate_up 48.9 vs 48.7 us, lm_head 52.8 vs
 // 52.6; profiles/kernels_decode_depth_shuffle.log): the default stays 2. 2 / 4 force (tuning).
-static int g_decode_depth = 0;
-extern "C" void rt_gemm_set_decode_depth(int d) { g_decode_depth = d; }
 // batch-1 GEMVs on the 16-row no-split kernel: narrow outputs (qkv, o, down) whose split-K tail
-// costs more than a second round of workgroups; RT_GEMV16=0 keeps them on gemm_decode_kernel
-// RT_GEMV16: 0 off, 1 narrow outputs only (N <= 8192: qkv, o, down), 2 also wide ones (SwiGLU
+// costs more than a second round of workgroups; tuning gemv16 = 0 keeps them on gemm_decode_kernel
+// tuning gemv16: 0 off, 1 narrow outputs only (N <= 8192: qkv, o, down), 2 also wide ones (SwiGLU
 // gate_up, lm_head)
-// rows of X on the no-split kernel (1..16; RT_GEMV16_MAXM)
+// rows of X on the no-split kernel (1..16; tuning gemv16_maxm)
 static int gemv16_max_m() {
-  static const int m = getenv("RT_GEMV16_MAXM") ? atoi(getenv("RT_GEMV16_MAXM")) : 16;
+  const int m = tuning().gemv16_maxm;
   return m < 1 ? 1 : (m > 16 ? 16 : m);
 }
 static bool use_gemv16(int N, int K, int act) {
-  static const int env = getenv("RT_GEMV16") ? atoi(getenv("RT_GEMV16")) : 2;
+  const int env = tuning().gemv16;
   if (!env || K % 64 || K < 1024) return false;
   if (act == ACT_SWIGLU) return env >= 2 && N % 32 == 0 && N / 32 >= 256;
   return N % 16 == 0 && N / 16 >= 256 && (N <= 8192 || env >= 2);
@@ -1516,7 +1506,8 @@ static bool use_gemv16(int N, int K, int act) {
 
 static int decode_depth(int MT, long blocks) {
   if (MT > 1) return 2;
-  if (g_decode_depth == 2 || g_decode_depth == 4) return g_decode_depth;
+  const int dd = tuning().decode_depth;
+  if (dd == 2 || dd == 4) return dd;
   (void)blocks;
   return 2;
 }
@@ -1526,8 +1517,8 @@ static int decode_depth(int MT, long blocks) {
 // (256 slots), the 128-tile kernel two (512 slots); the 256 kernel is ~10 % faster per FLOP
 // when both fill the chip.
 static bool use_256(int M, int N) {
-  if (g_gemm_variant == 1) return false;
-  if (g_gemm_variant == 2) return true;
+  if (tuning().gemm_variant == 1) return false;
+  if (tuning().gemm_variant == 2) return true;
   if (M < 256 || N < 256) return false;
   const double t256 = (double)((M + 255) / 256) * ((N + 255) / 256);
   const double t128 = (double)((M + 127) / 128) * ((N + 127) / 128);
@@ -1555,15 +1546,15 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   if (wshuf && (M > 64 || N % 16 != 0 || K % 64 != 0)) return -4;  // shuffled weights: decode kernel only
   if (act == ACT_SWIGLU && (M > 64 || N % 64 != 0 || (U && UB))) return -2;
   if ((R || norm_eps > 0.f) && M > 64) return -3;  // residual / in-GEMM norm: skinny kernels only
-  if (M > 16 && M <= 64 && p.Rp == 0 && g_gemm_variant != 1 && !wshuf) {
+  if (M > 16 && M <= 64 && p.Rp == 0 && tuning().gemm_variant != 1 && !wshuf) {
     const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64 + 64) : 1;
     dim3 grid(((N + 63) / 64) * split), block(256);
     if (out_f32) hipLaunchKernelGGL((gemm_m64_kernel<true>), grid, block, 0, stream, p, slabs, tickets, split);
     else hipLaunchKernelGGL((gemm_m64_kernel<false>), grid, block, 0, stream, p, slabs, tickets, split);
-  } else if (M <= gemv16_max_m() && wshuf && g_decode_split == 0 && use_gemv16(N, K, act) && p.Rp == 0) {
+  } else if (M <= gemv16_max_m() && wshuf && tuning().decode_split == 0 && use_gemv16(N, K, act) && p.Rp == 0) {
     const bool pair = act == ACT_SWIGLU;
     dim3 grid(pair ? N / 32 : N / 16), block(256);
-    static const int gd = getenv("RT_GEMV16_DEPTH") ? atoi(getenv("RT_GEMV16_DEPTH")) : 4;
+    const int gd = tuning().gemv16_depth;
 #define G16(D, P) if (out_f32) hipLaunchKernelGGL((gemv16_kernel<true, D, P>), grid, block, 0, stream, p); \
                   else hipLaunchKernelGGL((gemv16_kernel<false, D, P>), grid, block, 0, stream, p);
     if (pair) { G16(4, true) } else if (gd == 6) { G16(6, false) } else if (gd == 8) { G16(8, false) } else { G16(4, false) }
@@ -1630,11 +1621,11 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
       // tile-ordered fp8 image: the no-split 16-row kernel up to 16 rows (or RT variant 4), the
       // LDS-DMA ring above
       if (K % 128 || N % 16 || (pair && N % 64)) return -4;
-      if (M <= 16 && g_gemm_variant != 4) {
+      if (M <= 16 && tuning().gemm_variant != 4) {
         dim3 grid(pair ? N / 32 : N / 16), block(256);
         if (pair) hipLaunchKernelGGL((gemv16_kernel<false, 4, true, true>), grid, block, 0, stream, p);
         else hipLaunchKernelGGL((gemv16_kernel<false, 4, false, true>), grid, block, 0, stream, p);
-      } else if (N % 256 == 0 && g_gemm_variant != 5) {
+      } else if (N % 256 == 0 && tuning().gemm_variant != 5) {
         // 256 weight rows per workgroup (X read N / 256 times); RT variant 5 = the 64-column ring
         int split = slabs ? fit_split(wide_split(N, K), N / 256, WD_SLAB) : 1;
         split = std::min(split, std::max(1, K / 64));
@@ -1669,7 +1660,7 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
     // W8A8 (M > 64): the gemm_big schedule with the MX fp8 MFMA (RT_GEMM_FP8_256=1: the older
     // 256x256 8-phase kernel, kept for A/B); SwiGLU pairs [gate; up] in its epilogue
     if (K % 128 || N % 8) return -1;
-    static const int use256 = getenv("RT_GEMM_FP8_256") ? atoi(getenv("RT_GEMM_FP8_256")) : 0;
+    const int use256 = tuning().gemm_fp8_256;
     if (!use256 && lda % 16 == 0 && ldb % 16 == 0 && ldc % 8 == 0 && (act == 0 || (act == ACT_SWIGLU && N % 256 == 0)))
       return rt_gemm_big_fp8(A, lda, sa, B, ldb, sb, bias, C, ldc, M, N, K, act == ACT_SWIGLU ? 5 : 0, nullptr, 0,
                              nullptr, 0, 0, nullptr, 0, nullptr, stream);

@@ -74,6 +74,15 @@ struct Args {
   // sb[weight row] before bias / activation / SwiGLU
   const float* sa;
   const float* sb;
+  // SK (stream-K tail, gemm_big_kernel<..., SK = true>): the first sk_dp blocks run whole tiles
+  // [0, sk_dp) (XCD remap within them); the remaining sk_units blocks split the K-steps of tiles
+  // [sk_dp, sk_dp + sk_tiles) evenly, each up to two tile segments; a tile's partial accumulators
+  // go through sk_part (write-through, 2 slots of 256 x 256 fp32 per unit) and the last arriving
+  // unit (sk_tickets, self-resetting) sums them and runs the epilogue
+  int sk_dp, sk_tiles, sk_units;
+  float* sk_part;
+  unsigned* sk_tickets;
+  int b_layout_kmaj;  // host: NN form of the stream-K launch
 };
 
 __device__ __forceinline__ int row_swz(int row) { return (row >> 1) & 7; }
@@ -118,23 +127,68 @@ __device__ __forceinline__ void wait_granules(int n) {
 // each wave owns 2 B fragments instead of 4 (columns 64 (wc >> 1) + 16 (wc & 1) + 32 s): used for
 // M = 256 decode GEMMs (twice the workgroups, no split-K on the widest weights) and for the last,
 // partial wave of tiles of a large GEMM (rt_gemm_big_planned).
-template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false, bool F8 = false>
+template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false, bool F8 = false, bool SK = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   static_assert(BN == 256 || BN == 128, "BN");
   static_assert(!F8 || (LA == ROW && LB == ROW && OUT == O_BF16), "F8: NT with a bf16 output only");
+  static_assert(!SK || (OUT == O_BF16 && BN == 256), "SK: 256x256 tiles with a bf16 epilogue");
   constexpr int NB = BN / 128;  // B fragments per wave and B sub-block; LDS-DMA instructions per B granule
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];  // the only __shared__ object
 
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS bases
-  const int wr = wid >> 2, wc = wid & 3;
-  const int frow = lane & 15, fq = lane >> 4;
 
-  // ---- tile assignment: XCD remap, then GROUP_M-row groups (L2 reuse of B panels) ----
   const int tiles_m = (p.M + 255) / 256;
   const int tiles_n = EPI == E_SWIGLU ? p.N / BN : (p.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
+  // ---- K-steps ----
+  const int nk1 = (p.K + 63) / 64;
+  const int nk2 = p.A2 ? (p.K2 + 63) / 64 : 0;
+  const int nk = nk1 + nk2;
+
+  // ---- role: (tile, K-step range) segments of this block ----
+  int seg_tile0, seg_b0, seg_e0, seg_tile1 = 0, seg_b1 = 0, seg_e1 = 0, nseg = 1;
+  int sk_unit = -1;  // >= 0: this block is a stream-K unit
+  if constexpr (!SK) {
+    seg_tile0 = xcd_remap(blockIdx.x, nwg);
+    seg_b0 = (int)((long)blockIdx.y * nk / p.nsplit);
+    seg_e0 = (int)((long)(blockIdx.y + 1) * nk / p.nsplit);
+  } else if ((int)blockIdx.x < p.sk_dp) {
+    seg_tile0 = xcd_remap(blockIdx.x, p.sk_dp);
+    seg_b0 = 0;
+    seg_e0 = nk;
+  } else {
+    // units dealt to XCDs in contiguous runs (consecutive units share a tile: their partials stay
+    // in one L2 where the dispatch allows); the run order is a speed choice only
+    const int j = (int)blockIdx.x - p.sk_dp;
+    sk_unit = xcd_remap(j, p.sk_units);
+    const long S = (long)p.sk_tiles * nk;
+    const long g0 = (long)sk_unit * S / p.sk_units, g1 = (long)(sk_unit + 1) * S / p.sk_units;
+    seg_tile0 = p.sk_dp + (int)(g0 / nk);
+    seg_b0 = (int)(g0 % nk);
+    const long end0 = min(g1, (g0 / nk + 1) * nk);
+    seg_e0 = (int)(end0 - (g0 / nk) * nk);
+    if (g1 > end0) {  // the unit runs into the next tile
+      nseg = 2;
+      seg_tile1 = seg_tile0 + 1;
+      seg_b1 = 0;
+      seg_e1 = (int)(g1 - end0);
+    }
+  }
+
+  for (int seg = 0; seg < (SK ? nseg : 1); ++seg) {
+  // lane constants are (re)derived inside the segment loop from an opaque copy of the thread id:
+  // hoisted out of the loop they would stay live across it and push the 256-register body of the
+  // stream-K form into scratch (no effect on the one-segment forms)
+  int tid_raw = threadIdx.x;
+  if constexpr (SK) asm volatile("" : "+v"(tid_raw));
+  const int tid = tid_raw, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS bases
+  const int wr = wid >> 2, wc = wid & 3;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int seg_tile = seg == 0 ? seg_tile0 : seg_tile1;
+  const int t_begin = seg == 0 ? seg_b0 : seg_b1;
+  const int t_end = seg == 0 ? seg_e0 : seg_e1;
+  // ---- tile assignment: GROUP_M-row groups (L2 reuse of B panels) over the remapped id ----
+  const int bid = seg_tile;
   const int group = bid / (GROUP_M * tiles_n);
   const int first_m = group * GROUP_M;
   const int gsz = min(tiles_m - first_m, GROUP_M);
@@ -144,12 +198,6 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   const int Fh = p.N / 2;  // E_SWIGLU: gate rows [0, F), up rows [F, 2F)
   constexpr int HALF = BN / 2;  // E_SWIGLU: tile columns [0, HALF) gate, [HALF, BN) up
 
-  // ---- K-steps of this split ----
-  const int nk1 = (p.K + 63) / 64;
-  const int nk2 = p.A2 ? (p.K2 + 63) / 64 : 0;
-  const int nk = nk1 + nk2;
-  const int t_begin = (int)((long)blockIdx.y * nk / p.nsplit);
-  const int t_end = (int)((long)(blockIdx.y + 1) * nk / p.nsplit);
 
   // ---- LDS-DMA geometry of instruction j (0, 1) of this wave in granule g (0 a0, 1 a1, 2 b0, 3 b1) ----
   // ROW : 8 rows x 128 B per instruction; lane -> row rb + lane/8, 16-B slot lane%8 holding k-chunk
@@ -436,6 +484,71 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+  if constexpr (SK) {
+    if (sk_unit >= 0) {
+      // ---- stream-K hand-off of tile `bid` (cdna_hip_programming.md §6 Guideline 16, R1 form):
+      // the partial tile is stored write-through (sc1, no release fence), every wave drains its
+      // stores, the workgroup meets at a barrier, one lane takes a relaxed agent-scope ticket; the
+      // last arriver reads every other unit's partial with sc1 loads, adds it to its registers and
+      // runs the normal epilogue, then re-arms the ticket (self-resetting: zero before the first
+      // launch, zero after every launch). Correct for any placement of units on XCDs / CUs.
+      const int tl = bid - p.sk_dp;  // tile index within the stream-K region
+      const long S = (long)p.sk_tiles * nk;
+      const int U = p.sk_units;
+      const int u_first = (int)((((long)tl * nk + 1) * U - 1) / S);
+      const int u_last = (int)((((long)(tl + 1) * nk) * U - 1) / S);
+      constexpr int PART = 256 * 256;  // floats per partial slot
+      auto slot_rsrc = [&](int u, int sg) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(p.sk_part + ((long)u * 2 + sg) * PART), (short)0, PART * 4,
+                                                 0x00020000);
+      };
+      {
+        const auto rs = slot_rsrc(sk_unit, seg);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 2 * NB; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[i][j]), rs,
+                                                   ((i * 2 * NB + j) * 512 + tid) * 16, 0, 16 /* sc1 */);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+      __syncthreads();
+      int* flag = (int*)smem;  // the one LDS array (staging buffers are idle here)
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(p.sk_tickets + tl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = old == (unsigned)(u_last - u_first);
+      }
+      __syncthreads();
+      const bool last = *flag != 0;
+      __syncthreads();
+      if (!last) continue;  // another unit finishes this tile
+      for (int u = u_first; u <= u_last; ++u) {
+        if (u == sk_unit) continue;
+        // the tile is the first segment of unit u unless u started inside an earlier tile
+        const int sg = (int)(((long)u * S / U) / nk) == tl ? 0 : 1;
+        const auto rs = slot_rsrc(u, sg);
+        // two accumulator rows (32 registers) of loads in flight at a time: the registers hold the
+        // whole 256 x 256 accumulator already
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+          i32x4 v[2][2 * NB];
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 2 * NB; ++j)
+              v[ii][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((i + ii) * 2 * NB + j) * 512 + tid) * 16, 0,
+                                                               16 /* sc1 */);
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 2 * NB; ++j) acc[i + ii][j] += __builtin_bit_cast(f32x4, v[ii][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (tid == 0) __hip_atomic_store(p.sk_tickets + tl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+
   // ---- epilogue ----
   // SWAP: acc[i][j][r] = C[m0 + 128 wr + 16 i + frow][n0 + 64 wc + 16 j + 4 fq + r]
   // else: acc[i][j][r] = C[m0 + 128 wr + 16 i + 4 fq + r][n0 + 64 wc + 16 j + frow]
@@ -574,6 +687,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       __syncthreads();
     }
   }
+  }  // segments
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1122,7 +1236,7 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
   dim3 grid(((p.M + 255) / 256) * tiles_n, p.nsplit), block(512);
   const int key = layout_a * 100 + layout_b * 10 + out;
   // A/B switch: the NN / TN forms with the compiler's transposed-read builtin
-  static const bool trb = getenv("RT_GEMM_TR_BUILTIN") && atoi(getenv("RT_GEMM_TR_BUILTIN"));
+  const bool trb = tuning().gemm_tr_builtin != 0;
   if (trb && act == E_NONE && (key == 10 || key == 112)) {
     if (key == 10 && bn == 128) hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 128, true>), grid, block, 0, stream, p);
     else if (key == 10) hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 256, true>), grid, block, 0, stream, p);
@@ -1203,24 +1317,69 @@ static bool bn128_supported(int layout_a, int layout_b, int act, int out) {
   return (key == 0 && (act == E_NONE || act == E_SWIGLU)) || (act == E_NONE && (key == 1 || key == 3 || key == 10));
 }
 
+static int query_num_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  return n;
+}
+// a device property, computed once (thread-safe static initialisation)
 static int num_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
+  static const int n = query_num_cus();
   return n;
 }
 
 // Ratio of a 256x128 tile's time to a 256x256 tile's (same K), for the wave planner below.
-static float bn128_cost() {
-  static float r = -1.f;
-  if (r < 0.f) {
-    const char* e = getenv("RT_GEMM_BN128_COST");
-    r = e ? (float)atof(e) : 0.55f;
-  }
+static float bn128_cost() { return tuning().gemm_bn128_cost; }
+
+// Stream-K tail (gemm_big_kernel<..., SK = true>): T = tiles of 256 x 256 on C CUs with a partial
+// last wave (T % C = rem > 0). The first (T / C) * C tiles run whole, one block each (data
+// parallel); the K-steps of the last rem tiles are split evenly over `units` blocks (up to C), so
+// the tail costs rem / C of a tile's time plus a hand-off instead of a whole tile's time
+// (M = 9632 tokens x qkv: 912 tiles = 3.56 waves -> 3 + 0.56 instead of 4). Forms: NT (no
+// activation / SwiGLU) and NN, bf16 out.
+static bool streamk_form(int layout_a, int layout_b, int act, int out) {
+  const int key = layout_a * 100 + layout_b * 10 + out;
+  return (key == 0 && (act == E_NONE || act == E_SWIGLU)) || (key == 10 && act == E_NONE);
+}
+
+struct SkPlan {
+  int dp_tiles = 0, sk_tiles = 0, units = 0;
+  float cost = 1e30f;  // in 256x256 tile-wave times
+};
+
+static SkPlan streamk_plan(int tiles, int nk, int cus) {
+  SkPlan r;
+  const int full = tiles / cus, rem = tiles % cus;
+  if (full < 1 || rem == 0 || nk < 16) return r;
+  // at least 8 K-steps per unit: fewer units when the tail is small
+  const long S = (long)rem * nk;
+  r.units = (int)std::min<long>(cus, std::max<long>(rem, S / 8));
+  r.dp_tiles = full * cus;
+  r.sk_tiles = rem;
+  // tail = the longest unit's share of a tile + the hand-off (partial store, ticket, the last
+  // arriver's partial loads) and a second prologue, ~8 % of a K = 4096 tile
+  r.cost = (float)full + (float)((S + r.units - 1) / r.units) / (float)nk + 0.08f;
   return r;
+}
+
+static int launch_gemm_big_sk(const Args& p, int layout_a, int act, const SkPlan& pl, hipStream_t stream) {
+  Args q = p;
+  q.sk_dp = pl.dp_tiles;
+  q.sk_tiles = pl.sk_tiles;
+  q.sk_units = pl.units;
+  q.nsplit = 1;
+  dim3 grid(pl.dp_tiles + pl.units, 1), block(512);
+  if (layout_a != ROW) return -4;
+  if (p.b_layout_kmaj) {
+    hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 256, false, false, true>), grid, block, 0, stream, q);
+  } else if (act == E_SWIGLU) {
+    hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_SWIGLU, 256, false, false, true>), grid, block, 0, stream, q);
+  } else {
+    hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_NONE, 256, false, false, true>), grid, block, 0, stream, q);
+  }
+  RT_LAUNCH_CHECK();
+  return 0;
 }
 
 // layout_a / layout_b: 0 = ROW (K contiguous), 1 = KMAJ (M / N contiguous).
@@ -1231,10 +1390,13 @@ static float bn128_cost() {
 // (e.g. M = 9632 tokens x N = 4096: 608 tiles = 2.4 waves of 256 CUs -> 512 tiles + 192 half tiles).
 // Requirements (checked): KMAJ operands have M / N % 8 == 0 and 16-B aligned rows; ROW operands
 // 16-B aligned rows; K, K2 % 8 == 0; E_SWIGLU: ROW/ROW, bf16 out, N % 256 == 0.
+// sk_part / sk_tickets: the stream-K workspace (>= 2 * cus partial slots of 256 x 256 fp32, >= cus
+// zeroed tickets, one per stream) or null (no stream-K).
 extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb,
                            const void* A2, long lda2, const void* B2, long ldb2, int K2, const void* bias,
                            void* C, long ldc, void* C2, long ldc2, const void* R, long ldr, int M, int N, int K,
-                           int act, int out, int nsplit, const void* zpage, int bn, hipStream_t stream) {
+                           int act, int out, int nsplit, const void* zpage, int bn, float* sk_part,
+                           unsigned* sk_tickets, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   // a ROW operand reads 8-element k-chunks: its reduction length must be a multiple of 8
   const bool any_row = layout_a == ROW || layout_b == ROW;
@@ -1255,31 +1417,42 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   if ((bn == 4 || bn == 3) && (layout_a != ROW || layout_b != ROW || (out != O_BF16 && out != O_F32) || nsplit != 1 ||
                   (long)N * ldb * 2 >= (1L << 32) || (long)M * lda * 2 >= (1L << 32)))
     return -8;
-  Args p;
+  Args p{};
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
   p.A2 = (A2 && B2) ? (const bf16_t*)A2 : nullptr; p.lda2 = lda2;
   p.B2 = (const bf16_t*)B2; p.ldb2 = ldb2; p.K2 = K2;
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = (bf16_t*)C2; p.ldc2 = ldc2;
   p.R = (const bf16_t*)R; p.ldr = ldr;
   p.M = M; p.N = N; p.K = K; p.act = act; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
-  // RT_GEMM_B_NT=1: non-temporal weight stream when one row tile covers M (each B byte read once
-  // per launch). Measured neutral on the batch-256 decode GEMMs (profiles/decode_nt_ab.log): off
-  static const int bnt_env = getenv("RT_GEMM_B_NT") ? atoi(getenv("RT_GEMM_B_NT")) : 0;
-  p.b_nt = layout_b == ROW && M <= 256 && bnt_env > 0;
+  // tuning gemm_b_nt = 1: non-temporal weight stream when one row tile covers M (each B byte read
+  // once per launch). Measured neutral on the batch-256 decode GEMMs (profiles/decode_nt_ab.log): off
+  p.b_nt = layout_b == ROW && M <= 256 && tuning().gemm_b_nt > 0;
   if (bn != 0) return launch_gemm_big(p, layout_a, layout_b, act, out, bn, stream);
-  // ---- plan: m1 row tiles at BN = 256, the rest at BN = 128 ----
+  // ---- plan: m1 row tiles at BN = 256, the rest at BN = 128; or a stream-K tail ----
   const int tiles_m = (M + 255) / 256;
   const int tn256 = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
   const int tn128 = act == E_SWIGLU ? N / 128 : (N + 127) / 128;
   const long cus = (long)num_cus() * 1;  // one 512-thread, 128-KiB-LDS workgroup per CU
   int m1 = tiles_m;
+  float best = (float)((long)tiles_m * tn256 + cus - 1) / (float)cus;
   if (can128 && nsplit == 1 && (out == O_BF16 || out == O_F32)) {
     const float r = bn128_cost();
-    float best = 1e30f;
+    best = 1e30f;
     for (int m = tiles_m; m >= 0; --m) {
       const long w256 = ((long)m * tn256 + cus - 1) / cus, w128 = ((long)(tiles_m - m) * tn128 + cus - 1) / cus;
       const float cost = (float)w256 + r * (float)w128;
       if (cost < best - 1e-3f) { best = cost; m1 = m; }
+    }
+  }
+  if (tuning().gemm_streamk && sk_part && sk_tickets && nsplit == 1 && streamk_form(layout_a, layout_b, act, out)) {
+    const int nk = (K + 63) / 64 + (p.A2 ? (K2 + 63) / 64 : 0);
+    const SkPlan pl = streamk_plan(tiles_m * tn256, nk, (int)cus);
+    if (pl.units > 0 && (pl.cost < best || tuning().gemm_streamk == 2)) {
+      Args q = p;
+      q.sk_part = sk_part;
+      q.sk_tickets = sk_tickets;
+      q.b_layout_kmaj = layout_b == KMAJ;
+      return launch_gemm_big_sk(q, layout_a, act, pl, stream);
     }
   }
   if (m1 == tiles_m) return launch_gemm_big(p, layout_a, layout_b, act, out, 256, stream);

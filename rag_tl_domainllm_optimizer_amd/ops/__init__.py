@@ -1,6 +1,6 @@
 """Public op API. One entry per native kernel; GPU tensors run the gfx950 HIP kernels, CPU tensors
 the eager reference implementations (:mod:`.reference`, also the test oracles)."""
-from ._ext import native, native_available, on_gpu  # noqa: F401
+from ._ext import get_tuning, native, native_available, on_gpu, set_tuning, tuning  # noqa: F401
 from .linear import (  # noqa: F401
     ACT_IDS, ACT_SWIGLU, KMAJ, ROW, FoldCache, LoRAGroup, ShufCache, SplitK, gemm, gemm_big, gemm_decode, gemm_nn, gemm_tn, linear,
     refresh_lora_batched,

@@ -61,3 +61,34 @@ def on_gpu(*ts) -> bool:
         if t is not None and hasattr(t, "is_cuda"):
             return bool(t.is_cuda)
     return False
+
+
+def get_tuning() -> dict:
+    """The native launchers' kernel-selection knobs (csrc/include/rt_tuning.h: A/B switches of the
+    measured alternatives, forced split-K factors) as a dict."""
+    return dict(native().get_tuning())
+
+
+def set_tuning(**fields) -> dict:
+    """Update knobs by name (unknown names raise); returns the previous values of those fields."""
+    cur = get_tuning()
+    unknown = [k for k in fields if k not in cur]
+    if unknown:
+        raise KeyError(f"unknown tuning field(s): {unknown}; known: {sorted(cur)}")
+    native().set_tuning(dict(fields))
+    return {k: cur[k] for k in fields}
+
+
+class tuning:
+    """Context manager: ``with ops.tuning(decode_split=2): ...`` sets knobs and restores them."""
+
+    def __init__(self, **fields):
+        self.fields = fields
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = set_tuning(**self.fields)
+        return self
+
+    def __exit__(self, *exc):
+        native().set_tuning(self.prev)

@@ -325,11 +325,12 @@ def _decode_step_fp8kv_cpu(qkv, k_cache, v_cache, k_scale, v_scale, slot, attn_l
 
 def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, cos=None, sin=None, kv_start=None,
                           window=0, scale=None, workspace=None, out=None, sign: float = 1.0, k_scale=None,
-                          v_scale=None):
+                          v_scale=None, stamps=None):
     """One decode step of a layer, fused: rotate q / k_new (if ``cos`` is given), append k_new and
     v_new at cache slot ``slot[b]``, attend over ``attn_len[b]`` keys -> [B, Hq*D].
     ``qkv`` [B, (Hq + 2 Hkv) D] is left unrotated (the fused kernel rotates in registers).
-    ``k_scale`` / ``v_scale`` [B, Hkv, SmaxP]: the caches are fp8 (uint8) — see ``kv_store_fp8``."""
+    ``k_scale`` / ``v_scale`` [B, Hkv, SmaxP]: the caches are fp8 (uint8) — see ``kv_store_fp8``.
+    ``stamps``: debug int64 buffer for the 8-wave kernel's per-block phase stamps (tools/)."""
     from .linear import SplitK
 
     B, Hkv, Smax, D = k_cache.shape
@@ -341,11 +342,9 @@ def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, c
             workspace = decode_workspace(B, Hq, Hkv, D, Smax, k_cache.device)
         if out is None:
             out = torch.empty(B, Hq * D, dtype=qkv.dtype, device=qkv.device)
-        if fp8kv:
-            native().attn_decode_set_fp8kv(k_scale, v_scale)
         if native().attn_decode_fused_slabs(qkv.slabs, qkv.nsplit, k_cache, v_cache, slot, attn_len, kv_start, pos,
                                             cos, sin, sign, window, scale, Hq, workspace[0], workspace[2],
-                                            workspace[1], out):
+                                            workspace[1], out, k_scale, v_scale):
             return out
         qkv = qkv.reduce()
     if not on_gpu(qkv):
@@ -360,15 +359,13 @@ def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, c
     part, PS, tickets = workspace[0], workspace[1], workspace[2]
     if out is None:
         out = torch.empty(B, Hq * D, dtype=qkv.dtype, device=qkv.device)
-    if fp8kv:
-        native().attn_decode_set_fp8kv(k_scale, v_scale)
     native().attn_decode_fused(qkv, k_cache, v_cache, slot, attn_len, kv_start, pos, cos, sin, sign, window, scale,
-                               Hq, part, tickets, PS, out)
+                               Hq, part, tickets, PS, out, k_scale, v_scale, stamps)
     return out
 
 
 def decode_step_attention_o(qkv, k_cache, v_cache, slot, attn_len, Hq, w_o, residual, pos=None, cos=None, sin=None,
-                            kv_start=None, window=0, scale=None, workspace=None):
+                            kv_start=None, window=0, scale=None, workspace=None, stamps=None):
     """Batch-1 decode step of a layer in ONE launch: fused attention (as ``decode_step_attention``)
     followed by ``o_proj`` and the residual add: returns ``residual + attn @ w_o^T`` [1, H], or
     None when the shape is not covered (batch != 1, Hq*D != 4096, CPU, ...) — the caller then runs
@@ -383,7 +380,8 @@ def decode_step_attention_o(qkv, k_cache, v_cache, slot, attn_len, Hq, w_o, resi
     part, PS, sync = workspace[0], workspace[1], workspace[3]
     out = torch.empty_like(residual)
     ok = native().attn_o_fused(qkv.contiguous(), k_cache, v_cache, slot, attn_len, kv_start, pos, cos, sin, 1.0,
-                               window, scale, Hq, part, PS, w_o, residual.contiguous(), out, sync[:2], sync[2:])
+                               window, scale, Hq, part, PS, w_o, residual.contiguous(), out, sync[:2], sync[2:],
+                               stamps)
     return out if ok else None
 
 

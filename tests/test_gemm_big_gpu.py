@@ -224,3 +224,72 @@ def test_w4_identity_bias_act_lora_swiglu(bn):
     p_ref = (x.float() @ wg.float().t() + u.float() @ ub.float().t()).to(torch.bfloat16)
     _close(pre, p_ref)
     _close(y, torch.nn.functional.silu(p_ref[:, :F].float()) * p_ref[:, F:].float())
+
+
+# ---- stream-K tail (gemm_big_kernel<..., SK = true>): the last partial wave of 256x256 tiles split
+# over K across every CU, partial tiles handed to the last arriving unit ----
+# (M, N, K): tiles = ceil(M/256) * N/256 > 256 CUs with a remainder; ragged M / K; 1-3 segments
+_SK_SHAPES = [(4352, 4096, 1024), (4500, 4096, 1000), (2600, 6144, 2048), (9632, 6144, 4096)]
+
+
+@pytest.mark.parametrize("M,N,K", _SK_SHAPES)
+def test_streamk_nt_nn_matches_reference(M, N, K):
+    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
+    r = _r(M, N)
+    with ops.tuning(gemm_streamk=2):
+        got = ops.gemm_big(a, w, ops.ROW, ops.ROW)
+        out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        ops.gemm_big(a, w, ops.ROW, ops.ROW, out=out, residual=r)
+        wk = _r(K, N, s=1 / math.sqrt(K))
+        nn = ops.gemm_big(a, wk, ops.ROW, ops.KMAJ)
+    want = a.float() @ w.float().t()
+    _close(got, want)
+    assert not torch.isnan(out).any()
+    _close(out, want + r.float())
+    _close(nn, a.float() @ wk.float())
+    # the data-parallel planner on the same operands: same result up to the K-split summation order
+    with ops.tuning(gemm_streamk=0):
+        dp = ops.gemm_big(a, w, ops.ROW, ops.ROW)
+    _close(got, dp, rtol=1e-2, atol=1e-2)
+    torch.cuda.synchronize()
+    assert ops.native().streamk_dirty_tickets() == 0
+
+
+def test_streamk_lora_extension_and_swiglu():
+    """The K-extension steps (LoRA) are part of the split K range; SwiGLU + pre-activation output
+    from the reduced tile."""
+    M, K, F, R = 4352, 1024, 2048, 64  # 17 x 16 = 272 tiles of the [gate; up] weight
+    x, w = _r(M, K), _r(2 * F, K, s=1 / math.sqrt(K))
+    u, ub = _r(M, R), _r(2 * F, R, s=0.1)
+    with ops.tuning(gemm_streamk=2):
+        y = ops.gemm_big(x, w, ops.ROW, ops.ROW, u, ub)
+        pre = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+        f = ops.gemm_big(x, w, ops.ROW, ops.ROW, act=ops.ACT_SWIGLU, out2=pre)
+        dy, du, ap = _r(M, 2 * F), _r(M, R), _r(R, K, s=0.1)
+        dx = ops.gemm_nn(dy, w, du, ap)
+    _close(y, x.float() @ w.float().t() + u.float() @ ub.float().t())
+    p_ref = (x.float() @ w.float().t()).to(torch.bfloat16)
+    _close(pre, p_ref)
+    _close(f, torch.nn.functional.silu(p_ref[:, :F].float()) * p_ref[:, F:].float())
+    _close(dx, dy.float() @ w.float() + du.float() @ ap.float())
+    torch.cuda.synchronize()
+    assert ops.native().streamk_dirty_tickets() == 0
+
+
+def test_streamk_repeat_and_side_stream():
+    """Tickets re-arm themselves: many launches back to back (and on a second stream with its own
+    workspace) give identical results."""
+    M, N, K = 4500, 4096, 1536
+    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
+    with ops.tuning(gemm_streamk=2):
+        first = ops.gemm_big(a, w, ops.ROW, ops.ROW)
+        for _ in range(5):
+            assert torch.equal(ops.gemm_big(a, w, ops.ROW, ops.ROW), first)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            side = ops.gemm_big(a, w, ops.ROW, ops.ROW)
+        torch.cuda.current_stream().wait_stream(s)
+        assert torch.equal(side, first)
+    torch.cuda.synchronize()
+    assert ops.native().streamk_dirty_tickets() == 0

@@ -450,7 +450,7 @@ def test_decode_gemm_shuffled_weight_bitwise(M, N, K):
         args = (None, None, None, kw.get("act", 0), False, None, kw.get("residual"), kw.get("norm_eps", 0.0))
         try:
             for split in (0, 2):  # 0: each layout's own split heuristic; forced: the same split-K
-                C.gemm_set_decode_split(split)
+                C.set_tuning({"decode_split": split})
                 base = C.gemm(a, w, *args)
                 for _ in range(2):  # split-K tickets re-arm
                     got = C.gemm(a, ws, *args, True)
@@ -459,7 +459,7 @@ def test_decode_gemm_shuffled_weight_bitwise(M, N, K):
                     else:
                         _close(got, base, rtol=1e-2, atol=1e-2)
         finally:
-            C.gemm_set_decode_split(0)
+            C.set_tuning({"decode_split": 0})
     with pytest.raises(RuntimeError):
         C.gemm(torch.randn(65, K, device=DEV, dtype=torch.bfloat16), ws, w_shuffled=True)
 
@@ -605,7 +605,7 @@ def test_gemm_large_variants(variant, M, N, K, R):
     ub = torch.randn(N, R, device=DEV, dtype=torch.bfloat16) * 0.1 if R else None
     b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
     try:
-        C.gemm_set_variant(variant)
+        C.set_tuning({"gemm_variant": variant})
         for act in (0, 4):
             _close(ops.gemm(a, w, u, ub, b, act), ref.gemm(a, w, u, ub, b, act, out_f32=True))
         _close(ops.gemm(a, w, u, ub, None, 0, out_f32=True), ref.gemm(a, w, u, ub, None, 0, out_f32=True),
@@ -615,7 +615,7 @@ def test_gemm_large_variants(variant, M, N, K, R):
         for _ in range(5):
             assert torch.equal(ops.gemm(a, w, u, ub, b, 0), y0)
     finally:
-        C.gemm_set_variant(0)
+        C.set_tuning({"gemm_variant": 0})
 
 
 def test_gemm_256_identity():
@@ -624,10 +624,10 @@ def test_gemm_256_identity():
     a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
     w = (torch.arange(n * n, device=DEV).reshape(n, n) % 97).to(torch.bfloat16)
     try:
-        C.gemm_set_variant(2)
+        C.set_tuning({"gemm_variant": 2})
         assert torch.equal(ops.gemm(a, w).float(), w.t().float())
     finally:
-        C.gemm_set_variant(0)
+        C.set_tuning({"gemm_variant": 0})
 
 
 @pytest.mark.parametrize("B,Hq,Hkv,D,Smax,rot,window", [(1, 32, 8, 128, 456, True, 0), (64, 32, 8, 128, 456, True, 0),
@@ -783,7 +783,7 @@ def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split):
     """16 < M <= 64 ring kernel with every split-K and epilogue (plain, in-GEMM RMS norm, residual,
     SwiGLU pair) against fp32 references; tickets re-arm across launches."""
     C = ops.native()
-    C.gemm_set_m64_split(split)
+    C.set_tuning({"m64_split": split})
     try:
         torch.manual_seed(M + N + K)
         x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2
@@ -799,7 +799,7 @@ def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split):
             g, u = (x.float() * rstd) @ w[:F].float().t(), (x.float() * rstd) @ w[F:].float().t()
             _close(ops.gemm_decode(x, w, act=ops.ACT_SWIGLU, norm_eps=1e-5), torch.nn.functional.silu(g) * u)
     finally:
-        C.gemm_set_m64_split(0)
+        C.set_tuning({"m64_split": 0})
 
 
 @pytest.mark.parametrize("vclip", [None, 0.2])

@@ -102,7 +102,7 @@ def test_shuffled_decode_weights_match_row_major(monkeypatch):
     p = SamplingParams(max_new_tokens=12, temperature=0.7, top_k=0, seed=9)
     prompts = [[5, 9, 33, 41, 7, 8, 9, 10, 11]]
     outs = {}
-    ops.native().gemm_set_decode_split(2)  # same split-K for both layouts -> bitwise comparable
+    ops.native().set_tuning({"decode_split": 2})  # same split-K for both layouts -> bitwise comparable
     for flag in ("1", "0"):
         monkeypatch.setenv("RAGTL_DECODE_SHUF", flag)
         gen = Generator(m, 1, 64, DEV)
@@ -116,7 +116,7 @@ def test_shuffled_decode_weights_match_row_major(monkeypatch):
             out = gen.generate(prompts, p, pad_id=0, eos_ids=[-1])
             res.append((out.tokens.clone(), out.logprobs.clone()))
         outs[flag] = res
-    ops.native().gemm_set_decode_split(0)
+    ops.native().set_tuning({"decode_split": 0})
     assert any(len(layer._shufc) for layer in m.layers) and m._head_shuf is not None
     for (t1, l1), (t0, l0) in zip(outs["1"], outs["0"]):
         assert torch.equal(t1, t0)

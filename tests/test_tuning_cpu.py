@@ -1,0 +1,66 @@
+"""Launch paths carry no hidden state: no environment lookups and no mutable process globals in the
+native launchers (per-call operands are arguments; kernel-selection knobs live in ONE struct,
+rt::Tuning, set from Python). Static source checks plus the set/get round trip of the binding."""
+import glob
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip"))) + [os.path.join(ROOT, "csrc", "bindings.cpp")]
+
+
+def _code(path):
+    """Source without // and /* */ comments."""
+    s = open(path).read()
+    s = re.sub(r"/\*.*?\*/", "", s, flags=re.S)
+    return re.sub(r"//[^\n]*", "", s)
+
+
+def test_no_getenv_in_launchers():
+    hits = [(os.path.basename(p), m.group(0)) for p in NATIVE for m in re.finditer(r"\bgetenv\s*\(", _code(p))]
+    assert not hits, hits
+
+
+def test_no_mutable_globals_in_launchers():
+    """File-scope (or function-scope static) non-const variables would be state shared by every
+    launching thread. Allowed: constexpr / const tables, and the decode-workspace registry of the
+    bindings (a mutex-guarded per-stream cache, not a launch parameter)."""
+    decl = re.compile(r"^\s*static\s+(?!const\b|constexpr\b|inline\b|__device__|__global__|__forceinline__)"
+                      r"([\w:<>,\s\*]+?)\s+\**(\w+)\s*(=|;|\[)", re.M)
+    # mutex-guarded caches of the bindings: the decode / stream-K workspace registries and the zero page
+    allowed = {"g_ws_map", "g_ws_mu", "g_skws_map", "g_skws_mu", "mu", "map"}
+    bad = []
+    for p in NATIVE:
+        for m in decl.finditer(_code(p)):
+            name = m.group(2)
+            if "(" in m.group(0) or name in allowed:
+                continue
+            bad.append((os.path.basename(p), name))
+    assert not bad, bad
+
+
+def test_no_side_channel_setters():
+    for p in NATIVE:
+        code = _code(p)
+        for sym in ("rt_attn_decode_set_qkv_slabs", "rt_attn_decode_set_fp8kv", "rt_attn_o_set_stamps",
+                    "rt_attn_decode_set_nk", "rt_gemm_set_"):
+            assert sym not in code, (os.path.basename(p), sym)
+
+
+def test_tuning_roundtrip():
+    from rag_tl_domainllm_optimizer_amd import ops
+
+    if not ops.native_available():
+        pytest.skip("native extension not built")
+    t0 = ops.get_tuning()
+    assert t0["decode_mw"] == 1 and t0["gemm_variant"] == 0 and abs(t0["gemm_bn128_cost"] - 0.55) < 1e-6
+    with ops.tuning(decode_split=2, gemm_bn128_cost=0.7):
+        t = ops.get_tuning()
+        assert t["decode_split"] == 2 and abs(t["gemm_bn128_cost"] - 0.7) < 1e-6
+        assert {k: v for k, v in t.items() if k not in ("decode_split", "gemm_bn128_cost")} == \
+            {k: v for k, v in t0.items() if k not in ("decode_split", "gemm_bn128_cost")}
+    assert ops.get_tuning() == t0
+    with pytest.raises(KeyError):
+        ops.set_tuning(no_such_knob=1)

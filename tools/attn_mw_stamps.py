@@ -29,13 +29,11 @@ for L, cold in ((300, True), (300, False)):
     for it in range(30):
         if cold:
             junk.fill_(it)  # evict the K/V cache from the Infinity Cache (a decode step streams GBs)
-        C.attn_o_set_stamps(st)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        ops.decode_step_attention(qkv, kc, vc, slot, alen, Hq, pos, cos, sin, None, 0, workspace=ws)
+        ops.decode_step_attention(qkv, kc, vc, slot, alen, Hq, pos, cos, sin, None, 0, workspace=ws, stamps=st)
         e1.record()
         torch.cuda.synchronize()
-        C.attn_o_set_stamps(None)
         s = st.view(Hkv * 8, 8)[:, :4].double().cpu()
         t0 = s[:, 0].min()
         rows.append(((s - t0) / 100.0))  # us

@@ -105,11 +105,9 @@ def stamps():
         ops.decode_step_attention_o(qkv, kc, vc, slot, slot + 1, Hq, wo, res, slot.clone(), cos, sin,
                                     torch.zeros(1, device=dev, dtype=torch.int32), 0, workspace=ws)
     torch.cuda.synchronize()
-    C.attn_o_set_stamps(st)
     ops.decode_step_attention_o(qkv, kc, vc, slot, slot + 1, Hq, wo, res, slot.clone(), cos, sin,
-                                torch.zeros(1, device=dev, dtype=torch.int32), 0, workspace=ws)
+                                torch.zeros(1, device=dev, dtype=torch.int32), 0, workspace=ws, stamps=st)
     torch.cuda.synchronize()
-    C.attn_o_set_stamps(None)
     t = st.cpu().double()
     t0 = t[:, 0].min()
     P = Hkv * ((Smax + ws[1] - 1) // ws[1])

@@ -45,7 +45,7 @@ def main():
             for nk, ps in [(nk, ps) for nk in a.nk for ps in a.ps]:
                 if ps % (16 * nk):
                     continue
-                ops.native().attn_decode_set_nk(nk)
+                ops.native().set_tuning({"decode_nk": nk})
                 ws = ops.decode_workspace(B, Hq, Hkv, D, Smax, dev, PS=ps)
 
                 def run():
@@ -64,7 +64,7 @@ def main():
                 us = s.elapsed_time(e) / (10 * nl) * 1e3
                 gbs = B * Hkv * L * D * 2 * 2 / us / 1e3
                 res.append(f"nk{nk}/PS{ps}={us:6.1f}us({gbs:5.0f}GB/s)")
-            ops.native().attn_decode_set_nk(0)
+            ops.native().set_tuning({"decode_nk": 0})
             print(f"B={B} L={L} default_PS={default_ps}: " + " ".join(res), flush=True)
 
 

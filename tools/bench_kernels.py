@@ -56,13 +56,13 @@ def main():
             byts = 2 * (N * K + M * K + M * N)
             variants = [("auto", 0)] if M <= 64 else [("t128", 1), ("t256", 2), ("auto", 0)]
             for vname, v in variants:
-                C.gemm_set_variant(v)
+                C.set_tuning({"gemm_variant": v})
                 t_ours = timeit(lambda: ops.gemm(a, w))
                 r = dict(kind="gemm", variant=vname, name=name, M=M, N=N, K=K, us=t_ours, lib_us=t_lib,
                          tflops=flops / t_ours / 1e6, lib_tflops=flops / t_lib / 1e6, gbs=byts / t_ours / 1e3)
                 res.append(r)
                 print(json.dumps(r), flush=True)
-            C.gemm_set_variant(0)
+            C.set_tuning({"gemm_variant": 0})
     # skinny GEMMs with the weights streamed from HBM (rotating copies > the 256 MB Infinity
     # Cache), which is what a decode step sees
     for M in ((1, 8, 32, 64) if want("cold") else ()):
@@ -185,12 +185,12 @@ def main():
             for sp in (0, 1, 2, 4, 8, 16):
                 if (K // 64) // max(sp, 1) < 2:
                     continue
-                C.gemm_set_m64_split(sp)
+                C.set_tuning({"m64_split": sp})
                 t = timeit(run_m64, iters=ncopy * 2)
                 r = dict(kind="m64_split", name=name, M=M, split=sp, us=t, gbs=2 * N * K / t / 1e3)
                 res.append(r)
                 print(json.dumps(r), flush=True)
-            C.gemm_set_m64_split(0)
+            C.set_tuning({"m64_split": 0})
             del ws_
         torch.cuda.empty_cache()
     # LoRA-fused vs separate

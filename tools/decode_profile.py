@@ -39,7 +39,7 @@ def main():
     from rag_tl_domainllm_optimizer_amd import ops
 
     for it, depth in enumerate([int(d) for d in a.depths.split(",") for _ in range(3)]):
-        ops.native().gemm_set_decode_depth(depth)
+        ops.native().set_tuning({"decode_depth": depth})
         if it % 3 == 0:
             gen.runner.reset()  # the launch choice is baked into the captured decode graph
         torch.cuda.synchronize()

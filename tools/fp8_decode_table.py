@@ -80,10 +80,10 @@ def main():
                 if M > 16 and args.splits:
                     sw = {}
                     for sp in [int(v) for v in args.splits.split(",")]:
-                        C.gemm_set_wide_split(sp)
+                        C.set_tuning({"wide_split": sp})
                         with torch.no_grad():
                             sw[sp] = round(timeit(fp8, ncopy * 4), 2)
-                    C.gemm_set_wide_split(0)
+                    C.set_tuning({"wide_split": 0})
                     r["fp8_split_us"] = sw
                 rows.append(r)
                 print(json.dumps(r), flush=True)

@@ -27,6 +27,13 @@ def timeit(fn, iters=10):
     return s.elapsed_time(e) / iters * 1e3
 
 
+def tuned(fn, **kw):
+    def run():
+        with ops.tuning(**kw):
+            return fn()
+    return run
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, nargs="+", default=[9632])
@@ -72,9 +79,15 @@ def main():
                 "nn": lambda: ops.gemm_big(dy, w, 0, 1),
                 "nn_lora": lambda: ops.gemm_big(dy, w, 0, 1, du, ap_),
                 "lib_nn": lambda: torch.matmul(dy, w),
+                # stream-K tail off (the wave planner alone) / forced
+                "nt_nosk": tuned(lambda: ops.gemm_big(x, w, 0, 0), gemm_streamk=0),
+                "nn_nosk": tuned(lambda: ops.gemm_big(dy, w, 0, 1), gemm_streamk=0),
+                "nt_sk": tuned(lambda: ops.gemm_big(x, w, 0, 0), gemm_streamk=2),
+                "nn_sk": tuned(lambda: ops.gemm_big(dy, w, 0, 1), gemm_streamk=2),
             }
             if name == "gate_up":
                 cases["nt_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5)
+                cases["nt_swiglu_nosk"] = tuned(lambda: ops.gemm_big(x, w, 0, 0, act=5), gemm_streamk=0)
             if name == "gate_up":
                 cases["nt128_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5, bn=128)
                 cases["w4_192_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5, bn=3)

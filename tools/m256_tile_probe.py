@@ -21,8 +21,8 @@ for name, N, K in (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 40
     variants = {
         "big128": lambda w: ops.gemm_big(xs, w, ROW, ROW, bn=128),
         "big_auto": lambda w: ops.gemm(xs, w),
-        "tile128": lambda w: (C.gemm_set_variant(1), C.gemm(xs, w, None, None, None, 0, False, None))[1],
-        "k256": lambda w: (C.gemm_set_variant(2), C.gemm(xs, w, None, None, None, 0, False, None))[1],
+        "tile128": lambda w: (C.set_tuning({"gemm_variant": 1}), C.gemm(xs, w, None, None, None, 0, False, None))[1],
+        "k256": lambda w: (C.set_tuning({"gemm_variant": 2}), C.gemm(xs, w, None, None, None, 0, False, None))[1],
     }
     ref = None
     for vname, fn in variants.items():
@@ -38,7 +38,7 @@ for name, N, K in (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 40
             fn(ws[i % len(ws)])
         e1.record()
         torch.cuda.synchronize()
-        C.gemm_set_variant(0)
+        C.set_tuning({"gemm_variant": 0})
         res[vname] = (e0.elapsed_time(e1) / 40 * 1e3, err)
     print(f"M=256 {name:8s} N={N:6d} K={K:6d}: " + "  ".join(f"{k}={v[0]:7.1f}us(err {v[1]:.2g})" for k, v in res.items()), flush=True)
     del ws

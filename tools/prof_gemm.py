@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
     C = ops.native()
-    C.gemm_set_variant(a.variant)
+    C.set_tuning({"gemm_variant": a.variant})
     x = torch.randn(a.M, a.K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(a.N, a.K, device="cuda", dtype=torch.bfloat16) / 64
     u = torch.randn(a.M, a.rp, device="cuda", dtype=torch.bfloat16) if a.rp else None

@@ -62,8 +62,8 @@ def main():
             outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(reps)]
             byts = N * K * 2
             for sp, dp in [(int(v), int(d)) for v in args.splits.split(",") for d in args.depths.split(",")]:
-                (C.gemm_set_m64_split if M > 16 else C.gemm_set_decode_split)(sp)
-                C.gemm_set_decode_depth(dp)
+                C.set_tuning({"m64_split" if M > 16 else "decode_split": sp})
+                C.set_tuning({"decode_depth": dp})
 
                 def run():
                     for w, o in zip(ws, outs):
@@ -72,9 +72,9 @@ def main():
                 r = dict(kind="decode_gemm", name=name, M=M, N=N, K=K, split=sp, depth=dp, us=round(t, 2),
                          tbs=round(byts / t / 1e6, 2))
                 print(json.dumps(r), flush=True)
-            C.gemm_set_decode_split(0)
-            C.gemm_set_decode_depth(0)
-            C.gemm_set_m64_split(0)
+            C.set_tuning({"decode_split": 0})
+            C.set_tuning({"decode_depth": 0})
+            C.set_tuning({"m64_split": 0})
             # tile-ordered weight image (shuffle_decode_weight): same kernel, contiguous 1-KiB loads
             ref = C.gemm(x, ws[0])
             ws = [C.shuffle_decode_weight(w) for w in ws]
@@ -83,12 +83,12 @@ def main():
                 for w, o in zip(ws, outs):
                     C.gemm(x, w, out=o, w_shuffled=True)
             for sp in [int(v) for v in args.shuf_splits.split(",")]:
-                C.gemm_set_decode_split(sp)
+                C.set_tuning({"decode_split": sp})
                 t = graph_time(run_shuf) / reps
                 err = float((ref.float() - outs[0].float()).abs().max() / ref.float().abs().max())
                 print(json.dumps(dict(kind="decode_gemm", name=name, M=M, N=N, K=K, split=f"shuf{sp}",
                                       us=round(t, 2), tbs=round(byts / t / 1e6, 2), rel_err=err)), flush=True)
-            C.gemm_set_decode_split(0)
+            C.set_tuning({"decode_split": 0})
             del ws, outs
             torch.cuda.empty_cache()
 

@@ -49,18 +49,18 @@ def main():
             dy = torch.rand(M, N, device=dev, dtype=torch.bfloat16) * 2 - 1
             wt = w.t().contiguous()  # [K, N]
             cases = {
-                "fwd_lora_t128": lambda: (C.gemm_set_variant(1), C.gemm(x, w, u, ub, None, 0, False, None)),
-                "fwd_lora_t256": lambda: (C.gemm_set_variant(2), C.gemm(x, w, u, ub, None, 0, False, None)),
+                "fwd_lora_t128": lambda: (C.set_tuning({"gemm_variant": 1}), C.gemm(x, w, u, ub, None, 0, False, None)),
+                "fwd_lora_t256": lambda: (C.set_tuning({"gemm_variant": 2}), C.gemm(x, w, u, ub, None, 0, False, None)),
                 "fwd_lib_plain": lambda: torch.matmul(x, w.t()),
                 "dx_lib_nn": lambda: torch.matmul(dy, w),
-                "dx_ours_t256_wT": lambda: (C.gemm_set_variant(2), C.gemm(dy, wt, None, None, None, 0, False, None)),
+                "dx_ours_t256_wT": lambda: (C.set_tuning({"gemm_variant": 2}), C.gemm(dy, wt, None, None, None, 0, False, None)),
                 "dx_lib_nt_wT": lambda: torch.matmul(dy, wt.t()),
             }
             res = {k: [] for k in cases}
             for _ in range(a.rounds):
                 for k, fn in cases.items():
                     res[k].append(timeit(fn))
-            C.gemm_set_variant(0)
+            C.set_tuning({"gemm_variant": 0})
             fl = 2 * M * N * K
             line = " ".join(f"{k}={statistics.median(v):7.1f}us({fl / statistics.median(v) / 1e6:5.0f}TF)"
                             for k, v in res.items())
