@@ -35,8 +35,12 @@ struct Tuning {
   int gemm_tr_builtin = 0;    // NN / TN transposed reads through the compiler builtin
   int gemm_b_nt = 0;          // non-temporal weight stream when one row tile covers M
   float gemm_bn128_cost = 0.55f;  // planner: time of a 256x128 tile / a 256x256 tile
-  int gemm_streamk = 1;       // stream-K tail for the partial last wave of 256x256 tiles:
-                              // 0 off, 1 when the planner's cost model prefers it, 2 always (tests)
+  // stream-K tail for the partial last wave of 256x256 tiles: 0 off, 1 when the planner's cost
+  // model prefers it, 2 always (tests). Off by default: measured SLOWER than the wave planner at the
+  // update / reference shapes (M = 9632 qkv 422 vs 387 us, o 277 vs 260 us; the chip-wide burst of
+  // partial-tile hand-offs at the end of the launch costs more than the tail it removes;
+  // profiles/r4/gemm_streamk_vs_planner.log)
+  int gemm_streamk = 0;
 };
 
 }  // namespace rt

@@ -522,8 +522,9 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       const bool last = *flag != 0;
       __syncthreads();
       if (!last) continue;  // another unit finishes this tile
+      // sum every unit's partial in unit order (its own re-read from the slot it just stored), so
+      // the result does not depend on which unit arrives last: bitwise reproducible
       for (int u = u_first; u <= u_last; ++u) {
-        if (u == sk_unit) continue;
         // the tile is the first segment of unit u unless u started inside an earlier tile
         const int sg = (int)(((long)u * S / U) / nk) == tl ? 0 : 1;
         const auto rs = slot_rsrc(u, sg);
@@ -541,7 +542,9 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
 #pragma unroll
           for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-            for (int j = 0; j < 2 * NB; ++j) acc[i + ii][j] += __builtin_bit_cast(f32x4, v[ii][j]);
+            for (int j = 0; j < 2 * NB; ++j)
+              acc[i + ii][j] = u == u_first ? __builtin_bit_cast(f32x4, v[ii][j])
+                                            : acc[i + ii][j] + __builtin_bit_cast(f32x4, v[ii][j]);
           __builtin_amdgcn_sched_barrier(0);
         }
       }

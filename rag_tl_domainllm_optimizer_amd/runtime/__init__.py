@@ -38,15 +38,24 @@ class PhaseTimer:
     boundaries, so phases overlap freely; ``as_dict`` resolves the pending events (host wall clock
     on CPU-only runs). ``sync=True`` restores the old behaviour (device sync around each phase)."""
 
-    def __init__(self, sync: bool = False, device=None):
+    def __init__(self, sync: bool = False, device=None, range_sync: bool = None):
+        import os
+
         self.cuda = torch.cuda.is_available() and (device is None or torch.device(device).type == "cuda")
         self.sync = sync and self.cuda
+        # profiling mode (RAGTL_PHASE_SYNC=1): each phase's roctx range closes only after the device
+        # has finished the phase's kernels, and the next opens on an idle device, so a trace
+        # attributes every kernel to the phase that enqueued it (without it the host runs ahead and
+        # e.g. the reference forward's GEMMs execute after its range has closed)
+        if range_sync is None:
+            range_sync = os.environ.get("RAGTL_PHASE_SYNC", "0") == "1"
+        self.range_sync = bool(range_sync) and self.cuda
         self.totals = defaultdict(float)
         self._pending = []
 
     @contextlib.contextmanager
     def phase(self, name: str):
-        if self.sync:
+        if self.sync or self.range_sync:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         ev0 = None
@@ -55,9 +64,12 @@ class PhaseTimer:
             ev0.record()
         with range_(name):
             yield
+            if self.cuda:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record()
+                if self.range_sync:
+                    ev1.synchronize()  # inside the range: its kernels are all within it
         if self.cuda:
-            ev1 = torch.cuda.Event(enable_timing=True)
-            ev1.record()
             if self.sync:
                 torch.cuda.synchronize()
             self._pending.append((name, ev0, ev1))

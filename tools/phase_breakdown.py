@@ -49,14 +49,19 @@ def main():
                 g = grids[(ph, w, r.get("Grid_Size_X", r.get("Grid_Size", "?")), r.get("Workgroup_Size_X", "?"))]
                 g[0] += 1
                 g[1] += (e - s) / 1e6
+    count = collections.Counter()
     for (rs, re_, n) in ranges:
         span[n] += (re_ - rs) / 1e6
+        count[n] += 1
     out = {}
     for ph, ks in res.items():
         tot = sum(ks.values())
         top = sorted(ks.items(), key=lambda x: -x[1])[: a.top]
         out[ph] = {"kernel_ms": tot, "wall_ms": span.get(ph, 0.0), "top": [[k, round(v, 3)] for k, v in top]}
-        print(f"== {ph}: kernels {tot:.1f} ms / range {span.get(ph, 0.0):.1f} ms")
+        nr = max(count.get(ph, 1), 1)
+        out[ph]["ranges"] = count.get(ph, 0)
+        print(f"== {ph}: kernels {tot:.1f} ms / range {span.get(ph, 0.0):.1f} ms over {count.get(ph, 0)} range(s) "
+              f"= {tot / nr:.1f} ms kernels per range")
         for k, v in top:
             print(f"   {v:8.2f} ms  {k}")
     for (ph, w, gx, wx), (n, ms) in sorted(grids.items(), key=lambda x: -x[1][1]):

@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 4, GPU call B: full GPU test tier (tuning / side-channel refactor), then a phase-synced PPO profile
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out/r4
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread \
+  > gpurun_out/r4/b_gpu_tests.log 2>&1 || { echo "GPU tests failed"; tail -40 gpurun_out/r4/b_gpu_tests.log; exit 1; }
+tail -3 gpurun_out/r4/b_gpu_tests.log
+PROF_TAG=b_prof_ppo bash tools/r4/prof_ppo.sh
