@@ -119,6 +119,7 @@ static const TuningField kTuningFields[] = {
     {"gemm_tr_builtin", &rt::Tuning::gemm_tr_builtin, nullptr},
     {"gemm_b_nt", &rt::Tuning::gemm_b_nt, nullptr},
     {"gemm_bn128_cost", nullptr, &rt::Tuning::gemm_bn128_cost},
+    {"gemm_group_m", &rt::Tuning::gemm_group_m, nullptr},
     {"gemm_streamk", &rt::Tuning::gemm_streamk, nullptr},
 };
 

@@ -35,6 +35,7 @@ struct Tuning {
   int gemm_tr_builtin = 0;    // NN / TN transposed reads through the compiler builtin
   int gemm_b_nt = 0;          // non-temporal weight stream when one row tile covers M
   float gemm_bn128_cost = 0.55f;  // planner: time of a 256x128 tile / a 256x256 tile
+  int gemm_group_m = 4;       // rows of 256x256 tiles per L2-reuse group in the tile order
   // stream-K tail for the partial last wave of 256x256 tiles: 0 off, 1 when the planner's cost
   // model prefers it, 2 always (tests). Off by default: measured SLOWER than the wave planner at the
   // update / reference shapes (M = 9632 qkv 422 vs 387 us, o 277 vs 260 us; the chip-wide burst of

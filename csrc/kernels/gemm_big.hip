@@ -83,6 +83,7 @@ struct Args {
   float* sk_part;
   unsigned* sk_tickets;
   int b_layout_kmaj;  // host: NN form of the stream-K launch
+  int group_m;        // rows of tiles per L2 group (0 = GROUP_M); tuning gemm_group_m
 };
 
 __device__ __forceinline__ int row_swz(int row) { return (row >> 1) & 7; }
@@ -187,13 +188,14 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   const int seg_tile = seg == 0 ? seg_tile0 : seg_tile1;
   const int t_begin = seg == 0 ? seg_b0 : seg_b1;
   const int t_end = seg == 0 ? seg_e0 : seg_e1;
-  // ---- tile assignment: GROUP_M-row groups (L2 reuse of B panels) over the remapped id ----
+  // ---- tile assignment: group_m-row groups (L2 reuse of B panels) over the remapped id ----
   const int bid = seg_tile;
-  const int group = bid / (GROUP_M * tiles_n);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int GM = p.group_m > 0 ? p.group_m : GROUP_M;
+  const int group = bid / (GM * tiles_n);
+  const int first_m = group * GM;
+  const int gsz = min(tiles_m - first_m, GM);
   const int tm = first_m + (bid % gsz);
-  const int tn = (bid % (GROUP_M * tiles_n)) / gsz;
+  const int tn = (bid % (GM * tiles_n)) / gsz;
   const int m0 = tm * 256, n0 = tn * BN;
   const int Fh = p.N / 2;  // E_SWIGLU: gate rows [0, F), up rows [F, 2F)
   constexpr int HALF = BN / 2;  // E_SWIGLU: tile columns [0, HALF) gate, [HALF, BN) up
@@ -1427,6 +1429,7 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = (bf16_t*)C2; p.ldc2 = ldc2;
   p.R = (const bf16_t*)R; p.ldr = ldr;
   p.M = M; p.N = N; p.K = K; p.act = act; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
+  p.group_m = tuning().gemm_group_m;
   // tuning gemm_b_nt = 1: non-temporal weight stream when one row tile covers M (each B byte read
   // once per launch). Measured neutral on the batch-256 decode GEMMs (profiles/decode_nt_ab.log): off
   p.b_nt = layout_b == ROW && M <= 256 && tuning().gemm_b_nt > 0;

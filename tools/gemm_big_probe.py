@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--shapes", default="qkv,o,gate_up,down")
     ap.add_argument("--cases", default="", help="comma-separated subset of the case names")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--sweep", default="", help="tuning knob sweep, e.g. gemm_group_m=2,8,16: adds nt/nn cases "
+                    "per value (nt@gemm_group_m=8, ...)")
     a = ap.parse_args()
     dev = "cuda"
     C = ops.native()
@@ -99,6 +101,14 @@ def main():
             cases["auto"] = lambda: ops.gemm(x, w, act=5 if name == "gate_up" else 0)
             if a.cases:
                 cases = {k: v for k, v in cases.items() if k in a.cases.split(",")}
+            if a.sweep:
+                knob, vals = a.sweep.split("=")
+                for v in vals.split(","):
+                    kw = {knob: float(v) if "." in v else int(v)}
+                    cases[f"nt@{v}"] = tuned(lambda: ops.gemm_big(x, w, 0, 0), **kw)
+                    cases[f"nn@{v}"] = tuned(lambda: ops.gemm_big(dy, w, 0, 1), **kw)
+                    if name == "gate_up":
+                        cases[f"sw@{v}"] = tuned(lambda: ops.gemm_big(x, w, 0, 0, act=5), **kw)
             res = {k: [] for k in cases}
             for _ in range(a.rounds):
                 for k, fn in cases.items():
