@@ -15,7 +15,7 @@ namespace rt {
 constexpr int NORM_MAXV = 8;  // max 16-B vectors per thread -> H <= 256*8*8 = 16384
 
 template <bool LAYERNORM, int NV>
-__global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+__global__ __launch_bounds__(512) void norm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                        const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
                                                        bf16_t* __restrict__ y, bf16_t* __restrict__ h_out,
                                                        float* __restrict__ rstd_out, float* __restrict__ mean_out,
@@ -205,6 +205,13 @@ extern "C" int rt_norm_fwd(int layernorm, const void* x, const void* res, const 
   if (T == 0) return 0;
   int threads, nvpt;
   norm_geom(H, threads, nvpt);
+  // split-K slab reduce (decode at batch 65..512: one row per block, rows <= CUs): twice the waves
+  // per row (one 8-element chunk per thread) keep twice the slab loads in flight per CU
+  const int sl = tuning().norm_slab_threads;
+  if (xs && sl >= 512 && H / 8 >= 512 && H / 8 <= 512) {
+    threads = 512;
+    nvpt = 1;
+  }
   if (layernorm) {
     NORM_DISPATCH(true, norm_fwd_kernel, dim3(T), dim3(threads), 0, stream, (const bf16_t*)x, (const bf16_t*)res,
                   (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (bf16_t*)h_out, rstd, mean, H, eps, xs, nsplit,

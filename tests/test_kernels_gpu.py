@@ -227,6 +227,23 @@ def test_linear_lora_dropout():
     _close(b.grad, br.grad, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("threads", [256, 512])
+@pytest.mark.parametrize("H,ns", [(4096, 8), (4096, 5), (5120, 8)])
+def test_norm_split_k_slabs(H, ns, threads):
+    """Decode-batch RMSNorm that also reduces the producing GEMM's split-K slabs (256 or 512 threads
+    per row) against the fp32 reference: h = bf16(bf16(sum slabs) + residual), y = RMSNorm(h) w."""
+    B = 256
+    slabs = torch.randn(ns, B, H, device=DEV) * 0.2
+    r = torch.randn(B, H, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    with ops.tuning(norm_slab_threads=threads):
+        y, h = ops.rms_norm(ops.SplitK(slabs, ns, B, H, torch.bfloat16), w, 1e-5, r)
+    hr = (slabs.sum(0).to(torch.bfloat16).float() + r.float()).to(torch.bfloat16).float()
+    yr = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    _close(h, hr)
+    _close(y, yr)
+
+
 @pytest.mark.parametrize("H", [384, 768, 4096, 5120])
 @pytest.mark.parametrize("layernorm", [False, True])
 def test_norm(H, layernorm):

@@ -4,6 +4,10 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r4
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "norm" -x -q --timeout 120 --timeout-method thread \
+  > gpurun_out/r4/d_norm_tests.log 2>&1 || { echo "norm tests failed"; tail -30 gpurun_out/r4/d_norm_tests.log; exit 1; }
+tail -1 gpurun_out/r4/d_norm_tests.log
+timeout -k 10 120 python -u tools/r4/norm_slab_probe.py > gpurun_out/r4/d_norm_probe.log 2>&1 && grep -v amdgpu.ids gpurun_out/r4/d_norm_probe.log
 RAGTL_DIST_BACKEND=gloo timeout -k 10 500 python -u bench.py --gpus 2 --steps 1 --warmup 1 --skip-latency \
   > gpurun_out/r4/d_bench_gpus2_gloo.log 2>&1 || { echo "gloo 2-rank bench failed"; tail -30 gpurun_out/r4/d_bench_gpus2_gloo.log; exit 1; }
 grep '^{' gpurun_out/r4/d_bench_gpus2_gloo.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); print('gloo2', r['n_gpus'], r['world'], r['value'], r['allreduce_probe'])"
