@@ -52,11 +52,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--encoder", default="minilm-l6")
-    ap.add_argument("--rollout-batch", type=int, default=None,
-                    help="sequences per GPU per PPO step (default 256; 64 for --mode pipeline)")
+    ap.add_argument("--rollout-batch", type=int, default=256,
+                    help="sequences per GPU per PPO step (default 256, also for --mode pipeline: "
+                         "profiles/r4/pipeline13b_rollout_batch.log)")
     ap.add_argument("--new-tokens", type=int, default=128)
     ap.add_argument("--max-prompt", type=int, default=320)
-    ap.add_argument("--minibatch", type=int, default=None, help="PPO minibatch (default 32; 16 for pipeline)")
+    ap.add_argument("--minibatch", type=int, default=32, help="PPO minibatch (sequences per optimizer step)")
     ap.add_argument("--ref-minibatch", type=int, default=None,
                     help="sequences per reference-scoring forward (default: PPOConfig.ref_minibatch_size)")
     ap.add_argument("--top-k-docs", type=int, default=3)
@@ -93,13 +94,10 @@ def main():
     args = ap.parse_args()
     if args.mode == "pipeline" and args.model == "mistral-7b" and "--model" not in sys.argv:
         args.model = "llama2-13b"
-    # 256 rollouts per GPU: a decode step streams the 14.5 GB of weights once whatever the batch, so
-    # a larger rollout batch amortises it (64 -> 128 -> 256: 4660 -> 5108 -> 6101 tokens/s on one
-    # MI355X, profiles/bench_r1_rollout*.log); 288 GB of HBM hold its 15 GB KV cache
-    if args.rollout_batch is None:
-        args.rollout_batch = 64 if args.mode == "pipeline" else 256
-    if args.minibatch is None:
-        args.minibatch = 16 if args.mode == "pipeline" else 32
+    # 256 rollouts per GPU: a decode step streams the weights once whatever the batch, so a larger
+    # rollout batch amortises it (Mistral-7B 64 -> 128 -> 256: 4660 -> 5108 -> 6101 tokens/s,
+    # profiles/bench_r1_rollout*.log; Llama-2-13B config 5: 3343 -> 3614 -> 4444 tokens/s,
+    # profiles/r4/pipeline13b_rollout_batch.log); 288 GB of HBM hold the KV cache
     if args.fp8 is None:
         args.fp8 = args.mode == "pipeline"
     if args.fp8_kv is None:

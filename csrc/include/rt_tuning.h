@@ -22,7 +22,9 @@ struct Tuning {
   int decode_nk = 4;          // VALU split kernel: keys per lane per chunk (2, 4, 8)
   int attn_bwd_atomic_dq = 0; // attention backward: fp32-atomic dQ (round-1 form)
   // ---- norms (norm.hip) ----
-  int norm_slab_threads = 256;  // threads per row of the split-K-slab norm (256, or 512 at H = 4096)
+  // threads per row of the split-K-slab norm (256, or 512 at H = 4096: 6.76 -> 6.56 us at batch 256,
+  // profiles/r4/norm_slab_threads.log)
+  int norm_slab_threads = 512;
   // ---- decode / skinny GEMMs (gemm_bf16.hip) ----
   int gemm_variant = 0;       // M > 64 library-shaped kernel: 0 auto, 1 128x128, 2 256x256, 4/5 fp8 forms
   int gemv16 = 2;             // 16-row no-split GEMV at M <= 16: 0 off, 1 narrow outputs, 2 all

@@ -204,7 +204,8 @@ def test_cli_pipeline_config5_fp8_gpu(tmp_path):
                    "--data.synthetic_docs=64", "--data.doc_words=16", "--retrieval.index=flat",
                    f"--out_dir={tmp_path}", "--data.n_queries=8", "--data.batch_size=8", "--ppo.max_new_tokens=8",
                    "--ppo.max_prompt_tokens=96", "--ppo.minibatch_size=8", "--sft.batch_size=8",
-                   "--sft.save_full_policy=False", "--ppo.save_full_policy=False"])
+                   "--sft.save_full_policy=False", "--ppo.save_full_policy=False", "--eval.compare_items=8",
+                   "--eval.max_new_tokens=16"])
     pol = tr.policy
     assert pol.cfg.hidden_size == 5120 and pol.cfg.num_layers == 40
     assert all(layer.fp8_enabled for layer in pol.layers)
@@ -214,6 +215,12 @@ def test_cli_pipeline_config5_fp8_gpu(tmp_path):
     run = tmp_path / "run"
     lines = [json.loads(x) for x in open(run / "metrics.jsonl")]
     assert any("reward_mean" in x and math.isfinite(x["total_loss"]) for x in lines)
+    # the reference's model comparison closes the pipeline (rl.py:444-463, 521-525)
+    import pandas as pd
+
+    rep = pd.read_csv(run / "model_comparison_results.csv", index_col=0)
+    assert list(rep.columns) == ["Base Model", "RAG Model", "RL-finetuned Model", "Transfer-learned Model"]
+    assert "overall_score" in rep.index and rep.loc["overall_score"].notna().all()
     del tr, pol
     torch.cuda.empty_cache()
 
