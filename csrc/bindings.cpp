@@ -376,6 +376,29 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
     TORCH_CHECK((layout_a && layout_b) || K2 % 8 == 0, "gemm_big: K2 must be a multiple of 8");
   }
   const bool swiglu = act == 5;
+  // act 6: SwiGLU backward in the epilogue of the down projection's dX (NN): out = d[gate | up]
+  // [M, 2N] from residual = the forward's [gate | up] pre-activation [M, 2N]
+  const bool dswiglu = act == 6;
+  if (dswiglu) {
+    TORCH_CHECK(layout_a == 0 && layout_b == 1 && out_mode == 0 && nsplit <= 1, "gemm_big: act 6 is NN, bf16, no split");
+    TORCH_CHECK(out.has_value() && out->defined() && residual.has_value() && residual->defined(),
+                "gemm_big: act 6 needs out and residual = [gate | up] pre-activation");
+    const Tensor* both[2] = {&out.value(), &residual.value()};
+    for (const Tensor* t : both) {
+      CHECK_BF16(*t); CHECK_ALIGN16(*t);
+      TORCH_CHECK(t->dim() == 2 && t->size(0) == M && t->size(1) == 2 * N && t->stride(1) == 1 && t->stride(0) % 8 == 0,
+                  "gemm_big: act 6 out / residual must be bf16 [M, 2N]");
+    }
+    TORCH_CHECK(N % 8 == 0 && !(bias.has_value() && bias->defined()), "gemm_big: act 6 needs N % 8 == 0, no bias");
+    if (M == 0 || N == 0) return *out;
+    check_rc(rt_gemm_big(0, 1, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), ext ? a2->data_ptr() : nullptr,
+                         ext ? a2->stride(0) : 0, ext ? b2->data_ptr() : nullptr, ext ? b2->stride(0) : 0, (int)K2,
+                         nullptr, out->data_ptr(), out->stride(0), nullptr, 0, residual->data_ptr(),
+                         residual->stride(0), (int)M, (int)N, (int)K, 6, 0, 1, zero_page(a).data_ptr(), (int)bn,
+                         nullptr, nullptr, cur_stream()),
+             "gemm_big(act 6)");
+    return *out;
+  }
   if (bias.has_value() && bias->defined()) {
     CHECK_BF16(*bias);
     TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && !swiglu, "gemm_big: bias");

@@ -52,7 +52,12 @@ constexpr int GROUP_M = 4;
 
 enum Layout { ROW = 0, KMAJ = 1 };
 enum Out { O_BF16 = 0, O_F32 = 1, O_F32_ATOMIC = 2, O_F32_SLAB = 3 };
-enum Epi { E_NONE = 0, E_RELU = 1, E_GELU = 2, E_GELU_TANH = 3, E_SILU = 4, E_SWIGLU = 5 };
+// E_DSWIGLU (NN, bf16 out): the SwiGLU backward in the epilogue of the down projection's dX GEMM.
+// The accumulator is dF [M, F] (F = N); R = the forward's [gate | up] pre-activation [M, 2F] and C
+// = d[gate | up] [M, 2F] (ldr = ldc = 2F rows): dF is rounded to bf16 first, then exactly the
+// arithmetic of swiglu_bwd_kernel — bitwise the unfused GEMM + SwiGLU-backward pair, without the
+// dF round trip through HBM.
+enum Epi { E_NONE = 0, E_RELU = 1, E_GELU = 2, E_GELU_TANH = 3, E_SILU = 4, E_SWIGLU = 5, E_DSWIGLU = 6 };
 
 struct Args {
   const bf16_t* A; long lda;
@@ -665,6 +670,31 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
               *(uint4*)(p.C2 + (long)grow * p.ldc2 + fcol) = g4;
               *(uint4*)(p.C2 + (long)grow * p.ldc2 + Fh + fcol) = u4;
             }
+          }
+        }
+      } else if constexpr (EPI == E_DSWIGLU) {
+        bf16_t* C = (bf16_t*)p.C;
+        const int F = p.N;
+        constexpr int CH = BN / 8;
+        const int cc = tid % CH;
+#pragma unroll
+        for (int pass = 0; pass < 128 * CH / 512; ++pass) {
+          const int row = pass * (512 / CH) + tid / CH;
+          const int grow = m0 + hh * 128 + row, gcol = n0 + cc * 8;
+          if (grow < p.M && gcol < F) {
+            float d[8], g[8], u[8], dg[8], du[8];
+            unpack8(ld16(row, cc), d);
+            unpack8(*(const uint4*)(p.R + (long)grow * p.ldr + gcol), g);
+            unpack8(*(const uint4*)(p.R + (long)grow * p.ldr + F + gcol), u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float sg = 1.f / (1.f + __expf(-g[e]));
+              const float si = g[e] * sg;
+              du[e] = d[e] * si;
+              dg[e] = d[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
+            }
+            *(uint4*)(C + (long)grow * p.ldc + gcol) = pack8(dg);
+            *(uint4*)(C + (long)grow * p.ldc + F + gcol) = pack8(du);
           }
         }
       } else {
@@ -1285,6 +1315,7 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
       case 10: GB_LAUNCH(ROW, ROW, O_F32, E_NONE, 128); break;
       case 30: GB_LAUNCH(ROW, ROW, O_F32_SLAB, E_NONE, 128); break;
       case 100: GB_LAUNCH(ROW, KMAJ, O_BF16, E_NONE, 128); break;
+      case 100 + E_DSWIGLU: GB_LAUNCH(ROW, KMAJ, O_BF16, E_DSWIGLU, 128); break;
       default: return -4;
     }
   } else if (key == 0) {  // NT, bf16 out: the activation is a template parameter (no runtime switch in the epilogue)
@@ -1297,6 +1328,8 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
       case E_SWIGLU: GB_LAUNCH(ROW, ROW, O_BF16, E_SWIGLU, 256); break;
       default: return -4;
     }
+  } else if (key == 10 && act == E_DSWIGLU) {
+    GB_LAUNCH(ROW, KMAJ, O_BF16, E_DSWIGLU, 256);
   } else {
     if (act != E_NONE) return -5;  // fp32 outputs and the NN / TN forms carry no activation
     switch (key) {
@@ -1319,7 +1352,8 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
 
 static bool bn128_supported(int layout_a, int layout_b, int act, int out) {
   const int key = layout_a * 100 + layout_b * 10 + out;
-  return (key == 0 && (act == E_NONE || act == E_SWIGLU)) || (act == E_NONE && (key == 1 || key == 3 || key == 10));
+  return (key == 0 && (act == E_NONE || act == E_SWIGLU)) || (act == E_NONE && (key == 1 || key == 3 || key == 10)) ||
+         (key == 10 && act == E_DSWIGLU);
 }
 
 static int query_num_cus() {
@@ -1415,7 +1449,14 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   if (nsplit < 1) nsplit = 1;
   if (nsplit > 1 && out != O_F32_ATOMIC && out != O_F32_SLAB) return -2;
   if (act == E_SWIGLU && (layout_a != ROW || layout_b != ROW || out != O_BF16 || N % 256)) return -3;
-  if (act != E_NONE && (layout_a != ROW || layout_b != ROW || out != O_BF16)) return -5;
+  if (act == E_DSWIGLU) {
+    // the SwiGLU backward epilogue: NN, bf16 d[gate | up] [M, 2N] from the pre-activation R [M, 2N]
+    if (layout_a != ROW || layout_b != KMAJ || out != O_BF16 || !R || N % 8 || ldc < 2L * N || ldr < 2L * N ||
+        nsplit != 1)
+      return -5;
+  } else if (act != E_NONE && (layout_a != ROW || layout_b != ROW || out != O_BF16)) {
+    return -5;
+  }
   if (bn != 0 && bn != 128 && bn != 256 && bn != 4 && bn != 3) return -8;
   const bool can128 = bn128_supported(layout_a, layout_b, act, out);
   if (bn == 128 && !can128) return -8;

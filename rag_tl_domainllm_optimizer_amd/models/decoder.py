@@ -165,9 +165,15 @@ class DecoderLayer(nn.Module):
             d = ops.linear(f, self.fc2_w, self.fc2_b, lora=self._lg("fc2"), fp8=self._f8("fc2"))
         else:
             h, residual = ops.rms_norm(a, self.ln2_w, cfg.norm_eps, residual)
-            # act="swiglu": one fused skinny GEMM in no-grad decode, GEMM + SwiGLU kernel otherwise
-            f = ops.linear(h, self.gate_up_w, act="swiglu", lora=self._lg("gate_up"), fp8=self._f8("gate_up"))
-            d = lin(f, self.down_w, lora=self._lg("down"), fp8=self._f8("down"))
+            d = None
+            if not (self.fp8_enabled and self.fp8_train):
+                # training: one autograd node whose backward runs the SwiGLU backward inside the
+                # down projection's dX GEMM (ops.swiglu_mlp; None when it does not apply)
+                d = ops.swiglu_mlp(h, self.gate_up_w, self.down_w, self._lg("gate_up"), self._lg("down"))
+            if d is None:
+                # act="swiglu": one fused skinny GEMM in no-grad decode, GEMM + SwiGLU kernel otherwise
+                f = ops.linear(h, self.gate_up_w, act="swiglu", lora=self._lg("gate_up"), fp8=self._f8("gate_up"))
+                d = lin(f, self.down_w, lora=self._lg("down"), fp8=self._f8("down"))
         return d, residual
 
 

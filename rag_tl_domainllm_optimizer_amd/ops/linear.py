@@ -29,6 +29,7 @@ from ._ext import native, on_gpu
 
 ACT_IDS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "gelu_tanh": 3, "gelu_new": 3, "silu": 4, "swiglu": 5}
 ACT_SWIGLU = 5  # w = [gate; up] (2F rows) -> silu(x gate^T) * (x up^T), [.., F]
+ACT_DSWIGLU = 6  # gemm_big NN epilogue: d[gate | up] from dF and the [gate | up] pre-activation
 
 
 def splitk_plan(M: int, N: int, K: int, act: int = 0):
@@ -105,6 +106,11 @@ def gemm_big(a, b, la: int, lb: int, a2=None, b2=None, bias=None, act: int = 0, 
     y = A @ B
     if a2 is not None:
         y = y + _op(a2, la, True).float() @ _op(b2, lb, False).float()
+    if act == ACT_DSWIGLU:  # out = d[gate | up] from dF = y (rounded like the GEMM output) and residual
+        from .misc import _swiglu_grad
+
+        out.copy_(_swiglu_grad(residual, y.to(a.dtype)))
+        return out
     if act == ACT_SWIGLU:
         F = y.shape[1] // 2
         pre = y.to(a.dtype)
@@ -393,50 +399,126 @@ class _LinearFn(torch.autograd.Function):
                 (g,) = torch.autograd.grad(yact, p, dy.float())
             dy = g.to(dy.dtype)
         needs = ctx.needs_input_grad
-        dx = dw = db = None
-        gpu = on_gpu(dy)
-        ws = None
-        if lora is not None and gpu:
-            # one zero fill for the three fp32 accumulators of the adapter products: dU [M, Rp]
-            # (split-K over N), dA_all [Rp, K], dB_all [N, Rp]
-            Mr, Kr, Nr, Rp = dy.shape[0], x2.shape[1], dy.shape[1], lora.ub.shape[1]
-            ws = torch.zeros(Mr * Rp + Rp * Kr + Nr * Rp, dtype=torch.float32, device=dy.device)
-            du32 = ws[:Mr * Rp].view(Mr, Rp)
-            ga_out = ws[Mr * Rp:Mr * Rp + Rp * Kr].view(Rp, Kr)
-            gb_out = ws[Mr * Rp + Rp * Kr:].view(Nr, Rp)
-        du = _narrow(dy, lora.ub, KMAJ, zero32=du32 if ws is not None else None) if lora is not None else None
-        if needs[0]:
-            if lora is not None and mask is None:
-                # dX = dY W + dU A_pad in ONE NN GEMM (the adapter term as K-extension steps)
-                dx = gemm_big(dy, w, ROW, KMAJ, du, lora.a_pad)
-            else:
-                dx = gemm_big(dy, w, ROW, KMAJ)
-                if lora is not None:  # dropout: the adapter gradient flows through the mask
-                    dx = dx + gemm_big(du, lora.a_pad, ROW, KMAJ) * mask
-        if needs[1]:
-            # full fine-tuning: dW = dY^T X [N, K] (TN; bf16 compute-copy gradient)
-            dw = gemm_big(dy, x2, KMAJ, KMAJ) if (gpu and w.dtype == torch.bfloat16) else \
-                (dy.float().t() @ x2.float()).to(w.dtype)
+        db = None
         if ctx.has_bias and needs[2]:
             db = dy.float().sum(0).to(bias.dtype)
-        lora_grads = []
-        if lora is not None:
-            # all adapters of the projection in two TN GEMMs with fp32 output (bf16 in, fp32
-            # accumulate): dA_all = dU^T drop(X) [Rp, K]; dB_all = dY^T U [N, Rp] (adapter i uses
-            # its diagonal block)
-            xd = x2 * mask if mask is not None else x2
-            ga_all = gemm_tn(du, xd, out=ga_out, zeroed=True) if ws is not None else gemm_tn(du, xd)
-            gb_all = gemm_tn(dy, u, out=gb_out, zeroed=True) if ws is not None else gemm_tn(dy, u)
-            one_scale = len(set(lora.scale)) == 1
-            if one_scale:
-                ga_all.mul_(lora.scale[0])  # one launch for every adapter of the projection
-            for a, b, r0, c0, s in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
-                ri, ni = a.shape[0], b.shape[0]
-                ga = ga_all[r0:r0 + ri]
-                lora_grads.append((ga if one_scale else ga * s).to(a.dtype))
-                lora_grads.append(gb_all[c0:c0 + ni, r0:r0 + ri].to(b.dtype))
-            # parameter order in forward(*lora_params) is a0, b0, a1, b1, ...
+        dx, dw, lora_grads = _linear_bwd(dy, x2, w, u, lora, mask, needs[0], needs[1])
         return (dx, dw, db, None, None, None, *lora_grads)
+
+
+def _linear_bwd(dy, x2, w, u, lora, mask, need_x: bool, need_w: bool, dx_act: int = 0, dx_aux=None, dx_out=None):
+    """Gradients of y = x W^T (+ s (drop(x) A^T) B^T) given dL/dy: (dX, dW, [dA_i, dB_i, ...]).
+    ``dx_act`` = ACT_DSWIGLU: dX is the down projection's input gradient dF and goes through the
+    SwiGLU backward in the dX GEMM's epilogue (``dx_aux`` = the [gate | up] pre-activation,
+    ``dx_out`` = the d[gate | up] buffer it writes)."""
+    dx = dw = None
+    gpu = on_gpu(dy)
+    ws = None
+    if lora is not None and gpu:
+        # one zero fill for the three fp32 accumulators of the adapter products: dU [M, Rp]
+        # (split-K over N), dA_all [Rp, K], dB_all [N, Rp]
+        Mr, Kr, Nr, Rp = dy.shape[0], x2.shape[1], dy.shape[1], lora.ub.shape[1]
+        ws = torch.zeros(Mr * Rp + Rp * Kr + Nr * Rp, dtype=torch.float32, device=dy.device)
+        du32 = ws[:Mr * Rp].view(Mr, Rp)
+        ga_out = ws[Mr * Rp:Mr * Rp + Rp * Kr].view(Rp, Kr)
+        gb_out = ws[Mr * Rp + Rp * Kr:].view(Nr, Rp)
+    du = _narrow(dy, lora.ub, KMAJ, zero32=du32 if ws is not None else None) if lora is not None else None
+    if need_x:
+        if dx_act == ACT_DSWIGLU:
+            assert mask is None
+            dx = gemm_big(dy, w, ROW, KMAJ, du, lora.a_pad if lora is not None else None, act=ACT_DSWIGLU,
+                          out=dx_out, residual=dx_aux)
+        elif lora is not None and mask is None:
+            # dX = dY W + dU A_pad in ONE NN GEMM (the adapter term as K-extension steps)
+            dx = gemm_big(dy, w, ROW, KMAJ, du, lora.a_pad)
+        else:
+            dx = gemm_big(dy, w, ROW, KMAJ)
+            if lora is not None:  # dropout: the adapter gradient flows through the mask
+                dx = dx + gemm_big(du, lora.a_pad, ROW, KMAJ) * mask
+    if need_w:
+        # full fine-tuning: dW = dY^T X [N, K] (TN; bf16 compute-copy gradient)
+        dw = gemm_big(dy, x2, KMAJ, KMAJ) if (gpu and w.dtype == torch.bfloat16) else \
+            (dy.float().t() @ x2.float()).to(w.dtype)
+    lora_grads = []
+    if lora is not None:
+        # all adapters of the projection in two TN GEMMs with fp32 output (bf16 in, fp32
+        # accumulate): dA_all = dU^T drop(X) [Rp, K]; dB_all = dY^T U [N, Rp] (adapter i uses
+        # its diagonal block)
+        xd = x2 * mask if mask is not None else x2
+        ga_all = gemm_tn(du, xd, out=ga_out, zeroed=True) if ws is not None else gemm_tn(du, xd)
+        gb_all = gemm_tn(dy, u, out=gb_out, zeroed=True) if ws is not None else gemm_tn(dy, u)
+        one_scale = len(set(lora.scale)) == 1
+        if one_scale:
+            ga_all.mul_(lora.scale[0])  # one launch for every adapter of the projection
+        for a, b, r0, c0, s in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
+            ri, ni = a.shape[0], b.shape[0]
+            ga = ga_all[r0:r0 + ri]
+            lora_grads.append((ga if one_scale else ga * s).to(a.dtype))
+            lora_grads.append(gb_all[c0:c0 + ni, r0:r0 + ri].to(b.dtype))
+        # parameter order in forward(*lora_params) is a0, b0, a1, b1, ...
+    return dx, dw, lora_grads
+
+
+class _SwiGLUMLPFn(torch.autograd.Function):
+    """The Llama / Mistral MLP as one autograd node: f = silu(x Wg^T) * (x Wu^T) (gate / up in one
+    GEMM with the SwiGLU epilogue, LoRA as K-extension), d = f Wd^T (+ LoRA). Backward runs the down
+    projection's dX GEMM with the SwiGLU backward in its epilogue (ACT_DSWIGLU): d[gate | up] comes
+    straight out of that GEMM, so dF never goes to memory and there is no separate SwiGLU-backward
+    pass (two [M, F] bf16 streams per layer and minibatch; the [gate | up] streams are read / written
+    once either way). Numerics are bitwise those of the two-node form (dF is rounded to bf16 before
+    the epilogue's arithmetic, which is swiglu_bwd_kernel's). LoRA without dropout, bf16 weights."""
+
+    @staticmethod
+    def forward(ctx, x2, w_gu, w_d, lora_gu, lora_d, n_gu: int, *lora_params):
+        u_gu = _narrow(x2, lora_gu.a_pad, ROW) if lora_gu is not None else None
+        pre = torch.empty(x2.shape[0], w_gu.shape[0], dtype=x2.dtype, device=x2.device)
+        f = gemm_big(x2, w_gu, ROW, ROW, u_gu, lora_gu.ub if lora_gu is not None else None, None, ACT_SWIGLU,
+                     out2=pre)
+        u_d = _narrow(f, lora_d.a_pad, ROW) if lora_d is not None else None
+        d = gemm(f, w_d, u_d, lora_d.ub if lora_d is not None else None, None, 0)
+        e = torch.empty(0)
+        ctx.lora_gu, ctx.lora_d, ctx.n_gu = lora_gu, lora_d, n_gu
+        ctx.save_for_backward(x2, w_gu, w_d, u_gu if u_gu is not None else e, pre, f, u_d if u_d is not None else e)
+        return d
+
+    @staticmethod
+    def backward(ctx, dd):
+        x2, w_gu, w_d, u_gu, pre, f, u_d = ctx.saved_tensors
+        needs = ctx.needs_input_grad
+        dd = dd.contiguous()
+        dpre = torch.empty_like(pre)
+        _, dw_d, g_d = _linear_bwd(dd, f, w_d, u_d if ctx.lora_d is not None else None, ctx.lora_d, None, True,
+                                   needs[2], dx_act=ACT_DSWIGLU, dx_aux=pre, dx_out=dpre)
+        dx, dw_gu, g_gu = _linear_bwd(dpre, x2, w_gu, u_gu if ctx.lora_gu is not None else None, ctx.lora_gu, None,
+                                      needs[0], needs[1])
+        return (dx, dw_gu, dw_d, None, None, None, *g_gu, *g_d)
+
+
+def swiglu_mlp(x: torch.Tensor, w_gu: torch.Tensor, w_d: torch.Tensor, lora_gu: Optional[LoRAGroup] = None,
+               lora_d: Optional[LoRAGroup] = None, cpu: bool = False) -> Optional[torch.Tensor]:
+    """Training-forward MLP through :class:`_SwiGLUMLPFn` when it applies (GPU, bf16, autograd on,
+    LoRA without dropout, [gate; up] rows % 256); returns None otherwise (the caller runs the two
+    ``linear`` calls). ``cpu``: also on CPU tensors (the fp32 oracles of every step; tests)."""
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    lg = lora_gu if (lora_gu is not None and lora_gu.enabled) else None
+    ld = lora_d if (lora_d is not None and lora_d.enabled) else None
+    if not (on_gpu(x2) or cpu) or not torch.is_grad_enabled() or w_gu.shape[0] % 256 \
+            or (on_gpu(x2) and w_gu.dtype != torch.bfloat16) \
+            or w_d.shape[1] % 8 or any(g is not None and (g.dropout > 0 or g.use_merged) for g in (lg, ld)):
+        return None
+    params = []
+    for g in (lg, ld):
+        if g is not None:
+            if g.a_pad is None or g.a_pad.device != x.device:
+                g.refresh(dtype=w_gu.dtype)
+            for a, b in zip(g.a, g.b):
+                params += [a, b]
+    if not (x2.requires_grad or w_gu.requires_grad or w_d.requires_grad or any(p.requires_grad for p in params)):
+        return None
+    n_gu = 2 * len(lg.a) if lg is not None else 0
+    y = _SwiGLUMLPFn.apply(x2.contiguous(), w_gu, w_d, lg, ld, n_gu, *params)
+    return y.reshape(*shp[:-1], w_d.shape[0])
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional[LoRAGroup] = None, fp8=None):

@@ -1129,3 +1129,50 @@ def test_fp8_training_forward_loss_parity():
     assert abs(l8 - l16) <= 0.02 * abs(l16), (l8, l16)
     cos = torch.nn.functional.cosine_similarity(g8, g16, dim=0).item()
     assert cos > 0.98, cos
+
+
+def test_swiglu_bwd_epilogue_and_fused_mlp_bitwise():
+    """ACT_DSWIGLU (the SwiGLU backward in the down projection's dX GEMM epilogue) is bitwise the
+    separate GEMM + swiglu_bwd pair, and the fused MLP node (ops.swiglu_mlp) gives bitwise the
+    two-linear outputs and gradients with LoRA on gate, up and down."""
+    def _r(*shape, s=1.0):
+        return (torch.randn(*shape, device=DEV) * s).to(torch.bfloat16)
+
+    torch.manual_seed(0)
+    M, H, F, R = 700, 512, 1024, 64
+    dd, wd = _r(M, H), _r(H, F, s=1 / math.sqrt(H))
+    pre = _r(M, 2 * F)
+    du, ap = _r(M, R), _r(R, F, s=0.05)
+    out = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    for bn in (0, 128, 256):
+        fused = ops.gemm_big(dd, wd, ops.ROW, ops.KMAJ, du, ap, act=ops.ACT_DSWIGLU, out=out, residual=pre, bn=bn)
+        df = ops.gemm_big(dd, wd, ops.ROW, ops.KMAJ, du, ap, bn=bn)
+        assert torch.equal(fused, ops.native().swiglu_bwd(pre, df))
+    from rag_tl_domainllm_optimizer_amd import models
+
+    cfg = models.resolve_preset("tiny-mistral")
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
+    m.add_lora(8, 16.0, "all")
+    layer = m.layers[0]
+    with torch.no_grad():
+        for p in m.lora_parameters():
+            p.normal_(0, 0.02)
+    m.refresh_lora()
+    x = _r(300, cfg.hidden_size).requires_grad_(True)
+    gy = _r(300, cfg.hidden_size)
+    params = [x] + list(layer.lora_params.values())
+
+    def run(fused):
+        if fused:
+            y = ops.swiglu_mlp(x, layer.gate_up_w, layer.down_w, layer.lora["gate_up"], layer.lora["down"])
+            assert y is not None
+        else:
+            f = ops.linear(x, layer.gate_up_w, act="swiglu", lora=layer.lora["gate_up"])
+            y = ops.linear(f, layer.down_w, lora=layer.lora["down"])
+        return y, torch.autograd.grad((y.float() * gy.float()).sum(), params, allow_unused=True)
+
+    y1, g1 = run(True)
+    y2, g2 = run(False)
+    assert torch.equal(y1, y2)
+    for a, b in zip(g1, g2):
+        assert (a is None and b is None) or torch.equal(a, b)
