@@ -75,6 +75,9 @@ def main():
                          "packed forwards; RAGTL_PACK=0 for the padded comparison)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--torch-profile", default=None,
+                    help="PPO mode: run one extra (untimed) step under torch.profiler after the warm-up and "
+                         "write its per-op table, grouped by Python call site, to this path")
     ap.add_argument("--mode", default="ppo", choices=["ppo", "sft", "pipeline", "serve"])
     ap.add_argument("--serve-concurrency", default="1,4,16",
                     help="--mode serve: closed-loop client counts (one engine, max batch = the largest)")
@@ -225,6 +228,8 @@ def main():
         m = trainer.step(make_batch())
         log(f"[bench] warmup {w}: {m['step_time_s']:.2f}s tokens={m['rollout_tokens']:.0f} "
             f"reward={m['reward_mean']:.3f}")
+    if args.torch_profile:
+        torch_profile_step(trainer, make_batch, args.torch_profile)
     parallel.barrier()
     torch.cuda.synchronize()
     trainer.sync.comm_bytes = 0
@@ -290,6 +295,21 @@ def main():
             with open(args.json_out, "w") as f:
                 json.dump(res, f, indent=2)
     parallel.shutdown()
+
+
+def torch_profile_step(trainer, make_batch, path):
+    """One PPO step under torch.profiler (outside the timed region): device time per op, grouped by
+    the Python call site that launched it, so small torch glue kernels can be traced to source."""
+    from torch.profiler import ProfilerActivity, profile
+
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        trainer.step(make_batch())
+        torch.cuda.synchronize()
+    with open(path, "w") as f:
+        f.write(prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=80,
+                                                            max_name_column_width=60))
+    log(f"[bench] torch profile -> {path}")
 
 
 def rank_spread(step_s: float, dev) -> dict:

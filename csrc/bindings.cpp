@@ -27,6 +27,9 @@ int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, lon
                 int, float*, unsigned*, hipStream_t);
 int rt_gemm_small(int, int, const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
                   int, hipStream_t);
+int rt_gemm_big_rope(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*,
+                     void*, long, int, int, int, const int*, const float*, const float*, int, int, const void*, int,
+                     hipStream_t);
 int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
 int rt_gemm_big_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int,
                     int, int, int, const void*, long, const void*, long, int, void*, long, const void*, hipStream_t);
@@ -459,6 +462,55 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
                        sk.part.defined() ? sk.part.data_ptr<float>() : nullptr,
                        sk.tickets.defined() ? (unsigned*)sk.tickets.data_ptr<int>() : nullptr, cur_stream()),
            "gemm_big");
+  return c;
+}
+
+// Fused qkv projection with the rotary embedding in the epilogue (gemm_big NT, E_ROPE):
+// C = rope(a w^T (+ u ub^T) + bias); columns [0, rope_cols) are head_dim-wide heads rotated at
+// position pos[row] (int32 [M]) with the cos / sin tables [positions, head_dim / 2] (fp32).
+Tensor gemm_rope(const Tensor& a, const Tensor& w, const optional<Tensor>& u, const optional<Tensor>& ub,
+                 const optional<Tensor>& bias, const Tensor& pos, const Tensor& cos, const Tensor& sin,
+                 int64_t rope_cols, int64_t head_dim, optional<Tensor> out, int64_t bn) {
+  CHECK_CUDA(a); CHECK_CUDA(w); CHECK_BF16(a); CHECK_BF16(w); CHECK_ROWS(a); CHECK_ROWS(w);
+  CHECK_ALIGN16(a); CHECK_ALIGN16(w);
+  CHECK_I32(pos); CHECK_F32(cos); CHECK_F32(sin);
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && K % 8 == 0 && a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0,
+              "gemm_rope: [M, K] x [N, K] with K and row strides % 8 == 0");
+  TORCH_CHECK(N % 8 == 0, "gemm_rope: N must be a multiple of 8");
+  TORCH_CHECK(pos.dim() == 1 && pos.size(0) == M && pos.is_contiguous(), "gemm_rope: pos must be int32 [M]");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.dim() == 2 && cos.size(1) == head_dim / 2 &&
+                  sin.sizes() == cos.sizes(),
+              "gemm_rope: cos / sin must be contiguous fp32 [positions, head_dim / 2]");
+  TORCH_CHECK(rope_cols >= 0 && rope_cols <= N && head_dim > 0 && rope_cols % head_dim == 0,
+              "gemm_rope: rope_cols must be a multiple of head_dim within N");
+  int64_t K2 = 0;
+  const bool ext = u.has_value() && u->defined();
+  if (ext) {
+    TORCH_CHECK(ub.has_value() && ub->defined(), "gemm_rope: u without ub");
+    CHECK_BF16(*u); CHECK_BF16(*ub); CHECK_ROWS(*u); CHECK_ROWS(*ub); CHECK_ALIGN16(*u); CHECK_ALIGN16(*ub);
+    TORCH_CHECK(u->size(0) == M && ub->size(0) == N && u->size(1) == ub->size(1) && u->size(1) % 8 == 0 &&
+                    u->stride(0) % 8 == 0 && ub->stride(0) % 8 == 0,
+                "gemm_rope: LoRA extension shape");
+    K2 = u->size(1);
+  }
+  if (bias.has_value() && bias->defined()) { CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N && bias->is_contiguous()); }
+  Tensor c;
+  if (out.has_value() && out->defined()) {
+    c = *out;
+    CHECK_BF16(c); CHECK_ALIGN16(c);
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.stride(0) % 8 == 0,
+                "gemm_rope: bad out");
+  } else {
+    c = at::empty({M, N}, a.options());
+  }
+  if (M == 0) return c;
+  check_rc(rt_gemm_big_rope(a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), ext ? u->data_ptr() : nullptr,
+                            ext ? u->stride(0) : 0, ext ? ub->data_ptr() : nullptr, ext ? ub->stride(0) : 0, (int)K2,
+                            opt_ptr(bias), c.data_ptr(), c.stride(0), (int)M, (int)N, (int)K, pos.data_ptr<int>(),
+                            cos.data_ptr<float>(), sin.data_ptr<float>(), (int)rope_cols, (int)head_dim,
+                            zero_page(a).data_ptr(), (int)bn, cur_stream()),
+           "gemm_rope");
   return c;
 }
 
@@ -1277,6 +1329,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b2") = py::none(), py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("out_mode") = 0,
         py::arg("nsplit") = 1, py::arg("out") = py::none(), py::arg("out2") = py::none(),
         py::arg("residual") = py::none(), py::arg("bn") = 0);
+  m.def("gemm_rope", &gemm_rope, "NT GEMM with the rotary embedding of the q / k heads in the epilogue", py::arg("a"),
+        py::arg("w"), py::arg("u") = py::none(), py::arg("ub") = py::none(), py::arg("bias") = py::none(),
+        py::arg("pos"), py::arg("cos"), py::arg("sin"), py::arg("rope_cols"), py::arg("head_dim"),
+        py::arg("out") = py::none(), py::arg("bn") = 0);
   m.def("gemm_splitk", &gemm_splitk, "small-M NT GEMM: split-K fp32 slabs + fused reduce epilogue", py::arg("a"),
         py::arg("w"), py::arg("nsplit"), py::arg("slabs"), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("out") = py::none(), py::arg("residual") = py::none(), py::arg("bn") = 256);

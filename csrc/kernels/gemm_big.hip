@@ -57,7 +57,12 @@ enum Out { O_BF16 = 0, O_F32 = 1, O_F32_ATOMIC = 2, O_F32_SLAB = 3 };
 // = d[gate | up] [M, 2F] (ldr = ldc = 2F rows): dF is rounded to bf16 first, then exactly the
 // arithmetic of swiglu_bwd_kernel — bitwise the unfused GEMM + SwiGLU-backward pair, without the
 // dF round trip through HBM.
-enum Epi { E_NONE = 0, E_RELU = 1, E_GELU = 2, E_GELU_TANH = 3, E_SILU = 4, E_SWIGLU = 5, E_DSWIGLU = 6 };
+// E_ROPE (NT, bf16 out): rotary embedding of the q / k heads of a fused qkv projection in the
+// epilogue — output columns [0, rope_cols) are heads of rope_d columns whose halves (e, e + rope_d/2)
+// rotate by the angle table row rope_pos[row] (cos / sin [positions, rope_d / 2] fp32). A head never
+// straddles a tile (rope_d divides 128), so both halves are in the LDS-staged tile. Arithmetic of
+// rope_qkv_kernel (sign +1) on the bf16-rounded GEMM output: bitwise the GEMM + rope pair.
+enum Epi { E_NONE = 0, E_RELU = 1, E_GELU = 2, E_GELU_TANH = 3, E_SILU = 4, E_SWIGLU = 5, E_DSWIGLU = 6, E_ROPE = 7 };
 
 struct Args {
   const bf16_t* A; long lda;
@@ -89,6 +94,11 @@ struct Args {
   unsigned* sk_tickets;
   int b_layout_kmaj;  // host: NN form of the stream-K launch
   int group_m;        // rows of tiles per L2 group (0 = GROUP_M); tuning gemm_group_m
+  // E_ROPE: per-row rotary position, angle tables, rotated column count, head width
+  const int* rope_pos;
+  const float* rope_cos;
+  const float* rope_sin;
+  int rope_cols, rope_d;
 };
 
 __device__ __forceinline__ int row_swz(int row) { return (row >> 1) & 7; }
@@ -707,6 +717,25 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
           const int grow = m0 + hh * 128 + row, gcol = n0 + cc * 8;
           if (grow < p.M && gcol < p.N) {
             uint4 v = ld16(row, cc);
+            if constexpr (EPI == E_ROPE) {
+              if (gcol < p.rope_cols) {
+                const int hd2 = p.rope_d >> 1, e = gcol % p.rope_d;
+                const bool lo = e < hd2;
+                const uint4 pv = ld16(row, lo ? cc + (hd2 >> 3) : cc - (hd2 >> 3));  // the rotation partner
+                float x[8], y[8], o8[8];
+                unpack8(v, x);
+                unpack8(pv, y);
+                const long tb = (long)p.rope_pos[grow] * hd2 + (lo ? e : e - hd2);
+                const float4 c0 = *(const float4*)(p.rope_cos + tb), c1 = *(const float4*)(p.rope_cos + tb + 4);
+                const float4 s0 = *(const float4*)(p.rope_sin + tb), s1 = *(const float4*)(p.rope_sin + tb + 4);
+                const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+                const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+                for (int k = 0; k < 8; ++k)  // lo: x1 c - x2 s ; hi: x2 c + x1 s (rope_qkv_kernel's fma order)
+                  o8[k] = lo ? fmaf(x[k], cs[k], -(y[k] * sn[k])) : fmaf(x[k], cs[k], y[k] * sn[k]);
+                v = pack8(o8);
+              }
+            }
             if (p.R) {  // residual in fp32 on the bf16-rounded GEMM result (= a separate add kernel)
               float y[8], r[8];
               unpack8(v, y);
@@ -1312,6 +1341,7 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
     switch (key * 10 + act) {
       case 0: GB_LAUNCH(ROW, ROW, O_BF16, E_NONE, 128); break;
       case E_SWIGLU: GB_LAUNCH(ROW, ROW, O_BF16, E_SWIGLU, 128); break;
+      case E_ROPE: GB_LAUNCH(ROW, ROW, O_BF16, E_ROPE, 128); break;
       case 10: GB_LAUNCH(ROW, ROW, O_F32, E_NONE, 128); break;
       case 30: GB_LAUNCH(ROW, ROW, O_F32_SLAB, E_NONE, 128); break;
       case 100: GB_LAUNCH(ROW, KMAJ, O_BF16, E_NONE, 128); break;
@@ -1326,6 +1356,7 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
       case E_GELU_TANH: GB_LAUNCH(ROW, ROW, O_BF16, E_GELU_TANH, 256); break;
       case E_SILU: GB_LAUNCH(ROW, ROW, O_BF16, E_SILU, 256); break;
       case E_SWIGLU: GB_LAUNCH(ROW, ROW, O_BF16, E_SWIGLU, 256); break;
+      case E_ROPE: GB_LAUNCH(ROW, ROW, O_BF16, E_ROPE, 256); break;
       default: return -4;
     }
   } else if (key == 10 && act == E_DSWIGLU) {
@@ -1352,8 +1383,8 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
 
 static bool bn128_supported(int layout_a, int layout_b, int act, int out) {
   const int key = layout_a * 100 + layout_b * 10 + out;
-  return (key == 0 && (act == E_NONE || act == E_SWIGLU)) || (act == E_NONE && (key == 1 || key == 3 || key == 10)) ||
-         (key == 10 && act == E_DSWIGLU);
+  return (key == 0 && (act == E_NONE || act == E_SWIGLU || act == E_ROPE)) ||
+         (act == E_NONE && (key == 1 || key == 3 || key == 10)) || (key == 10 && act == E_DSWIGLU);
 }
 
 static int query_num_cus() {
@@ -1421,6 +1452,9 @@ static int launch_gemm_big_sk(const Args& p, int layout_a, int act, const SkPlan
   return 0;
 }
 
+static int gemm_big_planned(const Args& p, int layout_a, int layout_b, int act, int out, int bn, float* sk_part,
+                            unsigned* sk_tickets, hipStream_t stream);
+
 // layout_a / layout_b: 0 = ROW (K contiguous), 1 = KMAJ (M / N contiguous).
 // out: 0 bf16 (epilogue bias + act, or SwiGLU), 1 fp32 store (bias + act), 2 fp32 atomic add
 // (split-K; C must be initialised by the caller), 3 fp32 split-K slabs. bn: 256, 128, or 0 = plan:
@@ -1437,6 +1471,7 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
                            int act, int out, int nsplit, const void* zpage, int bn, float* sk_part,
                            unsigned* sk_tickets, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
+  if (act == E_ROPE) return -5;  // rt_gemm_big_rope (the rotary tables are its arguments)
   // a ROW operand reads 8-element k-chunks: its reduction length must be a multiple of 8
   const bool any_row = layout_a == ROW || layout_b == ROW;
   if ((any_row && (K % 8 || (A2 && K2 % 8))) || !zpage) return -1;
@@ -1458,10 +1493,9 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
     return -5;
   }
   if (bn != 0 && bn != 128 && bn != 256 && bn != 4 && bn != 3) return -8;
-  const bool can128 = bn128_supported(layout_a, layout_b, act, out);
-  if (bn == 128 && !can128) return -8;
-  if ((bn == 4 || bn == 3) && (layout_a != ROW || layout_b != ROW || (out != O_BF16 && out != O_F32) || nsplit != 1 ||
-                  (long)N * ldb * 2 >= (1L << 32) || (long)M * lda * 2 >= (1L << 32)))
+  if (bn == 128 && !bn128_supported(layout_a, layout_b, act, out)) return -8;
+  if ((bn == 4 || bn == 3) && (act == E_ROPE || layout_a != ROW || layout_b != ROW || (out != O_BF16 && out != O_F32) ||
+                               nsplit != 1 || (long)N * ldb * 2 >= (1L << 32) || (long)M * lda * 2 >= (1L << 32)))
     return -8;
   Args p{};
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
@@ -1474,7 +1508,17 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   // tuning gemm_b_nt = 1: non-temporal weight stream when one row tile covers M (each B byte read
   // once per launch). Measured neutral on the batch-256 decode GEMMs (profiles/decode_nt_ab.log): off
   p.b_nt = layout_b == ROW && M <= 256 && tuning().gemm_b_nt > 0;
+  return gemm_big_planned(p, layout_a, layout_b, act, out, bn, sk_part, sk_tickets, stream);
+}
+
+// bn = 0: the wave planner (and the optional stream-K tail) over validated arguments p
+static int gemm_big_planned(const Args& p, int layout_a, int layout_b, int act, int out, int bn, float* sk_part,
+                            unsigned* sk_tickets, hipStream_t stream) {
   if (bn != 0) return launch_gemm_big(p, layout_a, layout_b, act, out, bn, stream);
+  const int M = p.M, N = p.N, K = p.K, K2 = p.K2, nsplit = p.nsplit;
+  const long lda = p.lda, lda2 = p.lda2, ldc = p.ldc, ldc2 = p.ldc2, ldr = p.ldr;
+  void* C = p.C;
+  const bool can128 = bn128_supported(layout_a, layout_b, act, out);
   // ---- plan: m1 row tiles at BN = 256, the rest at BN = 128; or a stream-K tail ----
   const int tiles_m = (M + 255) / 256;
   const int tn256 = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
@@ -1517,7 +1561,36 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   q.C = (char*)C + r0 * ldc * (out == O_BF16 ? 2 : 4);
   if (p.C2) q.C2 = p.C2 + r0 * ldc2;
   if (p.R) q.R = p.R + r0 * ldr;
+  if (p.rope_pos) q.rope_pos = p.rope_pos + r0;
   return launch_gemm_big(q, layout_a, layout_b, act, out, 128, stream);
+}
+
+// NT GEMM + rotary epilogue (E_ROPE): C = rope(A B^T (+ A2 B2^T) + bias) for a fused qkv
+// projection — output columns [0, rope_cols) are rope_d-wide heads rotated at position pos[row]
+// with the [positions, rope_d / 2] fp32 tables; the rest (v heads) are stored as they are. Replaces
+// the separate rope_qkv pass over the projection output (one read + write of every q / k element).
+// Same wave planner as rt_gemm_big. Requirements: rope_d in {16, 32, 64, 128}, rope_cols % rope_d
+// == 0, rope_cols <= N, bf16 out with ldc % 8 == 0, K (K2) % 8 == 0.
+extern "C" int rt_gemm_big_rope(const void* A, long lda, const void* B, long ldb, const void* A2, long lda2,
+                                const void* B2, long ldb2, int K2, const void* bias, void* C, long ldc, int M, int N,
+                                int K, const int* pos, const float* cosT, const float* sinT, int rope_cols, int rope_d,
+                                const void* zpage, int bn, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 8 || (A2 && K2 % 8) || !zpage || ldc % 8 || (M > 1 && ldc < (long)((N + 7) / 8 * 8))) return -1;
+  if (!pos || !cosT || !sinT || (rope_d != 16 && rope_d != 32 && rope_d != 64 && rope_d != 128) ||
+      rope_cols % rope_d || rope_cols > N || rope_cols < 0)
+    return -5;
+  if (bn != 0 && bn != 128 && bn != 256) return -8;
+  Args p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
+  p.A2 = (A2 && B2) ? (const bf16_t*)A2 : nullptr; p.lda2 = lda2;
+  p.B2 = (const bf16_t*)B2; p.ldb2 = ldb2; p.K2 = K2;
+  p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc;
+  p.M = M; p.N = N; p.K = K; p.act = E_ROPE; p.nsplit = 1; p.zpage = (const bf16_t*)zpage;
+  p.group_m = tuning().gemm_group_m;
+  p.b_nt = M <= 256 && tuning().gemm_b_nt > 0;
+  p.rope_pos = pos; p.rope_cos = cosT; p.rope_sin = sinT; p.rope_cols = rope_cols; p.rope_d = rope_d;
+  return gemm_big_planned(p, ROW, ROW, E_ROPE, O_BF16, bn, nullptr, nullptr, stream);
 }
 
 // W8A8 on the gemm_big schedule (config 5 prefill / reference scoring): A [M, K] e4m3fn with

@@ -154,6 +154,20 @@ class DecoderLayer(nn.Module):
         qkv = lin(h, self.qkv_w, self._b("qkv_b"), lora=self._lg("qkv"), fp8=self._f8("qkv"))
         return qkv, residual
 
+    def attn_in_rope(self, x, residual, rope):
+        """Token-parallel forms (training / reference forwards, prefill): the qkv projection with the
+        rotary embedding in its GEMM epilogue where that applies (``ops.linear_rope``; ``rope`` =
+        (pos per row, cos, sin)). Returns (qkv, residual, rotated)."""
+        cfg = self.cfg
+        if rope is None or cfg.arch == "opt":
+            qkv, residual = self.attn_in(x, residual)
+            return qkv, residual, False
+        h, residual = ops.rms_norm(x, self.ln1_w, cfg.norm_eps, residual)
+        D = cfg.head_dim
+        qkv, rotated = ops.linear_rope(h, self.qkv_w, self._b("qkv_b"), lora=self._lg("qkv"), fp8=self._f8("qkv"),
+                                       rope=(rope[0], rope[1], rope[2], (cfg.num_heads + cfg.num_kv_heads) * D, D))
+        return qkv, residual, rotated
+
     def mlp(self, a, residual, defer: bool = False):
         cfg = self.cfg
         defer = defer and cfg.arch != "opt"
@@ -311,14 +325,17 @@ class CausalLM(nn.Module):
     def _layer_fwd(self, layer, x, residual, pos, cos, sin, B, S, ks, packed_idx=None, packed_inv=None,
                    out_rows=None):
         cfg = self.cfg
-        qkv, residual = layer.attn_in(x, residual)
         rope = (pos, cos, sin) if cos is not None else None
+        # the projection rotates its own rows: packed rows carry their own positions
+        rows_pos = pos.index_select(0, packed_idx) if (packed_idx is not None and rope is not None) else pos
+        qkv, residual, rotated = layer.attn_in_rope(x, residual, (rows_pos, cos, sin) if rope is not None else None)
         if packed_idx is not None:
             o = ops.flash_attention_packed(qkv, packed_idx, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
-                                           cfg.sliding_window, kv_start=ks, rope=rope, inv=packed_inv)
+                                           cfg.sliding_window, kv_start=ks, rope=rope, inv=packed_inv,
+                                           rope_done=rotated)
         else:
             o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
-                                        cfg.sliding_window, kv_start=ks, rope=rope)
+                                        cfg.sliding_window, kv_start=ks, rope=rope, rope_done=rotated)
         if out_rows is not None:
             # everything after attention is row-local: drop the rows nobody reads before o_proj
             inv = ops.packed_inverse(out_rows, o.shape[0])
@@ -348,17 +365,21 @@ class CausalLM(nn.Module):
         else:
             x = self.embed_tokens(input_ids.reshape(-1), pos)
         residual = None
+        rows_pos = pos.index_select(0, idx) if (idx is not None and cos is not None) else pos
         for li, layer in enumerate(self.layers):
-            qkv, residual = layer.attn_in(x, residual)
+            qkv, residual, rotated = layer.attn_in_rope(x, residual, (rows_pos, cos, sin) if cos is not None else None)
             if idx is not None:
                 qkv = ops.scatter_rows(qkv, idx, inv, B * S)
+            # rotated: q / k came out of the projection's epilogue already rotated (cache append only)
+            rc, rs = (None, None) if rotated else (cos, sin)
             if getattr(cache, "fp8", False):
                 # fp8 cache: rotate in place, then quantise the prompt K / V rows into it
-                ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S)
+                if not rotated:
+                    ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S)
                 k_sc, v_sc = cache.scales(li)
                 ops.kv_store_fp8(qkv, cache.k[li], cache.v[li], k_sc, v_sc, B, S, cfg.num_heads)
             else:
-                ops.rope_qkv_(qkv, pos, cos, sin, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S,
+                ops.rope_qkv_(qkv, pos, rc, rs, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, S=S,
                               k_cache=cache.k[li], v_cache=cache.v[li], slot_base=None)
             o = ops.flash_attention_qkv(qkv, B, S, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, True,
                                         cfg.sliding_window, kv_start=ks)

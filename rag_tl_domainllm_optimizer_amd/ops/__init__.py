@@ -3,7 +3,7 @@ the eager reference implementations (:mod:`.reference`, also the test oracles)."
 from ._ext import get_tuning, native, native_available, on_gpu, set_tuning, tuning  # noqa: F401
 from .linear import (  # noqa: F401
     ACT_DSWIGLU, ACT_IDS, ACT_SWIGLU, KMAJ, ROW, FoldCache, LoRAGroup, ShufCache, SplitK, gemm, gemm_big, gemm_decode, gemm_nn, gemm_tn, linear,
-    swiglu_mlp,
+    swiglu_mlp, gemm_rope, linear_rope, rope_fusable,
     refresh_lora_batched,
     linear_deferred)
 from .norm import layer_norm, rms_norm  # noqa: F401

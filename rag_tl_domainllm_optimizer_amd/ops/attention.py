@@ -71,8 +71,8 @@ class _FlashFn(torch.autograd.Function):
     this saves the CopySlices copy and the gradient clone of the whole qkv tensor per layer."""
 
     @staticmethod
-    def forward(ctx, qkv, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope=None):
-        if rope is not None:
+    def forward(ctx, qkv, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope=None, rope_done=False):
+        if rope is not None and not rope_done:
             # in place on the projection output: nothing else holds it (the linear saved its input)
             rope_qkv_(qkv, rope[0], rope[1], rope[2], Hq, Hkv, D)
         ctx.rope = rope
@@ -99,14 +99,20 @@ class _FlashFn(torch.autograd.Function):
         if ctx.rope is not None:
             pos, cos, sin = ctx.rope
             rope_qkv_(dqkv, pos, cos, sin, Hq, Hkv, D, sign=-1.0)
-        return dqkv, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
-def flash_attention_qkv(qkv, B, S, Hq, Hkv, D, causal=True, window=0, scale=None, kv_start=None, rope=None):
+def flash_attention_qkv(qkv, B, S, Hq, Hkv, D, causal=True, window=0, scale=None, kv_start=None, rope=None,
+                        rope_done=False):
     """Self-attention over fused qkv rows [B*S, (Hq+2Hkv)*D] -> o [B*S, Hq*D]. ``rope`` =
-    (pos, cos, sin) rotates q/k first (in place on ``qkv``, which must not be needed elsewhere)."""
+    (pos, cos, sin) rotates q/k first (in place on ``qkv``, which must not be needed elsewhere).
+    ``rope_done``: the projection already rotated q / k in its GEMM epilogue (ops.linear_rope);
+    the rotation's gradient (inverse rotation of dq / dk) still runs here."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    if rope is not None and not (on_gpu(qkv) and torch.is_grad_enabled() and qkv.requires_grad):
+    grad_gpu = on_gpu(qkv) and torch.is_grad_enabled() and qkv.requires_grad
+    if rope_done and not grad_gpu:
+        rope = None
+    if rope is not None and not grad_gpu:
         qkv = rope_qkv(qkv, rope[0], rope[1], rope[2], Hq, Hkv, D)
         rope = None
     if not on_gpu(qkv):
@@ -115,7 +121,7 @@ def flash_attention_qkv(qkv, B, S, Hq, Hkv, D, causal=True, window=0, scale=None
         v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D]
         return ref.attention(q, k, v, B, S, S, Hq, Hkv, D, causal, window, scale, kv_start)[0]
     if torch.is_grad_enabled() and qkv.requires_grad:
-        return _FlashFn.apply(qkv, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope)
+        return _FlashFn.apply(qkv, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope, rope_done)
     q = qkv[:, : Hq * D]
     k = qkv[:, Hq * D:(Hq + Hkv) * D]
     v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D]
@@ -179,7 +185,7 @@ def gather_rows(src, idx, inv):
 
 
 def flash_attention_packed(qkv_p, idx, B, S, Hq, Hkv, D, causal=True, window=0, scale=None, kv_start=None,
-                           rope=None, inv=None):
+                           rope=None, inv=None, rope_done=False):
     """Varlen self-attention over PACKED token rows (no pad rows in the GEMMs around it).
 
     ``qkv_p`` [N, W] holds only real tokens; ``idx`` [N] (int64) is each row's position b*S + s in
@@ -192,7 +198,7 @@ def flash_attention_packed(qkv_p, idx, B, S, Hq, Hkv, D, causal=True, window=0, 
     if inv is None:
         inv = packed_inverse(idx, B * S)
     grid = scatter_rows(qkv_p, idx, inv, B * S)
-    o = flash_attention_qkv(grid, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope)
+    o = flash_attention_qkv(grid, B, S, Hq, Hkv, D, causal, window, scale, kv_start, rope, rope_done)
     return gather_rows(o, idx, inv)
 
 

@@ -334,7 +334,7 @@ def _fp8_train_ok(f8, x2, w, bias, act, lora) -> bool:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], f8, *lora_params):
+    def forward(ctx, x2, w, bias, act, lora: Optional[LoRAGroup], f8, rope, *lora_params):
         u = ub = xd = None
         mask = None
         if lora is not None:
@@ -368,6 +368,11 @@ class _LinearFn(torch.autograd.Function):
             # the SwiGLU backward) from its epilogue — no separate SwiGLU pass over the activations
             pre = torch.empty(x2.shape[0], w.shape[0], dtype=x2.dtype, device=x2.device)
             y = gemm_big(x2, w, ROW, ROW, u, ub, None, ACT_SWIGLU, out2=pre)
+        elif rope is not None:
+            # q / k rotated in the epilogue; the rotation's backward is the attention node's
+            # (ops.flash_attention_qkv(..., rope_done=True) inverse-rotates dq / dk), so this node's
+            # backward is the plain projection's
+            y = gemm_rope(x2, w, u, ub, bias, rope)
         else:
             y = gemm(x2, w, u, ub, bias, act)
         # other activation epilogues: the pre-activation is recomputed in backward (no extra
@@ -403,7 +408,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.has_bias and needs[2]:
             db = dy.float().sum(0).to(bias.dtype)
         dx, dw, lora_grads = _linear_bwd(dy, x2, w, u, lora, mask, needs[0], needs[1])
-        return (dx, dw, db, None, None, None, *lora_grads)
+        return (dx, dw, db, None, None, None, None, *lora_grads)
 
 
 def _linear_bwd(dy, x2, w, u, lora, mask, need_x: bool, need_w: bool, dx_act: int = 0, dx_aux=None, dx_out=None):
@@ -546,7 +551,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
                 for a, b in zip(lora.a, lora.b):
                     params += [a, b]
             f8 = fp8.train_cache() if (fp8 is not None and fp8.train) else None
-            y = _LinearFn.apply(x2, w, None, ACT_SWIGLU, lora if use_lora else None, f8, *params)
+            y = _LinearFn.apply(x2, w, None, ACT_SWIGLU, lora if use_lora else None, f8, None, *params)
             return y.reshape(*shp[:-1], w.shape[0] // 2)
         if on_gpu(x2) and not grad_needed and bias is None and w.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0 \
                 and (x2.shape[0] <= 64 or w.shape[0] % 256 == 0):
@@ -594,8 +599,60 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
             for a, b in zip(lora.a, lora.b):
                 params += [a, b]
         f8 = fp8.train_cache() if (fp8 is not None and fp8.train) else None
-        y = _LinearFn.apply(x2, w, bias, act_id, lora if use_lora else None, f8, *params)
+        y = _LinearFn.apply(x2, w, bias, act_id, lora if use_lora else None, f8, None, *params)
     return y.reshape(*shp[:-1], w.shape[0])
+
+
+def gemm_rope(x2: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, rope=None) -> torch.Tensor:
+    """y = rope(x2 w^T (+ u ub^T) + bias) with ``rope`` = (pos int32 [M], cos, sin [positions, D/2] fp32,
+    rope_cols, D): output columns [0, rope_cols) are D-wide heads rotated at pos[row] (the q / k heads
+    of a fused qkv projection); GPU: one gemm_big launch with the rotary epilogue (E_ROPE)."""
+    pos, cos, sin, cols, D = rope
+    if on_gpu(x2):
+        return native().gemm_rope(x2, w, u, ub, bias, pos, cos, sin, cols, D)
+    y = ref.gemm(x2, w, u, ub, bias, 0, False)
+    return ref.rope_qkv(y, pos, cos, sin, cols // D, 0, D)
+
+
+# model-level A/B switch of the rotary epilogue (tests compare both forms; no native state)
+ROPE_EPILOGUE = True
+
+
+def rope_fusable(x2: torch.Tensor, w: torch.Tensor, lora: Optional[LoRAGroup], fp8) -> bool:
+    """The qkv projection takes the rotary epilogue: token-parallel bf16 GEMM on the GPU (M > 256,
+    the gemm_big planner's regime; no fp8 form for this projection; LoRA unmerged or merged)."""
+    M = x2.shape[0]
+    return (ROPE_EPILOGUE and on_gpu(x2) and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and M > 256 and
+            w.shape[0] % 8 == 0 and x2.shape[1] % 8 == 0 and fp8 is None and splitk_plan(M, w.shape[0], x2.shape[1], 0)[0] <= 1)
+
+
+def linear_rope(x: torch.Tensor, w: torch.Tensor, bias=None, lora: Optional[LoRAGroup] = None, fp8=None, rope=None):
+    """``linear`` of a fused qkv projection with its rotary embedding in the GEMM epilogue when that
+    applies (``rope_fusable``). Returns (y, rotated): rotated = False leaves the rotation to the
+    attention call as before (``rope`` = (pos, cos, sin, rope_cols, D), pos per row of x)."""
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    if rope is None or not rope_fusable(x2, w, lora, fp8):
+        return linear(x, w, bias, None, lora, fp8), False
+    x2 = x2.contiguous()
+    use_lora = lora is not None and lora.enabled
+    if use_lora and (lora.a_pad is None or lora.a_pad.device != x.device):
+        lora.refresh(dtype=w.dtype)
+    grad_needed = torch.is_grad_enabled() and (
+        x2.requires_grad or w.requires_grad or (bias is not None and bias.requires_grad)
+        or (use_lora and any(p.requires_grad for p in lora.a + lora.b)))
+    if grad_needed:
+        params = []
+        if use_lora:
+            for a, b in zip(lora.a, lora.b):
+                params += [a, b]
+        y = _LinearFn.apply(x2, w, bias, 0, lora if use_lora else None, None, rope, *params)
+    elif use_lora and lora.use_merged:
+        y = gemm_rope(x2, lora.merged_weight(w), None, None, bias, rope)
+    else:
+        u = _narrow(x2, lora.a_pad, ROW) if use_lora else None
+        y = gemm_rope(x2, w, u, lora.ub if use_lora else None, bias, rope)
+    return y.reshape(*shp[:-1], w.shape[0]), True
 
 
 class SplitK:

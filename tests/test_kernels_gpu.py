@@ -1176,3 +1176,91 @@ def test_swiglu_bwd_epilogue_and_fused_mlp_bitwise():
     assert torch.equal(y1, y2)
     for a, b in zip(g1, g2):
         assert (a is None and b is None) or torch.equal(a, b)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (64, 4, 2)])
+def test_gemm_rope_epilogue_bitwise(D, Hq, Hkv):
+    """gemm_rope (the rotary embedding in the qkv projection's GEMM epilogue, E_ROPE) is bitwise the
+    GEMM + rope_qkv pair — with a LoRA K-extension, a bias, both tile widths and the planner's
+    split into 256- and 128-wide tiles — and close to the fp32 oracle."""
+    from rag_tl_domainllm_optimizer_amd.ops import reference as ref
+
+    torch.manual_seed(1)
+    M, K, R = 1000, 512, 64
+    N = (Hq + 2 * Hkv) * D
+    x = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    u = (torch.randn(M, R, device=DEV) * 0.1).to(torch.bfloat16)
+    ub = (torch.randn(N, R, device=DEV) * 0.1).to(torch.bfloat16)
+    bias = (torch.randn(N, device=DEV) * 0.1).to(torch.bfloat16)
+    cos, sin = ref.rope_tables(D, 4096, 10000.0, DEV)
+    pos = torch.randint(0, 4096, (M,), device=DEV, dtype=torch.int32)
+    cols = (Hq + Hkv) * D
+    for ext, b in ((False, None), (True, None), (True, bias)):
+        uu, uub = (u, ub) if ext else (None, None)
+        for bn in (0, 128, 256):
+            fused = ops.native().gemm_rope(x, w, uu, uub, b, pos, cos, sin, cols, D, bn=bn)
+            plain = ops.gemm_big(x, w, ops.ROW, ops.ROW, uu, uub, b, bn=bn)
+            ops.rope_qkv_(plain, pos, cos, sin, Hq, Hkv, D)
+            assert torch.equal(fused, plain), (ext, b is not None, bn)
+    y32 = x.float() @ w.float().t() + u.float() @ ub.float().t() + bias.float()
+    want = ref.rope_qkv(y32.cpu(), pos.cpu(), cos.cpu(), sin.cpu(), Hq, Hkv, D)
+    _close(fused.float().cpu(), want, 0.02)
+
+
+def test_rope_epilogue_model_bitwise():
+    """A LoRA policy's scoring forward + backward (padded and packed) and its prefill give bitwise
+    the same log-probs, values, adapter gradients and greedy tokens with the rotary embedding in the
+    qkv GEMM epilogue as with the separate rope pass (ops.linear.ROPE_EPILOGUE off)."""
+    import numpy as np
+
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
+    from rag_tl_domainllm_optimizer_amd.models import ValueHead
+    from rag_tl_domainllm_optimizer_amd.ops import linear as lin
+    from rag_tl_domainllm_optimizer_amd.train.common import score_sequences
+
+    cfg = models.resolve_preset("tiny-mistral")
+    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=5)
+    m.add_lora(8, 16.0, None, seed=2)
+    with torch.no_grad():
+        for p in m.lora_parameters():
+            p.normal_(0, 0.02)
+    m.refresh_lora()
+    vh = ValueHead(cfg.hidden_size, device=DEV, seed=3)
+    g = torch.Generator().manual_seed(0)
+    B, S, T = 6, 80, 24
+    st = np.array([0, 30, 7, 50, 12, 64])
+    rl = np.array([24, 3, 17, 1, 20, 9])
+    pid = torch.randint(5, cfg.vocab_size, (B, S), generator=g)
+    resp = torch.randint(5, cfg.vocab_size, (B, T), generator=g)
+    for b in range(B):
+        pid[b, :st[b]] = 0
+        resp[b, rl[b]:] = 0
+    pid, resp = pid.to(DEV), resp.to(DEV)
+    start = torch.tensor(st, dtype=torch.int32, device=DEV)
+    rlen = torch.tensor(rl, device=DEV)
+    prompts = [list(range(7, 7 + n)) for n in (60, 5, 33, 17, 41, 70)]
+    res = {}
+    try:
+        for flag in (True, False):
+            lin.ROPE_EPILOGUE = flag
+            outs = []
+            for lengths in (None, (st, rl)):
+                for p in m.lora_parameters():
+                    p.grad = None
+                lp, ent, val, mask = score_sequences(m, pid, start, resp, rlen, 1.0, vh, lengths=lengths)
+                ((lp + 0.5 * val) * mask).sum().backward()
+                outs.append((lp.detach(), val.detach(), [p.grad.clone() for p in m.lora_parameters()]))
+            gen = Generator(m, max_batch=6, max_seq=96, device=DEV)
+            gen.use_graph = False
+            toks = gen.generate(prompts, SamplingParams(max_new_tokens=6, do_sample=False), pad_id=0, eos_ids=[-5]).tokens
+            res[flag] = (outs, toks.cpu())
+    finally:
+        lin.ROPE_EPILOGUE = True
+    (o1, t1), (o2, t2) = res[True], res[False]
+    for (lp1, v1, g1), (lp2, v2, g2) in zip(o1, o2):
+        assert torch.equal(lp1, lp2) and torch.equal(v1, v2)
+        for a, b in zip(g1, g2):
+            assert torch.equal(a, b)
+    assert torch.equal(t1, t2)

@@ -153,7 +153,8 @@ def test_forward_out_rows_matches_full(preset, packed):
     assert res[1][0].shape == (rows.numel(), cfg.hidden_size)
     torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-5, atol=1e-5)
     for ga, gb in zip(res[0][1], res[1][1]):
-        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=2e-5)
+        # fp32 sums over different row subsets block differently (MKL): ~1e-5 absolute noise
+        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-4)
     # prefill: hidden of the last position of every row == the full forward's
     if not packed:
         with torch.no_grad():

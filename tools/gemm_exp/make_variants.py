@@ -1,0 +1,70 @@
+"""Experiment copies of csrc/kernels/gemm_big.hip for tools/gemm_exp (timing-only diagnostics).
+
+Each variant removes ONE kind of stall from the 256x256 kernel's steady-state loop so its time
+shows how much that stall costs. Variants that drop a wait compute WRONG results on purpose; they
+are never built into the extension. Exact string edits with counted matches, so a source change
+that invalidates an edit fails loudly here instead of silently producing the base kernel.
+
+  python tools/gemm_exp/make_variants.py OUTDIR
+"""
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+SRC = os.path.join(ROOT, "csrc", "kernels", "gemm_big.hip")
+
+
+def _fast_loop_span(s):
+    a = s.index("for (; t < t_fast; ++t) {")
+    b = s.index("for (; t < t_end; ++t) {", a)
+    return a, b
+
+
+def _sub_in(s, span, old, new, count):
+    a, b = span
+    body = s[a:b]
+    n = body.count(old)
+    assert n == count, (old, n, count)
+    return s[:a] + body.replace(old, new) + s[b:]
+
+
+def _macro_line(s, needle, repl, count):
+    # GB_MMA_X lines end in padding + backslash: replace the statement, keep the continuation
+    pat = re.compile(r"^(\s*)" + re.escape(needle) + r"(\s*\\)$", re.M)
+    out, n = pat.subn(lambda m: m.group(1) + repl + m.group(2), s)
+    assert n == count, (needle, n, count)
+    return out
+
+
+def variants(s):
+    v = {"base": s}
+    # the steady-state loop without its counted LDS-DMA waits (granules may not have landed)
+    v["nowait"] = _sub_in(s, _fast_loop_span(s), "wait_granules<BN>(4);", "", 3)
+    # GB_MMA without the barrier that closes each MFMA cluster (the stagger then drifts)
+    t = s.replace("    __builtin_amdgcn_s_setprio(0);                                                          \\\n"
+                  "    GB_BARRIER();                                                                           \\\n",
+                  "    __builtin_amdgcn_s_setprio(0);                                                          \\\n", 1)
+    assert t != s
+    v["nobar_end"] = t
+    # no priority raise around the MFMA clusters
+    v["noprio"] = _macro_line(s, "__builtin_amdgcn_s_setprio(1);", ";", 1)
+    # MFMAs start without waiting for the fragment reads (LDS latency exposure)
+    v["nolgkm"] = _macro_line(s, 'asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");', ";", 1)
+    # both: no DMA waits and no closing barrier
+    v["nowait_nobar_end"] = _sub_in(t, _fast_loop_span(t), "wait_granules<BN>(4);", "", 3)
+    return v
+
+
+def main():
+    out = sys.argv[1]
+    os.makedirs(out, exist_ok=True)
+    s = open(SRC).read()
+    for name, text in variants(s).items():
+        with open(os.path.join(out, f"gemm_big_{name}.hip"), "w") as f:
+            f.write(text)
+        print(name)
+
+
+if __name__ == "__main__":
+    main()
