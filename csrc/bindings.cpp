@@ -61,7 +61,7 @@ int rt_attn_o_fused(const void*, void*, void*, int, const int*, const int*, cons
                     void*, int, unsigned*, int*, long long*, hipStream_t);
 int rt_attn_bwd(const void*, long, const void*, long, const void*, long, const void*, long, const void*, long,
                 const float*, float*, float*, void*, long, void*, long, void*, long, const int*, int, int, int, int,
-                int, int, int, float, hipStream_t);
+                int, int, int, float, const int*, const float*, const float*, hipStream_t);
 int rt_logprob_fwd(const void*, int, long, const long*, float, long, int, float*, float*, float*, float*, hipStream_t);
 int rt_logprob_bwd(const void*, int, long, const long*, float, long, int, const float*, const float*, const float*,
                    const float*, void*, long, hipStream_t);
@@ -1039,8 +1039,20 @@ bool attn_o_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& slot, c
 
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout, const Tensor& lse,
               Tensor dq, Tensor dk, Tensor dv, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D, bool causal,
-              int64_t window, double scale, const optional<Tensor>& kv_start) {
+              int64_t window, double scale, const optional<Tensor>& kv_start, const optional<Tensor>& rope_pos,
+              const optional<Tensor>& rope_cos, const optional<Tensor>& rope_sin) {
   CHECK_CUDA(q); CHECK_ROWS(q); CHECK_ROWS(k); CHECK_ROWS(v); CHECK_ROWS(o); CHECK_ROWS(dout);
+  // RoPE backward fused into the dQ / dK stores: pos int32 [B * S], cos / sin fp32 [positions, D / 2]
+  const bool rope = rope_cos.has_value() && rope_cos->defined();
+  if (rope) {
+    TORCH_CHECK(rope_pos.has_value() && rope_pos->defined() && rope_sin.has_value() && rope_sin->defined(),
+                "attn_bwd: rope needs pos, cos and sin");
+    CHECK_I32(*rope_pos); CHECK_F32(*rope_cos); CHECK_F32(*rope_sin);
+    TORCH_CHECK(rope_pos->numel() == B * S && rope_pos->is_contiguous() && rope_cos->is_contiguous() &&
+                    rope_sin->is_contiguous() && rope_cos->dim() == 2 && rope_cos->size(1) == D / 2 &&
+                    rope_sin->sizes() == rope_cos->sizes(),
+                "attn_bwd: rope tables [positions, D / 2] and pos [B * S]");
+  }
   CHECK_ROWS(dq); CHECK_ROWS(dk); CHECK_ROWS(dv); CHECK_F32(lse);
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
   // fp32 dQ accumulator: only the atomic form (tuning attn_bwd_atomic_dq) uses it
@@ -1051,7 +1063,9 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
                        o.stride(0), dout.data_ptr(), dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(),
                        dq32.data_ptr<float>(), dq.data_ptr(), dq.stride(0), dk.data_ptr(), dk.stride(0),
                        dv.data_ptr(), dv.stride(0), (const int*)opt_ptr(kv_start), (int)B, (int)S, (int)Hq, (int)Hkv,
-                       (int)D, causal ? 1 : 0, (int)window, (float)scale, cur_stream()),
+                       (int)D, causal ? 1 : 0, (int)window, (float)scale,
+                       rope ? rope_pos->data_ptr<int>() : nullptr, rope ? rope_cos->data_ptr<float>() : nullptr,
+                       rope ? rope_sin->data_ptr<float>() : nullptr, cur_stream()),
            "attn_bwd");
 }
 
@@ -1354,7 +1368,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed", &embed);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_decode", &attn_decode);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, "flash attention backward (RoPE backward optionally fused into dQ / dK)",
+        py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"), py::arg("lse"), py::arg("dq"),
+        py::arg("dk"), py::arg("dv"), py::arg("B"), py::arg("S"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"),
+        py::arg("causal"), py::arg("window"), py::arg("scale"), py::arg("kv_start") = py::none(),
+        py::arg("rope_pos") = py::none(), py::arg("rope_cos") = py::none(), py::arg("rope_sin") = py::none());
   m.def("logprob_fwd", &logprob_fwd);
   m.def("logprob_bwd", &logprob_bwd);
   m.def("sample", &sample);

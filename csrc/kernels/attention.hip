@@ -1766,7 +1766,21 @@ struct AttnBwdArgs {
   int causal, window;
   float scale_log2;            // scale * log2 e
   float scale;
+  // RoPE backward fused into the dQ / dK stores (null: none): q / k were rotated by angle row
+  // rope_pos[b * S + s] of the [positions, D / 2] tables; dq / dk are inverse-rotated from their
+  // bf16-rounded values with rope_qkv_kernel's arithmetic (sign -1): bitwise the separate pass
+  const int* rope_pos;
+  const float* rope_cos;
+  const float* rope_sin;
 };
+
+// inverse rotation of one (first-half, second-half) pair of a bf16-rounded gradient: x1 / x2 are
+// the rounded values at dims e / e + D/2; rope_qkv_kernel with sign = -1
+__device__ __forceinline__ void rope_bwd_pair(float x1, float x2, float c, float sn, float& o1, float& o2) {
+  const float s = -sn;
+  o1 = fmaf(x1, c, -(x2 * s));
+  o2 = fmaf(x2, c, x1 * s);
+}
 
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
@@ -1987,16 +2001,34 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
       }
     }
   }
-  // write dK, dV (lane holds dX^T[d = 16c + 4g + i][key = mykey])
+  // write dK, dV (lane holds dX^T[d = 16c + 4g + i][key = mykey]; dims d and d + D/2 are
+  // fragments c and c + DT/2 of the same lane: the RoPE backward pairs them in registers)
   if (mykey < a.S) {
+    bf16_t* dkrow = a.dk + ((long)b * a.S + mykey) * a.lddk + (long)hk * D;
+    if (a.rope_cos) {
+      const long tb = (long)a.rope_pos[(long)b * a.S + mykey] * (D / 2);
+#pragma unroll
+      for (int c = 0; c < DT / 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int d = 16 * c + 4 * g + i;
+          float o1, o2;
+          rope_bwd_pair(bf2f(f2bf(dk[c][i] * a.scale)), bf2f(f2bf(dk[c + DT / 2][i] * a.scale)), a.rope_cos[tb + d],
+                        a.rope_sin[tb + d], o1, o2);
+          dkrow[d] = f2bf(o1);
+          dkrow[d + D / 2] = f2bf(o2);
+        }
+    } else {
+#pragma unroll
+      for (int c = 0; c < DT; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dkrow[16 * c + 4 * g + i] = f2bf(dk[c][i] * a.scale);
+    }
 #pragma unroll
     for (int c = 0; c < DT; ++c)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int d = 16 * c + 4 * g + i;
-        a.dk[((long)b * a.S + mykey) * a.lddk + (long)hk * D + d] = f2bf(dk[c][i] * a.scale);
-        a.dv[((long)b * a.S + mykey) * a.lddv + (long)hk * D + d] = f2bf(dvv[c][i]);
-      }
+      for (int i = 0; i < 4; ++i)
+        a.dv[((long)b * a.S + mykey) * a.lddv + (long)hk * D + 16 * c + 4 * g + i] = f2bf(dvv[c][i]);
   }
 }
 
@@ -2122,14 +2154,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     if (has_next) store_tile();
     __syncthreads();
   }
-  // lane holds dQ[q0 + 4 g + i][16 c + r16]
+  // lane holds dQ[q0 + 4 g + i][16 c + r16] (dims d and d + D/2: fragments c and c + DT/2)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int qo = q0 + 4 * g + i;
     if (qo < a.S) {
       bf16_t* dst = a.dqb + ((long)b * a.S + qo) * a.lddq + (long)h * D;
+      if (a.rope_cos) {
+        const long tb = (long)a.rope_pos[(long)b * a.S + qo] * (D / 2);
 #pragma unroll
-      for (int c = 0; c < DT; ++c) dst[16 * c + r16] = f2bf(dq[c][i] * a.scale);
+        for (int c = 0; c < DT / 2; ++c) {
+          const int d = 16 * c + r16;
+          float o1, o2;
+          rope_bwd_pair(bf2f(f2bf(dq[c][i] * a.scale)), bf2f(f2bf(dq[c + DT / 2][i] * a.scale)), a.rope_cos[tb + d],
+                        a.rope_sin[tb + d], o1, o2);
+          dst[d] = f2bf(o1);
+          dst[d + D / 2] = f2bf(o2);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < DT; ++c) dst[16 * c + r16] = f2bf(dq[c][i] * a.scale);
+      }
     }
   }
 }
@@ -2368,16 +2413,25 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   return -1;
 }
 
+extern "C" int rt_rope_qkv(void* qkv, long ld, const int* pos, const float* cosT, const float* sinT, int T, int S,
+                           int Hq, int Hkv, int D, float sign, void* kc, void* vc, const int* slot_base, int Smax,
+                           int do_rope_q, hipStream_t stream);
+
+// rope_pos / rope_cos / rope_sin (all or none): the RoPE backward of the forward's q / k rotation,
+// fused into the dQ / dK stores (atomic-dQ form: a separate inverse rotation of dQ after conversion)
 extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv, const void* o,
                            long ldo, const void* dout, long lddo, const float* lse, float* delta, float* dq_f32,
                            void* dq, long lddq, void* dk, long lddk, void* dv, long lddv, const int* kv_start, int B,
-                           int S, int Hq, int Hkv, int D, int causal, int window, float scale, hipStream_t stream) {
+                           int S, int Hq, int Hkv, int D, int causal, int window, float scale, const int* rope_pos,
+                           const float* rope_cos, const float* rope_sin, hipStream_t stream) {
   AttnBwdArgs a;
   a.q = (const bf16_t*)q; a.ldq = ldq; a.k = (const bf16_t*)k; a.ldk = ldk; a.v = (const bf16_t*)v; a.ldv = ldv;
   a.o = (const bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.lse = lse; a.delta = delta;
   a.dq = dq_f32; a.dk = (bf16_t*)dk; a.lddk = lddk; a.dv = (bf16_t*)dv; a.lddv = lddv; a.kv_start = kv_start;
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.window = window;
   a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
+  if ((rope_pos != nullptr) != (rope_cos != nullptr) || (rope_cos != nullptr) != (rope_sin != nullptr)) return -2;
+  a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   if (B == 0 || S == 0) return 0;
   a.dqb = (bf16_t*)dq; a.lddq = lddq;
   const long rows = (long)B * S * Hq;
@@ -2403,6 +2457,13 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
     const long n = (long)B * S * Hq * D;
     hipLaunchKernelGGL(f32_to_bf16_strided_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_f32,
                        (long)Hq * D, (bf16_t*)dq, lddq, (long)B * S);
+    RT_LAUNCH_CHECK();
+    // dQ's RoPE backward: the q heads of the bf16 dQ rows (Hkv = 0: no k / v heads in this view)
+    if (rope_cos) {
+      const int rc = rt_rope_qkv(dq, lddq, rope_pos, rope_cos, rope_sin, B * S, S, Hq, 0, D, -1.f, nullptr, nullptr,
+                                 nullptr, 0, 1, stream);
+      if (rc) return rc;
+    }
   }
   RT_LAUNCH_CHECK();
   return 0;

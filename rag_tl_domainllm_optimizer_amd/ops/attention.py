@@ -62,6 +62,11 @@ def rope_qkv(qkv, pos, cos, sin, Hq, Hkv, D, rope_q=True):
 
 
 # ----------------------------------------------------------------------------- flash attention
+# the RoPE backward inside the attention backward's dQ / dK stores (A/B switch for the tests: off =
+# the separate inverse-rotation pass over d_qkv; bitwise the same result)
+ROPE_BWD_FUSED = True
+
+
 class _FlashFn(torch.autograd.Function):
     """Flash attention over fused qkv rows, optionally with RoPE applied in place first.
 
@@ -93,11 +98,13 @@ class _FlashFn(torch.autograd.Function):
         q = qkv[:, : Hq * D]
         k = qkv[:, Hq * D:(Hq + Hkv) * D]
         v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D]
+        rope = ctx.rope
+        fused = rope is not None and ROPE_BWD_FUSED and rope[0].dtype == torch.int32
         native().attn_bwd(q, k, v, o, do, lse, dqkv[:, : Hq * D], dqkv[:, Hq * D:(Hq + Hkv) * D],
                           dqkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D], B, S, Hq, Hkv, D, causal, window, scale,
-                          kv_start if has_start else None)
-        if ctx.rope is not None:
-            pos, cos, sin = ctx.rope
+                          kv_start if has_start else None, *(rope if fused else (None, None, None)))
+        if rope is not None and not fused:
+            pos, cos, sin = rope
             rope_qkv_(dqkv, pos, cos, sin, Hq, Hkv, D, sign=-1.0)
         return dqkv, None, None, None, None, None, None, None, None, None, None, None
 

@@ -1264,3 +1264,29 @@ def test_rope_epilogue_model_bitwise():
         for a, b in zip(g1, g2):
             assert torch.equal(a, b)
     assert torch.equal(t1, t2)
+
+
+def test_attention_bwd_fused_rope_bitwise(monkeypatch):
+    """The RoPE backward fused into the attention backward's dQ / dK stores gives bitwise the
+    gradient of the separate inverse-rotation pass (both dQ forms: the dQ kernel and the atomic one)."""
+    from rag_tl_domainllm_optimizer_amd.ops import attention as att
+    from rag_tl_domainllm_optimizer_amd.ops import reference as ref
+
+    torch.manual_seed(3)
+    B, S, Hq, Hkv, D = 3, 150, 8, 2, 128
+    W = (Hq + 2 * Hkv) * D
+    cos, sin = ref.rope_tables(D, 4096, 10000.0, DEV)
+    start = torch.tensor([0, 37, 100], dtype=torch.int32, device=DEV)
+    pos = (torch.arange(S, device=DEV)[None, :] - start[:, None].long()).clamp(min=0).reshape(-1).to(torch.int32)
+    base = (torch.randn(B * S, W, device=DEV) * 0.5).to(torch.bfloat16)
+    do = (torch.randn(B * S, Hq * D, device=DEV) * 0.1).to(torch.bfloat16)
+    for atomic in (0, 1):
+        grads = []
+        for fused in (True, False):
+            monkeypatch.setattr(att, "ROPE_BWD_FUSED", fused)
+            with ops.tuning(attn_bwd_atomic_dq=atomic):
+                x = base.clone().requires_grad_(True)
+                o = ops.flash_attention_qkv(x * 1, B, S, Hq, Hkv, D, True, 0, kv_start=start, rope=(pos, cos, sin))
+                (g,) = torch.autograd.grad(o, x, do)
+            grads.append(g)
+        assert torch.equal(grads[0], grads[1]), atomic
