@@ -53,6 +53,17 @@ def variants(s):
     v["nolgkm"] = _macro_line(s, 'asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");', ";", 1)
     # both: no DMA waits and no closing barrier
     v["nowait_nobar_end"] = _sub_in(t, _fast_loop_span(t), "wait_granules<BN>(4);", "", 3)
+    # no operand traffic in the steady state: no LDS-DMA issue (the waits then return at once)
+    nodma = _sub_in(s, _fast_loop_span(s), "stage_fast(", "if (0) stage_fast(", 4)
+    v["nodma"] = nodma
+    # no fragment reads from LDS in the steady state (MFMAs on the registers' stale contents)
+    noread = _sub_in(s, _fast_loop_span(s), "read_a(buf, ", "if (0) read_a(buf, ", 2)
+    noread = _sub_in(noread, _fast_loop_span(noread), "read_b(buf, ", "if (0) read_b(buf, ", 2)
+    v["noread"] = noread
+    # barriers + MFMAs only (no DMA, no reads): the schedule's ceiling
+    both = _sub_in(nodma, _fast_loop_span(nodma), "read_a(buf, ", "if (0) read_a(buf, ", 2)
+    both = _sub_in(both, _fast_loop_span(both), "read_b(buf, ", "if (0) read_b(buf, ", 2)
+    v["mfma_bar"] = both
     return v
 
 
