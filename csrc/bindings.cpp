@@ -125,6 +125,7 @@ static const TuningField kTuningFields[] = {
     {"gemm_bn128_cost", nullptr, &rt::Tuning::gemm_bn128_cost},
     {"gemm_group_m", &rt::Tuning::gemm_group_m, nullptr},
     {"gemm_streamk", &rt::Tuning::gemm_streamk, nullptr},
+    {"gemm_ring", &rt::Tuning::gemm_ring, nullptr},
 };
 
 py::dict get_tuning() {

@@ -46,6 +46,9 @@ struct Tuning {
   // partial-tile hand-offs at the end of the launch costs more than the tail it removes;
   // profiles/r4/gemm_streamk_vs_planner.log)
   int gemm_streamk = 0;
+  // NT 256x256 tiles (no activation / SwiGLU / RoPE epilogue) on the 10-slot granule ring (160 KiB
+  // LDS, granules issued ~2 K-steps ahead) instead of two K-step buffers
+  int gemm_ring = 0;
 };
 
 }  // namespace rt

@@ -143,13 +143,19 @@ __device__ __forceinline__ void wait_granules(int n) {
 // each wave owns 2 B fragments instead of 4 (columns 64 (wc >> 1) + 16 (wc & 1) + 32 s): used for
 // M = 256 decode GEMMs (twice the workgroups, no split-K on the widest weights) and for the last,
 // partial wave of tiles of a large GEMM (rt_gemm_big_planned).
-template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false, bool F8 = false, bool SK = false>
+// RING (NT, BN = 256): the K-step buffers become a ring of 10 granule slots (160 KiB, the whole
+// LDS): every granule is issued two phases earlier than in the two-buffer schedule (7-8 phases =
+// ~2 K-steps ahead instead of 5-6), with 6 granules (96 KiB) in flight per CU instead of 4.
+template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false, bool F8 = false, bool SK = false,
+          bool RING = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   static_assert(BN == 256 || BN == 128, "BN");
+  static_assert(!RING || (LA == ROW && LB == ROW && BN == 256 && !F8 && !SK && !TRB), "RING: NT 256x256 bf16 operands");
   static_assert(!F8 || (LA == ROW && LB == ROW && OUT == O_BF16), "F8: NT with a bf16 output only");
   static_assert(!SK || (OUT == O_BF16 && BN == 256), "SK: 256x256 tiles with a bf16 epilogue");
   constexpr int NB = BN / 128;  // B fragments per wave and B sub-block; LDS-DMA instructions per B granule
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];  // the only __shared__ object
+  constexpr int NSLOT = 10;  // RING: granule slots
+  __shared__ __attribute__((aligned(16))) char smem[RING ? NSLOT * GRAN : 2 * BUF];  // the only __shared__ object
 
 
   const int tiles_m = (p.M + 255) / 256;
@@ -264,10 +270,21 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       off[g][j] = (g < 2 || j < NB) ? src_off(g, j, (g >> 1) ? p.ldb : p.lda, true, ki) : 0u;
       if (g < 2) kin[g][j] = ki;
     }
+  // RING: the slot of granule g (0 a0, 1 a1, 2 b0, 3 b1) of K-step u — granules are issued in the
+  // order a0 b0 b1 a1 of every step, slot = issue index mod NSLOT; inside a slot the instruction
+  // (wave w, j) of the granule owns rows 8 (2 w + j) .. + 7 (A: tile rows 128 (r >> 7) + 64 s +
+  // (r & 63); B: 64 (r >> 6) + 32 s + (r & 31)) with the same 16-B chunk swizzle
+  auto gidx = [](int g, int u) { return 4 * u + (g == 0 ? 0 : g == 2 ? 1 : g == 3 ? 2 : 3); };
+  auto rslot = [&](int g, int u) -> char* { return smem + (gidx(g, u) % NSLOT) * GRAN; };
+  // LDS destination of instruction j of granule g of K-step t (relative to the image for the
+  // two-buffer form: `img` + lds_dst)
+  auto gdst = [&](int g, int j, int t) -> char* {
+    if constexpr (RING) return rslot(g, t) + (wid * 2 + j) * 1024;
+    else return smem + (t & 1) * BUF + lds_dst(g, j);
+  };
   // one granule g of K-step t into buffer t & 1 (g is a literal at every call site)
   auto stage = [&](int g, int t) {
     const int op = g >> 1;
-    char* img = smem + (t & 1) * BUF;
     if (t < nk1) {
       const int k0 = t * 64;
       const long adv = ((op ? LB : LA) == ROW) ? (long)k0 : (long)k0 * (op ? p.ldb : p.lda);
@@ -279,11 +296,11 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
           // (MI355X_MICROARCH.md 'nt-weights')
 #pragma unroll
           for (int j = 0; j < NB; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 2);
+            __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, t), 16, 0, 2);
         } else {
 #pragma unroll
           for (int j = 0; j < (op ? NB : 2); ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, t), 16, 0, 0);
         }
       } else {  // ragged reduction tail: out-of-range k reads the zero page
 #pragma unroll
@@ -291,7 +308,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
           int ki;
           src_off(g, j, 1, true, ki);
           const bf16_t* src = k0 + ki < p.K ? base + off[g][j] : p.zpage + (lane & 7) * 8;
-          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)gdst(g, j, t), 16, 0, 0);
         }
       }
     } else {  // K-extension (LoRA): a few steps, offsets recomputed with the extension strides
@@ -304,7 +321,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
         int ki;
         const uint32_t o2 = src_off(g, j, ld2, false, ki);
         const bf16_t* src = k0 + ki < p.K2 ? base + o2 : p.zpage + (lane & 7) * 8;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(img + lds_dst(g, j)), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)gdst(g, j, t), 16, 0, 0);
       }
     }
   };
@@ -428,6 +445,91 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     GB_BARRIER();                                                                           \
   } while (0)
 
+  if constexpr (RING) {
+    if (t_begin < t_end) {
+      // fragments of the in-slot rows: A granule s holds tile rows 128 wr + 64 s + (0..63) at slot
+      // rows 64 wr + (0..63); B granule s holds tile rows 128 (wc >> 1) + 64 (wc & 1) + 32 s + (0..31)
+      // at slot rows 32 wc + (0..31)
+      auto read_a_r = [&](const char* g) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = rd_row(g, wr * 64 + i * 16 + frow);
+      };
+      auto read_b_r = [&](const char* g, i32x8 (&fb)[2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = rd_row(g, wc * 32 + j * 16 + frow);
+      };
+      // retire every granule issued before the n newest (2 LDS-DMA instructions per granule)
+      auto wait_newer = [](int n) {
+        switch (n < 0 ? 0 : n) {
+          case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+          case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+          case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+          case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+          case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+          case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+          default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        }
+      };
+      // prologue: steps t_begin and t_begin + 1 complete; retire a0 / b0 of t_begin
+      stage(0, t_begin); stage(2, t_begin); stage(3, t_begin); stage(1, t_begin);
+      int last = gidx(1, t_begin);  // issue index of the newest granule
+      if (t_begin + 1 < t_end) {
+        stage(0, t_begin + 1); stage(2, t_begin + 1); stage(3, t_begin + 1); stage(1, t_begin + 1);
+        last = gidx(1, t_begin + 1);
+      }
+      wait_newer(last - gidx(2, t_begin));
+      GB_BARRIER();
+      if (wr == 1) GB_BARRIER();
+      // steady state: granules of step t + 2 go out in phases 1-4 of step t; every phase retires
+      // the granule the next phase reads (6 newer granules stay in flight)
+      const int nk1f = p.K / 64;
+      const int t_fast = min(t_end, nk1f) - 2;
+      auto stage_fast_r = [&](int g, int u) {
+        const bf16_t* base = ((g >> 1) ? p.B : p.A) + (long)u * 64;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, u), 16, 0, 0);
+      };
+      int t = t_begin;
+      for (; t < t_fast; ++t) {
+        read_a_r(rslot(0, t));
+        read_b_r(rslot(2, t), fb0);
+        stage_fast_r(0, t + 2);
+        wait_newer(6);  // b1(t)
+        GB_MMA(0, 0, fb0);
+        read_b_r(rslot(3, t), fb1);
+        stage_fast_r(2, t + 2);
+        wait_newer(6);  // a1(t)
+        GB_MMA(0, 1, fb1);
+        read_a_r(rslot(1, t));
+        stage_fast_r(3, t + 2);
+        GB_MMA(1, 1, fb1);
+        stage_fast_r(1, t + 2);
+        wait_newer(6);  // a0 / b0 (t + 1)
+        GB_MMA(1, 0, fb0);
+      }
+      if (t > t_begin) last = gidx(1, t + 1);  // the fast loop issued every granule through step t + 1
+      for (; t < t_end; ++t) {
+        const bool n1 = t + 1 < t_end, n2 = t + 2 < t_end;
+        read_a_r(rslot(0, t));
+        read_b_r(rslot(2, t), fb0);
+        if (n2) { stage(0, t + 2); last = gidx(0, t + 2); }
+        wait_newer(last - gidx(3, t));
+        GB_MMA(0, 0, fb0);
+        read_b_r(rslot(3, t), fb1);
+        if (n2) { stage(2, t + 2); last = gidx(2, t + 2); }
+        wait_newer(last - gidx(1, t));
+        GB_MMA(0, 1, fb1);
+        read_a_r(rslot(1, t));
+        if (n2) { stage(3, t + 2); last = gidx(3, t + 2); }
+        GB_MMA(1, 1, fb1);
+        if (n2) { stage(1, t + 2); last = gidx(1, t + 2); }
+        if (n1) wait_newer(last - gidx(2, t + 1));
+        GB_MMA(1, 0, fb0);
+      }
+      if (wr == 0) GB_BARRIER();
+    }
+  } else {
   if (t_begin < t_end) {
     // prologue: step t_begin complete (a0, b0, b1, a1) + a0, b0 of step t_begin + 1; granules are
     // always issued in key order a0(u) b0(u) b1(u) a1(u) a0(u+1) b0(u+1) ... (see header)
@@ -496,6 +598,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     }
     if (wr == 0) GB_BARRIER();
   }
+  }  // RING / two-buffer
 #undef GB_MMA
 #undef GB_MMA_X
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1348,6 +1451,15 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
       case 100 + E_DSWIGLU: GB_LAUNCH(ROW, KMAJ, O_BF16, E_DSWIGLU, 128); break;
       default: return -4;
     }
+  } else if (key == 0 && tuning().gemm_ring) {  // NT bf16 on the 10-slot granule ring (tuning gemm_ring)
+#define GB_RING(E) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E, 256, false, false, false, true>), grid, block, 0, stream, p)
+    switch (act) {
+      case E_NONE: GB_RING(E_NONE); break;
+      case E_SWIGLU: GB_RING(E_SWIGLU); break;
+      case E_ROPE: GB_RING(E_ROPE); break;
+      default: return -4;
+    }
+#undef GB_RING
   } else if (key == 0) {  // NT, bf16 out: the activation is a template parameter (no runtime switch in the epilogue)
     switch (act) {
       case E_NONE: GB_LAUNCH(ROW, ROW, O_BF16, E_NONE, 256); break;

@@ -293,3 +293,38 @@ def test_streamk_repeat_and_side_stream():
         assert torch.equal(side, first)
     torch.cuda.synchronize()
     assert ops.native().streamk_dirty_tickets() == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 520, 200), (77, 136, 4096), (1000, 768, 1024),
+                                   (2900, 1024, 192), (512, 512, 128), (768, 1024, 4160)])
+def test_ring_nt_bitwise(M, N, K):
+    """The 10-slot granule ring (tuning gemm_ring) runs the same MFMAs on the same operands in the same
+    order as the two-buffer schedule: bitwise-equal outputs for 1-, 2- and many-step K, ragged K
+    tails, partial row / column tiles, the LoRA K-extension, a residual, SwiGLU and RoPE epilogues."""
+    from rag_tl_domainllm_optimizer_amd.ops import reference as ref
+
+    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
+    u, ub = _r(M, 64), _r(N, 64, s=0.1)
+    r = _r(M, N)
+    outs = []
+    for ring in (0, 1):
+        with ops.tuning(gemm_ring=ring):
+            y = ops.gemm_big(a, w, ops.ROW, ops.ROW, bn=256)
+            yl = ops.gemm_big(a, w, ops.ROW, ops.ROW, u, ub, bn=0)
+            yr = ops.gemm_big(a, w, ops.ROW, ops.ROW, residual=r, bn=256)
+            outs.append((y, yl, yr))
+    for x0, x1 in zip(*outs):
+        assert torch.equal(x0, x1)
+    _close(outs[1][0], a.float() @ w.float().t())
+    if N % 512 == 0:
+        res = []
+        cos, sin = ref.rope_tables(128, 2048, 10000.0, DEV)
+        pos = torch.randint(0, 2048, (M,), device=DEV, dtype=torch.int32)
+        for ring in (0, 1):
+            with ops.tuning(gemm_ring=ring):
+                pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+                f = ops.gemm_big(a, w, ops.ROW, ops.ROW, act=ops.ACT_SWIGLU, out2=pre, bn=256)
+                q = ops.native().gemm_rope(a, w, None, None, None, pos, cos, sin, N // 2, 128, bn=256)
+                res.append((f, pre, q))
+        for x0, x1 in zip(*res):
+            assert torch.equal(x0, x1)

@@ -4,13 +4,16 @@
 // one hipcc line and one run. Prints one line per shape: us per launch, PF/s, and a checksum of C
 // (variants that skip waits produce wrong C on purpose; the checksum shows which ones are exact).
 //
-//   ./gemm_exp [reps]
+//   ./gemm_exp [reps] [ring]      (ring: tuning gemm_ring = 1, the 10-slot granule ring)
 #include <hip/hip_runtime.h>
+
+#include "rt_tuning.h"
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
+#include <string>
 #include <vector>
 
 extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb,
@@ -49,6 +52,12 @@ struct Shape { const char* name; int la, lb, M, N, K, act, bn; };
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 10;
+  if (argc > 2 && std::string(argv[2]) == "ring") {
+    rt::Tuning t = *rt_tuning();
+    t.gemm_ring = 1;
+    rt_set_tuning(&t);
+    printf("tuning: gemm_ring = 1\n");
+  }
   const Shape shapes[] = {
       {"nt_1024tiles_8192x8192x4096", 0, 0, 8192, 8192, 4096, 0, 256},
       {"nt_qkv_9632x6144x4096", 0, 0, 9632, 6144, 4096, 0, 0},

@@ -16,9 +16,14 @@ SRC = os.path.join(ROOT, "csrc", "kernels", "gemm_big.hip")
 
 
 def _fast_loop_span(s):
-    a = s.index("for (; t < t_fast; ++t) {")
-    b = s.index("for (; t < t_end; ++t) {", a)
-    return a, b
+    """The two-buffer steady-state loop of gemm_big_kernel (the RING form has its own loop)."""
+    a = 0
+    while True:
+        a = s.index("for (; t < t_fast; ++t) {", a)
+        b = s.index("for (; t < t_end; ++t) {", a)
+        if "stage_fast(" in s[a:b]:
+            return a, b
+        a = b
 
 
 def _sub_in(s, span, old, new, count):

@@ -8,7 +8,14 @@ for v in base nowait nobar_end noprio nolgkm nowait_nobar_end nodma noread mfma_
   echo "== $v" >> gpurun_out/r4/g_gemm_exp.log
   timeout -k 10 120 tools/gemm_exp/bin/gemm_exp_$v 10 >> gpurun_out/r4/g_gemm_exp.log 2>&1 || { echo "variant $v failed"; tail -5 gpurun_out/r4/g_gemm_exp.log; exit 1; }
 done
+echo "== base ring" >> gpurun_out/r4/g_gemm_exp.log
+timeout -k 10 120 tools/gemm_exp/bin/gemm_exp_base 10 ring >> gpurun_out/r4/g_gemm_exp.log 2>&1 || { echo "ring run failed"; tail -5 gpurun_out/r4/g_gemm_exp.log; exit 1; }
+echo "== base again" >> gpurun_out/r4/g_gemm_exp.log
+timeout -k 10 120 tools/gemm_exp/bin/gemm_exp_base 10 >> gpurun_out/r4/g_gemm_exp.log 2>&1 || exit 1
 cat gpurun_out/r4/g_gemm_exp.log
+timeout -k 10 300 python -u -m pytest tests/test_gemm_big_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread \
+  -k "ring" > gpurun_out/r4/g_ring_tests.log 2>&1 || { echo "ring tests failed"; tail -40 gpurun_out/r4/g_ring_tests.log; exit 1; }
+tail -2 gpurun_out/r4/g_ring_tests.log
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread \
   -k "rope" > gpurun_out/r4/g_rope_tests.log 2>&1 || { echo "rope tests failed"; tail -40 gpurun_out/r4/g_rope_tests.log; exit 1; }
 tail -2 gpurun_out/r4/g_rope_tests.log
