@@ -150,7 +150,7 @@ template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false, bool F8 = 
           bool RING = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   static_assert(BN == 256 || BN == 128, "BN");
-  static_assert(!RING || (LA == ROW && LB == ROW && BN == 256 && !F8 && !SK && !TRB), "RING: NT 256x256 bf16 operands");
+  static_assert(!RING || (LA == ROW && BN == 256 && !F8 && !SK && !TRB), "RING: NT / NN 256x256 bf16 operands");
   static_assert(!F8 || (LA == ROW && LB == ROW && OUT == O_BF16), "F8: NT with a bf16 output only");
   static_assert(!SK || (OUT == O_BF16 && BN == 256), "SK: 256x256 tiles with a bf16 epilogue");
   constexpr int NB = BN / 128;  // B fragments per wave and B sub-block; LDS-DMA instructions per B granule
@@ -455,8 +455,21 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
         for (int i = 0; i < 4; ++i) fa[i] = rd_row(g, wr * 64 + i * 16 + frow);
       };
       auto read_b_r = [&](const char* g, i32x8 (&fb)[2]) {
+        if constexpr (LB == ROW) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = rd_row(g, wc * 32 + j * 16 + frow);
+          for (int j = 0; j < 2; ++j) fb[j] = rd_row(g, wc * 32 + j * 16 + frow);
+        } else {
+          // KMAJ: B granule s holds the [64 k][32 mn] blocks 2 m + s of the two-buffer image as
+          // slot blocks m; this wave's columns are block wc, fragment columns 0 / 16
+          auto kaddr = [&](int c0) -> uint32_t {
+            const int col = c0 + 4 * (frow & 3), kr = fq * 8 + (frow >> 2);
+            return lds_addr(g + wc * 4096 + kr * 64 + (((col >> 3) ^ kmaj_swz(kr)) << 4) + (col & 7) * 2);
+          };
+          rt_s16x4 v[8];
+          ds_tr16_frag2<256, 2048, 2304>(kaddr(0), kaddr(16), v);
+          fb[0] = frag_of(v);
+          fb[1] = frag_of(v + 4);
+        }
       };
       // retire every granule issued before the n newest (2 LDS-DMA instructions per granule)
       auto wait_newer = [](int n) {
@@ -1451,7 +1464,8 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
       case 100 + E_DSWIGLU: GB_LAUNCH(ROW, KMAJ, O_BF16, E_DSWIGLU, 128); break;
       default: return -4;
     }
-  } else if (key == 0 && tuning().gemm_ring) {  // NT bf16 on the 10-slot granule ring (tuning gemm_ring)
+  } else if (key == 0 && tuning().gemm_ring && (act == E_NONE || act == E_SWIGLU || act == E_ROPE)) {
+    // NT bf16 on the 10-slot granule ring (tuning gemm_ring)
 #define GB_RING(E) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E, 256, false, false, false, true>), grid, block, 0, stream, p)
     switch (act) {
       case E_NONE: GB_RING(E_NONE); break;
@@ -1460,6 +1474,11 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
       default: return -4;
     }
 #undef GB_RING
+  } else if (key == 10 && tuning().gemm_ring && (act == E_NONE || act == E_DSWIGLU)) {  // NN bf16 on the ring
+    if (act == E_NONE)
+      hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 256, false, false, false, true>), grid, block, 0, stream, p);
+    else
+      hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_DSWIGLU, 256, false, false, false, true>), grid, block, 0, stream, p);
   } else if (key == 0) {  // NT, bf16 out: the activation is a template parameter (no runtime switch in the epilogue)
     switch (act) {
       case E_NONE: GB_LAUNCH(ROW, ROW, O_BF16, E_NONE, 256); break;

@@ -328,3 +328,23 @@ def test_ring_nt_bitwise(M, N, K):
                 res.append((f, pre, q))
         for x0, x1 in zip(*res):
             assert torch.equal(x0, x1)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 200), (1000, 4096, 1536), (256, 256, 64), (777, 1024, 4160)])
+def test_ring_nn_bitwise(M, N, K):
+    """NN (dX = dY W) on the granule ring: bitwise the two-buffer schedule, with the LoRA
+    K-extension and the SwiGLU-backward epilogue."""
+    dy, w = _r(M, K), _r(K, N, s=1 / math.sqrt(K))
+    du, ap = _r(M, 64), _r(64, N, s=0.1)
+    pre = _r(M, 2 * N)
+    outs = []
+    for ring in (0, 1):
+        with ops.tuning(gemm_ring=ring):
+            a = ops.gemm_big(dy, w, ops.ROW, ops.KMAJ, bn=256)
+            b = ops.gemm_big(dy, w, ops.ROW, ops.KMAJ, du, ap, bn=0)
+            o = torch.empty(M, 2 * N, device=DEV, dtype=torch.bfloat16)
+            c = ops.gemm_big(dy, w, ops.ROW, ops.KMAJ, du, ap, act=ops.ACT_DSWIGLU, out=o, residual=pre, bn=256)
+            outs.append((a, b, c))
+    for x0, x1 in zip(*outs):
+        assert torch.equal(x0, x1)
+    _close(outs[1][0], dy.float() @ w.float())
