@@ -75,6 +75,9 @@ def main():
                          "packed forwards; RAGTL_PACK=0 for the padded comparison)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--tuning", default="",
+                    help="kernel-selection overrides for A/B runs, e.g. gemm_ring=1,gemm_group_m=8 (ops.set_tuning; "
+                         "recorded in the JSON line)")
     ap.add_argument("--torch-profile", default=None,
                     help="PPO mode: run one extra (untimed) step under torch.profiler after the warm-up and "
                          "write its per-op table, grouped by Python call site, to this path")
@@ -133,6 +136,15 @@ def main():
     di = parallel.init()
     dev = di.device
     assert di.world == args.gpus, (di.world, args.gpus)
+    tuning_over = {}
+    if args.tuning:
+        from rag_tl_domainllm_optimizer_amd import ops
+
+        for kv in args.tuning.split(","):
+            k, v = kv.split("=")
+            tuning_over[k.strip()] = float(v) if "." in v else int(v)
+        ops.set_tuning(**tuning_over)
+        log(f"[bench] tuning overrides: {tuning_over}")
     assert dev.type == "cuda", "bench.py needs a GPU"
     # one-shot collective probe (outside every timed region): the bus bandwidth a 168 MiB fp32
     # all-reduce (the LoRA gradient payload) reaches on this job's process group (RCCL over xGMI)
@@ -288,6 +300,7 @@ def main():
         "allreduce_bytes_per_step": comm_bytes,
         "rank_step_s": spread,
         "allreduce_probe": ar_probe,
+        **({"tuning": tuning_over} if tuning_over else {}),
     }
     if di.is_main:
         print(json.dumps(res), flush=True)
