@@ -94,7 +94,9 @@ class _FlashFn(torch.autograd.Function):
         qkv, o, lse, kv_start = ctx.saved_tensors
         B, S, Hq, Hkv, D, causal, window, scale, has_start = ctx.cfg
         do = do.contiguous()
-        dqkv = torch.zeros_like(qkv)
+        # the backward kernels write every row of dq / dk / dv (masked rows as zeros): no zero fill
+        # unless the rows carry columns beyond q | k | v
+        dqkv = torch.empty_like(qkv) if qkv.shape[1] == (Hq + 2 * Hkv) * D else torch.zeros_like(qkv)
         q = qkv[:, : Hq * D]
         k = qkv[:, Hq * D:(Hq + Hkv) * D]
         v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D]

@@ -1290,3 +1290,24 @@ def test_attention_bwd_fused_rope_bitwise(monkeypatch):
                 (g,) = torch.autograd.grad(o, x, do)
             grads.append(g)
         assert torch.equal(grads[0], grads[1]), atomic
+
+
+@pytest.mark.parametrize("atomic", [0, 1])
+def test_attention_bwd_writes_every_row(atomic):
+    """attn_bwd writes every row and column of dq / dk / dv (masked / left-padded rows as zeros), so
+    the autograd node hands out an uninitialised buffer: NaN-poisoned outputs come back NaN-free."""
+    torch.manual_seed(5)
+    B, S, Hq, Hkv, D = 2, 130, 8, 2, 128
+    W = (Hq + 2 * Hkv) * D
+    qkv = (torch.randn(B * S, W, device=DEV) * 0.5).to(torch.bfloat16)
+    start = torch.tensor([0, 77], dtype=torch.int32, device=DEV)
+    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    o, lse = ops.native().attn_fwd(q, k, v, B, S, S, Hq, Hkv, D, True, 0, 1 / math.sqrt(D), start, None, None, 0, True)
+    do = (torch.randn(B * S, Hq * D, device=DEV) * 0.1).to(torch.bfloat16)
+    d = torch.full((B * S, W), float("nan"), device=DEV, dtype=torch.bfloat16)
+    with ops.tuning(attn_bwd_atomic_dq=atomic):
+        ops.native().attn_bwd(q, k, v, o, do, lse, d[:, :Hq * D], d[:, Hq * D:(Hq + Hkv) * D], d[:, (Hq + Hkv) * D:],
+                              B, S, Hq, Hkv, D, True, 0, 1 / math.sqrt(D), start)
+    assert not torch.isnan(d).any()
+    # left-pad keys of row 1 get no gradient
+    assert float(d[S:S + 77, Hq * D:].float().abs().max()) == 0.0
