@@ -1311,3 +1311,26 @@ def test_attention_bwd_writes_every_row(atomic):
     assert not torch.isnan(d).any()
     # left-pad keys of row 1 get no gradient
     assert float(d[S:S + 77, Hq * D:].float().abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("top_k", [1, 7, 50, 300, 1024])
+def test_sampler_search_kth_exact(top_k):
+    """Radix select of the k-th largest bf16 logit: with distinct logits every draw is one of the
+    exact top-k tokens, over many offsets (top-p off); top-p on top: the draw lies in the nucleus of
+    the top-k set (survivors sorted in one wave when <= 64)."""
+    B = 32
+    g = torch.Generator(device="cpu").manual_seed(7)
+    # 2048 distinct bf16 values (8 binades x 128 mantissas, both signs): every logit is unique
+    pos = torch.tensor([2.0 ** e * (1 + m / 128) for e in range(-4, 4) for m in range(128)])
+    grid = torch.cat([pos, -pos])
+    V = grid.numel()
+    logits = torch.stack([grid[torch.randperm(V, generator=g)] for _ in range(B)]).to(torch.bfloat16).to(DEV)
+    assert int(torch.unique(logits[0].float()).numel()) == V
+    topi = logits.float().topk(top_k, dim=1).indices
+    for o in range(4):
+        off = torch.full((1,), o, dtype=torch.long, device=DEV)
+        tok, _ = ops.sample(logits, 1 / 0.7, top_k=top_k, top_p=1.0, seed=5, offset=off)
+        assert bool((topi == tok[:, None]).any(1).all())
+        tok, _ = ops.sample(logits, 1 / 0.7, top_k=top_k, top_p=0.6, seed=5, offset=off)
+        keep = ref.filter_logits(logits.float(), 1 / 0.7, top_k, 0.6)
+        assert keep.gather(1, tok[:, None]).float().mean().item() >= 0.97
