@@ -55,6 +55,16 @@ __device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// (x, y, z) of a workgroup after an XCD-aware remap of the linear dispatch id: the workgroups that
+// share a K / V head (the query tiles of the G query heads of one kv head, or a kv head's key
+// blocks) are consecutive in (x, y, z) order and land on ONE XCD's L2 instead of being dealt round
+// robin over all eight (each of which would fetch the K / V / Q tiles from memory again)
+__device__ __forceinline__ int3 attn_block_xyz() {
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int lin = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
+  return make_int3(lin % nx, (lin / nx) % ny, lin / (nx * ny));
+}
+
 struct AttnArgs {
   const bf16_t* q; long ldq;
   const bf16_t* k; long ldk;
@@ -99,9 +109,10 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const int3 bx = attn_block_xyz();
+  const int b = bx.z, h = bx.y;
   const int hk = h / (a.Hq / a.Hkv);
-  const int qblk0 = blockIdx.x * 128;
+  const int qblk0 = bx.x * 128;
   const int q0 = qblk0 + wid * 32;
 
   const int start = a.kv_start ? a.kv_start[b] : 0;
@@ -1827,8 +1838,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int b = blockIdx.z, hk = blockIdx.y;
-  const int kb0 = blockIdx.x * 64;
+  const int3 bx = attn_block_xyz();
+  const int b = bx.z, hk = bx.y;
+  const int kb0 = bx.x * 64;
   const int G = a.Hq / a.Hkv;
   const int start = a.kv_start ? a.kv_start[b] : 0;
   const int mykey = kb0 + wid * 16 + r16;  // this lane's key column
@@ -2048,9 +2060,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   char* Vs = smem + TILE_BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const int3 bx = attn_block_xyz();
+  const int b = bx.z, h = bx.y;
   const int hk = h / (a.Hq / a.Hkv);
-  const int qblk0 = blockIdx.x * 64;
+  const int qblk0 = bx.x * 64;
   const int q0 = qblk0 + wid * 16;
   const int start = a.kv_start ? a.kv_start[b] : 0;
   int kend = a.S;

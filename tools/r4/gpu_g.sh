@@ -4,6 +4,11 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r4
+for bs in "32 301" "64 150" "8 1204"; do
+  set -- $bs
+  timeout -k 10 120 python -u tools/attn_train_probe.py --B $1 --S $2 >> gpurun_out/r4/g_attn_probe.log 2>&1 || { echo "attn probe failed"; tail -5 gpurun_out/r4/g_attn_probe.log; exit 1; }
+done
+grep -v amdgpu.ids gpurun_out/r4/g_attn_probe.log
 L=gpurun_out/r4/g_gemm_exp.log
 for v in base nowait nobar_end noprio nolgkm nowait_nobar_end nodma noread mfma_bar; do
   echo "== $v" >> $L
