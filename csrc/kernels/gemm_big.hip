@@ -498,7 +498,8 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       const int nk1f = p.K / 64;
       const int t_fast = min(t_end, nk1f) - 2;
       auto stage_fast_r = [&](int g, int u) {
-        const bf16_t* base = ((g >> 1) ? p.B : p.A) + (long)u * 64;
+        // K-step advance: 64 elements along a ROW operand, 64 rows of a KMAJ one (NN weight)
+        const bf16_t* base = (g >> 1) ? p.B + (LB == ROW ? (long)u * 64 : (long)u * 64 * p.ldb) : p.A + (long)u * 64;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, u), 16, 0, 0);
