@@ -143,9 +143,9 @@ __device__ __forceinline__ void wait_granules(int n) {
 // each wave owns 2 B fragments instead of 4 (columns 64 (wc >> 1) + 16 (wc & 1) + 32 s): used for
 // M = 256 decode GEMMs (twice the workgroups, no split-K on the widest weights) and for the last,
 // partial wave of tiles of a large GEMM (rt_gemm_big_planned).
-// RING (NT, BN = 256): the K-step buffers become a ring of 10 granule slots (160 KiB, the whole
-// LDS): every granule is issued two phases earlier than in the two-buffer schedule (7-8 phases =
-// ~2 K-steps ahead instead of 5-6), with 6 granules (96 KiB) in flight per CU instead of 4.
+// RING (NT / NN, BN = 256): the K-step buffers become a ring of 10 granule slots (160 KiB, the
+// whole LDS), which lets a K-step run as TWO phases of 32 MFMAs (one barrier per 512 MFMA cycles
+// instead of per 256) with every granule still issued >= 4 sections ahead of its first read.
 template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false, bool F8 = false, bool SK = false,
           bool RING = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
@@ -483,20 +483,15 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
           default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
         }
       };
-      // prologue: steps t_begin and t_begin + 1 complete; retire a0 / b0 of t_begin
-      stage(0, t_begin); stage(2, t_begin); stage(3, t_begin); stage(1, t_begin);
-      int last = gidx(1, t_begin);  // issue index of the newest granule
-      if (t_begin + 1 < t_end) {
-        stage(0, t_begin + 1); stage(2, t_begin + 1); stage(3, t_begin + 1); stage(1, t_begin + 1);
-        last = gidx(1, t_begin + 1);
-      }
-      wait_newer(last - gidx(2, t_begin));
-      GB_BARRIER();
-      if (wr == 1) GB_BARRIER();
-      // steady state: granules of step t + 2 go out in phases 1-4 of step t; every phase retires
-      // the granule the next phase reads (6 newer granules stay in flight)
+      // Two phases of 32 MFMAs per K-step (a0 x [b0 | b1], a1 x [b0 | b1]): one barrier per 512
+      // MFMA cycles instead of per 256, so the other wave group's read section (16 / 8 fragment
+      // reads + LDS-DMA issue) hides under a section twice as long. Granules are issued in the
+      // order a0 b0 b1 a1 of every step (issue ordinal = ring index - 4 t_begin): R_A(t) issues b1, a1
+      // of t + 1 and a0 of t + 2, R_B(t) b0 of t + 2 — every slot is rewritten >= 3 sections after
+      // its previous granule's last read (both wave groups past it).
+      const int t0 = t_begin;
+      auto ordg = [&](int g, int u) { return gidx(g, u) - 4 * t0; };
       const int nk1f = p.K / 64;
-      const int t_fast = min(t_end, nk1f) - 2;
       auto stage_fast_r = [&](int g, int u) {
         // K-step advance: 64 elements along a ROW operand, 64 rows of a KMAJ one (NN weight)
         const bf16_t* base = (g >> 1) ? p.B + (LB == ROW ? (long)u * 64 : (long)u * 64 * p.ldb) : p.A + (long)u * 64;
@@ -504,43 +499,55 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
         for (int j = 0; j < 2; ++j)
           __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, u), 16, 0, 0);
       };
-      int t = t_begin;
-      for (; t < t_fast; ++t) {
+      auto stg = [&](int g, int u) {
+        if (u < nk1f) stage_fast_r(g, u);
+        else stage(g, u);
+      };
+#define GB_MMA2(SA)                                                                         \
+  do {                                                                                      \
+    GB_BARRIER();                                                                           \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    __builtin_amdgcn_s_setprio(1);                                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                           \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                         \
+        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                    \
+          acc[(SA) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                   \
+              half(fb0[j], kk), half(fa[i], kk), acc[(SA) * 4 + i][j], 0, 0, 0);            \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                           \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                         \
+        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                    \
+          acc[(SA) * 4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(               \
+              half(fb1[j], kk), half(fa[i], kk), acc[(SA) * 4 + i][2 + j], 0, 0, 0);        \
+    __builtin_amdgcn_s_setprio(0);                                                          \
+    GB_BARRIER();                                                                           \
+  } while (0)
+      // prologue: a0 b0 b1 a1 of t0, a0 b0 of t0 + 1; retire through b1 (t0)
+      stage(0, t0); stage(2, t0); stage(3, t0); stage(1, t0);
+      int last = ordg(1, t0);  // issue ordinal of the newest granule
+      if (t0 + 1 < t_end) {
+        stg(0, t0 + 1); stg(2, t0 + 1);
+        last = ordg(2, t0 + 1);
+      }
+      wait_newer(last - ordg(3, t0));
+      GB_BARRIER();
+      if (wr == 1) GB_BARRIER();
+      for (int t = t0; t < t_end; ++t) {
+        // R_A: a0, b0, b1 of t; stage b1, a1 (t + 1), a0 (t + 2); retire a1 (t)
         read_a_r(rslot(0, t));
         read_b_r(rslot(2, t), fb0);
-        stage_fast_r(0, t + 2);
-        wait_newer(6);  // b1(t)
-        GB_MMA(0, 0, fb0);
         read_b_r(rslot(3, t), fb1);
-        stage_fast_r(2, t + 2);
-        wait_newer(6);  // a1(t)
-        GB_MMA(0, 1, fb1);
+        if (t + 1 < t_end) { stg(3, t + 1); stg(1, t + 1); last = ordg(1, t + 1); }
+        if (t + 2 < t_end) { stg(0, t + 2); last = ordg(0, t + 2); }
+        wait_newer(last - ordg(1, t));
+        GB_MMA2(0);
+        // R_B: a1 of t; stage b0 (t + 2); retire a0 / b0 / b1 (t + 1)
         read_a_r(rslot(1, t));
-        stage_fast_r(3, t + 2);
-        GB_MMA(1, 1, fb1);
-        stage_fast_r(1, t + 2);
-        wait_newer(6);  // a0 / b0 (t + 1)
-        GB_MMA(1, 0, fb0);
+        if (t + 2 < t_end) { stg(2, t + 2); last = ordg(2, t + 2); }
+        if (t + 1 < t_end) wait_newer(last - ordg(3, t + 1));
+        GB_MMA2(1);
       }
-      if (t > t_begin) last = gidx(1, t + 1);  // the fast loop issued every granule through step t + 1
-      for (; t < t_end; ++t) {
-        const bool n1 = t + 1 < t_end, n2 = t + 2 < t_end;
-        read_a_r(rslot(0, t));
-        read_b_r(rslot(2, t), fb0);
-        if (n2) { stage(0, t + 2); last = gidx(0, t + 2); }
-        wait_newer(last - gidx(3, t));
-        GB_MMA(0, 0, fb0);
-        read_b_r(rslot(3, t), fb1);
-        if (n2) { stage(2, t + 2); last = gidx(2, t + 2); }
-        wait_newer(last - gidx(1, t));
-        GB_MMA(0, 1, fb1);
-        read_a_r(rslot(1, t));
-        if (n2) { stage(3, t + 2); last = gidx(3, t + 2); }
-        GB_MMA(1, 1, fb1);
-        if (n2) { stage(1, t + 2); last = gidx(1, t + 2); }
-        if (n1) wait_newer(last - gidx(2, t + 1));
-        GB_MMA(1, 0, fb0);
-      }
+#undef GB_MMA2
       if (wr == 0) GB_BARRIER();
     }
   } else {
