@@ -53,9 +53,9 @@ def variants(s):
     assert t != s
     v["nobar_end"] = t
     # no priority raise around the MFMA clusters
-    v["noprio"] = _macro_line(s, "__builtin_amdgcn_s_setprio(1);", ";", 1)
+    v["noprio"] = _macro_line(s, "__builtin_amdgcn_s_setprio(1);", ";", 2)
     # MFMAs start without waiting for the fragment reads (LDS latency exposure)
-    v["nolgkm"] = _macro_line(s, 'asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");', ";", 1)
+    v["nolgkm"] = _macro_line(s, 'asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");', ";", 2)
     # both: no DMA waits and no closing barrier
     v["nowait_nobar_end"] = _sub_in(t, _fast_loop_span(t), "wait_granules<BN>(4);", "", 3)
     # no operand traffic in the steady state: no LDS-DMA issue (the waits then return at once)
