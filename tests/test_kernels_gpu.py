@@ -1217,7 +1217,9 @@ def test_rope_epilogue_model_bitwise():
     from rag_tl_domainllm_optimizer_amd import models
     from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
     from rag_tl_domainllm_optimizer_amd.models import ValueHead
-    from rag_tl_domainllm_optimizer_amd.ops import linear as lin
+    import importlib
+
+    lin = importlib.import_module("rag_tl_domainllm_optimizer_amd.ops.linear")  # (ops.linear is a function)
     from rag_tl_domainllm_optimizer_amd.train.common import score_sequences
 
     cfg = models.resolve_preset("tiny-mistral")
@@ -1269,7 +1271,9 @@ def test_rope_epilogue_model_bitwise():
 def test_attention_bwd_fused_rope_bitwise(monkeypatch):
     """The RoPE backward fused into the attention backward's dQ / dK stores gives bitwise the
     gradient of the separate inverse-rotation pass (both dQ forms: the dQ kernel and the atomic one)."""
-    from rag_tl_domainllm_optimizer_amd.ops import attention as att
+    import importlib
+
+    att = importlib.import_module("rag_tl_domainllm_optimizer_amd.ops.attention")  # (ops.attention is a function)
     from rag_tl_domainllm_optimizer_amd.ops import reference as ref
 
     torch.manual_seed(3)
