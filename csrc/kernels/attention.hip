@@ -102,10 +102,13 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TILE_BYTES = 64 * D * 2;
   constexpr int OROW = D + 8;  // O staging row stride (elements)
-  constexpr int SMEM = (2 * TILE_BYTES > 128 * OROW * 2) ? 2 * TILE_BYTES : 128 * OROW * 2;
+  // D >= 64: two K / V tile buffers — the next tile is stored into the other buffer right after the
+  // current one is consumed, so each tile costs one barrier (64 KiB per workgroup at D = 128: 2 per
+  // CU). D = 32 (4 workgroups per CU, 128 registers) keeps one buffer and two barriers.
+  constexpr bool DB = D >= 64;
+  constexpr int NBUF = DB ? 2 : 1;
+  constexpr int SMEM = (2 * NBUF * TILE_BYTES > 128 * OROW * 2) ? 2 * NBUF * TILE_BYTES : 128 * OROW * 2;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  char* Ks = smem;
-  char* Vs = smem + TILE_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
@@ -164,23 +167,26 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
       vreg[r] = *(const u32x4*)(vb + kk * a.ldv);
     }
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](char* kd, char* vd) {
 #pragma unroll
     for (int r = 0; r < CPT; ++r) {
-      *(u32x4*)(Ks + k_off<D>(lkey + KSTEP * r, lc)) = kreg[r];
-      *(u32x4*)(Vs + v_off<D>(lkey + KSTEP * r, lc)) = vreg[r];
+      *(u32x4*)(kd + k_off<D>(lkey + KSTEP * r, lc)) = kreg[r];
+      *(u32x4*)(vd + v_off<D>(lkey + KSTEP * r, lc)) = vreg[r];
     }
   };
 
   if (kbeg < kend) {
     load_tile(kbeg);
-    store_tile();
+    store_tile(smem, smem + TILE_BYTES);
   }
   __syncthreads();
 
+  int cur = 0;  // K / V buffer of the tile being consumed (always 0 without double buffering)
   for (int kv0 = kbeg; kv0 < kend; kv0 += 64) {
     const bool has_next = kv0 + 64 < kend;
     if (has_next) load_tile(kv0 + 64);
+    char* Ks = DB ? smem + cur * (2 * TILE_BYTES) : smem;
+    char* Vs = DB ? Ks + TILE_BYTES : smem + TILE_BYTES;
 
     // ---- S^T[t][u] = K[16t..][:] · Q[u]^T ----
     f32x4 st[4][2];
@@ -276,9 +282,18 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
         for (int u = 0; u < 2; ++u) o[u][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[u], vf, o[u][c], 0, 0, 0);
       }
     }
-    __syncthreads();
-    if (has_next) store_tile();
-    __syncthreads();
+    if constexpr (DB) {
+      // the other buffer was last read in the previous iteration, which every wave has left (its
+      // closing barrier): store the next tile there and swap
+      char* kn = smem + (cur ^ 1) * (2 * TILE_BYTES);
+      if (has_next) store_tile(kn, kn + TILE_BYTES);
+      __syncthreads();
+      cur ^= 1;
+    } else {
+      __syncthreads();
+      if (has_next) store_tile(Ks, Vs);
+      __syncthreads();
+    }
   }
 
   // ---- finalize ----
