@@ -368,6 +368,19 @@ __global__ __launch_bounds__(256) void sample_bf16_lds_kernel(const bf16_t* __re
 // Philox stream (seed, row, offset * V + token) as sample_bf16_lds_kernel, so the same token wins.
 constexpr int TK_CAP = 2048;
 
+__device__ __forceinline__ int block_sum_int1024(int v, int* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) t += red[w];
+  return t;
+}
+
 __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
     const bf16_t* __restrict__ logits, long ld, int V, float inv_temp, int top_k, float top_p, uint64_t seed,
     const int64_t* __restrict__ offset_ptr, const uint8_t* __restrict__ row_active, long* __restrict__ out_tok,
@@ -377,7 +390,6 @@ __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
   __shared__ float lval[TK_CAP];   // tempered logit of each survivor
   __shared__ int redi[16];
   __shared__ float redf[16];
-  __shared__ unsigned long long hcnt[16][4];  // per-wave digit counts of the radix select (16 x 16-bit fields)
   __shared__ int cnt;
   const long row = blockIdx.x;
   const bf16_t* x = logits + row * ld;
@@ -438,56 +450,19 @@ __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
   int tok = AM;
   const bool active = row_active ? row_active[row] != 0 : true;
   if (active) {
-    // k-th largest key (= the largest t with count(keys >= t) >= K): radix select over 4-bit
-    // digits from the top — per digit one pass counting the keys of the current prefix range per
-    // digit value (16 x 16-bit counters packed in 4 registers; V < 65536), a wave reduction and
-    // one cross-wave sum: 4 passes / 8 barriers instead of a 16-step bitwise search
+    // k-th largest key: largest t with count(keys >= t) >= K, bit by bit from the top
     const int K = min(top_k, V);
     uint32_t prefix = 0;
-    int above = 0;  // keys above the current prefix range
-#pragma unroll 1
-    for (int d = 3; d >= 0; --d) {
-      const int sh = 4 * d;
-      const uint32_t hmask = (0xFFFFu << (sh + 4)) & 0xFFFFu;  // digits already fixed
-      const uint32_t want = prefix & hmask;
-      unsigned long long c4[4] = {0ull, 0ull, 0ull, 0ull};
+    for (int b = 15; b >= 0; --b) {
+      const uint32_t cand = prefix | (1u << b);
+      int c = 0;
       for (int cc = tid; cc < nv; cc += 1024) {
         const uint4 kv = *(const uint4*)(keys + cc * 8);
         const uint16_t* k8 = (const uint16_t*)&kv;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t k = k8[e];
-          const uint32_t dg = (k >> sh) & 15u;
-          const unsigned long long inc = ((k & hmask) == want) ? (1ull << (16 * (dg & 3u))) : 0ull;
-          c4[0] += (dg >> 2) == 0 ? inc : 0ull;
-          c4[1] += (dg >> 2) == 1 ? inc : 0ull;
-          c4[2] += (dg >> 2) == 2 ? inc : 0ull;
-          c4[3] += (dg >> 2) == 3 ? inc : 0ull;
-        }
+        for (int e = 0; e < 8; ++e) c += k8[e] >= cand;
       }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c4[q] += __shfl_xor(c4[q], o, 64);
-      if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) hcnt[wid][q] = c4[q];
-      }
-      __syncthreads();
-      unsigned long long t4[4] = {0ull, 0ull, 0ull, 0ull};
-#pragma unroll
-      for (int w2 = 0; w2 < 16; ++w2)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t4[q] += hcnt[w2][q];
-      int dsel = 0, cum = above;
-      for (int v = 15; v >= 0; --v) {
-        const int c = (int)((t4[v >> 2] >> (16 * (v & 3))) & 0xFFFFull);
-        if (cum + c >= K) { dsel = v; break; }
-        cum += c;
-      }
-      prefix |= (uint32_t)dsel << sh;
-      above = cum;
-      __syncthreads();  // hcnt is rewritten by the next pass
+      if (block_sum_int1024(c, redi) >= K) prefix = cand;
     }
     const uint32_t kth = prefix;
     // compact the survivors (ties at the threshold kept)
