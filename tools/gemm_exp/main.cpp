@@ -4,7 +4,7 @@
 // one hipcc line and one run. Prints one line per shape: us per launch, PF/s, and a checksum of C
 // (variants that skip waits produce wrong C on purpose; the checksum shows which ones are exact).
 //
-//   ./gemm_exp [reps] [ring]      (ring: tuning gemm_ring = 1, the 10-slot granule ring)
+//   ./gemm_exp [reps] [ring | w4]   (ring: tuning gemm_ring = 1; w4: NT shapes on the 4-wave kernel)
 #include <hip/hip_runtime.h>
 
 #include "rt_tuning.h"
@@ -52,6 +52,8 @@ struct Shape { const char* name; int la, lb, M, N, K, act, bn; };
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 10;
+  // w4: the NT shapes on the 4-wave 128 x 128-per-wave kernel (bn = 4), NN skipped
+  const bool w4 = argc > 2 && std::string(argv[2]) == "w4";
   if (argc > 2 && std::string(argv[2]) == "ring") {
     rt::Tuning t = *rt_tuning();
     t.gemm_ring = 1;
@@ -85,7 +87,11 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (const Shape& s : shapes) {
+  for (Shape s : shapes) {
+    if (w4) {
+      if (s.lb != 0) continue;
+      s.bn = 4;
+    }
     // NT: A [M, K], B [N, K]; NN: A [M, K] (= dY), B [K, N] (= W, KMAJ)
     const long lda = s.K, ldb = s.lb == 0 ? s.K : s.N;
     const int nout = s.act == 5 ? s.N / 2 : s.N;

@@ -69,6 +69,13 @@ def variants(s):
     both = _sub_in(nodma, _fast_loop_span(nodma), "read_a(buf, ", "if (0) read_a(buf, ", 2)
     both = _sub_in(both, _fast_loop_span(both), "read_b(buf, ", "if (0) read_b(buf, ", 2)
     v["mfma_bar"] = both
+    # 4-wave kernel (gemm_w4_kernel, bn = 4): its stage loop without the LDS-DMA waits
+    a = s.index("auto stage_body = [&](int s, bool fast) {")
+    b = s.index("---- epilogue ----", a)
+    body = s[a:b]
+    w = 'if (fast || more2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(G::DMA) : "memory");'
+    assert body.count(w) == 1, body.count(w)
+    v["w4nowait"] = s[:a] + body.replace(w, "if (0) {}") + s[b:]
     return v
 
 
