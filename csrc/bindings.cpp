@@ -110,6 +110,7 @@ static const TuningField kTuningFields[] = {
     {"decode_g1_nw", &rt::Tuning::decode_g1_nw, nullptr},
     {"decode_nk", &rt::Tuning::decode_nk, nullptr},
     {"attn_bwd_atomic_dq", &rt::Tuning::attn_bwd_atomic_dq, nullptr},
+    {"attn_fwd_w8", &rt::Tuning::attn_fwd_w8, nullptr},
     {"norm_slab_threads", &rt::Tuning::norm_slab_threads, nullptr},
     {"gemm_variant", &rt::Tuning::gemm_variant, nullptr},
     {"gemv16", &rt::Tuning::gemv16, nullptr},

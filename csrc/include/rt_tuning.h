@@ -21,6 +21,7 @@ struct Tuning {
   int decode_g1_nw = 2;       // waves per row of that kernel (1, 2, 4)
   int decode_nk = 4;          // VALU split kernel: keys per lane per chunk (2, 4, 8)
   int attn_bwd_atomic_dq = 0; // attention backward: fp32-atomic dQ (round-1 form)
+  int attn_fwd_w8 = 0;        // training / prefill attention forward: 8 waves x 16 query rows (else 4 x 32)
   // ---- norms (norm.hip) ----
   // threads per row of the split-K-slab norm (256, or 512 at H = 4096: 6.76 -> 6.56 us at batch 256,
   // profiles/r4/norm_slab_threads.log)

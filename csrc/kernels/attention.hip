@@ -97,8 +97,13 @@ __device__ __forceinline__ int v_off(int r, int c) {
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fwd_kernel(AttnArgs a) {
+// NU = 16-row query blocks per wave: 2 -> 4 waves of 32 rows (256 threads), 1 -> 8 waves of 16 rows
+// (512 threads, half the registers per wave: twice the waves per SIMD to hide the per-tile load /
+// barrier latency of short sequences). Either way a workgroup owns 128 query rows.
+template <int D, int NU = 2>
+__global__ __launch_bounds__(64 * 8 / NU, NU == 1 ? 4 : (D == 128 ? 2 : (D == 64 ? 3 : 4)))
+void attn_fwd_kernel(AttnArgs a) {
+  constexpr int NT = 64 * 8 / NU;  // threads per workgroup
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TILE_BYTES = 64 * D * 2;
   constexpr int OROW = D + 8;  // O staging row stride (elements)
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
   const int b = bx.z, h = bx.y;
   const int hk = h / (a.Hq / a.Hkv);
   const int qblk0 = bx.x * 128;
-  const int q0 = qblk0 + wid * 32;
+  const int q0 = qblk0 + wid * 16 * NU;
 
   const int start = a.kv_start ? a.kv_start[b] : 0;
   int kend = a.kv_len ? min(a.kv_len[b], a.Sk) : a.Sk;
@@ -127,9 +132,9 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
   kbeg = max(kbeg, 0) & ~63;
 
   // Q fragments (B operand of S^T = K·Q^T): lane holds Q[q0+16u+r16][32s + 8g .. +8]
-  bf16x8 qf[2][DS];
+  bf16x8 qf[NU][DS];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < NU; ++u) {
     const int qrow = min(q0 + 16 * u + r16, a.Sq - 1);
     const bf16_t* qp = a.q + ((long)b * a.Sq + qrow) * a.ldq + (long)h * D + 8 * g;
 #pragma unroll
@@ -139,22 +144,24 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
   // and drains vmcnt(0) before the first S MFMA of EVERY tile — which also waits out the next
   // tile's prefetch and serialises load latency with compute
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int s = 0; s < DS; ++s) asm volatile("" : "+v"(qf[u][s]));
 
-  f32x4 o[2][DT];
+  f32x4 o[NU][DT];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int c = 0; c < DT; ++c) o[u][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  float m[NU], l[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) { m[u] = -INFINITY; l[u] = 0.f; }
 
   // register prefetch of one K/V tile: 64 rows x NCH chunks each, spread over 256 threads. Thread
   // tid always owns chunk c = tid % NCH of keys tid / NCH + (256 / NCH) r. Native vector registers
   // (an array of the HIP uint4 struct went to scratch, serialising every prefetch load)
-  constexpr int CPT = 64 * NCH / 256;  // chunks per thread per tensor (4 for D=128)
-  constexpr int KSTEP = 256 / NCH;     // key stride between a thread's chunks
+  constexpr int CPT = 64 * NCH / NT;  // chunks per thread per tensor (4 for D=128, 256 threads)
+  constexpr int KSTEP = NT / NCH;     // key stride between a thread's chunks
   const int lc = tid % NCH, lkey = tid / NCH;
   const bf16_t* kb = a.k + (long)b * a.Sk * a.ldk + (long)hk * D + lc * 8;
   const bf16_t* vb = a.v + (long)b * a.Sk * a.ldv + (long)hk * D + lc * 8;
@@ -189,27 +196,27 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
     char* Vs = DB ? Ks + TILE_BYTES : smem + TILE_BYTES;
 
     // ---- S^T[t][u] = K[16t..][:] · Q[u]^T ----
-    f32x4 st[4][2];
+    f32x4 st[4][NU];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) st[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < NU; ++u) st[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int s = 0; s < DS; ++s) {
         const bf16x8 kf = *(const bf16x8*)(Ks + k_off<D>(16 * t + r16, 4 * s + g));
 #pragma unroll
-        for (int u = 0; u < 2; ++u) st[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[u][s], st[t][u], 0, 0, 0);
+        for (int u = 0; u < NU; ++u) st[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[u][s], st[t][u], 0, 0, 0);
       }
 
     // ---- scale + mask ----
     const bool full = kv0 >= start && kv0 + 63 < kend && (!a.causal || kv0 + 63 <= q0) &&
-                      (a.window <= 0 || (q0 + 31) - kv0 < a.window) && !a.rel_bias;
+                      (a.window <= 0 || (q0 + 16 * NU - 1) - kv0 < a.window) && !a.rel_bias;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < NU; ++u)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float x = st[t][u][i] * a.scale_log2;
@@ -227,9 +234,9 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
         }
 
     // ---- online softmax (per q column = lane r16 of each u) ----
-    float alpha[2];
+    float alpha[NU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NU; ++u) {
       float mx = -INFINITY;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -256,7 +263,7 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
     }
     // rescale O rows (row q = 16u + 4g + i lives in lane 4g+i's alpha)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NU; ++u)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float al = __shfl(alpha[u], 4 * g + i, 64);
@@ -267,9 +274,9 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
     // ---- O += P · V ----
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 pa[2];
+      bf16x8 pa[NU];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) pa[u] = pack_bf16x8(st[2 * ks][u], st[2 * ks + 1][u]);
+      for (int u = 0; u < NU; ++u) pa[u] = pack_bf16x8(st[2 * ks][u], st[2 * ks + 1][u]);
       const int qrow = lane >> 2 & 3, pcol = lane & 3;  // tr-read addressing within the 16-lane group
 #pragma unroll
       for (int c = 0; c < DT; ++c) {
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
         const s16x4 hi = ds_tr16(Vs + v_off<D>(key_a + 16, col >> 3) + ((col & 7) << 1));
         const bf16x8 vf = cat_tr(lo, hi);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) o[u][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[u], vf, o[u][c], 0, 0, 0);
+        for (int u = 0; u < NU; ++u) o[u][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[u], vf, o[u][c], 0, 0, 0);
       }
     }
     if constexpr (DB) {
@@ -299,7 +306,7 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
   // ---- finalize ----
   if (a.lse && g == 0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NU; ++u) {
       const int qq = q0 + 16 * u + r16;
       if (qq < a.Sq) {
         const float v = l[u] > 0.f ? (m[u] + __log2f(l[u])) * 0.69314718055994531f : INFINITY;
@@ -309,17 +316,17 @@ __global__ __launch_bounds__(256, D == 128 ? 2 : (D == 64 ? 3 : 4)) void attn_fw
   }
   bf16_t* Os = (bf16_t*)smem;  // [128][OROW]
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float lr = __shfl(l[u], 4 * g + i, 64);
       const float inv = lr > 0.f ? 1.f / lr : 0.f;
-      const int row = wid * 32 + 16 * u + 4 * g + i;
+      const int row = wid * 16 * NU + 16 * u + 4 * g + i;
 #pragma unroll
       for (int c = 0; c < DT; ++c) Os[row * OROW + 16 * c + r16] = f2bf(o[u][c][i] * inv);
     }
   __syncthreads();
-  for (int e = tid; e < 128 * NCH; e += 256) {
+  for (int e = tid; e < 128 * NCH; e += NT) {
     const int row = e / NCH, c = e % NCH;
     const int qq = qblk0 + row;
     if (qq < a.Sq)
@@ -2230,6 +2237,13 @@ extern "C" int rt_attn_fwd(const void* q, long ldq, const void* k, long ldk, con
   a.scale_log2 = scale * 1.4426950408889634f;
   if (B == 0 || Sq == 0) return 0;
   dim3 grid((Sq + 127) / 128, Hq, B), block(256);
+  // tuning attn_fwd_w8 = 1: 8 waves of 16 query rows per workgroup (D = 64 / 128)
+  if (tuning().attn_fwd_w8 && (D == 64 || D == 128)) {
+    if (D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<128, 1>), grid, dim3(512), 0, stream, a);
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
   switch (D) {
     case 32: hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, block, 0, stream, a); break;
     case 64: hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, block, 0, stream, a); break;

@@ -1338,3 +1338,22 @@ def test_sampler_search_kth_exact(top_k):
         tok, _ = ops.sample(logits, 1 / 0.7, top_k=top_k, top_p=0.6, seed=5, offset=off)
         keep = ref.filter_logits(logits.float(), 1 / 0.7, top_k, 0.6)
         assert keep.gather(1, tok[:, None]).float().mean().item() >= 0.97
+
+
+@pytest.mark.parametrize("D,Hq,Hkv,B,S,window", [(128, 8, 2, 3, 301, 0), (64, 4, 4, 2, 150, 0), (128, 4, 1, 2, 700, 256)])
+def test_attention_fwd_8wave_bitwise(D, Hq, Hkv, B, S, window):
+    """The 8-wave x 16-row attention forward (tuning attn_fwd_w8) computes every query row with the same
+    operations in the same order as the 4-wave x 32-row form: bitwise-equal O and LSE (causal, left
+    padding, sliding window)."""
+    torch.manual_seed(9)
+    W = (Hq + 2 * Hkv) * D
+    qkv = (torch.randn(B * S, W, device=DEV) * 0.5).to(torch.bfloat16)
+    start = torch.tensor([0, 37, 100][:B], dtype=torch.int32, device=DEV)
+    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    outs = []
+    for w8 in (0, 1):
+        with ops.tuning(attn_fwd_w8=w8):
+            outs.append(ops.native().attn_fwd(q, k, v, B, S, S, Hq, Hkv, D, True, window, 1 / math.sqrt(D), start,
+                                              None, None, 0, True))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -20,7 +20,10 @@ def main():
     ap.add_argument("--B", type=int, default=32)
     ap.add_argument("--S", type=int, default=301)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tuning", default="", help="kernel-selection overrides, e.g. attn_fwd_w8=1")
     a = ap.parse_args()
+    if a.tuning:
+        ops.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in a.tuning.split(","))})
     Hq, Hkv, D = 32, 8, 128
     x = torch.randn(a.B * a.S, (Hq + 2 * Hkv) * D, device="cuda", dtype=torch.bfloat16).requires_grad_(True)
     go = torch.randn(a.B * a.S, Hq * D, device="cuda", dtype=torch.bfloat16)
@@ -47,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         res[name] = s.elapsed_time(e) / a.iters * 1e3
     flops = 4 * a.B * Hq * a.S * a.S / 2 * D
-    print(f"B={a.B} S={a.S} atomic_dq={os.environ.get('RT_ATTN_BWD_ATOMIC_DQ', '0')}: fwd {res['fwd']:.1f} us "
+    print(f"B={a.B} S={a.S} tuning={a.tuning or 'default'}: fwd {res['fwd']:.1f} us "
           f"({flops / res['fwd'] / 1e6:.0f} TF/s), fwd+bwd {res['fwd+bwd']:.1f} us, bwd ~{res['fwd+bwd'] - res['fwd']:.1f} us",
           flush=True)
 
