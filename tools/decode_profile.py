@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="fp8 weight images (config 5)")
     ap.add_argument("--fp8-kv", action="store_true", help="fp8 K/V cache (config 5)")
     ap.add_argument("--depths", default="0", help="M<=16 GEMM weight-pipeline depths to A/B (0 = auto)")
+    ap.add_argument("--iters", type=int, default=3, help="generations per depth")
+    ap.add_argument("--no-graph", action="store_true", help="eager decode steps (counter collection)")
     a = ap.parse_args()
     from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
     from rag_tl_domainllm_optimizer_amd.models import build_model
@@ -34,13 +36,13 @@ def main():
     g = torch.Generator().manual_seed(0)
     prompts = [torch.randint(5, m.cfg.vocab_size, (a.prompt - (i % 7) * 3,), generator=g).tolist()
                for i in range(a.batch)]
-    gen = Generator(m, a.batch, a.prompt + a.new + 8, dev, kv_fp8=a.fp8_kv)
+    gen = Generator(m, a.batch, a.prompt + a.new + 8, dev, kv_fp8=a.fp8_kv, use_graph=not a.no_graph)
     sp = SamplingParams(max_new_tokens=a.new, temperature=0.7, top_k=50)
     from rag_tl_domainllm_optimizer_amd import ops
 
-    for it, depth in enumerate([int(d) for d in a.depths.split(",") for _ in range(3)]):
+    for it, depth in enumerate([int(d) for d in a.depths.split(",") for _ in range(a.iters)]):
         ops.native().set_tuning({"decode_depth": depth})
-        if it % 3 == 0:
+        if it % a.iters == 0 and gen.use_graph:
             gen.runner.reset()  # the launch choice is baked into the captured decode graph
         torch.cuda.synchronize()
         t0 = time.perf_counter()
