@@ -116,6 +116,7 @@ static const TuningField kTuningFields[] = {
     {"gemv16", &rt::Tuning::gemv16, nullptr},
     {"gemv16_maxm", &rt::Tuning::gemv16_maxm, nullptr},
     {"gemv16_depth", &rt::Tuning::gemv16_depth, nullptr},
+    {"gemv16_waves", &rt::Tuning::gemv16_waves, nullptr},
     {"decode_split", &rt::Tuning::decode_split, nullptr},
     {"decode_depth", &rt::Tuning::decode_depth, nullptr},
     {"m64_split", &rt::Tuning::m64_split, nullptr},

@@ -31,6 +31,7 @@ struct Tuning {
   int gemv16 = 2;             // 16-row no-split GEMV at M <= 16: 0 off, 1 narrow outputs, 2 all
   int gemv16_maxm = 16;       // rows handled by it (1..16)
   int gemv16_depth = 4;       // its weight-pipeline depth (4, 6, 8)
+  int gemv16_waves = 0;       // waves per 16-row group: 0 auto (8 on grids <= 1 workgroup per CU, else 4), 4, 8, 16
   int decode_split = 0;       // force split-K of the M <= 16 decode kernel
   int decode_depth = 0;       // force weight-pipeline depth (2 / 4) of the M <= 16 decode kernel
   int m64_split = 0;          // force split-K of the 16 < M <= 64 ring kernel

@@ -790,6 +790,18 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
   }
 }
 
+// CU count of the current device, queried once (thread-safe static initialisation)
+static int gemv_cus() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        c <= 0)
+      c = 256;
+    return c;
+  }();
+  return n;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Decode GEMV (M <= 16) without split-K: one workgroup per 16 weight rows of a tile-ordered image
 // ---------------------------------------------------------------------------------------------
@@ -812,17 +824,18 @@ __global__ __launch_bounds__(256, 2) void gemm_decode_kernel(GemmArgs p, float* 
 // k [128 c + 64 h + 16 g, +16), widened in registers to two bf16x8 fragments (k-slot permutation
 // shared with the X fragments, so the MFMA sums the same products). Half the bytes per chunk of k
 // of the bf16 image; per-column scales sb[col] applied in the epilogue.
-template <bool OUT_F32, int DEPTH, bool PAIR, bool W8 = false>
-__global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
+template <bool OUT_F32, int DEPTH, bool PAIR, bool W8 = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemv16_kernel(GemmArgs p) {
   // M <= 16 rows of X: the MFMA's 16 A rows (row frow of lane (frow, g); rows >= M repeat M - 1)
-  __shared__ float red[4][16][PAIR ? 33 : 17];
-  __shared__ float rsq[4][16];
+  // NW waves split the group's K chunks (NW = 8: twice the weight bytes in flight per workgroup)
+  __shared__ float red[NW][16][PAIR ? 33 : 17];
+  __shared__ float rsq[NW][16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int frow = lane & 15, g = lane >> 4;
   const int grp = blockIdx.x;  // 16-row group (of the gate rows when PAIR)
   constexpr int KC = W8 ? 128 : 64;  // k per 2-KiB chunk
   const int nc = p.K / KC;
-  const int c_begin = wid * nc / 4, c_end = (wid + 1) * nc / 4;
+  const int c_begin = wid * nc / NW, c_end = (wid + 1) * nc / NW;
   const char* wbase = (const char*)p.B + (long)grp * nc * 2048 + lane * 16;
   const char* ubase = PAIR ? (const char*)p.B + ((long)(p.N / 32) + grp) * nc * 2048 + lane * 16 : wbase;
   const bf16_t* xrow = p.A + (long)min(frow, p.M - 1) * p.lda + g * (W8 ? 16 : 8);
@@ -919,12 +932,19 @@ __global__ __launch_bounds__(256) void gemv16_kernel(GemmArgs p) {
   const int row = tid >> 4, ci = tid & 15;
   if (row < p.M) {
     const int col = grp * 16 + ci;
-    const float rs = normed ? rsqrtf((rsq[0][row] + rsq[1][row] + rsq[2][row] + rsq[3][row]) / (float)p.K + p.norm_eps)
-                            : 1.f;
-    float y = (red[0][row][ci] + red[1][row][ci] + red[2][row][ci] + red[3][row][ci]) * rs;
+    // wave partials summed in wave order (NW = 4: the association of the original four-term sum)
+    float ss = 0.f, yy = 0.f, uu = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      ss += rsq[w][row];
+      yy += red[w][row][ci];
+      if constexpr (PAIR) uu += red[w][row][16 + ci];
+    }
+    const float rs = normed ? rsqrtf(ss / (float)p.K + p.norm_eps) : 1.f;
+    float y = yy * rs;
     if constexpr (PAIR) {
       const int F = p.N / 2;
-      float up = (red[0][row][16 + ci] + red[1][row][16 + ci] + red[2][row][16 + ci] + red[3][row][16 + ci]) * rs;
+      float up = uu * rs;
       if constexpr (W8) { y *= p.sb[col]; up *= p.sb[F + col]; }
       if (p.bias) { y += bf2f(p.bias[col]); up += bf2f(p.bias[F + col]); }
       y = y / (1.f + __expf(-y)) * up;
@@ -1557,7 +1577,20 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
     const int gd = tuning().gemv16_depth;
 #define G16(D, P) if (out_f32) hipLaunchKernelGGL((gemv16_kernel<true, D, P>), grid, block, 0, stream, p); \
                   else hipLaunchKernelGGL((gemv16_kernel<false, D, P>), grid, block, 0, stream, p);
-    if (pair) { G16(4, true) } else if (gd == 6) { G16(6, false) } else if (gd == 8) { G16(8, false) } else { G16(4, false) }
+    // waves per row group: 0 = auto — 8 when the grid has at most one workgroup per CU (o / down:
+    // N / 16 = 256), so each CU keeps twice the weight bytes in flight; 4 on wider grids (qkv 384,
+    // lm_head 2000 workgroups), where 8 measured the same or slower. Batch-1 p50 0.383 -> 0.376 s
+    // (profiles/r4/gemv16_waves_ab.log)
+    int nw = tuning().gemv16_waves;
+    if (nw == 0) nw = (int)grid.x <= gemv_cus() ? 8 : 4;
+    if (pair) { G16(4, true) } else if (gd == 6) { G16(6, false) } else if (gd == 8) { G16(8, false) }
+    else if (nw == 8) {
+      if (out_f32) hipLaunchKernelGGL((gemv16_kernel<true, 4, false, false, 8>), grid, dim3(512), 0, stream, p);
+      else hipLaunchKernelGGL((gemv16_kernel<false, 4, false, false, 8>), grid, dim3(512), 0, stream, p);
+    } else if (nw == 16) {
+      if (out_f32) hipLaunchKernelGGL((gemv16_kernel<true, 4, false, false, 16>), grid, dim3(1024), 0, stream, p);
+      else hipLaunchKernelGGL((gemv16_kernel<false, 4, false, false, 16>), grid, dim3(1024), 0, stream, p);
+    } else { G16(4, false) }
 #undef G16
   } else if (M <= 64) {
     const int MT = (M + 15) / 16;

@@ -916,11 +916,18 @@ def test_ppo_advantages_kernel():
             _close(a.cpu(), b, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("waves", [0, 4, 8, 16])
 @pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (5, 4096, 14336), (16, 4096, 4096), (1, 28672, 4096),
                                    (3, 32000, 4096)])
-def test_gemv16_no_split_matches_fp32(M, N, K):
+def test_gemv16_no_split_matches_fp32(M, N, K, waves):
     """Decode GEMV without split-K (M <= 16 over the tile-ordered image, N / 16 >= 256 workgroups):
-    in-GEMM RMS norm, residual, SwiGLU pair vs an fp32 PyTorch reference."""
+    in-GEMM RMS norm, residual, SwiGLU pair vs an fp32 PyTorch reference; 4, 8 or 16 waves per row group
+    or the automatic choice (tuning gemv16_waves = 0; the SwiGLU pair form stays at 4)."""
+    with ops.tuning(gemv16_waves=waves):
+        _gemv16_case(M, N, K)
+
+
+def _gemv16_case(M, N, K):
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2
     lnw = (1 + 0.1 * torch.randn(K, device=DEV)).to(torch.bfloat16)
