@@ -76,7 +76,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--tuning", default="",
-                    help="kernel-selection overrides for A/B runs, e.g. gemm_ring=1,gemm_group_m=8 (ops.set_tuning; "
+                    help="kernel-selection overrides for A/B runs, e.g. gemm_group_m=8,gemm_bn128_cost=0.6 (ops.set_tuning; "
                          "recorded in the JSON line)")
     ap.add_argument("--rope-fusion", default="on", choices=["on", "off"],
                     help="A/B: RoPE in the qkv GEMM epilogue and in the attention backward stores (on) or the "
@@ -100,6 +100,11 @@ def main():
     ap.add_argument("--full-ft", action="store_true",
                     help="PPO over every policy weight (the reference's full-parameter mode: bf16 compute copies "
                          "+ fp32 master, frozen reference copy) instead of LoRA r=16")
+    ap.add_argument("--old-logp", default="rollout", choices=["rollout", "recompute"],
+                    help="PPO ratio's theta_old log-probs: the rollout sampler's (free) or a training-numerics "
+                         "forward of the policy beside the reference forward (exact ratio 1 at theta_old)")
+    ap.add_argument("--merged-rollout", default="on", choices=["on", "off"],
+                    help="rollouts on the merged bf16 W + s*B*A copy (on) or on the unmerged LoRA K-extension (off)")
     args = ap.parse_args()
     if args.mode == "pipeline" and args.model == "mistral-7b" and "--model" not in sys.argv:
         args.model = "llama2-13b"
@@ -191,9 +196,14 @@ def main():
     # ---- PPO trainer ----
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
                    lora_r=16, lora_alpha=32.0, seed=0, rollout_chunks=1, overlap_reward=True,
-                   full_finetune=args.full_ft,
+                   full_finetune=args.full_ft, merged_lora_rollout=args.merged_rollout == "on",
+                   old_logp=args.old_logp,
                    **({"ref_minibatch_size": args.ref_minibatch} if args.ref_minibatch else {}))
     trainer = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
+    if args.merged_rollout == "off":
+        tuning_over["merged_rollout"] = "off"
+    if args.old_logp != "rollout":
+        tuning_over["old_logp"] = args.old_logp
     if args.no_graph:
         trainer.gen.use_graph = False
     rng = random.Random(100 + di.rank)
@@ -257,6 +267,7 @@ def main():
     t0 = time.perf_counter()
     tokens = 0.0
     phase = {}
+    gaps, egaps, clipf = [], [], []
     for s in range(args.steps):
         # inside the timed region: sample the rank's queries, encode them and search the IVF index
         # (retrieval), then the full PPO iteration on the retrieved RAG prompts
@@ -265,7 +276,11 @@ def main():
         for k, v in m.items():
             if k.startswith("time/"):
                 phase[k] = phase.get(k, 0.0) + v
-        log(f"[bench] step {s}: {m['step_time_s']:.2f}s loss={m['total_loss']:.4f} kl_ref={m['kl_ref']:.4f}")
+        gaps.append(m["behaviour_logp_gap"])
+        egaps.append(m["rollout_engine_logp_gap"])
+        clipf.append(m["clipfrac_first_mb"])
+        log(f"[bench] step {s}: {m['step_time_s']:.2f}s loss={m['total_loss']:.4f} kl_ref={m['kl_ref']:.4f} "
+            f"logp_gap={m['behaviour_logp_gap']:.2e} clipfrac0={m['clipfrac_first_mb']:.4f}")
     torch.cuda.synchronize()
     t_local = time.perf_counter() - t0  # this rank's wall time, before waiting for the others
     parallel.barrier()
@@ -304,12 +319,22 @@ def main():
                                           "stage_mean_s": v["stage_mean_s"]} for k, v in ctx_lat.items()}}
            if ctx_lat else {}),
         "phase_s_per_step": {k: v / args.steps for k, v in phase.items()},
+        # behaviour / target policy gap: mean |logp_update - old_logp| (nats per response token) and
+        # the clip fraction of the first minibatch of each step, scored at theta = theta_old
+        "behaviour_logp_gap": sum(gaps) / len(gaps),
+        # the rollout engine's sampler log-probs vs the training forward at theta_old (equal to the
+        # above unless --old-logp recompute)
+        "rollout_engine_logp_gap": sum(egaps) / len(egaps),
+        "old_logp_source": args.old_logp,
+        "clipfrac_first_mb": sum(clipf) / len(clipf),
         # data-parallel diagnostics: gradient payload each rank hands to RCCL per step, and the
         # spread of the per-rank step times (before the closing barrier) in seconds
         "allreduce_bytes_per_step": comm_bytes,
         "rank_step_s": spread,
         "allreduce_probe": ar_probe,
         **({"tuning": tuning_over} if tuning_over else {}),
+        **({"zero_state_bytes_per_rank": trainer.opt.state_bytes()} if getattr(trainer.opt, "sharded", False)
+           else {}),
     }
     if di.is_main:
         print(json.dumps(res), flush=True)

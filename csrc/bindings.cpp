@@ -24,7 +24,7 @@ int rt_shuffle_decode_weight(const void*, void*, long, long, hipStream_t);
 int rt_shuffle_decode_weight_fp8(const void*, void*, long, long, hipStream_t);
 int rt_gemm_big(int, int, const void*, long, const void*, long, const void*, long, const void*, long, int,
                 const void*, void*, long, void*, long, const void*, long, int, int, int, int, int, int, const void*,
-                int, float*, unsigned*, hipStream_t);
+                int, hipStream_t);
 int rt_gemm_small(int, int, const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
                   int, hipStream_t);
 int rt_gemm_big_rope(const void*, long, const void*, long, const void*, long, const void*, long, int, const void*,
@@ -56,9 +56,6 @@ int rt_attn_decode_fused(const void*, long, void*, void*, int, const int*, const
 int rt_attn_decode_fused_ps(int, int);
 int rt_kv_store_fp8(const void*, long, void*, void*, float*, float*, int, int, int, int, int, int, int, hipStream_t);
 int rt_attn_decode_mfma_ok(int, int, int, int, int);
-int rt_attn_o_fused(const void*, void*, void*, int, const int*, const int*, const int*, const int*, const float*,
-                    const float*, float, int, float*, int, int, int, int, int, float, const void*, long, const void*,
-                    void*, int, unsigned*, int*, long long*, hipStream_t);
 int rt_attn_bwd(const void*, long, const void*, long, const void*, long, const void*, long, const void*, long,
                 const float*, float*, float*, void*, long, void*, long, void*, long, const int*, int, int, int, int,
                 int, int, int, float, const int*, const float*, const float*, hipStream_t);
@@ -101,16 +98,7 @@ struct TuningField {
   float rt::Tuning::*f;
 };
 static const TuningField kTuningFields[] = {
-    {"decode_mw", &rt::Tuning::decode_mw, nullptr},
     {"decode_mw_kpp", &rt::Tuning::decode_mw_kpp, nullptr},
-    {"decode_mfma", &rt::Tuning::decode_mfma, nullptr},
-    {"attn_kv_nt", &rt::Tuning::attn_kv_nt, nullptr},
-    {"decode_fp8_mw", &rt::Tuning::decode_fp8_mw, nullptr},
-    {"decode_g1_valu", &rt::Tuning::decode_g1_valu, nullptr},
-    {"decode_g1_nw", &rt::Tuning::decode_g1_nw, nullptr},
-    {"decode_nk", &rt::Tuning::decode_nk, nullptr},
-    {"attn_bwd_atomic_dq", &rt::Tuning::attn_bwd_atomic_dq, nullptr},
-    {"attn_fwd_w8", &rt::Tuning::attn_fwd_w8, nullptr},
     {"norm_slab_threads", &rt::Tuning::norm_slab_threads, nullptr},
     {"gemm_variant", &rt::Tuning::gemm_variant, nullptr},
     {"gemv16", &rt::Tuning::gemv16, nullptr},
@@ -121,13 +109,8 @@ static const TuningField kTuningFields[] = {
     {"decode_depth", &rt::Tuning::decode_depth, nullptr},
     {"m64_split", &rt::Tuning::m64_split, nullptr},
     {"wide_split", &rt::Tuning::wide_split, nullptr},
-    {"gemm_fp8_256", &rt::Tuning::gemm_fp8_256, nullptr},
-    {"gemm_tr_builtin", &rt::Tuning::gemm_tr_builtin, nullptr},
-    {"gemm_b_nt", &rt::Tuning::gemm_b_nt, nullptr},
     {"gemm_bn128_cost", nullptr, &rt::Tuning::gemm_bn128_cost},
     {"gemm_group_m", &rt::Tuning::gemm_group_m, nullptr},
-    {"gemm_streamk", &rt::Tuning::gemm_streamk, nullptr},
-    {"gemm_ring", &rt::Tuning::gemm_ring, nullptr},
 };
 
 py::dict get_tuning() {
@@ -201,40 +184,6 @@ DecodeWS& decode_ws(const Tensor& like, hipStream_t st) {
   w->tickets = at::zeros({RT_SPLITK_TICKETS}, like.options().dtype(at::kInt));
   (*map)[key] = w;
   return *w;
-}
-
-// Stream-K workspace of the token-parallel GEMM (gemm_big.hip): 2 partial slots of 256 x 256 fp32
-// per unit (one unit per CU) and one self-resetting ticket per tail tile, one per (device, stream)
-// like DecodeWS. Allocated on first use (128 MiB at 256 CUs), never freed. An empty struct when the
-// stream-K tail is switched off (tuning gemm_streamk = 0).
-struct StreamKWS {
-  Tensor part, tickets;
-};
-static std::mutex g_skws_mu;
-static std::unordered_map<uint64_t, StreamKWS*>* g_skws_map = new std::unordered_map<uint64_t, StreamKWS*>();
-const StreamKWS& streamk_ws(const Tensor& like, hipStream_t st) {
-  static const StreamKWS none;
-  if (!rt::tuning().gemm_streamk) return none;
-  std::lock_guard<std::mutex> g(g_skws_mu);
-  const uint64_t key = (uint64_t)like.get_device() << 56 ^ (uint64_t)(uintptr_t)st;
-  auto it = g_skws_map->find(key);
-  if (it != g_skws_map->end()) return *it->second;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  auto* w = new StreamKWS();
-  w->part = at::empty({(int64_t)2 * cus * 256 * 256}, like.options().dtype(at::kFloat));
-  w->tickets = at::zeros({(int64_t)cus}, like.options().dtype(at::kInt));
-  (*g_skws_map)[key] = w;
-  return *w;
-}
-
-// diagnostics: stream-K tickets not back at zero (every launch leaves them at zero)
-int64_t streamk_dirty_tickets() {
-  std::lock_guard<std::mutex> g(g_skws_mu);
-  int64_t n = 0;
-  for (auto& kv : *g_skws_map) n += (kv.second->tickets.ne(0)).sum().item<int64_t>();
-  return n;
 }
 
 // diagnostics: per decode workspace, the number of arrival tickets not back at zero (every
@@ -401,7 +350,7 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
                          ext ? a2->stride(0) : 0, ext ? b2->data_ptr() : nullptr, ext ? b2->stride(0) : 0, (int)K2,
                          nullptr, out->data_ptr(), out->stride(0), nullptr, 0, residual->data_ptr(),
                          residual->stride(0), (int)M, (int)N, (int)K, 6, 0, 1, zero_page(a).data_ptr(), (int)bn,
-                         nullptr, nullptr, cur_stream()),
+                         cur_stream()),
              "gemm_big(act 6)");
     return *out;
   }
@@ -456,14 +405,12 @@ Tensor gemm_big(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layo
     CHECK_ALIGN16(*residual);
   }
   if (M == 0 || N == 0) return c;
-  const StreamKWS& sk = streamk_ws(a, cur_stream());
   check_rc(rt_gemm_big((int)layout_a, (int)layout_b, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                        ext ? a2->data_ptr() : nullptr, ext ? a2->stride(0) : 0, ext ? b2->data_ptr() : nullptr,
                        ext ? b2->stride(0) : 0, (int)K2, opt_ptr(bias), c.data_ptr(), c.stride(0), c2, ldc2,
                        has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, (int)M,
                        (int)N, (int)K, (int)act, (int)out_mode, (int)nsplit, zero_page(a).data_ptr(), (int)bn,
-                       sk.part.defined() ? sk.part.data_ptr<float>() : nullptr,
-                       sk.tickets.defined() ? (unsigned*)sk.tickets.data_ptr<int>() : nullptr, cur_stream()),
+                       cur_stream()),
            "gemm_big");
   return c;
 }
@@ -578,7 +525,7 @@ Tensor gemm_splitk(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor slab
   if (M == 0) return c;
   check_rc(rt_gemm_big(0, 0, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), nullptr, 0, nullptr, 0, 0,
                        nullptr, slabs.data_ptr(), N, nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, 0, 3,
-                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, nullptr, nullptr, cur_stream()),
+                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, cur_stream()),
            "gemm_splitk");
   check_rc(rt_gemm_splitk_reduce(slabs.data_ptr<float>(), (int)nsplit, (int)M, (int)N, opt_ptr(bias), (int)act,
                                  has_r ? residual->data_ptr() : nullptr, has_r ? residual->stride(0) : 0, c.data_ptr(),
@@ -747,7 +694,7 @@ void gemm_splitk_raw(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor sl
   if (M == 0) return;
   check_rc(rt_gemm_big(0, 0, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), nullptr, 0, nullptr, 0, 0,
                        nullptr, slabs.data_ptr(), N, nullptr, 0, nullptr, 0, (int)M, (int)N, (int)K, 0, 3,
-                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, nullptr, nullptr, cur_stream()),
+                       (int)nsplit, zero_page(a).data_ptr(), (int)bn, cur_stream()),
            "gemm_splitk_raw");
 }
 
@@ -1001,45 +948,6 @@ bool attn_decode_fused_slabs(const Tensor& slabs, int64_t nsplit, Tensor kc, Ten
   return true;
 }
 
-// batch-1 decode step of one layer: attention (RoPE + append + split-K) and o_proj + residual in
-// one launch. Returns false (nothing launched) when the shape is not supported.
-bool attn_o_fused(const Tensor& qkv, Tensor kc, Tensor vc, const Tensor& slot, const Tensor& attn_len,
-                  const optional<Tensor>& kv_start, const optional<Tensor>& pos, const optional<Tensor>& cos,
-                  const optional<Tensor>& sin, double sign, int64_t window, double scale, int64_t Hq, Tensor part,
-                  int64_t PS, const Tensor& w, const Tensor& residual, Tensor out, Tensor sync, Tensor err,
-                  const optional<Tensor>& stamps) {
-  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_BF16(kc); CHECK_BF16(vc); CHECK_I32(slot); CHECK_I32(attn_len);
-  CHECK_F32(part); CHECK_BF16(w); CHECK_ROWS(w); CHECK_ALIGN16(w); CHECK_BF16(residual); CHECK_BF16(out);
-  CHECK_I32(sync); CHECK_I32(err);
-  TORCH_CHECK(kc.dim() == 4 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes(),
-              "attn_o_fused: cache layout");
-  const int64_t B = kc.size(0), Hkv = kc.size(1), Smax = kc.size(2), D = kc.size(3);
-  if (B != 1 || qkv.size(0) != 1) return false;
-  const int64_t NP = (Smax + PS - 1) / PS, G = Hq / Hkv, H = w.size(0);
-  TORCH_CHECK(G * Hkv == Hq && w.size(1) == Hq * D, "attn_o_fused: o_proj weight must be [H, Hq*D]");
-  TORCH_CHECK(qkv.is_contiguous() && qkv.size(1) >= (Hq + 2 * Hkv) * D, "attn_o_fused: qkv row");
-  TORCH_CHECK(residual.is_contiguous() && residual.numel() == H && out.is_contiguous() && out.numel() == H,
-              "attn_o_fused: residual / out must be contiguous [1, H]");
-  TORCH_CHECK(D == 128 && part.numel() >= Hkv * NP * G * 132, "attn_o_fused: partial workspace too small");
-  TORCH_CHECK(sync.numel() >= 2 && err.numel() >= 1, "attn_o_fused: sync workspace");
-  const bool rot = cos.has_value() && cos->defined();
-  if (rot) {
-    CHECK_F32(*cos); CHECK_F32(*sin); CHECK_I32(*pos);
-    TORCH_CHECK(cos->size(-1) == D / 2 && cos->is_contiguous() && sin->is_contiguous(), "attn_o_fused: tables");
-  }
-  if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
-  const int rc = rt_attn_o_fused(qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), (int)Smax, slot.data_ptr<int>(),
-                                 attn_len.data_ptr<int>(), (const int*)opt_ptr(kv_start),
-                                 rot ? pos->data_ptr<int>() : nullptr, rot ? cos->data_ptr<float>() : nullptr,
-                                 rot ? sin->data_ptr<float>() : nullptr, (float)sign, (int)window,
-                                 part.data_ptr<float>(), (int)NP, (int)PS, (int)Hq, (int)Hkv, (int)D, (float)scale,
-                                 w.data_ptr(), w.stride(0), residual.data_ptr(), out.data_ptr(), (int)H,
-                                 (unsigned*)sync.data_ptr<int>(), err.data_ptr<int>(),
-                                 stamps.has_value() && stamps->defined() ? (long long*)stamps->data_ptr() : nullptr,
-                                 cur_stream());
-  return rc == 0;
-}
-
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout, const Tensor& lse,
               Tensor dq, Tensor dk, Tensor dv, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D, bool causal,
               int64_t window, double scale, const optional<Tensor>& kv_start, const optional<Tensor>& rope_pos,
@@ -1058,13 +966,10 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
   }
   CHECK_ROWS(dq); CHECK_ROWS(dk); CHECK_ROWS(dv); CHECK_F32(lse);
   auto delta = at::empty({B, Hq, S}, q.options().dtype(at::kFloat));
-  // fp32 dQ accumulator: only the atomic form (tuning attn_bwd_atomic_dq) uses it
-  const bool atomic_dq = rt::tuning().attn_bwd_atomic_dq != 0;
-  auto dq32 = at::empty({atomic_dq ? B * S : 1, atomic_dq ? Hq * D : 1}, q.options().dtype(at::kFloat));
   if (kv_start.has_value() && kv_start->defined()) CHECK_I32(*kv_start);
   check_rc(rt_attn_bwd(q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0), o.data_ptr(),
                        o.stride(0), dout.data_ptr(), dout.stride(0), lse.data_ptr<float>(), delta.data_ptr<float>(),
-                       dq32.data_ptr<float>(), dq.data_ptr(), dq.stride(0), dk.data_ptr(), dk.stride(0),
+                       nullptr, dq.data_ptr(), dq.stride(0), dk.data_ptr(), dk.stride(0),
                        dv.data_ptr(), dv.stride(0), (const int*)opt_ptr(kv_start), (int)B, (int)S, (int)Hq, (int)Hkv,
                        (int)D, causal ? 1 : 0, (int)window, (float)scale,
                        rope ? rope_pos->data_ptr<int>() : nullptr, rope ? rope_cos->data_ptr<float>() : nullptr,
@@ -1131,6 +1036,39 @@ void adamw(Tensor p, const Tensor& g, Tensor m, Tensor v, const optional<Tensor>
                     (float)max_norm, partials.data_ptr<float>(), nparts, norm_out.data_ptr<float>(),
                     skipped.data_ptr<int>(), cur_stream()),
            "adamw");
+}
+
+// The update half of adamw() on partials another pass (and a cross-rank sum) already produced:
+// ZeRO-1 (parallel.zero) reduces each rank's shard sum of squares over the ranks before any rank
+// applies its clipped update.
+void adamw_apply(Tensor p, const Tensor& g, Tensor m, Tensor v, const optional<Tensor>& pbf, double lr, double b1,
+                 double b2, double eps, double wd, int64_t step, double max_norm, const Tensor& partials,
+                 Tensor norm_out, Tensor skipped) {
+  CHECK_CUDA(p); CHECK_F32(p); CHECK_F32(g); CHECK_F32(m); CHECK_F32(v); CHECK_F32(partials);
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous() &&
+              partials.is_contiguous(), "adamw_apply: buffers must be contiguous");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adamw_apply: sizes");
+  CHECK_ALIGN16(p); CHECK_ALIGN16(g); CHECK_ALIGN16(m); CHECK_ALIGN16(v);
+  if (pbf.has_value() && pbf->defined()) {
+    CHECK_BF16(*pbf);
+    TORCH_CHECK(pbf->numel() == n && pbf->is_contiguous(), "adamw_apply: bf16 copy");
+  }
+  TORCH_CHECK(partials.numel() >= 1 && partials.numel() <= 1024, "adamw_apply: partials");
+  check_rc(rt_adamw(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                    (void*)opt_ptr(pbf), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step,
+                    (float)max_norm, partials.data_ptr<float>(), (int)partials.numel(), norm_out.data_ptr<float>(),
+                    skipped.data_ptr<int>(), cur_stream()),
+           "adamw_apply");
+}
+
+// per-workgroup partial sums of g^2 into partials (one launch of partials.numel() workgroups)
+void grad_sumsq(const Tensor& g, Tensor partials) {
+  CHECK_CUDA(g); CHECK_F32(g); CHECK_F32(partials);
+  TORCH_CHECK(g.is_contiguous() && partials.is_contiguous(), "grad_sumsq: contiguous");
+  check_rc(rt_grad_sumsq(g.data_ptr<float>(), g.numel(), partials.data_ptr<float>(), (int)partials.numel(),
+                         cur_stream()),
+           "grad_sumsq");
 }
 
 // Batched scaled fp32 -> bf16 scatter (LoRA compute images): tab int64 [n, 7] on the device =
@@ -1324,7 +1262,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("shuffle_decode_weight_fp8", &shuffle_decode_weight_fp8,
         "fp8 W [N, K] -> tile-ordered W8A16 decode image (gemm_fp8 w_shuffled=True)", py::arg("q"),
         py::arg("out") = py::none());
-  m.def("streamk_dirty_tickets", &streamk_dirty_tickets, "stream-K tickets not back at zero (diagnostic)");
   m.def("get_tuning", &get_tuning, "the launchers' kernel-selection knobs (rt::Tuning) as a dict");
   m.def("set_tuning", &set_tuning, "update rt::Tuning fields from a dict (unknown keys raise)");
   m.def("attn_decode_fused", &attn_decode_fused, "RoPE + KV append + split-K decode attention + combine",
@@ -1383,15 +1320,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scatter_scaled", &scatter_scaled, "batched scaled fp32 -> bf16 strided scatter (LoRA images)");
   m.def("adamw_mixed", &adamw_mixed);
   m.def("grad_norm", &grad_norm);
+  m.def("adamw_apply", &adamw_apply);
+  m.def("grad_sumsq", &grad_sumsq);
   m.def("pool_norm", &pool_norm);
   m.def("topk", &topk);
   m.def("ivf_scan", &ivf_scan);
   m.def("segment_mean", &segment_mean, "k-means update: per-segment mean of sorted rows (+ L2 normalise)");
-  m.def("attn_o_fused", &attn_o_fused, "batch-1 decode: attention + o_proj + residual in one launch (false = unsupported)",
-        py::arg("qkv"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("attn_len"), py::arg("kv_start"),
-        py::arg("pos"), py::arg("cos"), py::arg("sin"), py::arg("sign"), py::arg("window"), py::arg("scale"),
-        py::arg("Hq"), py::arg("part"), py::arg("PS"), py::arg("w"), py::arg("residual"), py::arg("out"),
-        py::arg("sync"), py::arg("err"), py::arg("stamps") = py::none());
   m.def("gae", &gae);
   m.def("ppo_advantages", &ppo_advantages, "token KL rewards + GAE + advantage whitening in one launch");
   m.def("ppo_loss", &ppo_loss, "fused token-level PPO loss: {stats[6], dlp, dv, dent}");

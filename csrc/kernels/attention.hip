@@ -1509,277 +1509,6 @@ __global__ __launch_bounds__(64 * W) void attn_decode_mfma_kernel(DecodeFusedArg
 }
 
 // ---------------------------------------------------------------------------------------------
-// Batch-1 decode: attention + o_proj + residual in ONE launch (RAG answer latency path)
-// ---------------------------------------------------------------------------------------------
-// At batch 1 the attention of a layer is latency-bound (~1.8 MB of K/V over 8 kv-heads) and the
-// o_proj GEMV that follows is a 33.5 MB weight stream whose own launch ramp and split-K hand-off
-// cost about as much as its bytes. Here the two share a launch and overlap:
-//   * every block owns AO_ROWS output rows of o_proj and DMAs its [AO_ROWS x Hq*D] weight slice
-//     into LDS (global_load_lds, 128 KiB) while the attention runs;
-//   * blocks 0 .. Hkv*NP-1 (the first dispatched) are also attention producers: each computes the
-//     (m, l, sum p*v) partial of one key partition of one kv-head (RoPE + cache append as in
-//     attn_decode_fused_kernel), publishes it with write-through stores and bumps sync[0];
-//   * every block waits for sync[0] == Hkv*NP (bounded spin; a give-up sets *err), merges the
-//     partials of its 16 elements of the attention vector per thread, and dots them with its LDS
-//     weight rows; row sums + residual -> the new residual stream (bf16).
-// Producers are the lowest block ids and wait on nothing before publishing, so the grid cannot
-// deadlock even when not every block is resident. The last block to finish re-arms sync[].
-constexpr int AO_ROWS = 16;  // o_proj rows per block: 16 x 4096 bf16 = 128 KiB of LDS
-constexpr int AO_K = 4096;   // Hq * D of the supported models (Llama-2-7B / Mistral-7B shapes)
-constexpr int AO_PSTR = 128 + 4;  // floats per (partition, q-head) partial record: o[D] | m | l | pad
-
-struct AttnOArgs {
-  DecodeFusedArgs at;          // attention of the single sequence; at.part = [Hkv, NP, G, D + 2]
-  const bf16_t* w; long ldw;   // o_proj weight [H, Hq * D] (row stride ldw)
-  const bf16_t* res;           // residual row [H]
-  bf16_t* out;                 // new residual row [H] = o_proj(attn) + res
-  int H;
-  unsigned* sync;              // [2] producers published / blocks done; zero between launches
-  int* err;                    // set to 1 if a block gave up waiting
-  long long* stamps;           // debug: [NB][8] s_memrealtime stamps per phase, or null
-};
-
-template <int D, int G, int NK>
-__global__ __launch_bounds__(256) void attn_o_fused_kernel(AttnOArgs args) {
-  __shared__ __attribute__((aligned(16))) char wsl[AO_ROWS * AO_K * 2];  // o_proj weight slice
-  __shared__ float red[4 * G * D];
-  __shared__ float wst[4][G][2];
-  __shared__ float rsum[4][AO_ROWS];
-  constexpr int LPK = D / 8, KPW = 64 / LPK, CH = 4 * KPW * NK;
-  constexpr int EPT = AO_K / 256;  // attention-vector elements per thread in the GEMV (16)
-  const DecodeFusedArgs& a = args.at;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int bid = blockIdx.x, NB = gridDim.x;
-  const int P = a.Hkv * a.NP;
-  const int r0 = bid * AO_ROWS;
-
-  auto issue_w = [&]() {  // each wave instruction moves 1 KiB (64 lanes x 16 B) of one weight row
-    constexpr int PER_ROW = AO_K / 512;
-    for (int i = wid; i < AO_ROWS * PER_ROW; i += 4) {
-      const int r = i / PER_ROW, c = i % PER_ROW;
-      const bf16_t* src = args.w + (long)(r0 + r) * args.ldw + c * 512 + lane * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(wsl + ((long)r * AO_K + c * 512) * 2), 16, 0,
-                                       0);
-    }
-  };
-#define AO_STAMP(k) \
-  if (args.stamps && tid == 0) args.stamps[(long)bid * 8 + (k)] = (long long)__builtin_amdgcn_s_memrealtime()
-  AO_STAMP(0);
-  // consumers start their weight stream at once; producers only after publishing (hipcc drains
-  // an outstanding LDS-DMA at the first use of a plain load, which would put the 128 KiB ahead of
-  // the attention everyone waits for)
-  if (bid >= P) issue_w();
-
-  if (bid < P) {
-    const int hk = bid % a.Hkv, part = bid / a.Hkv;
-    const int len = a.attn_len[0];
-    const int s_new = a.slot[0];
-    RT_ASSERT(len <= a.Smax && s_new >= 0 && s_new < a.Smax);
-    int kbeg = a.kv_start ? a.kv_start[0] : 0;
-    if (a.window > 0) kbeg = max(kbeg, len - a.window);
-    const int p0 = max(part * a.PS, kbeg), p1 = min((part + 1) * a.PS, len);
-    const int sub = lane / LPK, dl = lane % LPK;
-    const bool active = p0 < p1;
-    float mrow[G], lrow[G];
-    if (active) {
-      const int p = a.pos ? a.pos[0] : 0;
-      const bf16_t* kbase = a.kc + (long)hk * a.Smax * D;
-      const bf16_t* vbase = a.vc + (long)hk * a.Smax * D;
-      KVChunk<D, NK> ca, cb;
-      load_chunk<D, NK>(ca, kbase, vbase, p0, p1, wid, sub, dl, a.kv_nt);
-      float qv[G][8];
-#pragma unroll
-      for (int gg = 0; gg < G; ++gg) rope_chunk<D>(a.qkv + (long)(hk * G + gg) * D, dl, a, p, qv[gg]);
-      const bool has_new = s_new >= p0 && s_new < p1;
-      uint4 kp = make_uint4(0, 0, 0, 0), vp = kp;
-      if (has_new) {
-        float kn[8], vn[8];
-        rope_chunk<D>(a.qkv + (long)(a.Hq + hk) * D, dl, a, p, kn);
-        unpack8(*(const uint4*)(a.qkv + (long)(a.Hq + a.Hkv + hk) * D + dl * 8), vn);
-        kp = pack8(kn);
-        vp = pack8(vn);
-        if (wid == 0 && sub == 0) {
-          *(uint4*)(a.kc + ((long)hk * a.Smax + s_new) * D + dl * 8) = kp;
-          *(uint4*)(a.vc + ((long)hk * a.Smax + s_new) * D + dl * 8) = vp;
-        }
-      }
-      float m[G], l[G], acc[G][8];
-#pragma unroll
-      for (int gg = 0; gg < G; ++gg) {
-        m[gg] = -INFINITY;
-        l[gg] = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[gg][e] = 0.f;
-      }
-      for (int c0 = p0; c0 < p1; c0 += 2 * CH) {
-        if (c0 + CH < p1) load_chunk<D, NK>(cb, kbase, vbase, c0 + CH, p1, wid, sub, dl, a.kv_nt);
-        consume_chunk<D, G, NK>(ca, c0, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
-        if (c0 + CH < p1) {
-          if (c0 + 2 * CH < p1) load_chunk<D, NK>(ca, kbase, vbase, c0 + 2 * CH, p1, wid, sub, dl, a.kv_nt);
-          consume_chunk<D, G, NK>(cb, c0 + CH, p1, s_new, has_new, kp, vp, qv, m, l, acc, wid, sub, a.scale_log2);
-        }
-      }
-#pragma unroll
-      for (int gg = 0; gg < G; ++gg) {
-        float mw = m[gg];
-#pragma unroll
-        for (int off = LPK; off < 64; off <<= 1) mw = fmaxf(mw, __shfl_xor(mw, off, 64));
-        const float r = (m[gg] == -INFINITY) ? 0.f : exp2f(m[gg] - mw);
-        l[gg] *= r;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[gg][e] *= r;
-        m[gg] = mw;
-        if (lane == 0) wst[wid][gg][0] = mw;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int gg = 0; gg < G; ++gg) {
-        mrow[gg] = fmaxf(fmaxf(wst[0][gg][0], wst[1][gg][0]), fmaxf(wst[2][gg][0], wst[3][gg][0]));
-        const float r = (m[gg] == -INFINITY) ? 0.f : exp2f(m[gg] - mrow[gg]);
-        float lsum = l[gg] * r;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[gg][e] *= r;
-#pragma unroll
-        for (int off = LPK; off < 64; off <<= 1) {
-          lsum += __shfl_xor(lsum, off, 64);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[gg][e] += __shfl_xor(acc[gg][e], off, 64);
-        }
-        if (sub == 0) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) red[(wid * G + gg) * D + dl * 8 + e] = acc[gg][e];
-        }
-        if (lane == 0) wst[wid][gg][1] = lsum;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int gg = 0; gg < G; ++gg) lrow[gg] = wst[0][gg][1] + wst[1][gg][1] + wst[2][gg][1] + wst[3][gg][1];
-    }
-    // publish this partition's partial with write-through stores, then count it. Record stride
-    // AO_PSTR (16-B aligned) so consumers read it with vector loads.
-    float* outp = a.part + ((long)hk * a.NP + part) * G * AO_PSTR;
-    for (int e = tid; e < G * D; e += 256) {
-      const int gg = e / D, d = e % D;
-      if (active)
-        __hip_atomic_store(outp + gg * AO_PSTR + d,
-                           red[(0 * G + gg) * D + d] + red[(1 * G + gg) * D + d] + red[(2 * G + gg) * D + d] +
-                               red[(3 * G + gg) * D + d],
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid < G) {
-      __hip_atomic_store(outp + tid * AO_PSTR + D, active ? mrow[tid] : -INFINITY, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(outp + tid * AO_PSTR + D + 1, active ? lrow[tid] : 0.f, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(args.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    AO_STAMP(1);
-    issue_w();
-  }
-
-  // ---- wait for every partial (bounded: a stuck grid reports instead of hanging the GPU) ----
-  if (tid == 0) {
-    unsigned n = 0;
-    while (__hip_atomic_load(args.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)P) {
-      if (++n > (1u << 22)) {
-        __hip_atomic_store(args.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    // acquire once for the block, then plain vector loads of the partials (the guide's counter
-    // hand-off: stale lines of the previous replay's partials must not be read from this XCD's L2)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  AO_STAMP(2);
-
-  // ---- merge: thread t owns attention-vector elements [t*EPT, t*EPT + EPT) (one head's slice) ----
-  float ov[EPT];
-  {
-    const int e0 = tid * EPT;
-    const int h = e0 / D, d0 = e0 % D, hk = h / G, gg = h % G;
-    const float* base = a.part + (long)hk * a.NP * G * AO_PSTR;
-    float M = -INFINITY, L = 0.f;
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) ov[i] = 0.f;
-    // partitions in groups of 4 with every load of a group issued before any is used (clamped
-    // index, no per-load branch): one round trip per group instead of one per partition
-    for (int q0 = 0; q0 < a.NP; q0 += 4) {
-      float mq[4], lq[4], oq[4][EPT];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float* r = base + (min(q0 + j, a.NP - 1) * G + gg) * AO_PSTR;
-        const float2 ml = *(const float2*)(r + D);
-        mq[j] = ml.x;
-        lq[j] = ml.y;
-#pragma unroll
-        for (int i = 0; i < EPT; i += 4) {
-          const float4 v4 = *(const float4*)(r + d0 + i);
-          oq[j][i] = v4.x; oq[j][i + 1] = v4.y; oq[j][i + 2] = v4.z; oq[j][i + 3] = v4.w;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        // empty partition (o[] never written) or clamped duplicate: skip
-        if (q0 + j >= a.NP || mq[j] == -INFINITY) continue;
-        const float Mn = fmaxf(M, mq[j]);
-        const float s0 = exp2f(M - Mn), s1 = exp2f(mq[j] - Mn);
-        L = L * s0 + lq[j] * s1;
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) ov[i] = ov[i] * s0 + oq[j][i] * s1;
-        M = Mn;
-      }
-    }
-    // the unfused path hands o_proj a bf16 attention vector: round identically
-#pragma unroll
-    for (int i = 0; i < EPT; ++i) ov[i] = bf2f(f2bf(L > 0.f ? ov[i] / L : 0.f));
-  }
-
-  AO_STAMP(3);
-  // ---- o_proj rows of this block from the LDS weight slice ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  AO_STAMP(4);
-  float ps[AO_ROWS];
-#pragma unroll
-  for (int r = 0; r < AO_ROWS; ++r) {
-    const char* wr = wsl + ((long)r * AO_K + tid * EPT) * 2;
-    float w8[8], w8b[8];
-    unpack8(*(const uint4*)wr, w8);
-    unpack8(*(const uint4*)(wr + 16), w8b);
-    float s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s2 += w8[i] * ov[i] + w8b[i] * ov[8 + i];
-    ps[r] = s2;
-  }
-#pragma unroll
-  for (int r = 0; r < AO_ROWS; ++r)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) ps[r] += __shfl_xor(ps[r], off, 64);
-  if (lane == 0)
-#pragma unroll
-    for (int r = 0; r < AO_ROWS; ++r) rsum[wid][r] = ps[r];
-  __syncthreads();
-  if (tid < AO_ROWS) {
-    const int row = r0 + tid;
-    const float y = rsum[0][tid] + rsum[1][tid] + rsum[2][tid] + rsum[3][tid] + bf2f(args.res[row]);
-    args.out[row] = f2bf(y);
-  }
-  AO_STAMP(5);
-  // ---- re-arm: the last block out resets both counters (every block is past its wait) ----
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(args.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == (unsigned)(NB - 1)) {
-      __hip_atomic_store(args.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(args.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------------------
 struct AttnBwdArgs {
@@ -1845,7 +1574,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
   }
 }
 
-template <int D, bool DQ>
+template <int D>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TB = 64 * D * 2;
@@ -1990,48 +1719,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
           dvv[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oT, pb, dvv[c], 0, 0, 0);
           dk[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qT, db, dk[c], 0, 0, 0);
         }
-      }
-      if constexpr (!DQ) continue;  // dQ comes from attn_bwd_dq_kernel (no atomics)
-      // dS -> LDS as [q][key] (16-B chunk swizzle by q&7) for dQ = dS · K
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ql = 16 * u + 4 * g + i;
-          const int kl = wid * 16 + r16;
-          const int off = ql * 128 + (((kl >> 3) ^ (ql & 7)) << 4) + ((kl & 7) << 1);
-          *(bf16_t*)(dSs + off) = f2bf(dp[u][i]);
-        }
-      __syncthreads();
-      // dQ[q][d] for this wave's 16 q rows over the block's 64 keys
-      {
-        f32x4 dq[DT];
-#pragma unroll
-        for (int c = 0; c < DT; ++c) dq[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int ql = wid * 16 + r16;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int ch = 4 * ks + g;
-          const bf16x8 da = *(const bf16x8*)(dSs + ql * 128 + ((ch ^ (ql & 7)) << 4));
-#pragma unroll
-          for (int c = 0; c < DT; ++c) {
-            // B[k = key slot][col = d]: keys 32ks + 8g + j -> tr read rows 32ks + 8g + {0..3}, {4..7}
-            const int rowa = 32 * ks + 8 * g + qrow;
-            const int col = 16 * c + 4 * pcol;
-            const bf16x8 kb = cat_tr(ds_tr16(Ks + v_off<D>(rowa, col >> 3) + ((col & 7) << 1)),
-                                     ds_tr16(Ks + v_off<D>(rowa + 4, col >> 3) + ((col & 7) << 1)));
-            dq[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, kb, dq[c], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < DT; ++c)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int qq = qt + wid * 16 + 4 * g + i;
-            if (qq < a.S)
-              atomicAdd(a.dq + ((long)b * a.S + qq) * ((long)a.Hq * D) + (long)h * D + 16 * c + r16,
-                        dq[c][i] * a.scale);
-          }
       }
     }
   }
@@ -2214,14 +1901,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   }
 }
 
-__global__ void f32_to_bf16_strided_kernel(const float* __restrict__ x, long n_cols, bf16_t* __restrict__ y, long ldy,
-                                           long rows) {
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= rows * n_cols) return;
-  const long r = gid / n_cols, c = gid % n_cols;
-  y[r * ldy + c] = f2bf(x[gid]);
-}
-
 }  // namespace rt
 
 using namespace rt;
@@ -2237,13 +1916,6 @@ extern "C" int rt_attn_fwd(const void* q, long ldq, const void* k, long ldk, con
   a.scale_log2 = scale * 1.4426950408889634f;
   if (B == 0 || Sq == 0) return 0;
   dim3 grid((Sq + 127) / 128, Hq, B), block(256);
-  // tuning attn_fwd_w8 = 1: 8 waves of 16 query rows per workgroup (D = 64 / 128)
-  if (tuning().attn_fwd_w8 && (D == 64 || D == 128)) {
-    if (D == 64) hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<128, 1>), grid, dim3(512), 0, stream, a);
-    RT_LAUNCH_CHECK();
-    return 0;
-  }
   switch (D) {
     case 32: hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, block, 0, stream, a); break;
     case 64: hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, block, 0, stream, a); break;
@@ -2289,7 +1961,7 @@ extern "C" int rt_attn_decode_fused_ps(int D, int nk) { return 4 * (64 / (D / 8)
 constexpr int DEC_MW = 8;
 static bool rt_attn_decode_mw_ok(int B, int Hq, int Hkv, int D, int Smax) {
   const int G = Hkv ? Hq / Hkv : 0;
-  return tuning().decode_mw && D == 128 && (long)B * Hkv < 256 && (G == 1 || G == 2 || G == 4 || G == 8);
+  return D == 128 && (long)B * Hkv < 256 && (G == 1 || G == 2 || G == 4 || G == 8);
 }
 static int rt_attn_decode_mw_np(int Smax, int np_ws) {
   const int kpp = std::max(16, tuning().decode_mw_kpp);
@@ -2298,7 +1970,7 @@ static int rt_attn_decode_mw_np(int Smax, int np_ws) {
 }
 extern "C" int rt_attn_decode_mfma_ok(int B, int Hq, int Hkv, int D, int NP) {
   const int G = Hkv ? Hq / Hkv : 0;
-  return tuning().decode_mfma && NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
+  return NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
 }
 
 // Prompt K / V (rows [b * S + s] of the rotated qkv) -> fp8 cache slots [0, S): one 16-lane group
@@ -2361,9 +2033,8 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
   a.B = B; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
   a.qkv_slabs = qkv_slabs; a.qkv_nsplit = qkv_slabs ? qkv_nsplit : 0; a.qkv_sstride = (long)B * ldq;
   // K/V cache bytes are read once per decode step: non-temporal loads (batch 256: 56 -> 50 us per
-  // layer, profiles/decode_nt_ab.log); tuning attn_kv_nt = 0 for A/B runs
-  const Tuning& tu = tuning();
-  a.kv_nt = tu.attn_kv_nt;
+  // layer, profiles/decode_nt_ab.log)
+  a.kv_nt = 1;
   a.stamps = stamps;
   a.ksc = ksc; a.vsc = vsc; a.SmaxP = ksc ? SmaxP : 0;
   const bool kv8 = ksc != nullptr;
@@ -2375,18 +2046,13 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     // fp8 cache: the MFMA kernels only (large batch: one workgroup per (batch, kv head); small
     // batch: 8 waves per (batch, kv head), partitions for long caches)
     if (D != 128 || a.SmaxP < Smax || (G != 1 && G != 2 && G != 4 && G != 8)) return -3;
-    // tuning decode_fp8_mw = 1: the 8-wave kernel at every batch (A/B)
-    const int fp8_mw = tu.decode_fp8_mw;
-    // MHA at large batch: the VALU kernel (decode_g1_valu = 0: the MFMA form)
-    if (!fp8_mw && tu.decode_g1_valu && G == 1 && !a.qkv_slabs && rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
-      const int g1_nw = tu.decode_g1_nw;  // waves per row (1, 2, 4; default 2)
-      if (g1_nw == 4) hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<4>, dim3((unsigned)(B * Hkv)), dim3(256), 0, stream, a);
-      else if (g1_nw == 1) hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<1>, dim3((unsigned)(B * Hkv)), dim3(64), 0, stream, a);
-      else hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<2>, dim3((unsigned)(B * Hkv)), dim3(128), 0, stream, a);
+    // MHA (G = 1) at large batch: the VALU kernel, 2 waves per row (profiles/r3/dec13b_fp8kv_g1_valu_ab.txt)
+    if (G == 1 && !a.qkv_slabs && rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
+      hipLaunchKernelGGL(attn_decode_g1_fp8_kernel<2>, dim3((unsigned)(B * Hkv)), dim3(128), 0, stream, a);
       RT_LAUNCH_CHECK();
       return 0;
     }
-    if (!fp8_mw && rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
+    if (rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
       dim3 mgrid((unsigned)(B * Hkv)), mblock(64);
       switch (G) {
         case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, 1, true>), mgrid, mblock, 0, stream, a); break;
@@ -2410,7 +2076,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     RT_LAUNCH_CHECK();
     return 0;
   }
-  // large batch, one partition per (batch, kv head): the MFMA kernel (RT_DECODE_MFMA=0 disables)
+  // large batch, one partition per (batch, kv head): the MFMA kernel
   if (rt_attn_decode_mfma_ok(B, Hq, Hkv, D, NP)) {
     dim3 mgrid((unsigned)(B * Hkv)), mblock(64);
     switch (G) {
@@ -2423,7 +2089,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     RT_LAUNCH_CHECK();
     return 0;
   }
-  // small batch, short caches: 8 waves per (batch, kv head), merged in LDS (RT_DECODE_MW=0 disables)
+  // small batch, short caches: 8 waves per (batch, kv head), merged in LDS
   if (rt_attn_decode_mw_ok(B, Hq, Hkv, D, Smax) && !a.qkv_slabs && (NP <= 1 || (part && tickets))) {
     const int npm = rt_attn_decode_mw_np(Smax, NP);
     a.NP = npm;
@@ -2439,7 +2105,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     return 0;
   }
   if (a.qkv_slabs) return -2;  // the slab form exists only in the MFMA kernel (caller reduces first)
-  const int nk = tu.decode_nk > 0 ? tu.decode_nk : 4;  // keys per lane per chunk; PS must be a multiple of the chunk
+  const int nk = 4;  // keys per lane per chunk; PS must be a multiple of the chunk
   if (PS % (4 * (64 / (D / 8)) * nk) != 0) return -1;
   dim3 grid(NP, Hkv, B), block(256);
 #define DF_CASE(DD, GG, NN)                                                                   \
@@ -2449,7 +2115,7 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     return 0;                                                                                 \
   }
 #define DF_G(DD, NN) DF_CASE(DD, 1, NN) DF_CASE(DD, 2, NN) DF_CASE(DD, 4, NN) DF_CASE(DD, 8, NN)
-  DF_G(128, 4) DF_G(64, 4) DF_G(32, 4) DF_CASE(128, 4, 8) DF_CASE(128, 4, 2)
+  DF_G(128, 4) DF_G(64, 4) DF_G(32, 4)
 #undef DF_G
 #undef DF_CASE
   return -1;
@@ -2460,7 +2126,8 @@ extern "C" int rt_rope_qkv(void* qkv, long ld, const int* pos, const float* cosT
                            int do_rope_q, hipStream_t stream);
 
 // rope_pos / rope_cos / rope_sin (all or none): the RoPE backward of the forward's q / k rotation,
-// fused into the dQ / dK stores (atomic-dQ form: a separate inverse rotation of dQ after conversion)
+// fused into the dQ / dK stores. dq_f32: unused (kept in the signature; dQ is written in bf16 by
+// attn_bwd_dq_kernel, no fp32 accumulator).
 extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv, const void* o,
                            long ldo, const void* dout, long lddo, const float* lse, float* delta, float* dq_f32,
                            void* dq, long lddq, void* dk, long lddk, void* dv, long lddv, const int* kv_start, int B,
@@ -2479,70 +2146,18 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
   const long rows = (long)B * S * Hq;
   const long rows_per_block = 4L * (64 / (D / 8));
   dim3 pgrid((unsigned)((rows + rows_per_block - 1) / rows_per_block)), grid((S + 63) / 64, Hkv, B);
-  // dQ: a separate kernel per 64-query block (default) or fp32 atomics from the key-block kernel
-  // (tuning attn_bwd_atomic_dq = 1, the round-1 form)
-  const bool atomic_dq = tuning().attn_bwd_atomic_dq != 0;
+  // dK / dV per 64-key block, dQ by a separate kernel per 64-query block (no atomics)
   if (D != 64 && D != 128) return -1;
-  if (atomic_dq) RT_HIP_CHECK(hipMemsetAsync(dq_f32, 0, (size_t)B * S * Hq * D * sizeof(float), stream));
   dim3 qgrid((S + 63) / 64, Hq, B);
 #define BWD_CASE(DD)                                                                              \
   hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, pgrid, dim3(256), 0, stream, a);                    \
-  if (atomic_dq) {                                                                                \
-    hipLaunchKernelGGL((attn_bwd_kernel<DD, true>), grid, dim3(256), 0, stream, a);               \
-  } else {                                                                                        \
-    hipLaunchKernelGGL((attn_bwd_kernel<DD, false>), grid, dim3(256), 0, stream, a);              \
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<DD>, qgrid, dim3(256), 0, stream, a);                   \
-  }
+  hipLaunchKernelGGL(attn_bwd_kernel<DD>, grid, dim3(256), 0, stream, a);                         \
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<DD>, qgrid, dim3(256), 0, stream, a);
   if (D == 64) { BWD_CASE(64) } else { BWD_CASE(128) }
 #undef BWD_CASE
-  if (atomic_dq) {
-    const long n = (long)B * S * Hq * D;
-    hipLaunchKernelGGL(f32_to_bf16_strided_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_f32,
-                       (long)Hq * D, (bf16_t*)dq, lddq, (long)B * S);
-    RT_LAUNCH_CHECK();
-    // dQ's RoPE backward: the q heads of the bf16 dQ rows (Hkv = 0: no k / v heads in this view)
-    if (rope_cos) {
-      const int rc = rt_rope_qkv(dq, lddq, rope_pos, rope_cos, rope_sin, B * S, S, Hq, 0, D, -1.f, nullptr, nullptr,
-                                 nullptr, 0, 1, stream);
-      if (rc) return rc;
-    }
-  }
   RT_LAUNCH_CHECK();
   return 0;
 }
 
 
 
-// batch-1 attention + o_proj (+ residual); returns -1 when the shape is not supported (caller
-// falls back to the two-kernel path)
-extern "C" int rt_attn_o_fused(const void* qkv, void* kc, void* vc, int Smax, const int* slot, const int* attn_len,
-                               const int* kv_start, const int* pos, const float* cosT, const float* sinT, float sign,
-                               int window, float* part, int NP, int PS, int Hq, int Hkv, int D, float scale,
-                               const void* w, long ldw, const void* res, void* out, int H, unsigned* sync, int* err,
-                               long long* stamps, hipStream_t stream) {
-  AttnOArgs g;
-  DecodeFusedArgs& a = g.at;
-  a.qkv = (const bf16_t*)qkv; a.ldq = 0; a.kc = (bf16_t*)kc; a.vc = (bf16_t*)vc; a.Smax = Smax;
-  a.slot = slot; a.attn_len = attn_len; a.kv_start = kv_start; a.pos = pos; a.cosT = cosT; a.sinT = sinT;
-  a.sign = sign; a.window = window; a.part = part; a.tickets = nullptr; a.o = nullptr; a.ldo = 0;
-  a.B = 1; a.Hq = Hq; a.Hkv = Hkv; a.NP = NP; a.PS = PS; a.scale_log2 = scale * 1.4426950408889634f;
-  a.qkv_slabs = nullptr; a.qkv_nsplit = 0; a.qkv_sstride = 0; a.kv_nt = 0; a.stamps = nullptr;
-  g.w = (const bf16_t*)w; g.ldw = ldw; g.res = (const bf16_t*)res; g.out = (bf16_t*)out; g.H = H;
-  g.sync = sync; g.err = err; g.stamps = stamps;
-  const int G = Hq / Hkv;
-  const int nk = 4;
-  if (G * Hkv != Hq || Hq * D != AO_K || H % AO_ROWS != 0 || (ldw % 8) != 0) return -1;
-  if (PS % (4 * (64 / (D / 8)) * nk) != 0) return -1;
-  const int NB = H / AO_ROWS;
-  if (NB < Hkv * NP) return -1;
-#define AO_CASE(DD, GG)                                                                        \
-  if (D == DD && G == GG) {                                                                    \
-    hipLaunchKernelGGL((attn_o_fused_kernel<DD, GG, 4>), dim3(NB), dim3(256), 0, stream, g);   \
-    RT_LAUNCH_CHECK();                                                                         \
-    return 0;                                                                                  \
-  }
-  AO_CASE(128, 1) AO_CASE(128, 2) AO_CASE(128, 4) AO_CASE(128, 8)
-#undef AO_CASE
-  return -1;
-}
-#undef AO_STAMP

@@ -9,13 +9,10 @@
 // q|k|v). The adapter product therefore runs on the same MFMA pipeline and accumulators as the
 // frozen base weight — no separate output pass, no extra read/write of Y.
 //
-// Two kernels:
-//  * gemm_tile_kernel  — M > 64: 128x128x64 block tile, 4 waves (2x2, 64x64 each, 4x4
-//    mfma_f32_16x16x32_bf16 accumulators), global_load_lds (16 B/lane) into an XOR-swizzled
-//    lane-linear LDS image (source-address swizzle, cdna_hip_programming.md rule 21), two LDS
-//    stages, XCD-aware bijective block remap + grouped tile order, LDS-staged coalesced epilogue.
-//  * gemm_decode_kernel — M <= 64 (decode / small batch): weight streaming, 64 columns per wave,
-//    split-K over waves and workgroups with an in-launch last-arriver reduction (see below).
+// The weight-streaming kernels for M <= 64 (decode / small batch): gemm_decode_kernel (64 columns
+// per wave, split-K over waves and workgroups with an in-launch last-arriver reduction),
+// gemv16_kernel (M <= 16 on tile-ordered weight images), gemm_m64_kernel (16 < M <= 64, LDS-DMA
+// ring) and the W8A16 forms. M > 64 runs on the token-parallel family of gemm_big.hip.
 //
 // Replaces every projection GEMM of the reference's HF forward passes (reference
 // call sites reinforcement_learning_optimization_after_rag.py:38,200,207,313,318).
@@ -85,424 +82,6 @@ __device__ __forceinline__ i32x8 cat_frag(const bf16x8& lo, const bf16x8& hi) {
 // the read (rule 21).
 __device__ __forceinline__ int lds_swz(int row) { return (row >> 1) & 7; }
 
-// ---------------------------------------------------------------------------------------------
-// Large-M tile kernel
-// ---------------------------------------------------------------------------------------------
-constexpr int TBM = 128, TBN = 128, TBK = 64;
-constexpr int STAGE_BYTES = (TBM + TBN) * TBK * 2;  // 32 KiB per stage (A + B)
-constexpr int GROUP_M = 8;
-
-template <bool OUT_F32>
-__global__ __launch_bounds__(256, 2) void gemm_tile_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int tiles_m = (p.M + TBM - 1) / TBM, tiles_n = (p.N + TBN - 1) / TBN;
-  const int nwg = tiles_m * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int group = bid / (GROUP_M * tiles_n);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (bid % gsz);
-  const int tn = (bid % (GROUP_M * tiles_n)) / gsz;
-  const int m0 = tm * TBM, n0 = tn * TBN;
-
-  const int nk_main = p.K / TBK;
-  const int nk = nk_main + p.Rp / TBK;
-
-  // Per-lane staging source rows (4 A chunks + 4 B chunks per wave, 8 rows x 128 B each).
-  // LDS image is lane-linear: lane l of chunk c lands at row 8c + (l>>3), 16-B slot (l&7).
-  // It must hold k-chunk slot ^ lds_swz(row)  ->  source k-chunk = (l&7) ^ lds_swz(row).
-  const int r_in_chunk = lane >> 3;
-  long a_row_off[4], b_row_off[4], u_row_off[4], ub_row_off[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wid * 4 + i) * 8 + r_in_chunk;
-    const int src_kc = (lane & 7) ^ lds_swz(row);
-    const int ga = min(m0 + row, p.M - 1);
-    const int gb = min(n0 + row, p.N - 1);
-    a_row_off[i] = (long)ga * p.lda + src_kc * 8;
-    b_row_off[i] = (long)gb * p.ldb + src_kc * 8;
-    u_row_off[i] = (long)ga * p.ldu + src_kc * 8;
-    ub_row_off[i] = (long)gb * p.ldub + src_kc * 8;
-  }
-
-  auto stage = [&](int t, int buf) {
-    char* sA = smem + buf * STAGE_BYTES;
-    char* sB = sA + TBM * TBK * 2;
-    const bf16_t *pa, *pb;
-    long ka;
-    if (t < nk_main) {
-      ka = (long)t * TBK;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pa = p.A + a_row_off[i] + ka;
-        pb = p.B + b_row_off[i] + ka;
-        __builtin_amdgcn_global_load_lds((const void*)pa, (lds_void*)(sA + (wid * 4 + i) * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)pb, (lds_void*)(sB + (wid * 4 + i) * 1024), 16, 0, 0);
-      }
-    } else {
-      ka = (long)(t - nk_main) * TBK;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pa = p.U + u_row_off[i] + ka;
-        pb = p.UB + ub_row_off[i] + ka;
-        __builtin_amdgcn_global_load_lds((const void*)pa, (lds_void*)(sA + (wid * 4 + i) * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)pb, (lds_void*)(sB + (wid * 4 + i) * 1024), 16, 0, 0);
-      }
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int wr = wid >> 1, wc = wid & 1;
-  const int frow = lane & 15, fk = lane >> 4;
-
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nk) stage(t + 1, cur ^ 1);
-    const char* sA = smem + cur * STAGE_BYTES;
-    const char* sB = sA + TBM * TBK * 2;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], bfr[4];
-      const int kc = kk * 4 + fk;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wr * 64 + i * 16 + frow;
-        af[i] = *(const bf16x8*)(sA + row * 128 + ((kc ^ lds_swz(row)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wc * 64 + j * 16 + frow;
-        bfr[j] = *(const bf16x8*)(sB + row * 128 + ((kc ^ lds_swz(row)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // ---- epilogue: bias + activation, then store ----
-  float bcol[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wc * 64 + j * 16 + frow;
-    bcol[j] = (p.bias && col < p.N) ? bf2f(p.bias[col]) : 0.f;
-  }
-
-  if constexpr (OUT_F32) {
-    float* C = (float*)p.C;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wc * 64 + j * 16 + frow;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wr * 64 + i * 16 + fk * 4 + r;
-          if (row < p.M && col < p.N) C[(long)row * p.ldc + col] = apply_act(acc[i][j][r] + bcol[j], p.act);
-        }
-      }
-  } else {
-    // Stage the bf16 tile through LDS (row stride 136 elems = 272 B) for 16-B coalesced stores.
-    bf16_t* tile = (bf16_t*)smem;
-    constexpr int LDT = TBN + 8;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wc * 64 + j * 16 + frow;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wr * 64 + i * 16 + fk * 4 + r;
-          tile[row * LDT + col] = f2bf(apply_act(acc[i][j][r] + bcol[j], p.act));
-        }
-      }
-    __syncthreads();
-    bf16_t* C = (bf16_t*)p.C;
-    const int cc = tid & 15;
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-      const int row = pass * 16 + (tid >> 4);
-      const int grow = m0 + row, gcol = n0 + cc * 8;
-      if (grow < p.M && gcol < p.N) {
-        const uint4 v = *(const uint4*)(tile + row * LDT + cc * 8);
-        *(uint4*)(C + (long)grow * p.ldc + gcol) = v;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Large GEMM: 256x256x64 tile, 8 waves, 4 phases per K-tile with LDS-DMA kept in flight across
-// raw barriers (cdna_hip_programming.md §5 'The 256² 8-phase template', T1-T5)
-// ---------------------------------------------------------------------------------------------
-// LDS: two K-tile buffers x {A rows 0-127, A rows 128-255, B rows 0-127, B rows 128-255}, each a
-// 128-row x 64-k "half-tile" of 16 KiB (128-B rows, 16-B slot = k-chunk ^ lds_swz(row), written
-// lane-linearly by global_load_lds with the swizzle applied to the SOURCE address).
-// Wave (wr, wc) in a 2x4 grid owns C rows [128wr, +128) x cols [64wc, +64) = acc[8][4] fragments,
-// computed per K-tile as four 64x32 quadrants, one per phase:
-//   q0: (a0,b0)  reads A-sub0 (8 ds_read_b128) + B-sub0 (4)      stages A_lo of tile t+1
-//   q1: (a0,b1)  reads B-sub1 (4)                                stages A_hi of tile t+1
-//   q2: (a1,b1)  reads A-sub1 (8)
-//   q3: (a1,b0)  no reads (both in registers)                    stages B_lo, B_hi of tile t+2,
-//                                                                then vmcnt(4): tile t+1 landed
-// The two wave groups (wr = 0 / 1) are staggered by one barrier (T3: one group's MFMAs overlap
-// the other's ds_reads). Phase q of group 1 retires its reads before global barrier 8t+2q+2,
-// while group 0 issues phase q' DMAs after global barrier 8t'+2q'-1, so a refill must trail the
-// last read of its region by >= 2 phases: A of buffer (t+1)&1 was last read in q2 of tile t-1
-// (refilled from q0 of tile t), B of buffer t&1 in q1 of tile t (refilled in q3). RAW: tile t+1
-// is retired by q3's counted wait (leaving tile t+2's two B half-tiles = 4 DMAs in flight) before
-// the barrier that precedes either group's first read of it in q0 of tile t+1.
-constexpr int G2_HALF = 128 * 64 * 2;     // 16 KiB
-constexpr int G2_BUF = 4 * G2_HALF;       // 64 KiB per K-tile
-constexpr int G2_GROUP_M = 4;
-
-#define G2_BARRIER() asm volatile("s_barrier" ::: "memory")
-
-template <bool OUT_F32, int ACT>
-__device__ __forceinline__ void g2_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], char* smem, int m0, int n0) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  const int frow = lane & 15, fq = lane >> 4;
-  float bcol[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wc * 64 + j * 16 + frow;
-    bcol[j] = (p.bias && col < p.N) ? bf2f(p.bias[col]) : 0.f;
-  }
-  if constexpr (OUT_F32) {
-    float* C = (float*)p.C;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wc * 64 + j * 16 + frow;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wr * 128 + i * 16 + fq * 4 + r;
-          if (row < p.M && col < p.N) C[(long)row * p.ldc + col] = apply_act(acc[i][j][r] + bcol[j], ACT);
-        }
-      }
-  } else {
-    constexpr int LDT = 256 + 8;
-    bf16_t* tile = (bf16_t*)smem;
-    bf16_t* C = (bf16_t*)p.C;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (wr == half) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int col = wc * 64 + j * 16 + frow;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = i * 16 + fq * 4 + r;
-              tile[row * LDT + col] = f2bf(apply_act(acc[i][j][r] + bcol[j], ACT));
-            }
-          }
-      }
-      __syncthreads();
-      const int cc = tid & 31;
-#pragma unroll
-      for (int pass = 0; pass < 8; ++pass) {
-        const int row = pass * 16 + (tid >> 5);
-        const int grow = m0 + half * 128 + row, gcol = n0 + cc * 8;
-        if (grow < p.M && gcol < p.N) *(uint4*)(C + (long)grow * p.ldc + gcol) = *(const uint4*)(tile + row * LDT + cc * 8);
-      }
-      __syncthreads();
-    }
-  }
-}
-
-template <bool OUT_F32, bool FP8>
-__global__ __launch_bounds__(512, 2) void gemm_256_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * G2_BUF];  // the only __shared__ object
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
-  const int nwg = tiles_m * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int group = bid / (G2_GROUP_M * tiles_n);
-  const int first_m = group * G2_GROUP_M;
-  const int gsz = min(tiles_m - first_m, G2_GROUP_M);
-  const int tm = first_m + (bid % gsz);
-  const int tn = (bid % (G2_GROUP_M * tiles_n)) / gsz;
-  const int m0 = tm * 256, n0 = tn * 256;
-  constexpr int ESZ = FP8 ? 1 : 2;           // bytes per element; a K-tile is always 128 B per row
-  const int nk_main = p.K / (128 / ESZ);
-  const int nk = nk_main + (FP8 ? 0 : p.Rp / 64);
-  const int wr = wid >> 2, wc = wid & 3;
-  const int frow = lane & 15, fq = lane >> 4;
-
-  const int srow = lane >> 3;
-
-  // one half-tile (operand op: 0 = A, 1 = B; half h) of K-tile t -> buffer t & 1: 2 DMAs per lane
-  auto stage = [&](int op, int h, int t) {
-    const char* base;
-    long ldb;
-    long k0;
-    if (t < nk_main) {
-      base = (const char*)(op ? p.B : p.A);
-      ldb = (op ? p.ldb : p.lda) * ESZ;
-      k0 = (long)t * 128;
-    } else {
-      base = (const char*)(op ? p.UB : p.U);
-      ldb = (op ? p.ldub : p.ldu) * 2;
-      k0 = (long)(t - nk_main) * 128;
-    }
-    const int rmax = op ? p.N - 1 : p.M - 1;
-    const int r0 = (op ? n0 : m0) + h * 128;
-    char* dst = smem + (t & 1) * G2_BUF + (op * 2 + h) * G2_HALF;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int lr = (wid * 2 + j) * 8 + srow;
-      const int gr = min(r0 + lr, rmax);
-      const char* src = base + (long)gr * ldb + k0 + ((lane & 7) ^ lds_swz(lr)) * 16;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (wid * 2 + j) * 1024), 16, 0, 0);
-    }
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // a lane's 32 B of one 64-deep (bf16) / 128-deep (fp8) K-tile row: two 16-B LDS chunks held as
-  // one 8-register tuple (fp8 feeds it whole to the MX MFMA, bf16 as two k-halves)
-  i32x8 fa[4], fb0[2], fb1[2];
-
-  auto ld2 = [&](const char* hb, int lr) -> i32x8 {
-    const i32x4_t lo = *(const i32x4_t*)(hb + lr * 128 + ((fq ^ lds_swz(lr)) << 4));
-    const i32x4_t hi = *(const i32x4_t*)(hb + lr * 128 + (((4 + fq) ^ lds_swz(lr)) << 4));
-    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
-  auto read_a = [&](int buf, int s) {
-    const char* hb = smem + buf * G2_BUF + wr * G2_HALF;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = ld2(hb, s * 64 + i * 16 + frow);
-  };
-  auto read_b = [&](int buf, int s, i32x8 (&fb)[2]) {
-    const char* hb = smem + buf * G2_BUF + (2 + (wc >> 1)) * G2_HALF;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) fb[j] = ld2(hb, (wc & 1) * 64 + s * 32 + j * 16 + frow);
-  };
-  auto half = [](const i32x8& v, int h) -> bf16x8 {
-    return h == 0 ? __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 0, 1, 2, 3))
-                  : __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
-  };
-// bf16: 2 k-halves x mfma_16x16x32; fp8: one MX-scaled mfma_16x16x128 (unit block scales, e8m0
-// 127 = 2^0; the per-row / per-column scales are applied in the epilogue). The 32 bytes of a lane
-// are the same two 16-B LDS chunks for A and B, so the k pairing is consistent.
-#define G2_MMA(SA, SB, FB)                                                                        \
-  do {                                                                                           \
-    G2_BARRIER();                                                                                \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                           \
-    __builtin_amdgcn_sched_barrier(0);                                                           \
-    __builtin_amdgcn_s_setprio(1);                                                               \
-    if constexpr (FP8) {                                                                         \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
-        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
-          acc[(SA) * 4 + i][(SB) * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(    \
-              fa[i], FB[j], acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0, 127, 0, 127);              \
-    } else {                                                                                     \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                              \
-        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                            \
-          _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                       \
-            acc[(SA) * 4 + i][(SB) * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(           \
-                half(fa[i], kk), half(FB[j], kk), acc[(SA) * 4 + i][(SB) * 2 + j], 0, 0, 0);     \
-    }                                                                                            \
-    __builtin_amdgcn_s_setprio(0);                                                               \
-    G2_BARRIER();                                                                                \
-  } while (0)
-
-  // prologue: tile 0 complete + tile 1's B in flight
-  if (nk > 0) {
-    stage(0, 0, 0); stage(0, 1, 0); stage(1, 0, 0); stage(1, 1, 0);
-  }
-  if (nk > 1) {
-    stage(1, 0, 1); stage(1, 1, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  G2_BARRIER();
-
-  // Wave group 1 (wr = 1) runs one barrier behind group 0: each group's MFMA cluster then
-  // overlaps the other group's LDS reads and DMA issue on the same SIMD (waves w and w+4).
-  if (wr == 1) G2_BARRIER();
-
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    // q0
-    read_a(buf, 0);
-    read_b(buf, 0, fb0);
-    if (t + 1 < nk) stage(0, 0, t + 1);
-    G2_MMA(0, 0, fb0);
-    // q1
-    read_b(buf, 1, fb1);
-    if (t + 1 < nk) stage(0, 1, t + 1);
-    G2_MMA(0, 1, fb1);
-    // q2
-    read_a(buf, 1);
-    G2_MMA(1, 1, fb1);
-    // q3
-    if (t + 2 < nk) {
-      stage(1, 0, t + 2);
-      stage(1, 1, t + 2);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    G2_MMA(1, 0, fb0);
-  }
-  if (wr == 0) G2_BARRIER();
-#undef G2_MMA
-
-  // ---- epilogue: fp8 row/column scales, bias + activation (dispatched once), bf16 through LDS ----
-  if constexpr (FP8) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float sc = p.sb ? p.sb[min(n0 + wc * 64 + j * 16 + frow, p.N - 1)] : 1.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc;
-    }
-    if (p.sa) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float sr = p.sa[min(m0 + wr * 128 + i * 16 + fq * 4 + r, p.M - 1)];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j][r] *= sr;
-        }
-    }
-  }
-  switch (p.act) {
-    case ACT_RELU: g2_epilogue<OUT_F32, ACT_RELU>(p, acc, smem, m0, n0); break;
-    case ACT_GELU: g2_epilogue<OUT_F32, ACT_GELU>(p, acc, smem, m0, n0); break;
-    case ACT_GELU_TANH: g2_epilogue<OUT_F32, ACT_GELU_TANH>(p, acc, smem, m0, n0); break;
-    case ACT_SILU: g2_epilogue<OUT_F32, ACT_SILU>(p, acc, smem, m0, n0); break;
-    default: g2_epilogue<OUT_F32, ACT_NONE>(p, acc, smem, m0, n0); break;
-  }
-}
 
 // ---------------------------------------------------------------------------------------------
 // Decode GEMM (M <= 64): weight streaming with split-K and an in-launch last-arriver reduction
@@ -1502,7 +1081,6 @@ static int fit_split(int split, int groups, long slab_floats) {
   return split;
 }
 
-// 0 = automatic, 1 = force the 128x128 tile kernel, 2 = force the 256x256 kernel (M > 64)
 
 // register sets of the M <= 16 kernel's weight pipeline (DEPTH - 1 k-chunks in flight per wave).
 // 4 sets cost ~85 VGPRs at MT = 1 (occupancy 3 -> 2 blocks per CU; MT = 2 would spill) and
@@ -1533,20 +1111,6 @@ static int decode_depth(int MT, long blocks) {
 }
 
 
-// Wave quantisation decides between the kernels: the 256-tile kernel runs one workgroup per CU
-// (256 slots), the 128-tile kernel two (512 slots); the 256 kernel is ~10 % faster per FLOP
-// when both fill the chip.
-static bool use_256(int M, int N) {
-  if (tuning().gemm_variant == 1) return false;
-  if (tuning().gemm_variant == 2) return true;
-  if (M < 256 || N < 256) return false;
-  const double t256 = (double)((M + 255) / 256) * ((N + 255) / 256);
-  const double t128 = (double)((M + 127) / 128) * ((N + 127) / 128);
-  const double e256 = t256 / (std::ceil(t256 / 256.0) * 256.0);
-  const double e128 = t128 / (std::ceil(t128 / 512.0) * 512.0);
-  return 1.10 * e256 >= e128;
-}
-
 extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, const void* U, long ldu,
                           const void* UB, long ldub, int Rp, const void* bias, void* C, long ldc, int M,
                           int N, int K, int act, int out_f32, float* slabs, unsigned* tickets,
@@ -1565,8 +1129,8 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   if (M <= 0 || N <= 0) return 0;
   if (wshuf && (M > 64 || N % 16 != 0 || K % 64 != 0)) return -4;  // shuffled weights: decode kernel only
   if (act == ACT_SWIGLU && (M > 64 || N % 64 != 0 || (U && UB))) return -2;
-  if ((R || norm_eps > 0.f) && M > 64) return -3;  // residual / in-GEMM norm: skinny kernels only
-  if (M > 16 && M <= 64 && p.Rp == 0 && tuning().gemm_variant != 1 && !wshuf) {
+  if (M > 64) return -5;  // token-parallel GEMMs: rt_gemm_big
+  if (M > 16 && M <= 64 && p.Rp == 0 && !wshuf) {
     const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64 + 64) : 1;
     dim3 grid(((N + 63) / 64) * split), block(256);
     if (out_f32) hipLaunchKernelGGL((gemm_m64_kernel<true>), grid, block, 0, stream, p, slabs, tickets, split);
@@ -1592,7 +1156,7 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
       else hipLaunchKernelGGL((gemv16_kernel<false, 4, false, false, 16>), grid, dim3(1024), 0, stream, p);
     } else { G16(4, false) }
 #undef G16
-  } else if (M <= 64) {
+  } else {
     const int MT = (M + 15) / 16;
     const int want = wshuf ? decode_split_shuf(K) : decode_split(N, K);
     const int split = (slabs && tickets) ? fit_split(want, (N + DG_COLS - 1) / DG_COLS, MT * 16 * (DG_COLS + 1)) : 1;
@@ -1609,16 +1173,6 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
       default: return -1;
     }
 #undef DG_CASE
-  } else if (use_256(M, N) && (N % 8) == 0 && (ldc % 8) == 0) {
-    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-    dim3 grid(tiles), block(512);
-    if (out_f32) hipLaunchKernelGGL((gemm_256_kernel<true, false>), grid, block, 0, stream, p);
-    else hipLaunchKernelGGL((gemm_256_kernel<false, false>), grid, block, 0, stream, p);
-  } else {
-    const int tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
-    dim3 grid(tiles), block(256);
-    if (out_f32) hipLaunchKernelGGL((gemm_tile_kernel<true>), grid, block, 0, stream, p);
-    else hipLaunchKernelGGL((gemm_tile_kernel<false>), grid, block, 0, stream, p);
   }
   RT_LAUNCH_CHECK();
   return 0;
@@ -1629,7 +1183,7 @@ extern "C" int rt_gemm_big_fp8(const void*, long, const float*, const void*, lon
                                const void*, hipStream_t);
 
 // fp8 GEMMs: C[M,N] (bf16) = act( (A_q B_q^T) * sa[row] * sb[col] + bias ), A_q / B_q OCP e4m3fn.
-//  * M > 64 : W8A8, 256x256 8-phase kernel on MX-scaled mfma_16x16x128_f8f6f4 (2x the bf16 rate)
+//  * M > 64 : W8A8 on the gemm_big schedule, MX-scaled mfma_16x16x128_f8f6f4 (2x the bf16 rate)
 //  * M <= 64: W8A16 (A = bf16 activations, sa ignored): half the weight bytes.
 //      - M <= 16 with the tile-ordered fp8 image (wshuf, shuffle_decode_weight_fp8): gemv16_kernel<W8>,
 //        one workgroup per 16 weight rows, no split-K;
@@ -1690,16 +1244,12 @@ extern "C" int rt_gemm_fp8(const void* A, long lda, const float* sa, const void*
       }
     }
   } else {
-    // W8A8 (M > 64): the gemm_big schedule with the MX fp8 MFMA (RT_GEMM_FP8_256=1: the older
-    // 256x256 8-phase kernel, kept for A/B); SwiGLU pairs [gate; up] in its epilogue
-    if (K % 128 || N % 8) return -1;
-    const int use256 = tuning().gemm_fp8_256;
-    if (!use256 && lda % 16 == 0 && ldb % 16 == 0 && ldc % 8 == 0 && (act == 0 || (act == ACT_SWIGLU && N % 256 == 0)))
-      return rt_gemm_big_fp8(A, lda, sa, B, ldb, sb, bias, C, ldc, M, N, K, act == ACT_SWIGLU ? 5 : 0, nullptr, 0,
-                             nullptr, 0, 0, nullptr, 0, nullptr, stream);
-    if (act == ACT_SWIGLU) return -2;
-    const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-    hipLaunchKernelGGL((gemm_256_kernel<false, true>), dim3(tiles), dim3(512), 0, stream, p);
+    // W8A8 (M > 64): the gemm_big schedule with the MX fp8 MFMA; SwiGLU pairs [gate; up] in its
+    // epilogue
+    if (K % 128 || N % 8 || lda % 16 || ldb % 16 || ldc % 8) return -1;
+    if (act != 0 && !(act == ACT_SWIGLU && N % 256 == 0)) return -2;
+    return rt_gemm_big_fp8(A, lda, sa, B, ldb, sb, bias, C, ldc, M, N, K, act == ACT_SWIGLU ? 5 : 0, nullptr, 0,
+                           nullptr, 0, 0, nullptr, 0, nullptr, stream);
   }
   RT_LAUNCH_CHECK();
   return 0;

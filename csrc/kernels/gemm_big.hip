@@ -78,21 +78,11 @@ struct Args {
   int act;
   int nsplit;                     // split-K factor (gridDim.y)
   const bf16_t* zpage;            // >= 128 zero bytes
-  int b_nt;                       // B (weight) stream read once per launch: non-temporal LDS-DMA
   // F8 (W8A8, config 5): A / B are OCP e4m3fn bytes viewed as bf16 pairs (K and the strides in
   // 2-byte units), one MX-scaled 16x16x128 MFMA per fragment pair and K-step; C = acc * sa[row] *
   // sb[weight row] before bias / activation / SwiGLU
   const float* sa;
   const float* sb;
-  // SK (stream-K tail, gemm_big_kernel<..., SK = true>): the first sk_dp blocks run whole tiles
-  // [0, sk_dp) (XCD remap within them); the remaining sk_units blocks split the K-steps of tiles
-  // [sk_dp, sk_dp + sk_tiles) evenly, each up to two tile segments; a tile's partial accumulators
-  // go through sk_part (write-through, 2 slots of 256 x 256 fp32 per unit) and the last arriving
-  // unit (sk_tickets, self-resetting) sums them and runs the epilogue
-  int sk_dp, sk_tiles, sk_units;
-  float* sk_part;
-  unsigned* sk_tickets;
-  int b_layout_kmaj;  // host: NN form of the stream-K launch
   int group_m;        // rows of tiles per L2 group (0 = GROUP_M); tuning gemm_group_m
   // E_ROPE: per-row rotary position, angle tables, rotated column count, head width
   const int* rope_pos;
@@ -143,19 +133,12 @@ __device__ __forceinline__ void wait_granules(int n) {
 // each wave owns 2 B fragments instead of 4 (columns 64 (wc >> 1) + 16 (wc & 1) + 32 s): used for
 // M = 256 decode GEMMs (twice the workgroups, no split-K on the widest weights) and for the last,
 // partial wave of tiles of a large GEMM (rt_gemm_big_planned).
-// RING (NT / NN, BN = 256): the K-step buffers become a ring of 10 granule slots (160 KiB, the
-// whole LDS), which lets a K-step run as TWO phases of 32 MFMAs (one barrier per 512 MFMA cycles
-// instead of per 256) with every granule still issued >= 4 sections ahead of its first read.
-template <int LA, int LB, int OUT, int EPI, int BN, bool TRB = false, bool F8 = false, bool SK = false,
-          bool RING = false>
+template <int LA, int LB, int OUT, int EPI, int BN, bool F8 = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   static_assert(BN == 256 || BN == 128, "BN");
-  static_assert(!RING || (LA == ROW && BN == 256 && !F8 && !SK && !TRB), "RING: NT / NN 256x256 bf16 operands");
   static_assert(!F8 || (LA == ROW && LB == ROW && OUT == O_BF16), "F8: NT with a bf16 output only");
-  static_assert(!SK || (OUT == O_BF16 && BN == 256), "SK: 256x256 tiles with a bf16 epilogue");
   constexpr int NB = BN / 128;  // B fragments per wave and B sub-block; LDS-DMA instructions per B granule
-  constexpr int NSLOT = 10;  // RING: granule slots
-  __shared__ __attribute__((aligned(16))) char smem[RING ? NSLOT * GRAN : 2 * BUF];  // the only __shared__ object
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];  // the only __shared__ object
 
 
   const int tiles_m = (p.M + 255) / 256;
@@ -166,51 +149,14 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   const int nk2 = p.A2 ? (p.K2 + 63) / 64 : 0;
   const int nk = nk1 + nk2;
 
-  // ---- role: (tile, K-step range) segments of this block ----
-  int seg_tile0, seg_b0, seg_e0, seg_tile1 = 0, seg_b1 = 0, seg_e1 = 0, nseg = 1;
-  int sk_unit = -1;  // >= 0: this block is a stream-K unit
-  if constexpr (!SK) {
-    seg_tile0 = xcd_remap(blockIdx.x, nwg);
-    seg_b0 = (int)((long)blockIdx.y * nk / p.nsplit);
-    seg_e0 = (int)((long)(blockIdx.y + 1) * nk / p.nsplit);
-  } else if ((int)blockIdx.x < p.sk_dp) {
-    seg_tile0 = xcd_remap(blockIdx.x, p.sk_dp);
-    seg_b0 = 0;
-    seg_e0 = nk;
-  } else {
-    // units dealt to XCDs in contiguous runs (consecutive units share a tile: their partials stay
-    // in one L2 where the dispatch allows); the run order is a speed choice only
-    const int j = (int)blockIdx.x - p.sk_dp;
-    sk_unit = xcd_remap(j, p.sk_units);
-    const long S = (long)p.sk_tiles * nk;
-    const long g0 = (long)sk_unit * S / p.sk_units, g1 = (long)(sk_unit + 1) * S / p.sk_units;
-    seg_tile0 = p.sk_dp + (int)(g0 / nk);
-    seg_b0 = (int)(g0 % nk);
-    const long end0 = min(g1, (g0 / nk + 1) * nk);
-    seg_e0 = (int)(end0 - (g0 / nk) * nk);
-    if (g1 > end0) {  // the unit runs into the next tile
-      nseg = 2;
-      seg_tile1 = seg_tile0 + 1;
-      seg_b1 = 0;
-      seg_e1 = (int)(g1 - end0);
-    }
-  }
-
-  for (int seg = 0; seg < (SK ? nseg : 1); ++seg) {
-  // lane constants are (re)derived inside the segment loop from an opaque copy of the thread id:
-  // hoisted out of the loop they would stay live across it and push the 256-register body of the
-  // stream-K form into scratch (no effect on the one-segment forms)
-  int tid_raw = threadIdx.x;
-  if constexpr (SK) asm volatile("" : "+v"(tid_raw));
-  const int tid = tid_raw, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS bases
   const int wr = wid >> 2, wc = wid & 3;
   const int frow = lane & 15, fq = lane >> 4;
-  const int seg_tile = seg == 0 ? seg_tile0 : seg_tile1;
-  const int t_begin = seg == 0 ? seg_b0 : seg_b1;
-  const int t_end = seg == 0 ? seg_e0 : seg_e1;
+  const int t_begin = (int)((long)blockIdx.y * nk / p.nsplit);
+  const int t_end = (int)((long)(blockIdx.y + 1) * nk / p.nsplit);
   // ---- tile assignment: group_m-row groups (L2 reuse of B panels) over the remapped id ----
-  const int bid = seg_tile;
+  const int bid = xcd_remap(blockIdx.x, nwg);
   const int GM = p.group_m > 0 ? p.group_m : GROUP_M;
   const int group = bid / (GM * tiles_n);
   const int first_m = group * GM;
@@ -270,18 +216,7 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       off[g][j] = (g < 2 || j < NB) ? src_off(g, j, (g >> 1) ? p.ldb : p.lda, true, ki) : 0u;
       if (g < 2) kin[g][j] = ki;
     }
-  // RING: the slot of granule g (0 a0, 1 a1, 2 b0, 3 b1) of K-step u — granules are issued in the
-  // order a0 b0 b1 a1 of every step, slot = issue index mod NSLOT; inside a slot the instruction
-  // (wave w, j) of the granule owns rows 8 (2 w + j) .. + 7 (A: tile rows 128 (r >> 7) + 64 s +
-  // (r & 63); B: 64 (r >> 6) + 32 s + (r & 31)) with the same 16-B chunk swizzle
-  auto gidx = [](int g, int u) { return 4 * u + (g == 0 ? 0 : g == 2 ? 1 : g == 3 ? 2 : 3); };
-  auto rslot = [&](int g, int u) -> char* { return smem + (gidx(g, u) % NSLOT) * GRAN; };
-  // LDS destination of instruction j of granule g of K-step t (relative to the image for the
-  // two-buffer form: `img` + lds_dst)
-  auto gdst = [&](int g, int j, int t) -> char* {
-    if constexpr (RING) return rslot(g, t) + (wid * 2 + j) * 1024;
-    else return smem + (t & 1) * BUF + lds_dst(g, j);
-  };
+  auto gdst = [&](int g, int j, int t) -> char* { return smem + (t & 1) * BUF + lds_dst(g, j); };
   // one granule g of K-step t into buffer t & 1 (g is a literal at every call site)
   auto stage = [&](int g, int t) {
     const int op = g >> 1;
@@ -290,18 +225,9 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       const long adv = ((op ? LB : LA) == ROW) ? (long)k0 : (long)k0 * (op ? p.ldb : p.lda);
       const bf16_t* base = (op ? p.B : p.A) + adv;
       if (k0 + 64 <= p.K) {
-        if (op && p.b_nt) {
-          // a single row tile (M <= 256, decode): every weight byte is read by ONE workgroup once
-          // per launch and the other layers' weights evict it before the next step
-          // (MI355X_MICROARCH.md 'nt-weights')
 #pragma unroll
-          for (int j = 0; j < NB; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, t), 16, 0, 2);
-        } else {
-#pragma unroll
-          for (int j = 0; j < (op ? NB : 2); ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, t), 16, 0, 0);
-        }
+        for (int j = 0; j < (op ? NB : 2); ++j)
+          __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, t), 16, 0, 0);
       } else {  // ragged reduction tail: out-of-range k reads the zero page
 #pragma unroll
         for (int j = 0; j < (op ? NB : 2); ++j) {
@@ -351,23 +277,9 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
                       v[2][0], v[2][1], v[2][2], v[2][3], v[3][0], v[3][1], v[3][2], v[3][3]};
     return __builtin_bit_cast(i32x8, w);
   };
-  // TRB (A/B reference, RT_GEMM_TR_BUILTIN=1): the same reads through the builtin
-  auto rd_kmaj_builtin = [&](const char* img, int mn) -> i32x8 {
-    const uint32_t a0 = kmaj_addr(img, mn);
-    const char* base = img + (a0 - lds_addr(img));
-    rt_s16x4 v[4];
-    v[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
-    v[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 256));
-    v[2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 2048));
-    v[3] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 2304));
-    return frag_of(v);
-  };
   auto read_a = [&](int buf, int s) {
     const char* img = smem + buf * BUF;
-    if constexpr (LA == KMAJ && TRB) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = rd_kmaj_builtin(img, wr * 128 + s * 64 + i * 16);
-    } else if constexpr (LA == ROW) {
+    if constexpr (LA == ROW) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = rd_row(img, wr * 128 + s * 64 + i * 16 + frow);
     } else {
@@ -386,9 +298,6 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     if constexpr (LB == ROW) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) fb[j] = rd_row(img, brow(j) + frow);
-    } else if constexpr (TRB) {
-#pragma unroll
-      for (int j = 0; j < NB; ++j) fb[j] = rd_kmaj_builtin(img, brow(j));
     } else if constexpr (NB == 2) {
       rt_s16x4 v[8];
       ds_tr16_frag2<256, 2048, 2304>(kmaj_addr(img, brow(0)), kmaj_addr(img, brow(1)), v);
@@ -445,112 +354,6 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     GB_BARRIER();                                                                           \
   } while (0)
 
-  if constexpr (RING) {
-    if (t_begin < t_end) {
-      // fragments of the in-slot rows: A granule s holds tile rows 128 wr + 64 s + (0..63) at slot
-      // rows 64 wr + (0..63); B granule s holds tile rows 128 (wc >> 1) + 64 (wc & 1) + 32 s + (0..31)
-      // at slot rows 32 wc + (0..31)
-      auto read_a_r = [&](const char* g) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = rd_row(g, wr * 64 + i * 16 + frow);
-      };
-      auto read_b_r = [&](const char* g, i32x8 (&fb)[2]) {
-        if constexpr (LB == ROW) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) fb[j] = rd_row(g, wc * 32 + j * 16 + frow);
-        } else {
-          // KMAJ: B granule s holds the [64 k][32 mn] blocks 2 m + s of the two-buffer image as
-          // slot blocks m; this wave's columns are block wc, fragment columns 0 / 16
-          auto kaddr = [&](int c0) -> uint32_t {
-            const int col = c0 + 4 * (frow & 3), kr = fq * 8 + (frow >> 2);
-            return lds_addr(g + wc * 4096 + kr * 64 + (((col >> 3) ^ kmaj_swz(kr)) << 4) + (col & 7) * 2);
-          };
-          rt_s16x4 v[8];
-          ds_tr16_frag2<256, 2048, 2304>(kaddr(0), kaddr(16), v);
-          fb[0] = frag_of(v);
-          fb[1] = frag_of(v + 4);
-        }
-      };
-      // retire every granule issued before the n newest (2 LDS-DMA instructions per granule)
-      auto wait_newer = [](int n) {
-        switch (n < 0 ? 0 : n) {
-          case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-          case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-          case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-          case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-          case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-          case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-          default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        }
-      };
-      // Two phases of 32 MFMAs per K-step (a0 x [b0 | b1], a1 x [b0 | b1]): one barrier per 512
-      // MFMA cycles instead of per 256, so the other wave group's read section (16 / 8 fragment
-      // reads + LDS-DMA issue) hides under a section twice as long. Granules are issued in the
-      // order a0 b0 b1 a1 of every step (issue ordinal = ring index - 4 t_begin): R_A(t) issues b1, a1
-      // of t + 1 and a0 of t + 2, R_B(t) b0 of t + 2 — every slot is rewritten >= 3 sections after
-      // its previous granule's last read (both wave groups past it).
-      const int t0 = t_begin;
-      auto ordg = [&](int g, int u) { return gidx(g, u) - 4 * t0; };
-      const int nk1f = p.K / 64;
-      auto stage_fast_r = [&](int g, int u) {
-        // K-step advance: 64 elements along a ROW operand, 64 rows of a KMAJ one (NN weight)
-        const bf16_t* base = (g >> 1) ? p.B + (LB == ROW ? (long)u * 64 : (long)u * 64 * p.ldb) : p.A + (long)u * 64;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          __builtin_amdgcn_global_load_lds((const void*)(base + off[g][j]), (lds_void*)gdst(g, j, u), 16, 0, 0);
-      };
-      auto stg = [&](int g, int u) {
-        if (u < nk1f) stage_fast_r(g, u);
-        else stage(g, u);
-      };
-#define GB_MMA2(SA)                                                                         \
-  do {                                                                                      \
-    GB_BARRIER();                                                                           \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                      \
-    __builtin_amdgcn_sched_barrier(0);                                                      \
-    __builtin_amdgcn_s_setprio(1);                                                          \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                           \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                         \
-        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                    \
-          acc[(SA) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                   \
-              half(fb0[j], kk), half(fa[i], kk), acc[(SA) * 4 + i][j], 0, 0, 0);            \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                           \
-      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                         \
-        _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                    \
-          acc[(SA) * 4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(               \
-              half(fb1[j], kk), half(fa[i], kk), acc[(SA) * 4 + i][2 + j], 0, 0, 0);        \
-    __builtin_amdgcn_s_setprio(0);                                                          \
-    GB_BARRIER();                                                                           \
-  } while (0)
-      // prologue: a0 b0 b1 a1 of t0, a0 b0 of t0 + 1; retire through b1 (t0)
-      stage(0, t0); stage(2, t0); stage(3, t0); stage(1, t0);
-      int last = ordg(1, t0);  // issue ordinal of the newest granule
-      if (t0 + 1 < t_end) {
-        stg(0, t0 + 1); stg(2, t0 + 1);
-        last = ordg(2, t0 + 1);
-      }
-      wait_newer(last - ordg(3, t0));
-      GB_BARRIER();
-      if (wr == 1) GB_BARRIER();
-      for (int t = t0; t < t_end; ++t) {
-        // R_A: a0, b0, b1 of t; stage b1, a1 (t + 1), a0 (t + 2); retire a1 (t)
-        read_a_r(rslot(0, t));
-        read_b_r(rslot(2, t), fb0);
-        read_b_r(rslot(3, t), fb1);
-        if (t + 1 < t_end) { stg(3, t + 1); stg(1, t + 1); last = ordg(1, t + 1); }
-        if (t + 2 < t_end) { stg(0, t + 2); last = ordg(0, t + 2); }
-        wait_newer(last - ordg(1, t));
-        GB_MMA2(0);
-        // R_B: a1 of t; stage b0 (t + 2); retire a0 / b0 / b1 (t + 1)
-        read_a_r(rslot(1, t));
-        if (t + 2 < t_end) { stg(2, t + 2); last = ordg(2, t + 2); }
-        if (t + 1 < t_end) wait_newer(last - ordg(3, t + 1));
-        GB_MMA2(1);
-      }
-#undef GB_MMA2
-      if (wr == 0) GB_BARRIER();
-    }
-  } else {
   if (t_begin < t_end) {
     // prologue: step t_begin complete (a0, b0, b1, a1) + a0, b0 of step t_begin + 1; granules are
     // always issued in key order a0(u) b0(u) b1(u) a1(u) a0(u+1) b0(u+1) ... (see header)
@@ -619,79 +422,10 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
     }
     if (wr == 0) GB_BARRIER();
   }
-  }  // RING / two-buffer
 #undef GB_MMA
 #undef GB_MMA_X
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-
-  if constexpr (SK) {
-    if (sk_unit >= 0) {
-      // ---- stream-K hand-off of tile `bid` (cdna_hip_programming.md §6 Guideline 16, R1 form):
-      // the partial tile is stored write-through (sc1, no release fence), every wave drains its
-      // stores, the workgroup meets at a barrier, one lane takes a relaxed agent-scope ticket; the
-      // last arriver reads every other unit's partial with sc1 loads, adds it to its registers and
-      // runs the normal epilogue, then re-arms the ticket (self-resetting: zero before the first
-      // launch, zero after every launch). Correct for any placement of units on XCDs / CUs.
-      const int tl = bid - p.sk_dp;  // tile index within the stream-K region
-      const long S = (long)p.sk_tiles * nk;
-      const int U = p.sk_units;
-      const int u_first = (int)((((long)tl * nk + 1) * U - 1) / S);
-      const int u_last = (int)((((long)(tl + 1) * nk) * U - 1) / S);
-      constexpr int PART = 256 * 256;  // floats per partial slot
-      auto slot_rsrc = [&](int u, int sg) {
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(p.sk_part + ((long)u * 2 + sg) * PART), (short)0, PART * 4,
-                                                 0x00020000);
-      };
-      {
-        const auto rs = slot_rsrc(sk_unit, seg);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 2 * NB; ++j)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[i][j]), rs,
-                                                   ((i * 2 * NB + j) * 512 + tid) * 16, 0, 16 /* sc1 */);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-      __syncthreads();
-      int* flag = (int*)smem;  // the one LDS array (staging buffers are idle here)
-      if (tid == 0) {
-        const unsigned old = __hip_atomic_fetch_add(p.sk_tickets + tl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = old == (unsigned)(u_last - u_first);
-      }
-      __syncthreads();
-      const bool last = *flag != 0;
-      __syncthreads();
-      if (!last) continue;  // another unit finishes this tile
-      // sum every unit's partial in unit order (its own re-read from the slot it just stored), so
-      // the result does not depend on which unit arrives last: bitwise reproducible
-      for (int u = u_first; u <= u_last; ++u) {
-        // the tile is the first segment of unit u unless u started inside an earlier tile
-        const int sg = (int)(((long)u * S / U) / nk) == tl ? 0 : 1;
-        const auto rs = slot_rsrc(u, sg);
-        // two accumulator rows (32 registers) of loads in flight at a time: the registers hold the
-        // whole 256 x 256 accumulator already
-#pragma unroll
-        for (int i = 0; i < 8; i += 2) {
-          i32x4 v[2][2 * NB];
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-            for (int j = 0; j < 2 * NB; ++j)
-              v[ii][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (((i + ii) * 2 * NB + j) * 512 + tid) * 16, 0,
-                                                               16 /* sc1 */);
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-            for (int j = 0; j < 2 * NB; ++j)
-              acc[i + ii][j] = u == u_first ? __builtin_bit_cast(f32x4, v[ii][j])
-                                            : acc[i + ii][j] + __builtin_bit_cast(f32x4, v[ii][j]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if (tid == 0) __hip_atomic_store(p.sk_tickets + tl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 
   // ---- epilogue ----
   // SWAP: acc[i][j][r] = C[m0 + 128 wr + 16 i + frow][n0 + 64 wc + 16 j + 4 fq + r]
@@ -875,7 +609,6 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
       __syncthreads();
     }
   }
-  }  // segments
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1087,327 +820,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   *(uint4*)(C + (long)m * ldc + c0) = pack8(y);
 }
 
-// ---------------------------------------------------------------------------------------------
-// 4-wave NT tile (ROW / ROW) with a large per-wave block: wave (wr, wc) of a 2 x 2 grid owns a
-// (16 WM) x 128 output block = WM x 8 fragments of mfma_f32_16x16x32_bf16; the workgroup tile is
-// (32 WM) x 256. One wave per SIMD, so a wave owns the SIMD's whole register file: the 4 WM x 8
-// fp32 accumulators per lane live in AGPRs (WM = 8: 128 x 128 per wave, the wave shape of the
-// library's MT256x256 4-wave kernels; WM = 6: 96 x 128). LDS bytes read per MAC: 1/(16 WM) + 1/128
-// per k, vs 1/128 + 1/64 for gemm_big_kernel's 128 x 64 wave block.
-// Stages of 64 k through a 2-slot LDS-DMA ring: [rows][128 B] images filled by whole-line LDS-DMA
-// (8 rows x 128 B per instruction; a 64-B-per-row form measured 3.5e7 TA-stalled-by-TC cycles per
-// qkv GEMM, profiles/r3/gemm_w4_pmc_summary.txt), 16-B slot = k-chunk ^ ((row >> 1) & 7) as in
-// gemm_big_kernel (conflict-free ds_read_b128). A stage is computed in two k-halves of 32 with the
-// fragments register double-buffered: half 0 computes while the reads of half 1 go out (the stage
-// is resident: no barrier); half 1 retires stage s+1 (vmcnt), passes the stage's one raw barrier,
-// then issues the LDS-DMA of stage s+2 into the slot just read and the reads of stage s+1's half 0
-// between its MFMAs. Tile order, SwiGLU row pairing, K-extension and epilogues follow
-// gemm_big_kernel.
-template <int WM>
-struct W4Geom {
-  static constexpr int BM = 32 * WM;                 // tile rows
-  static constexpr int A_BYTES = BM * 128;           // A image of one stage (64 k)
-  static constexpr int SLOT = A_BYTES + 256 * 128;   // + B image
-  static constexpr int DMA_A = BM / 32;              // LDS-DMA instructions per lane per stage: A (8 rows x 128 B each)
-  static constexpr int DMA = DMA_A + 8;              // + B
-};
-
-template <int OUT, int EPI, int WM>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(Args p) {
-  using G = W4Geom<WM>;
-  constexpr int BM = G::BM, WROWS = 16 * WM;
-  static_assert(WM % 2 == 0 && G::DMA_A * 32 == BM && (WM - 1) * 8 >= G::DMA + WM + 8 && WM * 8 >= WM + 8, "WM");
-  __shared__ __attribute__((aligned(16))) char smem[2 * G::SLOT];  // the only __shared__ object
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-  const int frow = lane & 15, fq = lane >> 4;
-
-  const int tiles_m = (p.M + BM - 1) / BM;
-  const int tiles_n = EPI == E_SWIGLU ? p.N / 256 : (p.N + 255) / 256;
-  const int nwg = tiles_m * tiles_n;
-  if ((int)blockIdx.x >= nwg) return;  // grid / tile-count mismatch: never index past the tile grid
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int group = bid / (GROUP_M * tiles_n);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (bid % gsz);
-  const int tn = (bid % (GROUP_M * tiles_n)) / gsz;
-  const int m0 = tm * BM, n0 = tn * 256;
-  const int Fh = p.N / 2;
-
-  const int ns1 = (p.K + 63) / 64;             // main-K stages (the last may be ragged: zero page)
-  const int ns1f = p.K / 64;                   // full main-K stages
-  const int ns2 = p.A2 ? (p.K2 + 63) / 64 : 0;  // K-extension stages
-  const int ns = ns1 + ns2;
-  const int s_begin = (int)((long)blockIdx.y * ns / p.nsplit);
-  const int s_end = (int)((long)(blockIdx.y + 1) * ns / p.nsplit);
-
-  // LDS-DMA instruction x (A: x = DMA_A wid + j, B: x = 8 wid + j) covers rows 8 x + lane / 8; the
-  // lane's 16-B LDS slot lane % 8 receives k-chunk (lane % 8) ^ ((row >> 1) & 7) = (lane % 8) ^
-  // ((lane >> 4) + 4 (x & 1)) (source-side swizzle, guide rule 21); DMA_A is even, so x & 1 = j & 1
-  auto kc_of = [&](int j) -> int { return (lane & 7) ^ ((lane >> 4) + 4 * (j & 1)); };
-  auto row_of = [&](int op, int j) -> int { return 8 * ((op ? 8 : G::DMA_A) * wid + j) + (lane >> 3); };
-  auto grow_of = [&](int op, int row) -> int {
-    if (op == 0) return min(m0 + row, p.M - 1);
-    if (EPI == E_SWIGLU) return row < 128 ? tn * 128 + row : Fh + tn * 128 + row - 128;
-    return min(n0 + row, p.N - 1);
-  };
-  auto dst_of = [&](char* img, int op, int j) -> char* {
-    return img + (op ? G::A_BYTES : 0) + ((op ? 8 : G::DMA_A) * wid + j) * 1024;
-  };
-  // main-K sources: uniform operand base + 32-bit per-lane byte offset (one VGPR per instruction)
-  uint32_t offa[G::DMA_A], offb[8];
-#pragma unroll
-  for (int j = 0; j < G::DMA_A; ++j)
-    offa[j] = ((uint32_t)grow_of(0, row_of(0, j)) * (uint32_t)p.lda + (uint32_t)(kc_of(j) * 8)) * 2u;
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-    offb[j] = ((uint32_t)grow_of(1, row_of(1, j)) * (uint32_t)p.ldb + (uint32_t)(kc_of(j) * 8)) * 2u;
-  auto dma_main = [&](int s, int k) {  // instruction k (< DMA) of full main stage s
-    char* img = smem + (s & 1) * G::SLOT;
-    if (k < G::DMA_A)
-      __builtin_amdgcn_global_load_lds((const void*)((const char*)p.A + (size_t)s * 128 + offa[k]),
-                                       (lds_void*)dst_of(img, 0, k), 16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds((const void*)((const char*)p.B + (size_t)s * 128 + offb[k - G::DMA_A]),
-                                       (lds_void*)dst_of(img, 1, k - G::DMA_A), 16, 0, 0);
-  };
-  auto stage = [&](int s) {  // any stage: ragged main-K tail and K-extension chunks read the zero page
-    if (s < ns1f) {
-#pragma unroll
-      for (int k = 0; k < G::DMA; ++k) dma_main(s, k);
-      return;
-    }
-    char* img = smem + (s & 1) * G::SLOT;
-    const bool ext = s >= ns1;
-    const int k0 = (ext ? s - ns1 : s) * 64;
-    const int klim = ext ? p.K2 : p.K;
-    const bf16_t* zsrc = p.zpage + (lane & 7) * 8;
-#pragma unroll
-    for (int op = 0; op < 2; ++op) {
-      const long ld = ext ? (op ? p.ldb2 : p.lda2) : (op ? p.ldb : p.lda);
-      const bf16_t* base = ext ? (op ? p.B2 : p.A2) : (op ? p.B : p.A);
-#pragma unroll
-      for (int j = 0; j < (op ? 8 : G::DMA_A); ++j) {
-        const int kk = k0 + kc_of(j) * 8;
-        const bf16_t* src = kk < klim ? base + (long)grow_of(op, row_of(op, j)) * ld + kk : zsrc;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)dst_of(img, op, j), 16, 0, 0);
-      }
-    }
-  };
-
-  // fragment reads, k-half h of a stage: lane (frow, fq) of fragment f reads row 16 f + frow, k-chunk
-  // 4 h + fq, at slot (4 h + fq) ^ ((row >> 1) & 7) = (4 h + fq) ^ ((frow >> 1) & 7)
-  const int rdo0 = frow * 128 + ((fq ^ ((frow >> 1) & 7)) << 4);
-  const int rdo1 = frow * 128 + (((4 + fq) ^ ((frow >> 1) & 7)) << 4);
-  auto rd_a = [&](int s, int h, int i) -> rt_i32x4 {
-    return *(const rt_i32x4*)(smem + (s & 1) * G::SLOT + (wr * WROWS + i * 16) * 128 + (h ? rdo1 : rdo0));
-  };
-  auto rd_b = [&](int s, int h, int j) -> rt_i32x4 {
-    return *(const rt_i32x4*)(smem + (s & 1) * G::SLOT + G::A_BYTES + (wc * 128 + j * 16) * 128 + (h ? rdo1 : rdo0));
-  };
-
-  // SWAP (B fragment as the MFMA's A operand): acc[i][j][r] = C[WROWS wr + 16 i + frow][128 wc + 16 j + 4 fq + r]
-  f32x4 acc[WM][8];
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // The MFMAs are issued from asm with the accumulator tied to an AGPR ("+a"): with the builtin,
-  // hipcc selects the untied form for part of the accumulators and shuttles them through VGPRs
-  // (v_accvgpr_read / write / mov around every MFMA of the loop). Its "memory" clobber pins the
-  // LDS-DMA issues and ds_reads interleaved between the MFMAs (one per MFMA, in the MFMA's shadow).
-  // Hazards hipcc cannot see (tools/check_asm_hazards.py audits the ISA): an accumulator is re-used
-  // 8 WM - 1 MFMAs later; fragment VGPRs are rewritten by ds_reads a half-stage after their last
-  // MFMA; a row's first MFMA carries the VALU -> operand pad (s_nop 1) against a register copy at
-  // the row boundary (every MFMA outside the steady state); zero-init -> first MFMA and last MFMA ->
-  // epilogue reads are separated by explicit padding + agpr_fence.
-  auto mma = [&](int i, int j, const rt_i32x4 (&a)[WM], const rt_i32x4 (&b)[8], bool pad) {
-    if (pad) mfma_16x16x32_bf16_agpr<true>(acc[i][j], b[j], a[i]);
-    else mfma_16x16x32_bf16_agpr<false>(acc[i][j], b[j], a[i]);
-  };
-
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) agpr_fence(acc[i][j]);
-  asm volatile("s_nop 4" ::: "memory");  // zero-init (VALU) -> first MFMA srcC
-  if (s_begin < s_end) {
-    stage(s_begin);
-    if (s_begin + 1 < s_end) {
-      stage(s_begin + 1);
-      if (s_begin < ns1f && s_begin + 1 < ns1f) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(G::DMA) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    GB_BARRIER();
-    rt_i32x4 a0[WM], b0[8], a1[WM], b1[8];
-#pragma unroll
-    for (int i = 0; i < WM; ++i) a0[i] = rd_a(s_begin, 0, i);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b0[j] = rd_b(s_begin, 0, j);
-
-    // one stage s = two k-halves of WM x 8 MFMAs, one LDS-DMA / ds_read issued after an MFMA:
-    //   half 0 (a0/b0): reads of half 1 (-> a1/b1) after MFMAs 0 .. R0-1; lgkmcnt(0) + barrier B1
-    //           (every wave is done with slot s & 1) after MFMA B1-1; LDS-DMA of stage s+2 into it
-    //           after MFMAs B1 .. B1+DMA-1
-    //   half 1 (a1/b1): vmcnt (stage s+1 landed; s+2 may stay in flight) + barrier B2 after MFMA
-    //           B2-1; reads of stage s+1 half 0 (-> a0/b0) after MFMAs B2 .. B2+R0-1, the last 8
-    //           MFMAs cover their latency
-    // so a stage's DMA has ~3 half-stages (~3k MFMA cycles) to land.
-    constexpr int R0 = WM + 8, B1 = R0 + 4, B2 = WM * 8 - R0 - 8;
-    static_assert(B1 + G::DMA <= WM * 8 && B2 > 0, "w4 schedule");
-    auto stage_body = [&](int s, bool fast) {
-      const bool more = s + 1 < s_end, more2 = s + 2 < s_end;
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = i * 8 + j;
-          mma(i, j, a0, b0, !fast || j == 0);
-          if (k < WM) a1[k] = rd_a(s, 1, k);
-          else if (k < R0) b1[k - WM] = rd_b(s, 1, k - WM);
-          if (k == B1 - 1) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            GB_BARRIER();
-          }
-          if (fast && k >= B1 && k < B1 + G::DMA) dma_main(s + 2, k - B1);
-        }
-      if (!fast && more2) stage(s + 2);
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = i * 8 + j;
-          mma(i, j, a1, b1, !fast || j == 0);
-          if (k == B2 - 1) {
-            if (fast || more2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(G::DMA) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            GB_BARRIER();
-          }
-          if (k >= B2 && k < B2 + R0 && (fast || more)) {
-            if (k - B2 < WM) a0[k - B2] = rd_a(s + 1, 0, k - B2);
-            else b0[k - B2 - WM] = rd_b(s + 1, 0, k - B2 - WM);
-          }
-        }
-    };
-    int s = s_begin;
-    const int s_fast = min(s_end, ns1f) - 2;  // stage s + 2 is a full main-K stage (and s + 1 exists)
-    for (; s < s_fast; ++s) stage_body(s, true);
-    for (; s < s_end; ++s) stage_body(s, false);
-  }
-  // last MFMA (8 passes) -> v_accvgpr_read of its result; the fences keep every accumulator read
-  // below the padding
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) agpr_fence(acc[i][j]);
-  __syncthreads();
-
-  // ---- epilogue ----
-  if constexpr (OUT == O_F32) {
-    float* C = (float*)p.C;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int col = n0 + wc * 128 + j * 16 + fq * 4;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias && col < p.N) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[col + r]);
-      }
-#pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        const int row = m0 + wr * WROWS + i * 16 + frow;
-        if (row < p.M && col < p.N) {
-          float4 v;
-          v.x = act_fn(acc[i][j][0] + bv[0], EPI);
-          v.y = act_fn(acc[i][j][1] + bv[1], EPI);
-          v.z = act_fn(acc[i][j][2] + bv[2], EPI);
-          v.w = act_fn(acc[i][j][3] + bv[3], EPI);
-          *(float4*)(C + (long)row * p.ldc + col) = v;
-        }
-      }
-    }
-  } else {
-    // bf16 through LDS, one WROWS-row half at a time (the waves with wr == half write it); row
-    // stride 264 elements = 528 B: the 8-B writes of a 32-lane pass cover all 64 banks once, and
-    // 16-B aligned rows for the ds_read_b128 + 16-B global store pass
-    constexpr int LDT = 264;
-    static_assert(WROWS * LDT * 2 <= 2 * G::SLOT, "epilogue tile");
-    bf16_t* tile = (bf16_t*)smem;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      if (wr == hh) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int col = wc * 128 + j * 16 + fq * 4;
-          float bv[4] = {0.f, 0.f, 0.f, 0.f};
-          if (EPI != E_SWIGLU && p.bias && n0 + col < p.N) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[n0 + col + r]);
-          }
-#pragma unroll
-          for (int i = 0; i < WM; ++i) {
-            float y[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) y[r] = EPI == E_SWIGLU ? acc[i][j][r] : act_fn(acc[i][j][r] + bv[r], EPI);
-            *(uint2*)(tile + (i * 16 + frow) * LDT + col) = make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
-          }
-        }
-      }
-      __syncthreads();
-      if constexpr (EPI == E_SWIGLU) {
-        bf16_t* Cf = (bf16_t*)p.C;
-        const int cc = tid & 15;  // 16-B chunk of the 128-column gate half
-#pragma unroll
-        for (int pass = 0; pass < WROWS / 16; ++pass) {
-          const int row = pass * 16 + (tid >> 4);
-          const int grow = m0 + hh * WROWS + row;
-          if (grow < p.M) {
-            const uint4 g4 = *(const uint4*)(tile + row * LDT + cc * 8);
-            const uint4 u4 = *(const uint4*)(tile + row * LDT + 128 + cc * 8);
-            float g[8], u[8], f[8];
-            unpack8(g4, g);
-            unpack8(u4, u);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = g[e] / (1.f + __expf(-g[e])) * u[e];
-            const int fcol = tn * 128 + cc * 8;
-            *(uint4*)(Cf + (long)grow * p.ldc + fcol) = pack8(f);
-            if (p.C2) {
-              *(uint4*)(p.C2 + (long)grow * p.ldc2 + fcol) = g4;
-              *(uint4*)(p.C2 + (long)grow * p.ldc2 + Fh + fcol) = u4;
-            }
-          }
-        }
-      } else {
-        bf16_t* C = (bf16_t*)p.C;
-        const int cc = tid & 31;  // 16-B chunk of the 256-column row
-#pragma unroll
-        for (int pass = 0; pass < WROWS / 8; ++pass) {
-          const int row = pass * 8 + (tid >> 5);
-          const int grow = m0 + hh * WROWS + row, gcol = n0 + cc * 8;
-          if (grow < p.M && gcol < p.N) {
-            uint4 v = *(const uint4*)(tile + row * LDT + cc * 8);
-            if (p.R) {  // residual in fp32 on the bf16-rounded GEMM result (= a separate add kernel)
-              float y[8], r[8];
-              unpack8(v, y);
-              unpack8(*(const uint4*)(p.R + (long)grow * p.ldr + gcol), r);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) y[e] += r[e];
-              v = pack8(y);
-            }
-            *(uint4*)(C + (long)grow * p.ldc + gcol) = v;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
 }  // namespace gb
 }  // namespace rt
 
@@ -1423,43 +835,6 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
   const int tiles_n = act == E_SWIGLU ? p.N / bn : (p.N + bn - 1) / bn;
   dim3 grid(((p.M + 255) / 256) * tiles_n, p.nsplit), block(512);
   const int key = layout_a * 100 + layout_b * 10 + out;
-  // A/B switch: the NN / TN forms with the compiler's transposed-read builtin
-  const bool trb = tuning().gemm_tr_builtin != 0;
-  if (trb && act == E_NONE && (key == 10 || key == 112)) {
-    if (key == 10 && bn == 128) hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 128, true>), grid, block, 0, stream, p);
-    else if (key == 10) hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 256, true>), grid, block, 0, stream, p);
-    else hipLaunchKernelGGL((gemm_big_kernel<KMAJ, KMAJ, O_F32_ATOMIC, E_NONE, 256, true>), grid, block, 0, stream, p);
-    RT_LAUNCH_CHECK();
-    return 0;
-  }
-  if (bn == 4 || bn == 3) {  // 4-wave tiles: bn 3 = 192 x 256 (WM 6), bn 4 = 256 x 256 (WM 8); NT, bf16 / fp32
-    const int bm = bn == 4 ? 256 : 192;
-    const int tn4 = act == E_SWIGLU ? p.N / 256 : (p.N + 255) / 256;  // 256 output columns per tile
-    dim3 g4(((p.M + bm - 1) / bm) * tn4, p.nsplit), b4(256);
-#define W4_LAUNCH(O, E)                                                                       \
-  do {                                                                                        \
-    if (bn == 4) hipLaunchKernelGGL((gemm_w4_kernel<O, E, 8>), g4, b4, 0, stream, p);         \
-    else hipLaunchKernelGGL((gemm_w4_kernel<O, E, 6>), g4, b4, 0, stream, p);                 \
-  } while (0)
-    if (key == 0) {
-      switch (act) {
-        case E_NONE: W4_LAUNCH(O_BF16, E_NONE); break;
-        case E_RELU: W4_LAUNCH(O_BF16, E_RELU); break;
-        case E_GELU: W4_LAUNCH(O_BF16, E_GELU); break;
-        case E_GELU_TANH: W4_LAUNCH(O_BF16, E_GELU_TANH); break;
-        case E_SILU: W4_LAUNCH(O_BF16, E_SILU); break;
-        case E_SWIGLU: W4_LAUNCH(O_BF16, E_SWIGLU); break;
-        default: return -4;
-      }
-    } else if (key == 1 && act == E_NONE) {
-      W4_LAUNCH(O_F32, E_NONE);
-    } else {
-      return -4;
-    }
-#undef W4_LAUNCH
-    RT_LAUNCH_CHECK();
-    return 0;
-  }
 #define GB_LAUNCH(LA, LB, O, E, BN) hipLaunchKernelGGL((gemm_big_kernel<LA, LB, O, E, BN>), grid, block, 0, stream, p)
   if (bn == 128) {  // the 128-column tile: NT (bf16 / SwiGLU / fp32 / slab) and NN bf16
     switch (key * 10 + act) {
@@ -1472,22 +847,7 @@ static int launch_gemm_big(const Args& p, int layout_a, int layout_b, int act, i
       case 100 + E_DSWIGLU: GB_LAUNCH(ROW, KMAJ, O_BF16, E_DSWIGLU, 128); break;
       default: return -4;
     }
-  } else if (key == 0 && tuning().gemm_ring && (act == E_NONE || act == E_SWIGLU || act == E_ROPE)) {
-    // NT bf16 on the 10-slot granule ring (tuning gemm_ring)
-#define GB_RING(E) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E, 256, false, false, false, true>), grid, block, 0, stream, p)
-    switch (act) {
-      case E_NONE: GB_RING(E_NONE); break;
-      case E_SWIGLU: GB_RING(E_SWIGLU); break;
-      case E_ROPE: GB_RING(E_ROPE); break;
-      default: return -4;
-    }
-#undef GB_RING
-  } else if (key == 10 && tuning().gemm_ring && (act == E_NONE || act == E_DSWIGLU)) {  // NN bf16 on the ring
-    if (act == E_NONE)
-      hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 256, false, false, false, true>), grid, block, 0, stream, p);
-    else
-      hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_DSWIGLU, 256, false, false, false, true>), grid, block, 0, stream, p);
-  } else if (key == 0) {  // NT, bf16 out: the activation is a template parameter (no runtime switch in the epilogue)
+    } else if (key == 0) {  // NT, bf16 out: the activation is a template parameter (no runtime switch in the epilogue)
     switch (act) {
       case E_NONE: GB_LAUNCH(ROW, ROW, O_BF16, E_NONE, 256); break;
       case E_RELU: GB_LAUNCH(ROW, ROW, O_BF16, E_RELU, 256); break;
@@ -1541,58 +901,7 @@ static int num_cus() {
 // Ratio of a 256x128 tile's time to a 256x256 tile's (same K), for the wave planner below.
 static float bn128_cost() { return tuning().gemm_bn128_cost; }
 
-// Stream-K tail (gemm_big_kernel<..., SK = true>): T = tiles of 256 x 256 on C CUs with a partial
-// last wave (T % C = rem > 0). The first (T / C) * C tiles run whole, one block each (data
-// parallel); the K-steps of the last rem tiles are split evenly over `units` blocks (up to C), so
-// the tail costs rem / C of a tile's time plus a hand-off instead of a whole tile's time
-// (M = 9632 tokens x qkv: 912 tiles = 3.56 waves -> 3 + 0.56 instead of 4). Forms: NT (no
-// activation / SwiGLU) and NN, bf16 out.
-static bool streamk_form(int layout_a, int layout_b, int act, int out) {
-  const int key = layout_a * 100 + layout_b * 10 + out;
-  return (key == 0 && (act == E_NONE || act == E_SWIGLU)) || (key == 10 && act == E_NONE);
-}
-
-struct SkPlan {
-  int dp_tiles = 0, sk_tiles = 0, units = 0;
-  float cost = 1e30f;  // in 256x256 tile-wave times
-};
-
-static SkPlan streamk_plan(int tiles, int nk, int cus) {
-  SkPlan r;
-  const int full = tiles / cus, rem = tiles % cus;
-  if (full < 1 || rem == 0 || nk < 16) return r;
-  // at least 8 K-steps per unit: fewer units when the tail is small
-  const long S = (long)rem * nk;
-  r.units = (int)std::min<long>(cus, std::max<long>(rem, S / 8));
-  r.dp_tiles = full * cus;
-  r.sk_tiles = rem;
-  // tail = the longest unit's share of a tile + the hand-off (partial store, ticket, the last
-  // arriver's partial loads) and a second prologue, ~8 % of a K = 4096 tile
-  r.cost = (float)full + (float)((S + r.units - 1) / r.units) / (float)nk + 0.08f;
-  return r;
-}
-
-static int launch_gemm_big_sk(const Args& p, int layout_a, int act, const SkPlan& pl, hipStream_t stream) {
-  Args q = p;
-  q.sk_dp = pl.dp_tiles;
-  q.sk_tiles = pl.sk_tiles;
-  q.sk_units = pl.units;
-  q.nsplit = 1;
-  dim3 grid(pl.dp_tiles + pl.units, 1), block(512);
-  if (layout_a != ROW) return -4;
-  if (p.b_layout_kmaj) {
-    hipLaunchKernelGGL((gemm_big_kernel<ROW, KMAJ, O_BF16, E_NONE, 256, false, false, true>), grid, block, 0, stream, q);
-  } else if (act == E_SWIGLU) {
-    hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_SWIGLU, 256, false, false, true>), grid, block, 0, stream, q);
-  } else {
-    hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_NONE, 256, false, false, true>), grid, block, 0, stream, q);
-  }
-  RT_LAUNCH_CHECK();
-  return 0;
-}
-
-static int gemm_big_planned(const Args& p, int layout_a, int layout_b, int act, int out, int bn, float* sk_part,
-                            unsigned* sk_tickets, hipStream_t stream);
+static int gemm_big_planned(const Args& p, int layout_a, int layout_b, int act, int out, int bn, hipStream_t stream);
 
 // layout_a / layout_b: 0 = ROW (K contiguous), 1 = KMAJ (M / N contiguous).
 // out: 0 bf16 (epilogue bias + act, or SwiGLU), 1 fp32 store (bias + act), 2 fp32 atomic add
@@ -1602,13 +911,10 @@ static int gemm_big_planned(const Args& p, int layout_a, int layout_b, int act, 
 // (e.g. M = 9632 tokens x N = 4096: 608 tiles = 2.4 waves of 256 CUs -> 512 tiles + 192 half tiles).
 // Requirements (checked): KMAJ operands have M / N % 8 == 0 and 16-B aligned rows; ROW operands
 // 16-B aligned rows; K, K2 % 8 == 0; E_SWIGLU: ROW/ROW, bf16 out, N % 256 == 0.
-// sk_part / sk_tickets: the stream-K workspace (>= 2 * cus partial slots of 256 x 256 fp32, >= cus
-// zeroed tickets, one per stream) or null (no stream-K).
 extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb,
                            const void* A2, long lda2, const void* B2, long ldb2, int K2, const void* bias,
                            void* C, long ldc, void* C2, long ldc2, const void* R, long ldr, int M, int N, int K,
-                           int act, int out, int nsplit, const void* zpage, int bn, float* sk_part,
-                           unsigned* sk_tickets, hipStream_t stream) {
+                           int act, int out, int nsplit, const void* zpage, int bn, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (act == E_ROPE) return -5;  // rt_gemm_big_rope (the rotary tables are its arguments)
   // a ROW operand reads 8-element k-chunks: its reduction length must be a multiple of 8
@@ -1631,11 +937,8 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   } else if (act != E_NONE && (layout_a != ROW || layout_b != ROW || out != O_BF16)) {
     return -5;
   }
-  if (bn != 0 && bn != 128 && bn != 256 && bn != 4 && bn != 3) return -8;
+  if (bn != 0 && bn != 128 && bn != 256) return -8;
   if (bn == 128 && !bn128_supported(layout_a, layout_b, act, out)) return -8;
-  if ((bn == 4 || bn == 3) && (act == E_ROPE || layout_a != ROW || layout_b != ROW || (out != O_BF16 && out != O_F32) ||
-                               nsplit != 1 || (long)N * ldb * 2 >= (1L << 32) || (long)M * lda * 2 >= (1L << 32)))
-    return -8;
   Args p{};
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
   p.A2 = (A2 && B2) ? (const bf16_t*)A2 : nullptr; p.lda2 = lda2;
@@ -1644,21 +947,17 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
   p.R = (const bf16_t*)R; p.ldr = ldr;
   p.M = M; p.N = N; p.K = K; p.act = act; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
   p.group_m = tuning().gemm_group_m;
-  // tuning gemm_b_nt = 1: non-temporal weight stream when one row tile covers M (each B byte read
-  // once per launch). Measured neutral on the batch-256 decode GEMMs (profiles/decode_nt_ab.log): off
-  p.b_nt = layout_b == ROW && M <= 256 && tuning().gemm_b_nt > 0;
-  return gemm_big_planned(p, layout_a, layout_b, act, out, bn, sk_part, sk_tickets, stream);
+  return gemm_big_planned(p, layout_a, layout_b, act, out, bn, stream);
 }
 
-// bn = 0: the wave planner (and the optional stream-K tail) over validated arguments p
-static int gemm_big_planned(const Args& p, int layout_a, int layout_b, int act, int out, int bn, float* sk_part,
-                            unsigned* sk_tickets, hipStream_t stream) {
+// bn = 0: the wave planner over validated arguments p
+static int gemm_big_planned(const Args& p, int layout_a, int layout_b, int act, int out, int bn, hipStream_t stream) {
   if (bn != 0) return launch_gemm_big(p, layout_a, layout_b, act, out, bn, stream);
-  const int M = p.M, N = p.N, K = p.K, K2 = p.K2, nsplit = p.nsplit;
+  const int M = p.M, N = p.N, nsplit = p.nsplit;
   const long lda = p.lda, lda2 = p.lda2, ldc = p.ldc, ldc2 = p.ldc2, ldr = p.ldr;
   void* C = p.C;
   const bool can128 = bn128_supported(layout_a, layout_b, act, out);
-  // ---- plan: m1 row tiles at BN = 256, the rest at BN = 128; or a stream-K tail ----
+  // ---- plan: m1 row tiles at BN = 256, the rest at BN = 128 ----
   const int tiles_m = (M + 255) / 256;
   const int tn256 = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
   const int tn128 = act == E_SWIGLU ? N / 128 : (N + 127) / 128;
@@ -1672,17 +971,6 @@ static int gemm_big_planned(const Args& p, int layout_a, int layout_b, int act, 
       const long w256 = ((long)m * tn256 + cus - 1) / cus, w128 = ((long)(tiles_m - m) * tn128 + cus - 1) / cus;
       const float cost = (float)w256 + r * (float)w128;
       if (cost < best - 1e-3f) { best = cost; m1 = m; }
-    }
-  }
-  if (tuning().gemm_streamk && sk_part && sk_tickets && nsplit == 1 && streamk_form(layout_a, layout_b, act, out)) {
-    const int nk = (K + 63) / 64 + (p.A2 ? (K2 + 63) / 64 : 0);
-    const SkPlan pl = streamk_plan(tiles_m * tn256, nk, (int)cus);
-    if (pl.units > 0 && (pl.cost < best || tuning().gemm_streamk == 2)) {
-      Args q = p;
-      q.sk_part = sk_part;
-      q.sk_tickets = sk_tickets;
-      q.b_layout_kmaj = layout_b == KMAJ;
-      return launch_gemm_big_sk(q, layout_a, act, pl, stream);
     }
   }
   if (m1 == tiles_m) return launch_gemm_big(p, layout_a, layout_b, act, out, 256, stream);
@@ -1727,9 +1015,8 @@ extern "C" int rt_gemm_big_rope(const void* A, long lda, const void* B, long ldb
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc;
   p.M = M; p.N = N; p.K = K; p.act = E_ROPE; p.nsplit = 1; p.zpage = (const bf16_t*)zpage;
   p.group_m = tuning().gemm_group_m;
-  p.b_nt = M <= 256 && tuning().gemm_b_nt > 0;
   p.rope_pos = pos; p.rope_cos = cosT; p.rope_sin = sinT; p.rope_cols = rope_cols; p.rope_d = rope_d;
-  return gemm_big_planned(p, ROW, ROW, E_ROPE, O_BF16, bn, nullptr, nullptr, stream);
+  return gemm_big_planned(p, ROW, ROW, E_ROPE, O_BF16, bn, stream);
 }
 
 // W8A8 on the gemm_big schedule (config 5 prefill / reference scoring): A [M, K] e4m3fn with
@@ -1752,7 +1039,7 @@ extern "C" int rt_gemm_big_fp8(const void* A, long lda, const float* sa, const v
   p.A = (const bf16_t*)A; p.lda = lda / 2; p.B = (const bf16_t*)B; p.ldb = ldb / 2;
   p.A2 = (const bf16_t*)A2; p.lda2 = lda2; p.B2 = (const bf16_t*)B2; p.ldb2 = ldb2; p.K2 = A2 ? K2 : 0;
   p.bias = (const bf16_t*)bias; p.C = C; p.ldc = ldc; p.C2 = (bf16_t*)C2; p.ldc2 = ldc2; p.R = nullptr; p.ldr = 0;
-  p.M = M; p.N = N; p.K = K / 2; p.act = act; p.nsplit = 1; p.zpage = (const bf16_t*)(zpage ? zpage : A); p.b_nt = 0;
+  p.M = M; p.N = N; p.K = K / 2; p.act = act; p.nsplit = 1; p.zpage = (const bf16_t*)(zpage ? zpage : A);
   p.sa = sa; p.sb = sb;
   const int tiles_m = (M + 255) / 256;
   const int tn256 = act == E_SWIGLU ? N / 256 : (N + 255) / 256;
@@ -1769,11 +1056,11 @@ extern "C" int rt_gemm_big_fp8(const void* A, long lda, const float* sa, const v
     const int tn = bn == 256 ? (act == E_SWIGLU ? q.N / 256 : (q.N + 255) / 256) : (act == E_SWIGLU ? q.N / 128 : (q.N + 127) / 128);
     dim3 grid(((q.M + 255) / 256) * tn, 1), block(512);
     if (bn == 256) {
-      if (act == E_SWIGLU) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_SWIGLU, 256, false, true>), grid, block, 0, stream, q);
-      else hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_NONE, 256, false, true>), grid, block, 0, stream, q);
+      if (act == E_SWIGLU) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_SWIGLU, 256, true>), grid, block, 0, stream, q);
+      else hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_NONE, 256, true>), grid, block, 0, stream, q);
     } else {
-      if (act == E_SWIGLU) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_SWIGLU, 128, false, true>), grid, block, 0, stream, q);
-      else hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_NONE, 128, false, true>), grid, block, 0, stream, q);
+      if (act == E_SWIGLU) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_SWIGLU, 128, true>), grid, block, 0, stream, q);
+      else hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_BF16, E_NONE, 128, true>), grid, block, 0, stream, q);
     }
   };
   if (m1 > 0) {

@@ -254,12 +254,26 @@ def _adapter_view(policy, path: Optional[str]):
 
 
 def _held_out_records(cfg, st, n: int):
-    """Evaluation queries disjoint from the training sample of ``_records`` (another seed) with
-    their retrieved documents; the configured training file when one is given."""
-    if cfg.data.train_path or n <= 0:
-        return _records(cfg, st, n)[:n] if n > 0 else []
+    """Evaluation queries with their retrieved documents, none of which occurs in the training
+    sample of ``_records`` (the synthetic fact set is finite: a second seed alone can repeat
+    training queries). With a configured training file the items come from that file and are NOT
+    held out; that is printed."""
+    if n <= 0:
+        return []
+    if cfg.data.train_path:
+        print(f"[eval] data.train_path is set: evaluating on items of {cfg.data.train_path} (not held out)")
+        return _records(cfg, st, n)[:n]
     corpus, index, enc = st["corpus"], st["index"], st["encoder"]
-    items = corpus.sample_queries(n, seed=cfg.model.seed + 1013)
+    train = {it.query for it in corpus.sample_queries(cfg.data.n_queries, seed=cfg.model.seed + 11)}
+    items, seen = [], set()
+    for it in corpus.sample_queries(max(8 * n, 64), seed=cfg.model.seed + 1013):
+        if it.query not in train and it.query not in seen:
+            seen.add(it.query)
+            items.append(it)
+            if len(items) == n:
+                break
+    if not items:
+        raise RuntimeError("no evaluation query outside the training sample: enlarge the corpus")
     _, ids = index.search(enc.encode([it.query for it in items]), cfg.retrieval.top_k)
     return [{"query": it.query, "retrieved_docs": [st["docs"][i] for i in row if i >= 0],
              "ground_truth": it.ground_truth} for it, row in zip(items, ids.tolist())]

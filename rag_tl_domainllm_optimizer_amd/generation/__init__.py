@@ -135,6 +135,11 @@ class Generator:
         self.use_graph = use_graph and self.device.type == "cuda"
         self.value_head = value_head
         self.sync_every = sync_every
+        # generation never differentiates: by default adapters run on merged bf16 weights (one
+        # weight stream per projection). False: the unmerged LoRA K-extension, i.e. exactly the
+        # weights the training forward scores with (PPO behaviour policy == target policy at
+        # theta_old, PPOConfig.merged_lora_rollout = False)
+        self.merge_lora = True
         # fp8 K/V cache (config 5): the model's setting unless given; GPU MFMA decode kernels only
         # (head_dim 128), the CPU path runs the quantise / dequantise reference
         kv_fp8 = getattr(model, "kv_fp8", False) if kv_fp8 is None else kv_fp8
@@ -296,7 +301,7 @@ class Generator:
         sub = _SubCache(self.cache, B)
         # generation never differentiates: run adapters on merged weights (one weight stream per
         # projection; the merged images are refreshed in place after each adapter update)
-        prev_merged = self.model.set_lora_merged(True) if hasattr(self.model, "set_lora_merged") else None
+        prev_merged = self.model.set_lora_merged(self.merge_lora) if hasattr(self.model, "set_lora_merged") else None
         try:
             return self._enqueue(params, B, S, T, ids, start, eos, eos_list, pad_id, sub, early_stop, t0, ev)
         finally:
@@ -445,7 +450,7 @@ class _Pending:
             # adapters merged (generate_async restored the caller's mode on return; the eager
             # non-graph path would otherwise decode with unmerged adapters)
             m = g.model
-            prev = m.set_lora_merged(True) if hasattr(m, "set_lora_merged") else None
+            prev = m.set_lora_merged(g.merge_lora) if hasattr(m, "set_lora_merged") else None
             try:
                 self.loop.run(to_end=True)
             finally:
@@ -556,7 +561,7 @@ class ContinuousBatcher:
             g.out_values = torch.zeros(MB, T, dtype=torch.float32, device=dev)
             g.runner.reset()
         g._nb = 1
-        self._prev_merged = g.model.set_lora_merged(True) if hasattr(g.model, "set_lora_merged") else None
+        self._prev_merged = g.model.set_lora_merged(g.merge_lora) if hasattr(g.model, "set_lora_merged") else None
         if hasattr(g.model, "refresh_decode_weights"):
             g.model.refresh_decode_weights()
         if T > 1:

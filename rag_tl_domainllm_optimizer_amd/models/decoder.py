@@ -117,11 +117,10 @@ class DecoderLayer(nn.Module):
             if name in self._shufc:  # images exist once a batch <= 16 decode ran
                 self._shufc[name].get(w)
 
-    def decode_fused(self, h, attend, attend_o=None):
+    def decode_fused(self, h, attend):
         """One Llama/Mistral layer of a decode step in four kernels: [RMSNorm folded into the qkv
         GEMM] -> attention (RoPE + append + split-K) -> [o GEMM + residual] -> [RMSNorm folded into
-        the gate/up GEMM + SwiGLU] -> [down GEMM + residual]. ``h`` is the bf16 residual stream.
-        ``attend_o`` (batch 1): attention and o GEMM + residual in one launch — three kernels."""
+        the gate/up GEMM + SwiGLU] -> [down GEMM + residual]. ``h`` is the bf16 residual stream."""
         cfg = self.cfg
         eps = cfg.norm_eps
         m = h.shape[0]
@@ -130,10 +129,7 @@ class DecoderLayer(nn.Module):
         qkv = ops.gemm_decode(h, wq, norm_eps=eps, fp8=f8, shuf=sh)
         wo = self._w_eff("o_w", "o")
         f8, sh = self._dec_caches("o", "o", wo, m)
-        h_new = attend_o(qkv, wo, h) if (attend_o is not None and f8 is None) else None
-        if h_new is None:
-            h_new = ops.gemm_decode(attend(qkv), wo, residual=h, fp8=f8, shuf=sh)
-        h = h_new
+        h = ops.gemm_decode(attend(qkv), wo, residual=h, fp8=f8, shuf=sh)
         wgu = self._fold.setdefault("gate_up", ops.FoldCache()).get(self._w_eff("gate_up_w", "gate_up"), self.ln2_w)
         f8, sh = self._dec_caches("gate_up_folded", "gate_up", wgu, m)
         f = ops.gemm_decode(h, wgu, act=ops.ACT_SWIGLU, norm_eps=eps, fp8=f8, shuf=sh)
@@ -219,10 +215,6 @@ class CausalLM(nn.Module):
         self.fused_decode_max_batch_fp8 = 64
         # decode at batch > 64: leave split-K partials for the consumer kernels to sum
         self.defer_splitk = True
-        # batch 1: attention + o_proj + residual in one launch (ops.decode_step_attention_o). Off by
-        # default: measured 26.4 vs 25.0 us per layer for the two-kernel path (docs/DESIGN.md,
-        # profiles/kernels_attn_o_fused_rejected.log); RAGTL_ATTN_O=1 turns it on
-        self.fused_attn_o = os.environ.get("RAGTL_ATTN_O", "0") == "1"
         # fp8 (e4m3fn) K/V cache for generators built on this model (config 5, ``model.fp8_kv``)
         self.kv_fp8 = False
         if init:
@@ -414,12 +406,7 @@ class CausalLM(nn.Module):
                     return ops.decode_step_attention(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads,
                                                      pos, cos, sin, kv_start, cfg.sliding_window,
                                                      workspace=workspace, k_scale=ks, v_scale=vs)
-
-                def attend_o(qkv, w_o, res, li=li):
-                    return ops.decode_step_attention_o(qkv, cache.k[li], cache.v[li], slot, attn_len, cfg.num_heads,
-                                                       w_o, res, pos, cos, sin, kv_start, cfg.sliding_window,
-                                                       workspace=workspace)
-                h = layer.decode_fused(h, attend, attend_o if (self.fused_attn_o and not kv8) else None)
+                h = layer.decode_fused(h, attend)
             y, _ = ops.rms_norm(h, self.norm_w, cfg.norm_eps)
             return y
         residual = None

@@ -8,7 +8,7 @@ from .linear import (  # noqa: F401
     linear_deferred)
 from .norm import layer_norm, rms_norm  # noqa: F401
 from .attention import (  # noqa: F401
-    attention, decode_attention, decode_step_attention, decode_step_attention_o, decode_workspace, flash_attention_packed, gather_rows, packed_inverse, scatter_rows,
+    attention, decode_attention, decode_step_attention, decode_workspace, flash_attention_packed, gather_rows, packed_inverse, scatter_rows,
     flash_attention_qkv, rope_qkv, rope_qkv_, FP8_KV_D, kv_dequantize, kv_quantize_rows, kv_store_fp8,
 )
 from .misc import (embedding, gae, ivf_scan, ppo_advantages, pool_normalize, ppo_loss, sample, segment_mean, swiglu,  # noqa: F401

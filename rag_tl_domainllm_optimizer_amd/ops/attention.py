@@ -379,27 +379,6 @@ def decode_step_attention(qkv, k_cache, v_cache, slot, attn_len, Hq, pos=None, c
     return out
 
 
-def decode_step_attention_o(qkv, k_cache, v_cache, slot, attn_len, Hq, w_o, residual, pos=None, cos=None, sin=None,
-                            kv_start=None, window=0, scale=None, workspace=None, stamps=None):
-    """Batch-1 decode step of a layer in ONE launch: fused attention (as ``decode_step_attention``)
-    followed by ``o_proj`` and the residual add: returns ``residual + attn @ w_o^T`` [1, H], or
-    None when the shape is not covered (batch != 1, Hq*D != 4096, CPU, ...) — the caller then runs
-    the two-kernel path. The o_proj weight slice of every workgroup streams into LDS while the
-    attention partials are computed (csrc/kernels/attention.hip, attn_o_fused_kernel)."""
-    if not on_gpu(qkv) or qkv.shape[0] != 1 or workspace is None or len(workspace) < 4:
-        return None
-    B, Hkv, Smax, D = k_cache.shape
-    if Hq * D != 4096 or w_o.shape[0] % 16 or w_o.stride(1) != 1:
-        return None
-    scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    part, PS, sync = workspace[0], workspace[1], workspace[3]
-    out = torch.empty_like(residual)
-    ok = native().attn_o_fused(qkv.contiguous(), k_cache, v_cache, slot, attn_len, kv_start, pos, cos, sin, 1.0,
-                               window, scale, Hq, part, PS, w_o, residual.contiguous(), out, sync[:2], sync[2:],
-                               stamps)
-    return out if ok else None
-
-
 def decode_attention(q, k_cache, v_cache, kv_len, Hq, kv_start=None, window=0, scale=None, workspace=None, out=None):
     """One query token per sequence against a KV cache [B, Hkv, Smax, D] -> [B, Hq*D]."""
     B, Hkv, Smax, D = k_cache.shape

@@ -46,7 +46,15 @@ def gemm_fp8(x: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor, bias=None, act
         if M <= 64:
             return C.gemm_fp8(x, None, wq, sw, bias, act, out)
         xq, sx = quantize_fp8(x)
-        return C.gemm_fp8(xq, sx, wq, sw, bias, act, out)
+        if act in (0, 5):
+            return C.gemm_fp8(xq, sx, wq, sw, bias, act, out)
+        # W8A8 kernels fuse bias and SwiGLU only (the decoder presets use nothing else): other
+        # activations run on the bf16 GEMM output
+        y = ref.apply_act(C.gemm_fp8(xq, sx, wq, sw, bias, 0, None).float(), act).to(x.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
     xf = x.float() if M <= 64 else dequantize_fp8(*quantize_fp8(x))
     y = xf @ dequantize_fp8(wq, sw).t()
     if bias is not None:

@@ -88,7 +88,11 @@ class MixedFlatParams:
     one 288 GB MI355X beside a frozen reference copy, the KV cache and the activations.
     """
 
-    def __init__(self, params: Iterable[torch.nn.Parameter], align: int = 16):
+    def __init__(self, params: Iterable[torch.nn.Parameter], align: int = 16, keep_master: bool = True):
+        """``keep_master=False`` (ZeRO-1, :class:`parallel.zero.ZeroAdamW`): no fp32 master of the
+        bf16 members here — each rank's optimizer keeps the master of its own shard — and ``data``
+        holds only the fp32 tail (``master_base = n16``). ``align``: element alignment of every
+        member; ZeRO passes 16 x world so every bucket splits into equal 16-element shards."""
         params = list(params)
         if not params:
             raise ValueError("MixedFlatParams: no parameters")
@@ -108,22 +112,27 @@ class MixedFlatParams:
             self.offsets.append(off)
             off += _round(p.numel(), align)
         self.numel = off
-        self.data = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.align = align
+        self.master_base = 0 if keep_master else self.n16
+        self.data = torch.zeros(off - self.master_base, dtype=torch.float32, device=dev)
         self.data16 = torch.zeros(self.n16, dtype=torch.bfloat16, device=dev)
         self.grad16 = torch.zeros(self.n16, dtype=torch.bfloat16, device=dev)
         self.grad32 = torch.zeros(off - self.n16, dtype=torch.float32, device=dev)
         with torch.no_grad():
             for p, o in zip(self.params, self.offsets):
                 n = p.numel()
-                self.data[o:o + n].copy_(p.detach().reshape(-1))
+                if o >= self.master_base:
+                    self.data[o - self.master_base:o - self.master_base + n].copy_(p.detach().reshape(-1))
                 if p.dtype == torch.bfloat16:
                     self.data16[o:o + n].copy_(p.detach().reshape(-1))
                 p.data = self._param_view(p, o)
                 p.grad = self._grad_view(p, o)
 
     def _param_view(self, p, o):
-        buf = self.data16 if p.dtype == torch.bfloat16 else self.data
-        return buf[o:o + p.numel()].view(p.shape)
+        if p.dtype == torch.bfloat16:
+            return self.data16[o:o + p.numel()].view(p.shape)
+        o -= self.master_base
+        return self.data[o:o + p.numel()].view(p.shape)
 
     def _grad_view(self, p, o):
         n = p.numel()
@@ -167,6 +176,8 @@ class MixedFlatParams:
 
     def refresh_shadow(self):
         """bf16 compute copies <- fp32 master (after a checkpoint load or a CPU optimizer step)."""
+        if self.master_base:
+            raise RuntimeError("MixedFlatParams(keep_master=False): the master lives in the ZeRO shards")
         with torch.no_grad():
             self.data16.copy_(self.data[:self.n16])
         self.bump_versions()
@@ -179,12 +190,12 @@ class MixedFlatParams:
             torch.autograd.graph.increment_version(self.params[:self.n_params16])
 
 
-def flat_params(params: Iterable[torch.nn.Parameter], align: int = 16):
+def flat_params(params: Iterable[torch.nn.Parameter], align: int = 16, keep_master: bool = True):
     """FlatParams for fp32 trainables (LoRA adapters, value head, fp32 CPU models);
     MixedFlatParams as soon as a bf16 weight trains (full-parameter fine-tuning on the GPU)."""
     params = list(params)
     if any(p.dtype == torch.bfloat16 for p in params):
-        return MixedFlatParams(params, align)
+        return MixedFlatParams(params, align, keep_master)
     return FlatParams(params, align)
 
 

@@ -197,7 +197,12 @@ def save_checkpoint(prefix: str, model, tokenizer, value_head=None, optimizer=No
 
         tmp = _atomic_dir(f"{prefix}_trainer_state")
         st = dict(trainer_state or {})
-        if optimizer is not None:
+        if optimizer is not None and getattr(optimizer, "sharded", False):
+            # ZeRO-1: metadata here, tensors per rank (ZeroAdamW.save_shard, called on every rank)
+            osd = optimizer.state_dict()
+            st["optimizer"] = {k: v for k, v in osd.items() if k != "skipped"}
+            st["optimizer"]["skipped"] = int(osd["skipped"])
+        elif optimizer is not None:
             osd = optimizer.state_dict()
             save_file({"exp_avg": osd["exp_avg"].cpu().contiguous(), "exp_avg_sq": osd["exp_avg_sq"].cpu().contiguous(),
                        "params": optimizer.flat.data.cpu().contiguous()},
@@ -234,7 +239,11 @@ def load_checkpoint(prefix: str, model, value_head=None, optimizer=None, load_po
     if os.path.isdir(tsd):
         with open(os.path.join(tsd, "state.json")) as f:
             st = json.load(f)
-        if optimizer is not None and os.path.exists(os.path.join(tsd, "optimizer.safetensors")):
+        if optimizer is not None and getattr(optimizer, "sharded", False):
+            osd = dict(st.get("optimizer", {}))
+            optimizer.load_state_dict(osd)
+            optimizer.load_shard(tsd)  # collective: every rank loads its shard, bf16 copy all-gathered
+        elif optimizer is not None and os.path.exists(os.path.join(tsd, "optimizer.safetensors")):
             from safetensors.torch import load_file
 
             t = load_file(os.path.join(tsd, "optimizer.safetensors"))

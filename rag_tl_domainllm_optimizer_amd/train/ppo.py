@@ -34,6 +34,7 @@ from .. import ops
 from ..generation import Generator, SamplingParams
 from ..models import ValueHead
 from ..parallel import GradSync, info as dist_info, reduce_metrics
+from ..parallel.zero import ZeroAdamW, zero_enabled
 from ..rag.prompt import build_prompt, encode_prompt, extract_answer
 from ..runtime import PhaseTimer, StreamPair
 from ..utils import MetricsSink, maybe_inject_fault
@@ -72,10 +73,17 @@ class PPOConfig:
     lora_alpha: float = 32.0
     lora_targets: Sequence[str] = ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj")
     full_finetune: bool = False         # True: every weight (the reference's mode, rl.py:153)
+    zero: bool = True                   # full_finetune at world > 1: ZeRO-1 sharded fp32 optimizer state
     gradient_checkpointing: bool = False
     overlap_reward: bool = True      # reward encoder on a side stream beside the reference forward
     rollout_chunks: int = 1          # >1: score chunk i while chunk i+1 decodes
     merged_lora_rollout: bool = True  # decode/prefill rollouts on W + sBA (refreshed per update)
+    # where the PPO ratio's theta_old log-probs / values come from: "rollout" = the sampler of the
+    # decode engine (free; differs from the training forward by the two engines' bf16 numerics,
+    # ~0.09 nats / token on a random-init Mistral-7B, profiles/r5/behaviour_gap_7b.log), or
+    # "recompute" = one no-grad training-numerics forward of the policy over the rollouts beside the
+    # reference forward (ratio exactly 1 at theta = theta_old; costs a forward)
+    old_logp: str = "rollout"
     lr_schedule: str = "constant"
     save_every: int = 0              # CLI: mid-epoch "latest" checkpoint every N steps (0 = epoch ends)
     save_full_policy: bool = True    # epoch / best checkpoints also write the merged HF policy
@@ -161,15 +169,26 @@ class PPOTrainer:
         self.value_head = value_head or ValueHead(policy.cfg.hidden_size, device=self.device, seed=c.seed + 17)
         # trainables + value head re-homed into one flat buffer (fused AdamW, bucketed all-reduce):
         # fp32 LoRA adapters, or bf16 compute copies + fp32 master under full fine-tuning
-        self.flat = ops.flat_params(trainable + list(self.value_head.parameters()))
+        if zero_enabled(c.full_finetune, c.zero) and any(p.dtype == torch.bfloat16 for p in trainable):
+            # ZeRO-1 (parallel.zero): each rank keeps the fp32 master / moments of 1/N of every
+            # bucket; fp32 reduce-scatter of the gradients, bf16 all-gather of the updated weights
+            w = dist_info().world
+            self.flat = ops.flat_params(trainable + list(self.value_head.parameters()), align=16 * w,
+                                        keep_master=False)
+            self.opt = ZeroAdamW(self.flat, lr=c.lr, betas=c.betas, eps=c.eps, weight_decay=c.weight_decay,
+                                 max_grad_norm=c.max_grad_norm, bucket_bytes=int(4 * c.bucket_mb * (1 << 20)))
+            self.sync = self.opt.sync
+        else:
+            self.flat = ops.flat_params(trainable + list(self.value_head.parameters()))
+            self.opt = ops.FusedAdamW(self.flat, lr=c.lr, betas=c.betas, eps=c.eps, weight_decay=c.weight_decay,
+                                      max_grad_norm=c.max_grad_norm)
+            self.sync = GradSync(self.flat, bucket_bytes=int(c.bucket_mb * (1 << 20)))
         policy.refresh_lora()
-        self.opt = ops.FusedAdamW(self.flat, lr=c.lr, betas=c.betas, eps=c.eps, weight_decay=c.weight_decay,
-                                  max_grad_norm=c.max_grad_norm)
-        self.sync = GradSync(self.flat, bucket_bytes=int(c.bucket_mb * (1 << 20)))
         self.kl = AdaptiveKL(c.kl_coef, c.target_kl, c.kl_horizon) if c.adaptive_kl else None
         self.max_batch = max_batch
         self.gen = Generator(policy, max_batch, c.max_prompt_tokens + c.max_new_tokens + 8, self.device,
                              value_head=self.value_head)
+        self.gen.merge_lora = c.merged_lora_rollout
         self.sampling = SamplingParams(max_new_tokens=c.max_new_tokens, temperature=c.temperature, top_k=c.top_k,
                                        top_p=c.top_p, do_sample=True, seed=c.seed + 1000 * dist_info().rank)
         self.streams = StreamPair(self.device)
@@ -309,6 +328,22 @@ class PPOTrainer:
                 self.overlap_events["ref_start"] = _event()
             # the frozen reference: adapters off (LoRA) or the starting-weight copy (full FT)
             ref_model = self.ref_policy if self.ref_policy is not None else self.policy
+            if c.old_logp == "recompute":
+                # theta_old log-probs and values in the training forward's numerics (LoRA on, unmerged)
+                self.policy.set_lora_enabled(True)
+                old_lp, old_v = [], []
+                mb = max(c.minibatch_size, c.ref_minibatch_size)
+                hl = ro.host_lengths
+                for s in range(0, ro.resp.shape[0], mb):
+                    lp, _, v, _ = score_sequences(self.policy, ro.prompt_ids[s:s + mb], ro.start[s:s + mb],
+                                                  ro.resp[s:s + mb], ro.resp_len[s:s + mb], 1.0 / c.temperature,
+                                                  self.value_head,
+                                                  lengths=(hl[0][s:s + mb], hl[1][s:s + mb]) if hl else None)
+                    old_lp.append(lp)
+                    old_v.append(v)
+                ro.rollout_logp = ro.old_logp
+                ro.old_logp = torch.cat(old_lp, 0).to(ro.old_logp.dtype)
+                ro.old_values = torch.cat(old_v, 0).to(ro.old_values.dtype)
             ref_model.set_lora_enabled(False)
             try:
                 ref_lp = []
@@ -360,6 +395,19 @@ class PPOTrainer:
                     loss, st = ops.ppo_loss(lp, vals, ent, ro.old_logp[idx], ro.adv[idx], ro.returns[idx], mask,
                                             c.clip_range, c.value_coef, c.entropy_coef, c.value_clip,
                                             ro.old_values[idx] if c.value_clip is not None else None)
+                    if not stats:
+                        # behaviour / target policy gap: the first minibatch scores the
+                        # rollouts at theta = theta_old, so |logp - old_logp| is the rollout engine's
+                        # (merged LoRA, decode kernels) deviation from the training forward
+                        with torch.no_grad():
+                            mf = mask.float()
+                            first_gap = ((lp.detach().float() - ro.old_logp[idx].float()).abs() * mf).sum() / \
+                                mf.sum().clamp(min=1.0)
+                            # the rollout engine's own deviation (sampler log-probs vs the training
+                            # forward at theta_old), whatever old_logp source the ratio uses
+                            rl_lp = getattr(ro, "rollout_logp", None)
+                            engine_gap = first_gap if rl_lp is None else \
+                                ((lp.detach().float() - rl_lp[idx].float()).abs() * mf).sum() / mf.sum().clamp(min=1.0)
                     self.opt.zero_grad()
                     self.sync.start()
                     loss.backward()
@@ -372,6 +420,9 @@ class PPOTrainer:
         sm = torch.stack(stats).mean(0).tolist()
         out = {"total_loss": sm[0], "policy_loss": sm[1], "value_loss": sm[2], "entropy": sm[3],
                "entropy_loss": -c.entropy_coef * sm[3], "approx_kl": sm[4], "clipfrac": sm[5]}
+        out["behaviour_logp_gap"] = float(first_gap)
+        out["rollout_engine_logp_gap"] = float(engine_gap)
+        out["clipfrac_first_mb"] = float(stats[0][5])
         out["grad_norm"] = float(self.opt.last_norm)
         out["skipped_steps"] = float(self.opt.skipped)
         out["time/allreduce_wait"] = self.sync.wait_s
@@ -436,6 +487,8 @@ class PPOTrainer:
         barrier()
         if not di.is_main:
             save_rank_rng(prefix, di.rank, rng_state())
+        if getattr(self.opt, "sharded", False):  # ZeRO-1: every rank writes its optimizer shard
+            self.opt.save_shard(f"{prefix}_trainer_state")
         barrier()
 
     def load_checkpoint(self, prefix: str) -> dict:

@@ -148,3 +148,14 @@ def test_cli_sft_resume_and_epoch_checkpoints(tmp_path, capsys):
     assert (ck / "epoch_2_trainer_state").is_dir()
     # a PPO resume in the same run directory must not pick up an SFT checkpoint
     assert cli.latest_checkpoint(str(tmp_path / "run")) is None
+
+
+def test_held_out_eval_records_disjoint_from_training(tmp_path):
+    """Evaluation items never repeat a training query (the synthetic fact set is finite, so a
+    second sampling seed alone would)."""
+    cfg = C.load(overrides=_tiny(tmp_path) + ["--data.n_queries=48"])
+    st = cli.build_stack(cfg, cli._device().device, need_policy=False)
+    train = {r["query"] for r in cli._records(cfg, st, cfg.data.n_queries)}
+    held = cli._held_out_records(cfg, st, 16)
+    assert held and not ({r["query"] for r in held} & train)
+    assert len({r["query"] for r in held}) == len(held)

@@ -237,3 +237,69 @@ def test_dp_cli_pipeline_world2(tmp_path):
     run = tmp_path / "run"
     assert os.path.isdir(run / "sft_adapter") and os.path.isdir(run / "best_model_adapter")
     assert os.path.exists(run / "metrics.jsonl")
+
+
+def _zero_ppo_worker(rank, world, port, out_dir, zero):
+    _env(rank, world, port)
+    from rag_tl_domainllm_optimizer_amd import models, parallel
+    from rag_tl_domainllm_optimizer_amd.data import RecordLoader, SyntheticCorpus
+    from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
+    from rag_tl_domainllm_optimizer_amd.retrieval import Encoder
+    from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
+    from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
+    from rag_tl_domainllm_optimizer_amd.train.ppo import PPOConfig, PPOTrainer
+
+    parallel.init(device="cpu")
+
+    def setup():
+        torch.manual_seed(0)
+        cfg = PRESETS["tiny-llama"]
+        tok = Tokenizer.synthetic(cfg.vocab_size, "llama")
+        policy = models.CausalLM(cfg, dtype=torch.bfloat16, seed=1)
+        ecfg = PRESETS["tiny-bert"]
+        enc = Encoder(models.SentenceEncoder(ecfg, dtype=torch.float32, seed=2).eval(),
+                      Tokenizer.synthetic(ecfg.vocab_size, "bert"), max_length=64)
+        corpus = SyntheticCorpus(tok.words(), n_docs=40, doc_words=20, seed=3)
+        recs = [{"query": it.query, "retrieved_docs": [corpus.docs[it.gold_doc]], "ground_truth": it.ground_truth}
+                for it in corpus.sample_queries(32, seed=4)]
+        pc = PPOConfig(full_finetune=True, zero=zero, max_new_tokens=6, max_prompt_tokens=64, minibatch_size=4,
+                       lr=1e-3, bucket_mb=2e-3)
+        return PPOTrainer(policy, tok, RewardModel(enc), pc, max_batch=8), recs
+
+    tr, recs = setup()
+    assert bool(getattr(tr.opt, "sharded", False)) == zero
+    batches = list(RecordLoader(recs, 4, seed=0, rank=rank, world=world))
+    m1 = tr.step(batches[0])
+    ck = os.path.join(out_dir, f"ck{int(zero)}", "s1")
+    tr.save_checkpoint(ck, 0, m1["reward_mean"], full_policy=True, batch_in_epoch=1)
+    m2 = tr.step(batches[1])
+    params = torch.cat([p.detach().float().reshape(-1) for p in tr.policy.parameters()])
+    tr2, _ = setup()
+    tr2.load_checkpoint(ck)
+    m2b = tr2.step(batches[1])
+    params_b = torch.cat([p.detach().float().reshape(-1) for p in tr2.policy.parameters()])
+    torch.save({"m1": m1, "m2": m2, "m2b": m2b, "params": params, "params_b": params_b},
+               os.path.join(out_dir, f"zppo{int(zero)}_{rank}.pt"))
+    parallel.barrier()
+    parallel.shutdown()
+
+
+def test_dp_ppo_full_finetune_zero_world2(tmp_path):
+    """Full-parameter PPO at world 2 with ZeRO-1 (fp32 reduce-scatter, sharded fp32 master and
+    moments, bf16 all-gather): every rank ends with the same bf16 weights; the step tracks the
+    replicated optimizer (which rounds the reduced gradient to bf16 once) to bf16 tolerance; a
+    checkpoint (rank-0 policy + per-rank optimizer shards) resumes the next step exactly."""
+    world = 2
+    for zero in (True, False):
+        mp.start_processes(_zero_ppo_worker, args=(world, _free_port(), str(tmp_path), zero), nprocs=world,
+                           start_method="spawn", join=True)
+    z = [torch.load(tmp_path / f"zppo1_{i}.pt", weights_only=False) for i in range(world)]
+    rep = [torch.load(tmp_path / f"zppo0_{i}.pt", weights_only=False) for i in range(world)]
+    assert torch.equal(z[0]["params"], z[1]["params"])
+    d = (z[0]["params"] - rep[0]["params"]).abs()
+    # the two optimizers see the same mean gradient up to one bf16 rounding: a few bf16 ulps apart
+    assert float(d.max()) < 0.05 and float((d > 0).float().mean()) < 0.2
+    assert z[0]["m1"]["grad_norm"] == pytest.approx(rep[0]["m1"]["grad_norm"], rel=1e-2)
+    for x in z:
+        assert torch.equal(x["params_b"], x["params"])
+        assert abs(x["m2b"]["total_loss"] - x["m2"]["total_loss"]) < 1e-6

@@ -102,3 +102,47 @@ def test_ppo_full_finetune_cpu():
     for n, p in tr.ref_policy.named_parameters():
         assert torch.equal(p, before[n]) and not p.requires_grad, n
     assert m2["kl_ref"] != 0.0
+
+
+def _fullft_kl(lr, steps=2):
+    from rag_tl_domainllm_optimizer_amd import models
+    from rag_tl_domainllm_optimizer_amd.data import RecordLoader, SyntheticCorpus
+    from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
+    from rag_tl_domainllm_optimizer_amd.retrieval import Encoder
+    from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
+    from rag_tl_domainllm_optimizer_amd.tokenizer import Tokenizer
+    from rag_tl_domainllm_optimizer_amd.train.ppo import PPOConfig, PPOTrainer
+
+    torch.manual_seed(0)
+    cfg = PRESETS["tiny-llama"]
+    tok = Tokenizer.synthetic(cfg.vocab_size, "llama")
+    policy = models.CausalLM(cfg, dtype=torch.float32, seed=1)
+    ecfg = PRESETS["tiny-bert"]
+    enc = Encoder(models.SentenceEncoder(ecfg, dtype=torch.float32, seed=2).eval(),
+                  Tokenizer.synthetic(ecfg.vocab_size, "bert"), max_length=64)
+    corpus = SyntheticCorpus(tok.words(), n_docs=40, doc_words=20, seed=3)
+    recs = [{"query": it.query, "retrieved_docs": [corpus.docs[it.gold_doc]], "ground_truth": it.ground_truth}
+            for it in corpus.sample_queries(8)]
+    tr = PPOTrainer(policy, tok, RewardModel(enc), PPOConfig(full_finetune=True, max_new_tokens=8,
+                                                             max_prompt_tokens=64, minibatch_size=4, lr=lr),
+                    max_batch=8)
+    batch = next(iter(RecordLoader(recs, batch_size=8, seed=0)))
+    return [tr.step(batch) for _ in range(steps)]
+
+
+def test_full_finetune_kl_and_ratio_at_theta_old():
+    """Full-parameter PPO (the reference's mode): (1) the first minibatch scores the rollouts at
+    theta = theta_old, so |logp - old_logp| is numerics only and nothing clips; (2) the frozen-
+    reference KL after one update grows with the learning rate (0.035 -> 0.37 nats per 8-token
+    sequence for lr 5e-6 -> 5e-5 on this tiny model) — AdamW's first steps
+    move EVERY weight by ~lr whatever its gradient's size, so on a random-init model at the
+    reference's lr 5e-5 the per-sequence KL is large (docs/DESIGN.md 'Round 5': the bench's
+    full-FT kl_ref of ~500 nats / 128-token sequence is this effect, not a bug in MixedFlatParams)."""
+    lo = _fullft_kl(5e-6)
+    hi = _fullft_kl(5e-5)
+    for ms in (lo, hi):
+        for m in ms:
+            assert m["behaviour_logp_gap"] < 1e-4, m["behaviour_logp_gap"]
+            assert m["clipfrac_first_mb"] == 0.0
+        assert abs(ms[0]["kl_ref"]) < 1e-4  # no update yet: policy == reference
+    assert hi[1]["kl_ref"] > 5 * lo[1]["kl_ref"] > 0

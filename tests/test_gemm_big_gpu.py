@@ -187,164 +187,3 @@ def test_decode_plan_m256(M, N, K, act):
         ref_ = ref_.to(torch.bfloat16).float()
         ref_ = torch.nn.functional.silu(ref_[:, :N // 2]) * ref_[:, N // 2:]
     _close(y, ref_)
-
-
-# ---- 4-wave tiles (bn 3: 192 x 256, 96 x 128 per wave; bn 4: 256 x 256, 128 x 128 per wave) ----
-@pytest.mark.parametrize("bn", [3, 4])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 520, 224), (77, 136, 4096), (1000, 768, 1024),
-                                   (2900, 1024, 192), (193, 6144, 4096)])
-def test_w4_nt(bn, M, N, K):
-    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
-    ref_nt = a.float() @ w.float().t()
-    _close(ops.gemm_big(a, w, ops.ROW, ops.ROW, bn=bn), ref_nt)
-    _close(ops.gemm_big(a, w, ops.ROW, ops.ROW, out_mode=1, bn=bn), ref_nt, rtol=5e-3, atol=5e-3)
-    r = _r(M, N)
-    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-    ops.gemm_big(a, w, ops.ROW, ops.ROW, out=out, residual=r, bn=bn)
-    assert not torch.isnan(out).any()
-    _close(out, ref_nt + r.float())
-
-
-@pytest.mark.parametrize("bn", [3, 4])
-def test_w4_identity_bias_act_lora_swiglu(bn):
-    n = 512
-    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
-    w = (torch.arange(n * n, device=DEV).reshape(n, n) % 97).to(torch.bfloat16)
-    torch.testing.assert_close(ops.gemm_big(a, w, ops.ROW, ops.ROW, bn=bn).float(), w.float().t())
-    M, K, F, R = 700, 512, 384, 16
-    x, wg = _r(M, K), _r(2 * F, K, s=1 / math.sqrt(K))
-    b = _r(2 * F)
-    for act in (0, 1, 2, 3, 4):
-        want = ops.reference.apply_act(x.float() @ wg.float().t() + b.float(), act)
-        _close(ops.gemm_big(x, wg, ops.ROW, ops.ROW, bias=b, act=act, bn=bn), want)
-    u, ub = _r(M, R), _r(2 * F, R, s=0.1)  # LoRA K-extension with a ragged (K2 = 16) step
-    _close(ops.gemm_big(x, wg, ops.ROW, ops.ROW, u, ub, bn=bn), x.float() @ wg.float().t() + u.float() @ ub.float().t())
-    pre = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
-    y = ops.gemm_big(x, wg, ops.ROW, ops.ROW, u, ub, act=ops.ACT_SWIGLU, out2=pre, bn=bn)
-    p_ref = (x.float() @ wg.float().t() + u.float() @ ub.float().t()).to(torch.bfloat16)
-    _close(pre, p_ref)
-    _close(y, torch.nn.functional.silu(p_ref[:, :F].float()) * p_ref[:, F:].float())
-
-
-# ---- stream-K tail (gemm_big_kernel<..., SK = true>): the last partial wave of 256x256 tiles split
-# over K across every CU, partial tiles handed to the last arriving unit ----
-# (M, N, K): tiles = ceil(M/256) * N/256 > 256 CUs with a remainder; ragged M / K; 1-3 segments
-_SK_SHAPES = [(4352, 4096, 1024), (4500, 4096, 1000), (2600, 6144, 2048), (9632, 6144, 4096)]
-
-
-@pytest.mark.parametrize("M,N,K", _SK_SHAPES)
-def test_streamk_nt_nn_matches_reference(M, N, K):
-    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
-    r = _r(M, N)
-    with ops.tuning(gemm_streamk=2):
-        got = ops.gemm_big(a, w, ops.ROW, ops.ROW)
-        out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-        ops.gemm_big(a, w, ops.ROW, ops.ROW, out=out, residual=r)
-        wk = _r(K, N, s=1 / math.sqrt(K))
-        nn = ops.gemm_big(a, wk, ops.ROW, ops.KMAJ)
-    want = a.float() @ w.float().t()
-    _close(got, want)
-    assert not torch.isnan(out).any()
-    _close(out, want + r.float())
-    _close(nn, a.float() @ wk.float())
-    # the data-parallel planner on the same operands: same result up to the K-split summation order
-    with ops.tuning(gemm_streamk=0):
-        dp = ops.gemm_big(a, w, ops.ROW, ops.ROW)
-    _close(got, dp, rtol=1e-2, atol=1e-2)
-    torch.cuda.synchronize()
-    assert ops.native().streamk_dirty_tickets() == 0
-
-
-def test_streamk_lora_extension_and_swiglu():
-    """The K-extension steps (LoRA) are part of the split K range; SwiGLU + pre-activation output
-    from the reduced tile."""
-    M, K, F, R = 4352, 1024, 2048, 64  # 17 x 16 = 272 tiles of the [gate; up] weight
-    x, w = _r(M, K), _r(2 * F, K, s=1 / math.sqrt(K))
-    u, ub = _r(M, R), _r(2 * F, R, s=0.1)
-    with ops.tuning(gemm_streamk=2):
-        y = ops.gemm_big(x, w, ops.ROW, ops.ROW, u, ub)
-        pre = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
-        f = ops.gemm_big(x, w, ops.ROW, ops.ROW, act=ops.ACT_SWIGLU, out2=pre)
-        dy, du, ap = _r(M, 2 * F), _r(M, R), _r(R, K, s=0.1)
-        dx = ops.gemm_nn(dy, w, du, ap)
-    _close(y, x.float() @ w.float().t() + u.float() @ ub.float().t())
-    p_ref = (x.float() @ w.float().t()).to(torch.bfloat16)
-    _close(pre, p_ref)
-    _close(f, torch.nn.functional.silu(p_ref[:, :F].float()) * p_ref[:, F:].float())
-    _close(dx, dy.float() @ w.float() + du.float() @ ap.float())
-    torch.cuda.synchronize()
-    assert ops.native().streamk_dirty_tickets() == 0
-
-
-def test_streamk_repeat_and_side_stream():
-    """Tickets re-arm themselves: many launches back to back (and on a second stream with its own
-    workspace) give identical results."""
-    M, N, K = 4500, 4096, 1536
-    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
-    with ops.tuning(gemm_streamk=2):
-        first = ops.gemm_big(a, w, ops.ROW, ops.ROW)
-        for _ in range(5):
-            assert torch.equal(ops.gemm_big(a, w, ops.ROW, ops.ROW), first)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            side = ops.gemm_big(a, w, ops.ROW, ops.ROW)
-        torch.cuda.current_stream().wait_stream(s)
-        assert torch.equal(side, first)
-    torch.cuda.synchronize()
-    assert ops.native().streamk_dirty_tickets() == 0
-
-
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 520, 200), (77, 136, 4096), (1000, 768, 1024),
-                                   (2900, 1024, 192), (512, 512, 128), (768, 1024, 4160)])
-def test_ring_nt_bitwise(M, N, K):
-    """The 10-slot granule ring (tuning gemm_ring) runs the same MFMAs on the same operands in the same
-    order as the two-buffer schedule: bitwise-equal outputs for 1-, 2- and many-step K, ragged K
-    tails, partial row / column tiles, the LoRA K-extension, a residual, SwiGLU and RoPE epilogues."""
-    from rag_tl_domainllm_optimizer_amd.ops import reference as ref
-
-    a, w = _r(M, K), _r(N, K, s=1 / math.sqrt(K))
-    u, ub = _r(M, 64), _r(N, 64, s=0.1)
-    r = _r(M, N)
-    outs = []
-    for ring in (0, 1):
-        with ops.tuning(gemm_ring=ring):
-            y = ops.gemm_big(a, w, ops.ROW, ops.ROW, bn=256)
-            yl = ops.gemm_big(a, w, ops.ROW, ops.ROW, u, ub, bn=0)
-            yr = ops.gemm_big(a, w, ops.ROW, ops.ROW, residual=r, bn=256)
-            outs.append((y, yl, yr))
-    for x0, x1 in zip(*outs):
-        assert torch.equal(x0, x1)
-    _close(outs[1][0], a.float() @ w.float().t())
-    if N % 512 == 0:
-        res = []
-        cos, sin = ref.rope_tables(128, 2048, 10000.0, DEV)
-        pos = torch.randint(0, 2048, (M,), device=DEV, dtype=torch.int32)
-        for ring in (0, 1):
-            with ops.tuning(gemm_ring=ring):
-                pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-                f = ops.gemm_big(a, w, ops.ROW, ops.ROW, act=ops.ACT_SWIGLU, out2=pre, bn=256)
-                q = ops.native().gemm_rope(a, w, None, None, None, pos, cos, sin, N // 2, 128, bn=256)
-                res.append((f, pre, q))
-        for x0, x1 in zip(*res):
-            assert torch.equal(x0, x1)
-
-
-@pytest.mark.parametrize("M,N,K", [(300, 512, 200), (1000, 4096, 1536), (256, 256, 64), (777, 1024, 4160)])
-def test_ring_nn_bitwise(M, N, K):
-    """NN (dX = dY W) on the granule ring: bitwise the two-buffer schedule, with the LoRA
-    K-extension and the SwiGLU-backward epilogue."""
-    dy, w = _r(M, K), _r(K, N, s=1 / math.sqrt(K))
-    du, ap = _r(M, 64), _r(64, N, s=0.1)
-    pre = _r(M, 2 * N)
-    outs = []
-    for ring in (0, 1):
-        with ops.tuning(gemm_ring=ring):
-            a = ops.gemm_big(dy, w, ops.ROW, ops.KMAJ, bn=256)
-            b = ops.gemm_big(dy, w, ops.ROW, ops.KMAJ, du, ap, bn=0)
-            o = torch.empty(M, 2 * N, device=DEV, dtype=torch.bfloat16)
-            c = ops.gemm_big(dy, w, ops.ROW, ops.KMAJ, du, ap, act=ops.ACT_DSWIGLU, out=o, residual=pre, bn=256)
-            outs.append((a, b, c))
-    for x0, x1 in zip(*outs):
-        assert torch.equal(x0, x1)
-    _close(outs[1][0], dy.float() @ w.float())

@@ -610,43 +610,6 @@ def test_pool_topk_ivf_gae():
     _close(r1, r2, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-@pytest.mark.parametrize("M,N,K,R", [(512, 512, 256, 0), (700, 1000, 512, 64), (2048, 6144, 4096, 0),
-                                     (300, 264, 128, 128), (256, 32000, 4096, 0)])
-def test_gemm_large_variants(variant, M, N, K, R):
-    """128x128 and 256x256 (8-phase) tile kernels on ragged shapes, with LoRA K-extension, bias, act."""
-    C = ops.native()
-    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / math.sqrt(K)
-    u = torch.randn(M, R, device=DEV, dtype=torch.bfloat16) if R else None
-    ub = torch.randn(N, R, device=DEV, dtype=torch.bfloat16) * 0.1 if R else None
-    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
-    try:
-        C.set_tuning({"gemm_variant": variant})
-        for act in (0, 4):
-            _close(ops.gemm(a, w, u, ub, b, act), ref.gemm(a, w, u, ub, b, act, out_f32=True))
-        _close(ops.gemm(a, w, u, ub, None, 0, out_f32=True), ref.gemm(a, w, u, ub, None, 0, out_f32=True),
-               rtol=5e-3, atol=5e-3)
-        # repeated launches must agree bitwise (no race between LDS-DMA refills and reads)
-        y0 = ops.gemm(a, w, u, ub, b, 0)
-        for _ in range(5):
-            assert torch.equal(ops.gemm(a, w, u, ub, b, 0), y0)
-    finally:
-        C.set_tuning({"gemm_variant": 0})
-
-
-def test_gemm_256_identity():
-    C = ops.native()
-    n = 512
-    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
-    w = (torch.arange(n * n, device=DEV).reshape(n, n) % 97).to(torch.bfloat16)
-    try:
-        C.set_tuning({"gemm_variant": 2})
-        assert torch.equal(ops.gemm(a, w).float(), w.t().float())
-    finally:
-        C.set_tuning({"gemm_variant": 0})
-
-
 @pytest.mark.parametrize("B,Hq,Hkv,D,Smax,rot,window", [(1, 32, 8, 128, 456, True, 0), (64, 32, 8, 128, 456, True, 0),
                                                         (3, 8, 8, 64, 200, False, 0), (5, 8, 2, 32, 300, True, 64),
                                                         (2, 16, 2, 128, 64, True, 0),
@@ -841,72 +804,6 @@ def test_ppo_loss_fused(B, T, vclip):
     torch.testing.assert_close(st, rst, rtol=1e-4, atol=1e-5)
     for a, t in zip(g, (lp, vals, ent)):
         torch.testing.assert_close(a, t.grad, rtol=1e-4, atol=1e-6)
-
-
-@pytest.mark.parametrize("Hkv,Smax,window,kv0", [(8, 456, 0, 3), (32, 300, 0, 0), (8, 2048, 256, 40), (8, 64, 0, 0)])
-def test_attn_o_fused(Hkv, Smax, window, kv0):
-    """Batch-1 attention + o_proj + residual in one launch == decode_step_attention, then o GEMM +
-    residual. The appended slot and everything after it start as NaN (fresh cache)."""
-    torch.manual_seed(Hkv + Smax)
-    Hq, D, H = 32, 128, 4096
-    W = (Hq + 2 * Hkv) * D
-    kc = torch.randn(1, Hkv, Smax, D, device=DEV, dtype=torch.bfloat16)
-    vc = torch.randn_like(kc)
-    slot = torch.tensor([Smax - 9], device=DEV, dtype=torch.int32)
-    tail = torch.arange(Smax, device=DEV)[None, None, :, None] >= slot.long()[:, None, None, None]
-    kc.masked_fill_(tail, float("nan"))
-    vc.masked_fill_(tail, float("nan"))
-    attn_len = slot + 1
-    kv_start = torch.tensor([kv0], device=DEV, dtype=torch.int32)
-    pos = (slot - kv_start).to(torch.int32)
-    cos, sin = ref.rope_tables(D, 4096, 10000.0, DEV)
-    w_o = (torch.randn(H, Hq * D, device=DEV) / math.sqrt(Hq * D)).to(torch.bfloat16)
-    ws = ops.decode_workspace(1, Hq, Hkv, D, Smax, DEV)
-    for it in range(3):  # repeated launches: the sync counters must re-arm
-        qkv = torch.randn(1, W, device=DEV, dtype=torch.bfloat16)
-        res = torch.randn(1, H, device=DEV, dtype=torch.bfloat16)
-        kc2, vc2 = kc.clone(), vc.clone()
-        y = ops.decode_step_attention_o(qkv, kc, vc, slot, attn_len, Hq, w_o, res, pos, cos, sin, kv_start, window,
-                                        workspace=ws)
-        assert y is not None, "fused path must take this shape"
-        o = ops.decode_step_attention(qkv, kc2, vc2, slot, attn_len, Hq, pos, cos, sin, kv_start, window,
-                                      workspace=ops.decode_workspace(1, Hq, Hkv, D, Smax, DEV))
-        y_ref = o.float() @ w_o.float().t() + res.float()
-        assert torch.equal(kc.nan_to_num(), kc2.nan_to_num()) and torch.equal(vc.nan_to_num(), vc2.nan_to_num())
-        assert torch.isfinite(y).all()
-        _close(y, y_ref)
-    torch.cuda.synchronize()
-    assert ws[3].tolist() == [0, 0, 0], ws[3].tolist()  # re-armed, no give-up
-
-
-def test_attn_o_fused_generation_matches_unfused():
-    """Greedy batch-1 generation through the fused decode layer is the same with and without the
-    single-launch attention + o_proj (a 2-layer model with Mistral's attention shape). The unfused
-    o_proj runs on 4 waves per row group here: the fused kernel sums its K chunks in that order
-    (the automatic 8-wave form sums the same products in another order, and a near-tie between
-    two logits of this random model can then pick a different greedy token)."""
-    with ops.tuning(gemv16_waves=4):
-        _attn_o_fused_generation_case()
-
-
-def _attn_o_fused_generation_case():
-    import dataclasses
-
-    from rag_tl_domainllm_optimizer_amd import models
-    from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
-    from rag_tl_domainllm_optimizer_amd.models.config import PRESETS
-
-    cfg = dataclasses.replace(PRESETS["mistral-7b"], num_layers=2, intermediate_size=1024, vocab_size=512,
-                              name="mistral-attn-2l")
-    m = models.CausalLM(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
-    prompt = [[5, 9, 33, 41, 7, 8, 9, 10, 77, 3, 200]]
-    p = SamplingParams(max_new_tokens=12, do_sample=False)
-    outs = []
-    for fused in (False, True):
-        m.fused_attn_o = fused
-        outs.append(Generator(m, 1, 64, DEV).generate(prompt, p, pad_id=0, eos_ids=[-1]))
-    assert torch.equal(outs[0].tokens, outs[1].tokens)
-    torch.testing.assert_close(outs[0].logprobs, outs[1].logprobs, rtol=0, atol=0.05)
 
 
 def test_ppo_advantages_kernel():
@@ -1285,7 +1182,7 @@ def test_rope_epilogue_model_bitwise():
 
 def test_attention_bwd_fused_rope_bitwise(monkeypatch):
     """The RoPE backward fused into the attention backward's dQ / dK stores gives bitwise the
-    gradient of the separate inverse-rotation pass (both dQ forms: the dQ kernel and the atomic one)."""
+    gradient of the separate inverse-rotation pass."""
     import importlib
 
     att = importlib.import_module("rag_tl_domainllm_optimizer_amd.ops.attention")  # (ops.attention is a function)
@@ -1299,20 +1196,17 @@ def test_attention_bwd_fused_rope_bitwise(monkeypatch):
     pos = (torch.arange(S, device=DEV)[None, :] - start[:, None].long()).clamp(min=0).reshape(-1).to(torch.int32)
     base = (torch.randn(B * S, W, device=DEV) * 0.5).to(torch.bfloat16)
     do = (torch.randn(B * S, Hq * D, device=DEV) * 0.1).to(torch.bfloat16)
-    for atomic in (0, 1):
-        grads = []
-        for fused in (True, False):
-            monkeypatch.setattr(att, "ROPE_BWD_FUSED", fused)
-            with ops.tuning(attn_bwd_atomic_dq=atomic):
-                x = base.clone().requires_grad_(True)
-                o = ops.flash_attention_qkv(x * 1, B, S, Hq, Hkv, D, True, 0, kv_start=start, rope=(pos, cos, sin))
-                (g,) = torch.autograd.grad(o, x, do)
-            grads.append(g)
-        assert torch.equal(grads[0], grads[1]), atomic
+    grads = []
+    for fused in (True, False):
+        monkeypatch.setattr(att, "ROPE_BWD_FUSED", fused)
+        x = base.clone().requires_grad_(True)
+        o = ops.flash_attention_qkv(x * 1, B, S, Hq, Hkv, D, True, 0, kv_start=start, rope=(pos, cos, sin))
+        (g,) = torch.autograd.grad(o, x, do)
+        grads.append(g)
+    assert torch.equal(grads[0], grads[1])
 
 
-@pytest.mark.parametrize("atomic", [0, 1])
-def test_attention_bwd_writes_every_row(atomic):
+def test_attention_bwd_writes_every_row():
     """attn_bwd writes every row and column of dq / dk / dv (masked / left-padded rows as zeros), so
     the autograd node hands out an uninitialised buffer: NaN-poisoned outputs come back NaN-free."""
     torch.manual_seed(5)
@@ -1324,9 +1218,8 @@ def test_attention_bwd_writes_every_row(atomic):
     o, lse = ops.native().attn_fwd(q, k, v, B, S, S, Hq, Hkv, D, True, 0, 1 / math.sqrt(D), start, None, None, 0, True)
     do = (torch.randn(B * S, Hq * D, device=DEV) * 0.1).to(torch.bfloat16)
     d = torch.full((B * S, W), float("nan"), device=DEV, dtype=torch.bfloat16)
-    with ops.tuning(attn_bwd_atomic_dq=atomic):
-        ops.native().attn_bwd(q, k, v, o, do, lse, d[:, :Hq * D], d[:, Hq * D:(Hq + Hkv) * D], d[:, (Hq + Hkv) * D:],
-                              B, S, Hq, Hkv, D, True, 0, 1 / math.sqrt(D), start)
+    ops.native().attn_bwd(q, k, v, o, do, lse, d[:, :Hq * D], d[:, Hq * D:(Hq + Hkv) * D], d[:, (Hq + Hkv) * D:],
+                          B, S, Hq, Hkv, D, True, 0, 1 / math.sqrt(D), start)
     assert not torch.isnan(d).any()
     # left-pad keys of row 1 get no gradient
     assert float(d[S:S + 77, Hq * D:].float().abs().max()) == 0.0
@@ -1355,20 +1248,3 @@ def test_sampler_search_kth_exact(top_k):
         assert keep.gather(1, tok[:, None]).float().mean().item() >= 0.97
 
 
-@pytest.mark.parametrize("D,Hq,Hkv,B,S,window", [(128, 8, 2, 3, 301, 0), (64, 4, 4, 2, 150, 0), (128, 4, 1, 2, 700, 256)])
-def test_attention_fwd_8wave_bitwise(D, Hq, Hkv, B, S, window):
-    """The 8-wave x 16-row attention forward (tuning attn_fwd_w8) computes every query row with the same
-    operations in the same order as the 4-wave x 32-row form: bitwise-equal O and LSE (causal, left
-    padding, sliding window)."""
-    torch.manual_seed(9)
-    W = (Hq + 2 * Hkv) * D
-    qkv = (torch.randn(B * S, W, device=DEV) * 0.5).to(torch.bfloat16)
-    start = torch.tensor([0, 37, 100][:B], dtype=torch.int32, device=DEV)
-    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
-    outs = []
-    for w8 in (0, 1):
-        with ops.tuning(attn_fwd_w8=w8):
-            outs.append(ops.native().attn_fwd(q, k, v, B, S, S, Hq, Hkv, D, True, window, 1 / math.sqrt(D), start,
-                                              None, None, 0, True))
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])

@@ -133,3 +133,19 @@ def test_ppo_advantages_oracle_matches_eager_path():
     torch.testing.assert_close(r2, ret)
     torch.testing.assert_close(w2, rew)
     torch.testing.assert_close(k2, kl.sum(-1))
+
+
+def test_ppo_old_logp_recompute_ratio_is_one_at_theta_old():
+    """old_logp = "recompute": the ratio's theta_old log-probs come from a training-numerics forward
+    (LoRA on, unmerged), so the first minibatch scores exactly theta_old: no gap, nothing clipped.
+    The rollout engine's own deviation is still reported (rollout_engine_logp_gap)."""
+    import dataclasses
+
+    tr, recs = _setup()
+    tr.cfg = dataclasses.replace(tr.cfg, old_logp="recompute")
+    loader = RecordLoader(recs, batch_size=8, seed=0)
+    for _ in range(2):  # the second step runs with trained (non-zero) adapters
+        m = tr.step(next(iter(loader)))
+        assert m["behaviour_logp_gap"] < 1e-5, m["behaviour_logp_gap"]
+        assert m["clipfrac_first_mb"] == 0.0
+        assert math.isfinite(m["rollout_engine_logp_gap"]) and m["rollout_engine_logp_gap"] >= 0.0

@@ -55,7 +55,11 @@ def test_tuning_roundtrip():
     if not ops.native_available():
         pytest.skip("native extension not built")
     t0 = ops.get_tuning()
-    assert t0["decode_mw"] == 1 and t0["gemm_variant"] == 0 and abs(t0["gemm_bn128_cost"] - 0.55) < 1e-6
+    assert t0["decode_mw_kpp"] == 512 and t0["gemm_variant"] == 0 and abs(t0["gemm_bn128_cost"] - 0.55) < 1e-6
+    # only knobs with a live alternative remain (measured-slower paths left the product kernels)
+    for gone in ("gemm_streamk", "gemm_ring", "attn_fwd_w8", "attn_bwd_atomic_dq", "gemm_fp8_256", "gemm_tr_builtin",
+                 "decode_mw", "decode_mfma"):
+        assert gone not in t0, gone
     with ops.tuning(decode_split=2, gemm_bn128_cost=0.7):
         t = ops.get_tuning()
         assert t["decode_split"] == 2 and abs(t["gemm_bn128_cost"] - 0.7) < 1e-6

@@ -1,6 +1,6 @@
 """Training flash attention (ops.flash_attention_qkv) forward + backward at PPO-update shapes
 (32 sequences x 301 tokens, 32 q-heads / 8 kv-heads, D 128): time per fwd and per fwd+bwd.
-Compare the dQ forms with RT_ATTN_BWD_ATOMIC_DQ=1 (round-1 fp32 atomics) vs default.
+(The round-1 fp32-atomic dQ form left the product kernels in round 5; the dQ kernel is the only form.)
 
     python tools/attn_train_probe.py [--B 32] [--S 301]
 """

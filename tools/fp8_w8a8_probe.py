@@ -1,5 +1,5 @@
 """W8A8 GEMM (M > 64) timing on the prefill / reference-scoring shapes: the gemm_big fp8 schedule
-(default) or the older 256x256 8-phase kernel (RT_GEMM_FP8_256=1), plus the fused SwiGLU form.
+(the older 256x256 8-phase kernel left the product kernels in round 5), plus the fused SwiGLU form.
 
     python tools/fp8_w8a8_probe.py [--M 7168 20480]
 """
@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--M", type=int, nargs="+", default=[7168, 20480])
     a = ap.parse_args()
     C = ops.native()
-    tag = "gemm_256" if os.environ.get("RT_GEMM_FP8_256") == "1" else "gemm_big"
+    tag = "gemm_big"
     for model, shapes in SHAPES.items():
         for M in a.M:
             for name, N, K in shapes:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build tools/gemm_exp: one standalone timing binary per experiment variant of gemm_big.hip
 # (tools/gemm_exp/make_variants.py). CPU-side only (hipcc cross-compiles gfx950); run the binaries
-# on the GPU box: for b in tools/gemm_exp/bin/*; do timeout -k 10 60 $b 10; done
+# on the GPU box: for b in tools/gemm_exp/bin/gemm_exp_*; do timeout -k 10 120 $b 10; done
 set -euo pipefail
 cd "$(dirname "$0")/../.."
 OUT=tools/gemm_exp/bin

@@ -4,7 +4,8 @@
 // one hipcc line and one run. Prints one line per shape: us per launch, PF/s, and a checksum of C
 // (variants that skip waits produce wrong C on purpose; the checksum shows which ones are exact).
 //
-//   ./gemm_exp [reps] [ring | w4]   (ring: tuning gemm_ring = 1; w4: NT shapes on the 4-wave kernel)
+//   ./gemm_exp [reps] [-] [cus,...]   (cus: run every shape again on a stream restricted to that many
+//   CUs by a CU mask, spread evenly over the 256 mask bits)
 #include <hip/hip_runtime.h>
 
 #include "rt_tuning.h"
@@ -19,8 +20,7 @@
 extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb,
                            const void* A2, long lda2, const void* B2, long ldb2, int K2, const void* bias,
                            void* C, long ldc, void* C2, long ldc2, const void* R, long ldr, int M, int N, int K,
-                           int act, int out, int nsplit, const void* zpage, int bn, float* sk_part,
-                           unsigned* sk_tickets, hipStream_t stream);
+                           int act, int out, int nsplit, const void* zpage, int bn, hipStream_t stream);
 
 #define CK(x)                                                                           \
   do {                                                                                  \
@@ -31,11 +31,11 @@ extern "C" int rt_gemm_big(int layout_a, int layout_b, const void* A, long lda, 
     }                                                                                   \
   } while (0)
 
-__global__ void fill_bf16(uint16_t* p, long n, uint32_t seed) {
+__global__ void fill_bf16(uint16_t* p, long n, uint32_t seed, float scale) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     uint32_t h = (uint32_t)i * 2654435761u ^ seed;
     h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
-    const float f = ((int)(h & 0xFFFF) - 32768) * (1.f / 32768.f) * 0.05f;  // |x| < 0.05
+    const float f = ((int)(h & 0xFFFF) - 32768) * (1.f / 32768.f) * scale;  // uniform in (-scale, scale)
     uint32_t u = __float_as_uint(f);
     p[i] = (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
   }
@@ -52,13 +52,17 @@ struct Shape { const char* name; int la, lb, M, N, K, act, bn; };
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 10;
-  // w4: the NT shapes on the 4-wave 128 x 128-per-wave kernel (bn = 4), NN skipped
-  const bool w4 = argc > 2 && std::string(argv[2]) == "w4";
-  if (argc > 2 && std::string(argv[2]) == "ring") {
-    rt::Tuning t = *rt_tuning();
-    t.gemm_ring = 1;
-    rt_set_tuning(&t);
-    printf("tuning: gemm_ring = 1\n");
+  std::vector<int> cus_list = {0};  // 0 = default stream (all CUs)
+  if (argc > 3) {
+    cus_list.clear();
+    std::string a = argv[3];
+    size_t pos = 0;
+    while (pos < a.size()) {
+      size_t q = a.find(',', pos);
+      if (q == std::string::npos) q = a.size();
+      cus_list.push_back(atoi(a.substr(pos, q - pos).c_str()));
+      pos = q + 1;
+    }
   }
   const Shape shapes[] = {
       {"nt_1024tiles_8192x8192x4096", 0, 0, 8192, 8192, 4096, 0, 256},
@@ -81,32 +85,41 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&Z, 4096));
   CK(hipMalloc(&cs, sizeof(double)));
   CK(hipMemset(Z, 0, 4096));
-  fill_bf16<<<4096, 256>>>(A, maxA, 17u);
-  fill_bf16<<<4096, 256>>>(B, maxB, 91u);
+  // activations uniform in (-1, 1), weights in (-1/64, 1/64): the operand statistics of
+  // tools/gemm_big_probe.py (the chip's clock under load depends on the operands' switching)
+  fill_bf16<<<4096, 256>>>(A, maxA, 17u, 1.f);
+  fill_bf16<<<4096, 256>>>(B, maxB, 91u, 1.f / 64.f);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (Shape s : shapes) {
-    if (w4) {
-      if (s.lb != 0) continue;
-      s.bn = 4;
+  for (int ncu : cus_list) {
+  hipStream_t st = 0;
+  if (ncu > 0 && ncu < 256) {
+    uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < ncu; ++i) {
+      const int b = (int)((long)i * 256 / ncu);  // evenly spread enabled bits
+      mask[b >> 5] |= 1u << (b & 31);
     }
+    CK(hipExtStreamCreateWithCUMask(&st, 8, mask));
+  }
+  printf("# cus %d\n", ncu > 0 ? ncu : 256);
+  for (const Shape& s : shapes) {
     // NT: A [M, K], B [N, K]; NN: A [M, K] (= dY), B [K, N] (= W, KMAJ)
     const long lda = s.K, ldb = s.lb == 0 ? s.K : s.N;
     const int nout = s.act == 5 ? s.N / 2 : s.N;
     auto run = [&]() {
       const int rc = rt_gemm_big(s.la, s.lb, A, lda, B, ldb, nullptr, 0, nullptr, 0, 0, nullptr, C, nout, nullptr, 0,
-                                 nullptr, 0, s.M, s.N, s.K, s.act, 0, 1, Z, s.bn, nullptr, nullptr, 0);
+                                 nullptr, 0, s.M, s.N, s.K, s.act, 0, 1, Z, s.bn, st);
       if (rc) { fprintf(stderr, "rt_gemm_big rc=%d on %s\n", rc, s.name); exit(1); }
     };
     for (int i = 0; i < 3; ++i) run();
-    CK(hipDeviceSynchronize());
+    CK(hipStreamSynchronize(st));
     std::vector<float> ts;
     for (int i = 0; i < reps; ++i) {
-      CK(hipEventRecord(e0, 0));
+      CK(hipEventRecord(e0, st));
       run();
-      CK(hipEventRecord(e1, 0));
+      CK(hipEventRecord(e1, st));
       CK(hipEventSynchronize(e1));
       float ms = 0.f;
       CK(hipEventElapsedTime(&ms, e0, e1));
@@ -114,6 +127,7 @@ int main(int argc, char** argv) {
     }
     std::sort(ts.begin(), ts.end());
     const double med = ts[ts.size() / 2] * 1e3;
+    CK(hipStreamSynchronize(st));
     CK(hipMemset(cs, 0, sizeof(double)));
     checksum<<<1024, 256>>>(C, (long)s.M * nout, cs);
     double h = 0.0;
@@ -121,6 +135,8 @@ int main(int argc, char** argv) {
     const double fl = 2.0 * s.M * (double)s.N * s.K;
     printf("%-36s med %8.1f us  min %8.1f us  %.3f PF/s  checksum %.6e\n", s.name, med, ts[0] * 1e3,
            fl / (med * 1e-6) / 1e15, h);
+  }
+  if (st) CK(hipStreamDestroy(st));
   }
   return 0;
 }

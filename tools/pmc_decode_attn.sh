@@ -1,5 +1,6 @@
 #!/bin/bash
-# PMC passes for the batch-256 decode attention kernels (MFMA default, RT_DECODE_MFMA=0 = VALU)
+# PMC passes for the batch-256 decode attention kernels (the MFMA kernel; the VALU form is only the
+# fallback for head_dim != 128 since round 5)
 set -o pipefail
 R=$PWD
 out=$R/gpurun_out/pmc
