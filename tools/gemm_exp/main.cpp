@@ -67,6 +67,7 @@ int main(int argc, char** argv) {
   const Shape shapes[] = {
       {"nt_1024tiles_8192x8192x4096", 0, 0, 8192, 8192, 4096, 0, 256},
       {"nt_qkv_9632x6144x4096", 0, 0, 9632, 6144, 4096, 0, 0},
+      {"nt_o_9632x4096x4096", 0, 0, 9632, 4096, 4096, 0, 0},
       {"nt_gateup_swiglu_9632x28672x4096", 0, 0, 9632, 28672, 4096, 5, 0},
       {"nt_down_9632x4096x14336", 0, 0, 9632, 4096, 14336, 0, 0},
       {"nn_qkv_dx_9632x4096x6144", 0, 1, 9632, 4096, 6144, 0, 0},

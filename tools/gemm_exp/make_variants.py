@@ -1,6 +1,11 @@
 """Experiment copies of csrc/kernels/gemm_big.hip for tools/gemm_exp (timing-only diagnostics).
 
-Round 5: MFMA issue order inside one phase of the 256x256 kernel. The K-step's 16 MFMAs of a
+Round 5 (current): cost of the epilogue inside the large GEMMs — `nostore` skips the bf16
+epilogue's global stores, `noepi` the whole bf16 epilogue (LDS staging + stores); both at run time
+(M >= 0), so the K-loop is unchanged. Their gap to `base` bounds what overlapping a tile's epilogue
+with the next tile's K-loop can gain.
+
+Earlier in round 5: MFMA issue order inside one phase of the 256x256 kernel. The K-step's 16 MFMAs of a
 phase run over (A fragment i, B fragment j, k-half kk). The product kernel iterates i, j, kk, so
 BOTH operand registers change between consecutive MFMAs (kk switches the A and the B half). The
 kernel is bound by the clock the chip holds under its switching power (zero-filled operands run
@@ -39,8 +44,68 @@ def _order(s, seq):
     return s.replace(old, lines)
 
 
+def _sub(s, old, new):
+    assert s.count(old) == 1, (old, s.count(old))
+    return s.replace(old, new)
+
+
+def _nostore(s):
+    # the bf16 epilogue's global stores skipped at run time (M >= 0 always): LDS staging and the
+    # fused elementwise work stay
+    s = _sub(s, "            *(uint4*)(C + (long)grow * p.ldc + gcol) = v;\n",
+             "            if (p.M < 0) *(uint4*)(C + (long)grow * p.ldc + gcol) = v;\n")
+    return _sub(s, "            *(uint4*)(Cf + (long)grow * p.ldc + fcol) = pack8(f);\n",
+                "            if (p.M < 0) *(uint4*)(Cf + (long)grow * p.ldc + fcol) = pack8(f);\n")
+
+
+def _noepi(s):
+    # the whole bf16 epilogue (LDS staging + stores) skipped at run time
+    return _sub(s, "    constexpr int LDT = BN + 4;\n", "    if (p.M >= 0) return;\n    constexpr int LDT = BN + 4;\n")
+
+
+FAST_B = ("      read_b(buf, 0, fb0);\n      stage_fast(3, t + 1);\n",
+          "      read_b(buf, 1, fb1);\n      stage_fast(1, t + 1);\n",
+          "      stage_fast(2, t + 2);\n")
+
+
+def _nob(s):
+    # steady-state loop without the B operand's LDS traffic: no b0 / b1 LDS-DMA, no B fragment
+    # reads (the B fragments of the prologue step are reused): the ceiling of a kernel whose B
+    # operand never touches LDS
+    s = _sub(s, FAST_B[0], "      stage_fast(3, t + 1);\n".replace("stage_fast(3, t + 1)", "(void)0"))
+    s = _sub(s, FAST_B[1], "      stage_fast(1, t + 1);\n")
+    s = _sub(s, FAST_B[2], "")
+    return _sub(s, "    int t = t_begin;\n    for (; t < t_fast; ++t) {\n",
+                "    int t = t_begin;\n    read_b(0, 0, fb0);\n    read_b(0, 1, fb1);\n    for (; t < t_fast; ++t) {\n")
+
+
+def _bglb(s):
+    # B fragments straight from the weight rows in global memory into VGPRs, one K-step ahead
+    # (plain row-major W: each fragment row's 128 B of the K-step are one cache line); A as before
+    s = _nob(s)
+    s = _sub(s, "    int t = t_begin;\n    read_b(0, 0, fb0);\n    read_b(0, 1, fb1);\n    for (; t < t_fast; ++t) {\n",
+             """    auto gload_b = [&](int u, int sb, i32x8 (&fb)[2]) {
+      for (int j = 0; j < 2; ++j) {
+        const int row = min(n0 + wc * 64 + sb * 32 + j * 16 + frow, p.N - 1);
+        const bf16_t* src = p.B + (long)row * p.ldb + u * 64 + fq * 8;
+        const i32x4 lo = *(const i32x4*)src, hi = *(const i32x4*)(src + 32);
+        fb[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    };
+    int t = t_begin;
+    gload_b(t, 0, fb0);
+    gload_b(t, 1, fb1);
+    for (; t < t_fast; ++t) {
+      i32x8 fbn0[2], fbn1[2];
+      gload_b(t + 1, 0, fbn0);
+      gload_b(t + 1, 1, fbn1);
+""")
+    return _sub(s, "      GB_MMA(1, 0, fb0);\n    }\n",
+                "      GB_MMA(1, 0, fb0);\n      fb0[0] = fbn0[0]; fb0[1] = fbn0[1]; fb1[0] = fbn1[0]; fb1[1] = fbn1[1];\n    }\n")
+
+
 def variants(s):
-    return {"base": s, "kij": _order(s, "kij"), "kji": _order(s, "kji"), "ikj": _order(s, "ikj")}
+    return {"base": s, "nob": _nob(s), "bglb": _bglb(s)}
 
 
 def main():
