@@ -111,6 +111,7 @@ static const TuningField kTuningFields[] = {
     {"wide_split", &rt::Tuning::wide_split, nullptr},
     {"gemm_bn128_cost", nullptr, &rt::Tuning::gemm_bn128_cost},
     {"gemm_group_m", &rt::Tuning::gemm_group_m, nullptr},
+    {"sample_window", &rt::Tuning::sample_window, nullptr},
 };
 
 py::dict get_tuning() {

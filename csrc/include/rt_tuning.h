@@ -33,6 +33,9 @@ struct Tuning {
   // ---- token-parallel GEMMs (gemm_big.hip) ----
   float gemm_bn128_cost = 0.55f;  // planner: time of a 256x128 tile / a 256x256 tile
   int gemm_group_m = 4;       // rows of 256x256 tiles per L2-reuse group in the tile order
+  // ---- sampler (sampling.hip) ----
+  int sample_window = 1;      // top-k: candidates from a window below the row max, k-th key in one
+                              // wave (0: 16 block-wide counting passes over the whole row; same draw)
 };
 
 }  // namespace rt

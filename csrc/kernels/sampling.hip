@@ -368,6 +368,72 @@ __global__ __launch_bounds__(256) void sample_bf16_lds_kernel(const bf16_t* __re
 // Philox stream (seed, row, offset * V + token) as sample_bf16_lds_kernel, so the same token wins.
 constexpr int TK_CAP = 2048;
 
+// In-row (16-lane) all-reduce steps by DPP (xor 1, xor 2, half-mirror, mirror: afterwards every
+// lane of a row holds the row's total) — register crossbar moves, where __shfl_xor is an LDS
+// ds_bpermute round trip per step. A wave total is then the four row totals (v_readlane, scalar).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+__device__ __forceinline__ int row_sum_i(int v) {
+  v += dpp_i<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_i<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_i<0x141>(v);  // row_half_mirror
+  v += dpp_i<0x140>(v);  // row_mirror
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+  v = row_sum_i(v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+__device__ __forceinline__ float wave_sum_f(float v) {
+  auto step = [](float x, int sel) -> float {
+    const int xi = __float_as_int(x);
+    const int o = sel == 0 ? dpp_i<0xB1>(xi) : sel == 1 ? dpp_i<0x4E>(xi) : sel == 2 ? dpp_i<0x141>(xi) : dpp_i<0x140>(xi);
+    return x + __int_as_float(o);
+  };
+  v = step(v, 0);
+  v = step(v, 1);
+  v = step(v, 2);
+  v = step(v, 3);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+// (key desc, index asc) argmax over the wave, result in every lane
+__device__ __forceinline__ void wave_argmax(uint32_t& k, int& i) {
+  auto step = [&](int sel) {
+    const int ok = sel == 0 ? dpp_i<0xB1>((int)k) : sel == 1 ? dpp_i<0x4E>((int)k) : sel == 2 ? dpp_i<0x141>((int)k) : dpp_i<0x140>((int)k);
+    const int oi = sel == 0 ? dpp_i<0xB1>(i) : sel == 1 ? dpp_i<0x4E>(i) : sel == 2 ? dpp_i<0x141>(i) : dpp_i<0x140>(i);
+    if ((uint32_t)ok > k || ((uint32_t)ok == k && oi < i)) { k = (uint32_t)ok; i = oi; }
+  };
+  step(0);
+  step(1);
+  step(2);
+  step(3);
+  // the four row results (scalar), folded in row order
+  uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)k, 0);
+  int ib = __builtin_amdgcn_readlane(i, 0);
+  uint32_t kr_[3];
+  int ir_[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    kr_[r] = (uint32_t)__builtin_amdgcn_readlane((int)k, 16 * (r + 1));
+    ir_[r] = __builtin_amdgcn_readlane(i, 16 * (r + 1));
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+    if (kr_[r] > kb || (kr_[r] == kb && ir_[r] < ib)) { kb = kr_[r]; ib = ir_[r]; }
+  k = kb;
+  i = ib;
+}
+// candidate windows below the row maximum, in key steps (bf16 ulps): 8, 12, 16, 24, ... 1536
+// (x sqrt 2), counted on a 1-in-8 subsample of the keys (element 0 of every 8-key chunk), two 16-bit
+// counts per int
+constexpr int NWIN = 16;
+__device__ __forceinline__ constexpr uint32_t kwin(int q) { return (q & 1 ? 12u : 8u) << (q >> 1); }
+
 __device__ __forceinline__ int block_sum_int1024(int v, int* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -384,11 +450,12 @@ __device__ __forceinline__ int block_sum_int1024(int v, int* red) {
 __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
     const bf16_t* __restrict__ logits, long ld, int V, float inv_temp, int top_k, float top_p, uint64_t seed,
     const int64_t* __restrict__ offset_ptr, const uint8_t* __restrict__ row_active, long* __restrict__ out_tok,
-    float* __restrict__ out_logp) {
+    float* __restrict__ out_logp, int use_window) {
   extern __shared__ __attribute__((aligned(16))) uint16_t keys[];  // [V]
   __shared__ int lidx[TK_CAP];
   __shared__ float lval[TK_CAP];   // tempered logit of each survivor
-  __shared__ int redi[16];
+  __shared__ uint16_t lkey[TK_CAP];  // window path: key of each candidate
+  __shared__ int redi[16][NWIN / 2 + 1];
   __shared__ float redf[16];
   __shared__ int cnt;
   const long row = blockIdx.x;
@@ -396,89 +463,282 @@ __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nv = V / 8;
 
-  // pass 1: stage keys, max + argmax
+  // pass 1: stage keys (the first RC chunks of every thread stay in registers, raw bf16 words and
+  // keys), row max. All of a thread's register-chunk loads are issued before the first is used (one
+  // round trip); keys are built two per 32-bit word and maxed with packed 16-bit ops (the kernel is
+  // VALU-bound on its one CU at batch 1). The argmax index (smallest index of the max key) is found
+  // in pass 2 by the few threads that hold the max.
+  constexpr int RC = 4;
+  typedef __attribute__((ext_vector_type(2))) unsigned short u16x2_t;
+  uint4 rr[RC], kr[RC];
+#pragma unroll
+  for (int i = 0; i < RC; ++i) {
+    const int c = tid + i * 1024;
+    rr[i] = c < nv ? *(const uint4*)(x + (long)c * 8) : make_uint4(0, 0, 0, 0);
+  }
+  // key of each bf16 half: negatives bit-flipped, positives with the sign bit set (= key16)
+  auto keyw = [](uint32_t w) -> uint32_t { return w ^ (((w & 0x80008000u) >> 15) * 0x7FFFu | 0x80008000u); };
+  auto pmax = [](uint32_t a, uint32_t b) -> uint32_t {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, a), __builtin_bit_cast(u16x2_t, b)));
+  };
+  auto keys_of = [&](const uint4& v) -> uint4 { return make_uint4(keyw(v.x), keyw(v.y), keyw(v.z), keyw(v.w)); };
+  auto cmax_of = [&](const uint4& k) -> uint32_t {  // max key of a chunk
+    const uint32_t m = pmax(pmax(k.x, k.y), pmax(k.z, k.w));
+    return max(m & 0xFFFFu, m >> 16);
+  };
   uint32_t kmax = 0;
-  int amx = 0;
-  for (int c = tid; c < nv; c += 1024) {
-    const uint4 v = *(const uint4*)(x + (long)c * 8);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint16_t k8[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      k8[2 * q] = (uint16_t)key16((uint16_t)(w[q] & 0xFFFF));
-      k8[2 * q + 1] = (uint16_t)key16((uint16_t)(w[q] >> 16));
+  for (int i = 0; i < RC; ++i) {
+    const int c = tid + i * 1024;
+    if (c < nv) {
+      kr[i] = keys_of(rr[i]);
+      *(uint4*)(keys + c * 8) = kr[i];
+      kmax = max(kmax, cmax_of(kr[i]));
+    } else {
+      kr[i] = make_uint4(0, 0, 0, 0);
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      if (k8[e] > kmax) { kmax = k8[e]; amx = c * 8 + e; }
-    *(uint4*)(keys + c * 8) = *(const uint4*)k8;
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint32_t ok = __shfl_xor(kmax, off, 64);
-    const int oi = __shfl_xor(amx, off, 64);
-    if (ok > kmax || (ok == kmax && oi < amx)) { kmax = ok; amx = oi; }
+  for (int c = tid + RC * 1024; c < nv; c += 1024) {
+    const uint4 kv = keys_of(*(const uint4*)(x + (long)c * 8));
+    *(uint4*)(keys + c * 8) = kv;
+    kmax = max(kmax, cmax_of(kv));
   }
-  if (tid == 0) cnt = 0;
-  if (lane == 0) { redi[wid] = amx; redf[wid] = __uint_as_float(kmax); }
+  const uint32_t kmax_own = kmax;
+  {
+    int ki = (int)kmax, dummy = 0;
+    // wave max (index unused: every lane passes 0)
+    uint32_t ku = (uint32_t)ki;
+    wave_argmax(ku, dummy);
+    kmax = ku;
+  }
+  __shared__ int amin;
+  if (tid == 0) { cnt = 0; amin = 0x7fffffff; }
+  if (lane == 0) redf[wid] = __uint_as_float(kmax);
   __syncthreads();
   uint32_t KM = __float_as_uint(redf[0]);
-  int AM = redi[0];
-  for (int w2 = 1; w2 < 16; ++w2) {
-    const uint32_t k = __float_as_uint(redf[w2]);
-    if (k > KM || (k == KM && redi[w2] < AM)) { KM = k; AM = redi[w2]; }
-  }
+  for (int w2 = 1; w2 < 16; ++w2) KM = max(KM, __float_as_uint(redf[w2]));
   const float M = key16_to_f(KM) * inv_temp;
-  // pass 2: normaliser of the full tempered distribution (behaviour log-prob)
+  // pass 2: normaliser of the full tempered distribution (behaviour log-prob); for the window path,
+  // how many subsample keys lie within kwin(q) key steps (bf16 ulps) below the maximum; and the
+  // argmax index (threads holding a max key: first match in index order, LDS atomicMin)
   float s = 0.f;
-  for (int c = tid; c < nv; c += 1024) {
-    const uint4 kv = *(const uint4*)(keys + c * 8);
-    const uint16_t* k8 = (const uint16_t*)&kv;
+  int wc[NWIN / 2] = {};  // field q & 1 (16 bits) of wc[q / 2]
+  auto pass2 = [&](const uint4& raw, const uint4& kv) {
+    const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s += __expf(key16_to_f(k8[e]) * inv_temp - M);
+    for (int e = 0; e < 8; ++e) {
+      const float f = __uint_as_float(e & 1 ? (w[e >> 1] & 0xFFFF0000u) : (w[e >> 1] << 16));
+      s += __expf(f * inv_temp - M);
+    }
+    const uint32_t d = KM - (kv.x & 0xFFFFu);
+#pragma unroll
+    for (int q = 0; q < NWIN; ++q) wc[q >> 1] += (d < kwin(q)) ? (1 << (16 * (q & 1))) : 0;
+  };
+#pragma unroll
+  for (int i = 0; i < RC; ++i)
+    if (tid + i * 1024 < nv) pass2(rr[i], kr[i]);
+  for (int c = tid + RC * 1024; c < nv; c += 1024) pass2(*(const uint4*)(x + (long)c * 8), *(const uint4*)(keys + c * 8));
+  if (kmax_own == KM) {
+    int idx = 0x7fffffff;
+    for (int c = tid; c < nv && idx == 0x7fffffff; c += 1024) {
+      const uint4 kv = *(const uint4*)(keys + c * 8);
+      const uint16_t* k8 = (const uint16_t*)&kv;
+      for (int e = 0; e < 8; ++e)
+        if (k8[e] == KM) { idx = c * 8 + e; break; }
+    }
+    atomicMin(&amin, idx);
   }
+  s = wave_sum_f(s);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  for (int q = 0; q < NWIN / 2; ++q) wc[q] = wave_sum_i(wc[q]);
   __syncthreads();
-  if (lane == 0) redf[wid] = s;
+  if (lane == 0) {
+    redf[wid] = s;
+#pragma unroll
+    for (int q = 0; q < NWIN / 2; ++q) redi[wid][q] = wc[q];
+  }
   __syncthreads();
   float S = 0.f;
 #pragma unroll
   for (int w2 = 0; w2 < 16; ++w2) S += redf[w2];
   const float lse = M + __logf(S);
+  const int AM = amin;
 
   int tok = AM;
   const bool active = row_active ? row_active[row] != 0 : true;
   if (active) {
-    // k-th largest key: largest t with count(keys >= t) >= K, bit by bit from the top
     const int K = min(top_k, V);
-    uint32_t prefix = 0;
-    for (int b = 15; b >= 0; --b) {
-      const uint32_t cand = prefix | (1u << b);
-      int c = 0;
+    // window path: a window below the maximum holding >= K keys and at most TK_CAP (typically
+    // 2-3 K) — every key >= the k-th largest is in it, so the k-th largest over the window's
+    // candidates IS the k-th largest over the row. The window is sized from the subsample counts
+    // (the narrowest with >= K / 4 + 2 subsample keys: ~2 K candidates); its exact count is known
+    // after the compaction, and a window holding < K or > TK_CAP keys falls back to the full-row
+    // search.
+    // The candidates go to LDS (wave-aggregated slots) and ONE wave finds the k-th key with wave
+    // reductions only, instead of 16 block-wide passes.
+    uint32_t win = 0;
+    if (use_window) {
+      // every wave: lane l < 16 holds wave l's packed counts, a row reduce sums them (no barrier)
+      const int need = K / 4 + 2;
+      int tot[NWIN / 2];
+#pragma unroll
+      for (int q = 0; q < NWIN / 2; ++q)
+        tot[q] = __builtin_amdgcn_readlane(row_sum_i(redi[lane & 15][q]), 0);
+#pragma unroll
+      for (int q = NWIN - 1; q >= 0; --q)
+        if (((tot[q >> 1] >> (16 * (q & 1))) & 0xFFFF) >= need) win = kwin(q);
+    }
+    uint32_t kth = 0;
+    bool done = false;
+    if (win) {
+      // chunks with a key in the window (chunk max vs the window floor, packed) place their
+      // candidates through an LDS slot counter — a few hundred of 32000 keys
+      auto cand = [&](const uint4& kv, int c) {
+        if (c < nv && KM - cmax_of(kv) < win) {
+          const uint16_t* k8 = (const uint16_t*)&kv;
+          for (int e = 0; e < 8; ++e)
+            if (KM - k8[e] < win) {
+              const int pos = atomicAdd(&cnt, 1);
+              if (pos < TK_CAP) { lidx[pos] = c * 8 + e; lkey[pos] = k8[e]; }
+            }
+        }
+      };
+#pragma unroll
+      for (int i = 0; i < RC; ++i) cand(kr[i], tid + i * 1024);
+      for (int c = tid + RC * 1024; c < nv; c += 1024) cand(*(const uint4*)(keys + c * 8), c);
+      __syncthreads();
+      const int n = cnt;
+      if (n >= K && n <= TK_CAP) {
+        done = true;
+        if (wid == 0) {
+          // k-th largest key: largest t with count(keys >= t) >= K, bit by bit from the top; the
+          // lane's first 8 candidates in registers
+          constexpr int CR = 8;
+          uint32_t ck[CR];
+#pragma unroll
+          for (int i = 0; i < CR; ++i) ck[i] = lane + 64 * i < n ? lkey[lane + 64 * i] : 0u;
+          uint32_t prefix = 0;
+          for (int b = 15; b >= 0; --b) {
+            const uint32_t cnd = prefix | (1u << b);
+            int c = 0;  // wave-uniform: ballot popcounts
+#pragma unroll
+            for (int i = 0; i < CR; ++i) c += (int)__popcll(__ballot(ck[i] >= cnd && lane + 64 * i < n));
+            for (int j0 = 64 * CR; j0 < n; j0 += 64)
+              c += (int)__popcll(__ballot(j0 + lane < n && lkey[min(j0 + lane, n - 1)] >= cnd));
+            if (c >= K) prefix = cnd;
+          }
+          kth = prefix;
+          // survivors (key >= kth, ties kept) compacted in place, in candidate order
+          int ns = 0;
+          for (int j0 = 0; j0 < n; j0 += 64) {
+            const int j = j0 + lane;
+            const bool in = j < n;
+            const int idx = in ? lidx[j] : 0;
+            const uint32_t key = in ? lkey[j] : 0u;
+            const bool keep = in && key >= kth;
+            const unsigned long long bal = __ballot(keep);
+            const int pos = ns + (int)__popcll(bal & ((1ull << lane) - 1ull));
+            if (keep) { lidx[pos] = idx; lval[pos] = key16_to_f(key) * inv_temp; }
+            ns += (int)__popcll(bal);
+          }
+          if (lane == 0) cnt = ns;
+        }
+      } else {
+        __syncthreads();  // every thread has read cnt
+        if (tid == 0) cnt = 0;
+        __syncthreads();
+      }
+    }
+    if (!done) {
+      // k-th largest key over the LDS-resident keys: 16 block-wide counting passes
+      uint32_t prefix = 0;
+      for (int b = 15; b >= 0; --b) {
+        const uint32_t cnd = prefix | (1u << b);
+        int c = 0;
+        for (int cc = tid; cc < nv; cc += 1024) {
+          const uint4 kv = *(const uint4*)(keys + cc * 8);
+          const uint16_t* k8 = (const uint16_t*)&kv;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) c += k8[e] >= cnd;
+        }
+        if (block_sum_int1024(c, &redi[0][0]) >= K) prefix = cnd;
+      }
+      kth = prefix;
+      // compact the survivors (ties at the threshold kept)
       for (int cc = tid; cc < nv; cc += 1024) {
         const uint4 kv = *(const uint4*)(keys + cc * 8);
         const uint16_t* k8 = (const uint16_t*)&kv;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) c += k8[e] >= cand;
+        for (int e = 0; e < 8; ++e)
+          if (k8[e] >= kth) {
+            const int pos = atomicAdd(&cnt, 1);
+            if (pos < TK_CAP) { lidx[pos] = cc * 8 + e; lval[pos] = key16_to_f(k8[e]) * inv_temp; }
+          }
       }
-      if (block_sum_int1024(c, redi) >= K) prefix = cand;
-    }
-    const uint32_t kth = prefix;
-    // compact the survivors (ties at the threshold kept)
-    for (int cc = tid; cc < nv; cc += 1024) {
-      const uint4 kv = *(const uint4*)(keys + cc * 8);
-      const uint16_t* k8 = (const uint16_t*)&kv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (k8[e] >= kth) {
-          const int pos = atomicAdd(&cnt, 1);
-          if (pos < TK_CAP) { lidx[pos] = cc * 8 + e; lval[pos] = key16_to_f(k8[e]) * inv_temp; }
-        }
     }
     __syncthreads();
     const bool overflow = cnt > TK_CAP;  // > TK_CAP - top_k ties at the k-th value: draw from the keys
     const int n = min(cnt, TK_CAP);
+    if (!overflow && n <= 64) {
+      // <= 64 survivors (top-k 50): sort, nucleus cut and Gumbel draw in wave 0's registers, no
+      // block barrier — the same arithmetic, lane assignment and reduction order as the general
+      // path below, so the same token
+      if (wid != 0) return;
+      float v = lane < n ? lval[lane] : -INFINITY;
+      int ix = lane < n ? lidx[lane] : 0x7fffffff;
+      float vthr = -INFINITY;
+      if (top_p < 1.f && n > 1) {
+#pragma unroll
+        for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+          for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const float ov = __shfl_xor(v, stride, 64);
+            const int oi = __shfl_xor(ix, stride, 64);
+            const bool i_lo = (lane & stride) == 0;
+            const bool desc = ((lane & ~stride) & size) == 0;
+            const bool mine_first = v > ov || (v == ov && ix < oi);
+            if (!((i_lo == desc) ? mine_first : !mine_first)) { v = ov; ix = oi; }
+          }
+        // one survivor per lane (per = 1): the general path's chunked prefix with a chunk of one
+        const float part = lane < n ? __expf(v - M) : 0.f;
+        float incl = part;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const float t = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += t;
+        }
+        const float total = __shfl(incl, 63, 64);
+        const float target = top_p * total;
+        float run = incl - part;
+        bool found = false;
+        if (lane < n) {
+          run += __expf(v - M);
+          found = run >= target;
+        }
+        const unsigned long long m = __ballot(found);
+        const int src = m ? __ffsll((long long)m) - 1 : n - 1;
+        vthr = __shfl(v, src, 64);
+      }
+      const uint64_t off = offset_ptr ? (uint64_t)offset_ptr[0] : 0ull;
+      float best = -INFINITY;
+      int bi = AM;
+      if (lane < n && v >= vthr) {
+        const uint4 r = Philox::gen(seed, (uint64_t)row, off * (uint64_t)V + (uint64_t)ix);
+        best = v - __logf(-__logf(u32_to_unit(r.x)));
+        bi = ix;
+      }
+#pragma unroll
+      for (int o2 = 32; o2 > 0; o2 >>= 1) {
+        const float ob = __shfl_xor(best, o2, 64);
+        const int oi = __shfl_xor(bi, o2, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      if (lane == 0) {
+        out_tok[row] = bi;
+        if (out_logp) out_logp[row] = key16_to_f(keys[bi]) * inv_temp - lse;
+      }
+      return;
+    }
     float vthr = -INFINITY;  // kept: lval >= vthr
     if (top_p < 1.f && n > 1 && !overflow) {
       // sort survivors by (value desc, token asc) — a total order, so every sorting network gives
@@ -583,17 +843,17 @@ __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
       if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
     }
     __syncthreads();
-    if (lane == 0) { redf[wid] = best; redi[wid] = bi; }
+    if (lane == 0) { redf[wid] = best; redi[wid][0] = bi; }
     __syncthreads();
     if (tid == 0) {
       float Bv = redf[0];
-      int BI = redi[0];
+      int BI = redi[0][0];
       for (int w2 = 1; w2 < 16; ++w2)
-        if (redf[w2] > Bv || (redf[w2] == Bv && redi[w2] < BI)) { Bv = redf[w2]; BI = redi[w2]; }
-      redi[0] = BI;
+        if (redf[w2] > Bv || (redf[w2] == Bv && redi[w2][0] < BI)) { Bv = redf[w2]; BI = redi[w2][0]; }
+      redi[0][0] = BI;
     }
     __syncthreads();
-    tok = redi[0];
+    tok = redi[0][0];
   }
   if (tid == 0) {
     out_tok[row] = tok;
@@ -612,7 +872,8 @@ extern "C" int rt_sample(const void* logits, int is_f32, long ld, long B, int V,
   if (!is_f32 && !greedy && top_k > 0 && top_k <= 1024 && V % 8 == 0 && ld % 8 == 0 && (size_t)V * 2 <= 96 * 1024) {
     const size_t shm = ((size_t)V * 2 + 15) / 16 * 16;
     hipLaunchKernelGGL(sample_topk_search_kernel, dim3(B), dim3(1024), shm, stream, (const bf16_t*)logits, ld, V,
-                       inv_temp, top_k, top_p, seed, offset_ptr, row_active, out_tok, out_logp);
+                       inv_temp, top_k, top_p, seed, offset_ptr, row_active, out_tok, out_logp,
+                       tuning().sample_window);
     RT_LAUNCH_CHECK();
     return 0;
   }

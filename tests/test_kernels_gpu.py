@@ -1248,3 +1248,25 @@ def test_sampler_search_kth_exact(top_k):
         assert keep.gather(1, tok[:, None]).float().mean().item() >= 0.97
 
 
+
+
+@pytest.mark.parametrize("top_k,top_p,scale", [(50, 1.0, 2.0), (50, 0.9, 2.0), (7, 0.5, 0.3), (300, 0.95, 8.0),
+                                               (1024, 1.0, 1.0), (50, 0.9, 0.02)])
+def test_sampler_window_path_bitwise(top_k, top_p, scale):
+    """Top-k candidates from a window below the row maximum (one wave finds the k-th key) vs the 16
+    block-wide counting passes over the whole row: the same k-th key, kept set, Philox draw and
+    behaviour log-prob, bitwise — over logit scales that pick different windows (and, at tiny
+    scales, the full-row fallback when no window holds <= 2048 keys)."""
+    B, V = 48, 32000
+    g = torch.Generator(device="cpu").manual_seed(top_k)
+    logits = (torch.randn(B, V, generator=g) * scale).to(torch.bfloat16).to(DEV)
+    logits[3, 100:140] = logits[3].max()  # ties at the top
+    off = torch.full((1,), 5, dtype=torch.long, device=DEV)
+    with ops.tuning(sample_window=1):
+        t1, l1 = ops.sample(logits, 1 / 0.7, top_k=top_k, top_p=top_p, seed=9, offset=off)
+    with ops.tuning(sample_window=0):
+        t0, l0 = ops.sample(logits, 1 / 0.7, top_k=top_k, top_p=top_p, seed=9, offset=off)
+    assert torch.equal(t1, t0)
+    assert torch.equal(l1, l0)
+    keep = ref.filter_logits(logits.float(), 1 / 0.7, top_k, top_p)
+    assert keep.gather(1, t1[:, None]).float().mean().item() >= 0.97

@@ -11,9 +11,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 SRC = os.path.join(ROOT, "csrc", "kernels", "sampling.hip")
 
 P1 = "  const float M = key16_to_f(KM) * inv_temp;\n  // pass 2:"
-P2 = "  const float lse = M + __logf(S);\n\n  int tok = AM;\n"
+P2 = "  const int AM = amin;\n\n  int tok = AM;\n"
 P3 = "    }\n    __syncthreads();\n    const bool overflow = cnt > TK_CAP;"
-EXIT = "  if (use_window >= 100) { if (tid == 0) out_tok[row] = AM; return; }\n"
+EXIT = "  if (use_window >= 100) { if (tid == 0) out_tok[row] = (long)KM; return; }\n"
 
 
 def _sub(s, old, new):
