@@ -60,7 +60,7 @@ class PPOConfig:
     kl_horizon: int = 10000
     ppo_epochs: int = 1                  # reference: one update per batch (rl.py:328)
     minibatch_size: int = 16
-    ref_minibatch_size: int = 64        # reference log-prob scoring (no grad)
+    ref_minibatch_size: int = 128       # reference log-prob scoring (no grad): 38k-token GEMMs (0.895 -> 0.879 s, profiles/r5/bench_ref_minibatch_ab.log)
     whiten_advantages: bool = True
     # generation (rl.py:38-44)
     max_new_tokens: int = 128
