@@ -103,6 +103,9 @@ def main():
     ap.add_argument("--old-logp", default="rollout", choices=["rollout", "recompute"],
                     help="PPO ratio's theta_old log-probs: the rollout sampler's (free) or a training-numerics "
                          "forward of the policy beside the reference forward (exact ratio 1 at theta_old)")
+    ap.add_argument("--defer-splitk", default="on", choices=["on", "off"],
+                    help="decode at batch > 64: split-K partials summed by the norm / attention kernels (on) or "
+                         "reduced after each GEMM (off; A/B)")
     ap.add_argument("--merged-rollout", default="on", choices=["on", "off"],
                     help="rollouts on the merged bf16 W + s*B*A copy (on) or on the unmerged LoRA K-extension (off)")
     args = ap.parse_args()
@@ -173,6 +176,9 @@ def main():
     pcfg = models.resolve_preset(args.model)
     tok = Tokenizer.synthetic(pcfg.vocab_size, pcfg.arch)
     policy = build_model(args.model, device=dev, dtype=torch.bfloat16, seed=0, fast_init=True)
+    policy.defer_splitk = args.defer_splitk == "on"
+    if args.defer_splitk == "off":
+        tuning_over["defer_splitk"] = "off"
     enc_model = build_model(args.encoder, device=dev, dtype=torch.bfloat16, seed=1, fast_init=True).eval()
     encoder = Encoder(enc_model, Tokenizer.synthetic(enc_model.cfg.vocab_size, enc_model.cfg.arch), max_length=128)
     log(f"[bench] models ready: {args.model} ({pcfg.num_params() / 1e9:.2f} B params) + {args.encoder}")

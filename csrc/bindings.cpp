@@ -31,6 +31,8 @@ int rt_gemm_big_rope(const void*, long, const void*, long, const void*, long, co
                      void*, long, int, int, int, const int*, const float*, const float*, int, int, const void*, int,
                      hipStream_t);
 int rt_gemm_splitk_reduce(const float*, int, int, int, const void*, int, const void*, long, void*, long, hipStream_t);
+int rt_gemm_big_fp8_slabs(const void*, long, const float*, const void*, long, const float*, float*, int, int, int, int,
+                          int, hipStream_t);
 int rt_gemm_big_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int,
                     int, int, int, const void*, long, const void*, long, int, void*, long, const void*, hipStream_t);
 int rt_gemm_fp8(const void*, long, const float*, const void*, long, const float*, const void*, void*, long, int, int,
@@ -684,6 +686,23 @@ std::vector<Tensor> norm_fwd_slabs(bool layernorm, const Tensor& slabs, int64_t 
   return {y, h};
 }
 
+// W8A8 split-K into fp32 slabs (config-5 decode at batch > 64; the consumer sums them)
+void gemm_fp8_splitk_raw(const Tensor& xq, const Tensor& sx, const Tensor& wq, const Tensor& sw, int64_t nsplit,
+                         Tensor slabs, int64_t bn) {
+  CHECK_CUDA(xq); CHECK_F32(sx); CHECK_F32(sw); CHECK_ROWS(xq); CHECK_ROWS(wq); CHECK_F32(slabs);
+  TORCH_CHECK(xq.scalar_type() == at::kByte && wq.scalar_type() == at::kByte, "gemm_fp8_splitk_raw: e4m3fn operands");
+  const int64_t M = xq.size(0), K = xq.size(1), N = wq.size(0);
+  TORCH_CHECK(wq.size(1) == K && sx.numel() == M && sw.numel() == N && K % 128 == 0 && N % 8 == 0,
+              "gemm_fp8_splitk_raw: shapes");
+  TORCH_CHECK(xq.stride(0) % 16 == 0 && wq.stride(0) % 16 == 0, "gemm_fp8_splitk_raw: row strides % 16");
+  TORCH_CHECK(slabs.is_contiguous() && slabs.numel() >= nsplit * M * N, "gemm_fp8_splitk_raw: workspace too small");
+  if (M == 0) return;
+  check_rc(rt_gemm_big_fp8_slabs(xq.data_ptr(), xq.stride(0), sx.data_ptr<float>(), wq.data_ptr(), wq.stride(0),
+                                 sw.data_ptr<float>(), slabs.data_ptr<float>(), (int)M, (int)N, (int)K, (int)nsplit,
+                                 (int)bn, cur_stream()),
+           "gemm_fp8_splitk_raw");
+}
+
 // split-K partial slabs only (the reduce is fused into the consumer): slabs [nsplit, M, N] fp32
 void gemm_splitk_raw(const Tensor& a, const Tensor& w, int64_t nsplit, Tensor slabs, int64_t bn) {
   CHECK_CUDA(a); CHECK_BF16(a); CHECK_BF16(w); CHECK_ROWS(a); CHECK_ROWS(w); CHECK_F32(slabs);
@@ -1302,6 +1321,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_reduce", &splitk_reduce, "sum of split-K slabs -> bf16");
   m.def("norm_fwd_slabs", &norm_fwd_slabs, "residual-add + norm whose input is a sum of split-K slabs");
   m.def("gemm_splitk_raw", &gemm_splitk_raw, "split-K NT GEMM into fp32 slabs (reduce fused into the consumer)");
+  m.def("gemm_fp8_splitk_raw", &gemm_fp8_splitk_raw, "W8A8 split-K NT GEMM into fp32 slabs (scales applied per split)");
   m.def("norm_bwd", &norm_bwd);
   m.def("rope_qkv", &rope_qkv);
   m.def("swiglu_fwd", &swiglu_fwd);

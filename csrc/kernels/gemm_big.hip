@@ -136,7 +136,8 @@ __device__ __forceinline__ void wait_granules(int n) {
 template <int LA, int LB, int OUT, int EPI, int BN, bool F8 = false>
 __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   static_assert(BN == 256 || BN == 128, "BN");
-  static_assert(!F8 || (LA == ROW && LB == ROW && OUT == O_BF16), "F8: NT with a bf16 output only");
+  static_assert(!F8 || (LA == ROW && LB == ROW && (OUT == O_BF16 || OUT == O_F32_SLAB)),
+                "F8: NT with a bf16 output or split-K slabs only");
   constexpr int NB = BN / 128;  // B fragments per wave and B sub-block; LDS-DMA instructions per B granule
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];  // the only __shared__ object
 
@@ -447,24 +448,32 @@ __global__ __launch_bounds__(512, 2) void gemm_big_kernel(Args p) {
   } else if constexpr (OUT == O_F32 || OUT == O_F32_SLAB) {
     // O_F32_SLAB: split ks writes its partial tile to slab ks ([nsplit][M][ldc], plain stores);
     // splitk_reduce_kernel sums the slabs and runs the epilogue. N % 4 == 0 (launcher).
+    // F8 (slabs): each split's partial carries the per-token x per-channel scales (the reduce is a
+    // plain sum)
     float* C = (float*)p.C + (OUT == O_F32_SLAB ? (long)blockIdx.y * p.M * p.ldc : 0L);
 #pragma unroll
     for (int j = 0; j < 2 * NB; ++j) {
       const int col = n0 + col_of(j) + fq * 4;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      float sc[4] = {1.f, 1.f, 1.f, 1.f};
       if (OUT == O_F32 && p.bias && col < p.N) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[r] = bf2f(p.bias[col + r]);
+      }
+      if (F8) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[r] = p.sb[min(col + r, p.N - 1)];
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int row = m0 + wr * 128 + i * 16 + frow;
         if (row < p.M && col < p.N) {
+          const float sr = F8 ? p.sa[row] : 1.f;
           float4 v;
-          v.x = act_fn(acc[i][j][0] + bv[0], EPI);
-          v.y = act_fn(acc[i][j][1] + bv[1], EPI);
-          v.z = act_fn(acc[i][j][2] + bv[2], EPI);
-          v.w = act_fn(acc[i][j][3] + bv[3], EPI);
+          v.x = act_fn((F8 ? acc[i][j][0] * (sr * sc[0]) : acc[i][j][0]) + bv[0], EPI);
+          v.y = act_fn((F8 ? acc[i][j][1] * (sr * sc[1]) : acc[i][j][1]) + bv[1], EPI);
+          v.z = act_fn((F8 ? acc[i][j][2] * (sr * sc[2]) : acc[i][j][2]) + bv[2], EPI);
+          v.w = act_fn((F8 ? acc[i][j][3] * (sr * sc[3]) : acc[i][j][3]) + bv[3], EPI);
           *(float4*)(C + (long)row * p.ldc + col) = v;
         }
       }
@@ -1079,6 +1088,27 @@ extern "C" int rt_gemm_big_fp8(const void* A, long lda, const float* sa, const v
     if (p.C2) q.C2 = p.C2 + r0 * p.ldc2;
     launch(q, 128);
   }
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+// W8A8 split-K into fp32 slabs [nsplit][M][N] (decode at batch > 64, config 5): the split
+// partials carry sa[row] * sb[col] and are summed by the consumer (the norm / attention
+// prologue, as the bf16 slab GEMMs' — ops.linear_deferred). bn 128 or 256, N % 8 == 0.
+extern "C" int rt_gemm_big_fp8_slabs(const void* A, long lda, const float* sa, const void* B, long ldb, const float* sb,
+                                     float* slabs, int M, int N, int K, int nsplit, int bn, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 128 || lda % 16 || ldb % 16 || N % 8 || nsplit < 1 || (bn != 128 && bn != 256)) return -1;
+  Args p{};
+  p.A = (const bf16_t*)A; p.lda = lda / 2; p.B = (const bf16_t*)B; p.ldb = ldb / 2;
+  p.C = slabs; p.ldc = N;
+  p.M = M; p.N = N; p.K = K / 2; p.act = E_NONE; p.nsplit = nsplit; p.zpage = (const bf16_t*)A;
+  p.sa = sa; p.sb = sb;
+  p.group_m = tuning().gemm_group_m;
+  const int tn = bn == 256 ? (N + 255) / 256 : (N + 127) / 128;
+  dim3 grid(((M + 255) / 256) * tn, nsplit), block(512);
+  if (bn == 256) hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_F32_SLAB, E_NONE, 256, true>), grid, block, 0, stream, p);
+  else hipLaunchKernelGGL((gemm_big_kernel<ROW, ROW, O_F32_SLAB, E_NONE, 128, true>), grid, block, 0, stream, p);
   RT_LAUNCH_CHECK();
   return 0;
 }

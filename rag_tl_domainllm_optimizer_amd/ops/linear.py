@@ -677,16 +677,32 @@ class SplitK:
 
 def linear_deferred(x: torch.Tensor, w: torch.Tensor, bias=None, lora: Optional[LoRAGroup] = None, fp8=None):
     """``linear`` for no-grad decode steps that may return a :class:`SplitK` (unreduced) when the
-    plan splits K (bf16 weights, no bias / activation, merged or absent LoRA); else a tensor."""
+    plan splits K (no bias / activation, merged or absent LoRA); else a tensor. ``fp8`` (config 5):
+    the W8A8 split-K form — per-token fp8 activations, each split's partial scaled in its epilogue,
+    the same slab consumers (the o / down projections of a 13B layer are 40 output tiles: without
+    the split they ran on 40 of 256 CUs)."""
     x2 = x.reshape(-1, x.shape[-1])
     use_lora = lora is not None and lora.enabled
-    if (not on_gpu(x2) or torch.is_grad_enabled() or bias is not None or fp8 is not None or w.dtype != torch.bfloat16
+    if (not on_gpu(x2) or torch.is_grad_enabled() or bias is not None or w.dtype != torch.bfloat16
             or x2.dtype != torch.bfloat16 or (use_lora and not lora.use_merged) or x2.shape[0] <= 64
             or w.shape[0] % 16 or x2.shape[1] % 8):
         return linear(x, w, bias, None, lora, fp8)
     w_eff = lora.merged_weight(w) if use_lora else w
     M, K = x2.shape
     N = w_eff.shape[0]
+    if fp8 is not None:
+        from .fp8 import fp8_supported, quantize_fp8
+
+        if not fp8_supported(w_eff) or K % 128:
+            return linear(x, w, bias, None, lora, fp8)
+        s, bn = splitk_plan(M, N, K // 2, 0)  # an fp8 K-step is 128 bytes: half the bf16 steps
+        if s <= 1:
+            return linear(x, w, bias, None, lora, fp8)
+        q, sc = fp8.get(w_eff)
+        xq, sx = quantize_fp8(x2)
+        slabs = torch.empty(s * M * N, dtype=torch.float32, device=x2.device)
+        native().gemm_fp8_splitk_raw(xq, sx, q, sc, s, slabs, bn or 256)
+        return SplitK(slabs, s, M, N, x2.dtype)
     s, bn = splitk_plan(M, N, K, 0)
     if s <= 1:
         return gemm(x2.contiguous(), w_eff).reshape(*x.shape[:-1], N)
