@@ -14,8 +14,8 @@ namespace rt {
 
 constexpr int NORM_MAXV = 8;  // max 16-B vectors per thread -> H <= 256*8*8 = 16384
 
-template <bool LAYERNORM, int NV>
-__global__ __launch_bounds__(512) void norm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+template <bool LAYERNORM, int NV, int MAXT = 512>
+__global__ __launch_bounds__(MAXT) void norm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                        const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
                                                        bf16_t* __restrict__ y, bf16_t* __restrict__ h_out,
                                                        float* __restrict__ rstd_out, float* __restrict__ mean_out,
@@ -23,7 +23,7 @@ __global__ __launch_bounds__(512) void norm_fwd_kernel(const bf16_t* __restrict_
                                                        long sstride) {
   // xs != null: x is the bf16-rounded sum of nsplit fp32 split-K slabs (stride sstride floats):
   // the split-K reduce of the producing GEMM fused into this pass (decode at batch 65..512)
-  __shared__ float sbuf[8];
+  __shared__ float sbuf[16];  // <= 16 waves
   const long row = blockIdx.x;
   const int nv = H / 8;
   const bf16_t* xr = x + row * H;
@@ -211,6 +211,21 @@ extern "C" int rt_norm_fwd(int layernorm, const void* x, const void* res, const 
   if (xs && sl >= 512 && H / 8 >= 512 && H / 8 <= 512) {
     threads = 512;
     nvpt = 1;
+  }
+  // H = 5120 (Llama-2-13B, config 5): one chunk per thread over 640 threads — the 256-thread form
+  // sums three chunks' slabs one memory round trip after another (19.6 us per norm at batch 256)
+  if (xs && sl >= 512 && H / 8 > 512 && H / 8 <= 1024) {
+    const int t = (H / 8 + 63) / 64 * 64;
+    if (layernorm)
+      hipLaunchKernelGGL((norm_fwd_kernel<true, 1, 1024>), dim3(T), dim3(t), 0, stream, (const bf16_t*)x,
+                         (const bf16_t*)res, (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (bf16_t*)h_out, rstd, mean,
+                         H, eps, xs, nsplit, (long)T * H);
+    else
+      hipLaunchKernelGGL((norm_fwd_kernel<false, 1, 1024>), dim3(T), dim3(t), 0, stream, (const bf16_t*)x,
+                         (const bf16_t*)res, (const bf16_t*)w, (const bf16_t*)b, (bf16_t*)y, (bf16_t*)h_out, rstd, mean,
+                         H, eps, xs, nsplit, (long)T * H);
+    RT_LAUNCH_CHECK();
+    return 0;
   }
   if (layernorm) {
     NORM_DISPATCH(true, norm_fwd_kernel, dim3(T), dim3(threads), 0, stream, (const bf16_t*)x, (const bf16_t*)res,

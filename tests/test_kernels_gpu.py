@@ -228,10 +228,11 @@ def test_linear_lora_dropout():
 
 
 @pytest.mark.parametrize("threads", [256, 512])
-@pytest.mark.parametrize("H,ns", [(4096, 8), (4096, 5), (5120, 8)])
+@pytest.mark.parametrize("H,ns", [(4096, 8), (4096, 5), (5120, 8), (5120, 6)])
 def test_norm_split_k_slabs(H, ns, threads):
     """Decode-batch RMSNorm that also reduces the producing GEMM's split-K slabs (256 or 512 threads
-    per row) against the fp32 reference: h = bf16(bf16(sum slabs) + residual), y = RMSNorm(h) w."""
+    per row; H = 5120: 640 threads) against the fp32 reference: h = bf16(bf16(sum slabs) + residual),
+    y = RMSNorm(h) w."""
     B = 256
     slabs = torch.randn(ns, B, H, device=DEV) * 0.2
     r = torch.randn(B, H, device=DEV, dtype=torch.bfloat16)
