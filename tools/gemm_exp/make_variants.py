@@ -104,8 +104,16 @@ def _bglb(s):
                 "      GB_MMA(1, 0, fb0);\n      fb0[0] = fbn0[0]; fb0[1] = fbn0[1]; fb1[0] = fbn1[0]; fb1[1] = fbn1[1];\n    }\n")
 
 
+def _ntstore(s):
+    # the bf16 epilogue's 16-B global stores non-temporal (no L2 / MALL allocation for the output)
+    s = _sub(s, "            *(uint4*)(C + (long)grow * p.ldc + gcol) = v;\n",
+             "            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4*)(C + (long)grow * p.ldc + gcol));\n")
+    return _sub(s, "            *(uint4*)(Cf + (long)grow * p.ldc + fcol) = pack8(f);\n",
+                "            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, pack8(f)), (u32x4*)(Cf + (long)grow * p.ldc + fcol));\n")
+
+
 def variants(s):
-    return {"base": s, "nob": _nob(s), "bglb": _bglb(s)}
+    return {"base": s, "ntstore": _ntstore(s)}
 
 
 def main():
