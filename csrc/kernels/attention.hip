@@ -1965,7 +1965,7 @@ static bool rt_attn_decode_mw_ok(int B, int Hq, int Hkv, int D, int Smax) {
 }
 static int rt_attn_decode_mw_np(int Smax, int np_ws) {
   const int kpp = std::max(16, tuning().decode_mw_kpp);
-  if (Smax <= 1024 || np_ws <= 1) return 1;
+  if (Smax <= tuning().decode_mw_smax || np_ws <= 1) return 1;
   return std::max(1, std::min(np_ws, (Smax + kpp - 1) / kpp));
 }
 extern "C" int rt_attn_decode_mfma_ok(int B, int Hq, int Hkv, int D, int NP) {

@@ -261,13 +261,10 @@ class DecodeWorkspace(tuple):
 def decode_workspace(B, Hq, Hkv, D, Smax, device, PS=None):
     PS = PS or decode_partition(B * Hkv, D, Smax)
     NP = (Smax + PS - 1) // PS
-    # records of D + 2 floats (o | m | l); the batch-1 attention + o_proj kernel uses 16-B aligned
-    # records of 132 floats
-    part = torch.empty(max(B * (D + 2), 132) * Hkv * NP * (Hq // Hkv), dtype=torch.float32, device=device)
+    # records of D + 2 floats (o | m | l) per (batch, kv head, partition, query head)
+    part = torch.empty(B * (D + 2) * Hkv * NP * (Hq // Hkv), dtype=torch.float32, device=device)
     tickets = torch.zeros(B * Hkv, dtype=torch.int32, device=device)
-    # batch-1 attention + o_proj launch: [producers published, blocks done] counters + give-up flag
-    sync = torch.zeros(3, dtype=torch.int32, device=device)
-    return DecodeWorkspace((part, PS, tickets, sync))
+    return DecodeWorkspace((part, PS, tickets))
 
 
 # ----------------------------------------------------------------------------- fp8 K/V cache
