@@ -97,11 +97,12 @@ __device__ __forceinline__ int v_off(int r, int c) {
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
-// NU = 16-row query blocks per wave: 2 -> 4 waves of 32 rows (256 threads), 1 -> 8 waves of 16 rows
-// (512 threads, half the registers per wave: twice the waves per SIMD to hide the per-tile load /
-// barrier latency of short sequences). Either way a workgroup owns 128 query rows.
+// NU = 16-row query blocks per wave: 2 -> 4 waves of 32 rows (256 threads; the launched form), 1 -> 8
+// waves of 16 rows (512 threads). Either way a workgroup owns 128 query rows. The occupancy hint
+// follows the LDS footprint (D = 128: two 64-KiB double-buffered workgroups per CU), not the wave
+// count, so the register cap never forces spills that the LDS would not allow to pay off.
 template <int D, int NU = 2>
-__global__ __launch_bounds__(64 * 8 / NU, NU == 1 ? 4 : (D == 128 ? 2 : (D == 64 ? 3 : 4)))
+__global__ __launch_bounds__(64 * 8 / NU, D == 128 ? 2 : (D == 64 ? 3 : 4))
 void attn_fwd_kernel(AttnArgs a) {
   constexpr int NT = 64 * 8 / NU;  // threads per workgroup
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
