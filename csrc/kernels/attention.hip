@@ -101,9 +101,18 @@ __device__ __forceinline__ int v_off(int r, int c) {
 // waves of 16 rows (512 threads). Either way a workgroup owns 128 query rows. The occupancy hint
 // follows the LDS footprint (D = 128: two 64-KiB double-buffered workgroups per CU), not the wave
 // count, so the register cap never forces spills that the LDS would not allow to pay off.
-template <int D, int NU = 2>
+//
+// HP (head-packed, GQA with G = 4, NU = 2): a workgroup = 32 query positions x the 4 query heads of
+// one kv head (wave w = head 4 hk + w), instead of 128 positions of one head. The 4 waves share
+// every K / V tile as before, but all of them have the same causal key range, so short sequences
+// (training / reference forwards at S ~ 300) stop spending tiles on rows the diagonal has already
+// passed: the 128-row tile's waves ran every key tile up to the tile's LAST row. Per row the same
+// key tiles in the same order with the same arithmetic (trailing fully masked tiles change
+// nothing: alpha = 1, p = 0), so the output and lse are bitwise the 128-row form's.
+template <int D, int NU = 2, bool HP = false>
 __global__ __launch_bounds__(64 * 8 / NU, D == 128 ? 2 : (D == 64 ? 3 : 4))
 void attn_fwd_kernel(AttnArgs a) {
+  static_assert(!HP || NU == 2, "HP: 4 waves of 32 rows");
   constexpr int NT = 64 * 8 / NU;  // threads per workgroup
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TILE_BYTES = 64 * D * 2;
@@ -119,14 +128,16 @@ void attn_fwd_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   const int3 bx = attn_block_xyz();
-  const int b = bx.z, h = bx.y;
-  const int hk = h / (a.Hq / a.Hkv);
-  const int qblk0 = bx.x * 128;
-  const int q0 = qblk0 + wid * 16 * NU;
+  const int b = bx.z;
+  const int h = HP ? bx.y * 4 + wid : bx.y;
+  const int hk = HP ? bx.y : h / (a.Hq / a.Hkv);
+  constexpr int QROWS = HP ? 32 : 128;  // query positions per workgroup
+  const int qblk0 = bx.x * QROWS;
+  const int q0 = HP ? qblk0 : qblk0 + wid * 16 * NU;
 
   const int start = a.kv_start ? a.kv_start[b] : 0;
   int kend = a.kv_len ? min(a.kv_len[b], a.Sk) : a.Sk;
-  const int qlast = min(qblk0 + 127, a.Sq - 1);
+  const int qlast = min(qblk0 + QROWS - 1, a.Sq - 1);
   if (a.causal) kend = min(kend, qlast + 1);
   int kbeg = start;
   if (a.window > 0) kbeg = max(kbeg, qblk0 - a.window + 1);
@@ -329,9 +340,11 @@ void attn_fwd_kernel(AttnArgs a) {
   __syncthreads();
   for (int e = tid; e < 128 * NCH; e += NT) {
     const int row = e / NCH, c = e % NCH;
-    const int qq = qblk0 + row;
+    // HP: staging row 32 w + r = position qblk0 + r of head 4 hk + w
+    const int qq = HP ? qblk0 + (row & 31) : qblk0 + row;
+    const int hh = HP ? hk * 4 + (row >> 5) : h;
     if (qq < a.Sq)
-      *(uint4*)(a.o + ((long)b * a.Sq + qq) * a.ldo + (long)h * D + c * 8) = *(const uint4*)(Os + row * OROW + c * 8);
+      *(uint4*)(a.o + ((long)b * a.Sq + qq) * a.ldo + (long)hh * D + c * 8) = *(const uint4*)(Os + row * OROW + c * 8);
   }
 }
 
@@ -1916,6 +1929,14 @@ extern "C" int rt_attn_fwd(const void* q, long ldq, const void* k, long ldk, con
   a.rb_L = rb_L; a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.window = window;
   a.scale_log2 = scale * 1.4426950408889634f;
   if (B == 0 || Sq == 0) return 0;
+  // GQA (4 query heads per kv head), D = 128, short sequences: the head-packed 32-position tiles
+  // (every wave of a workgroup on the same causal key range)
+  if (D == 128 && Hkv * 4 == Hq && causal && Sq <= tuning().attn_fwd_hp_maxs && !rel_bias) {
+    dim3 grid((Sq + 31) / 32, Hkv, B), block(256);
+    hipLaunchKernelGGL((attn_fwd_kernel<128, 2, true>), grid, block, 0, stream, a);
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
   dim3 grid((Sq + 127) / 128, Hq, B), block(256);
   switch (D) {
     case 32: hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, block, 0, stream, a); break;

@@ -352,6 +352,27 @@ def test_flash_fwd_bwd(S, causal, window, left):
     _close(gx[:, Hq * D:], gr[:, Hq * D:], rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("S,window,left", [(1, 0, False), (31, 0, True), (77, 0, False), (301, 0, True),
+                                           (301, 100, False), (700, 0, True)])
+def test_flash_fwd_head_packed_bitwise(S, window, left):
+    """The head-packed forward (4 query heads x 32 positions per workgroup, GQA-4 causal) writes
+    bitwise the output and log-sum-exp of the 128-position-per-head form."""
+    B, Hq, Hkv, D = 3, 32, 8, 128
+    torch.manual_seed(S + window)
+    qkv = _qkv(B, S, Hq, Hkv, D)
+    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    kv_start = torch.tensor([0, min(37, S - 1), min(5, S - 1)], device=DEV, dtype=torch.int32) if left else None
+    scale = 1.0 / math.sqrt(D)
+    outs = []
+    for maxs in (4096, 0):
+        with ops.tuning(attn_fwd_hp_maxs=maxs):
+            outs.append(ops.native().attn_fwd(q, k, v, B, S, S, Hq, Hkv, D, True, window, scale, kv_start, None, None,
+                                              0, True))
+    (o1, l1), (o2, l2) = outs
+    assert torch.equal(o1, o2)
+    assert torch.equal(l1, l2)
+
+
 @pytest.mark.parametrize("D,H", [(32, 12), (64, 12)])
 def test_encoder_attention_relbias(D, H):
     B, S = 3, 70
