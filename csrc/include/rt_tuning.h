@@ -18,8 +18,9 @@ struct Tuning {
   int decode_mw_smax = 1024;  // cache slots up to which it runs one partition per kv head (fewer: measured slower
                               // at 456 slots, profiles/r5/decode_b1_deferred_partition_merge.log)
   // ---- training / prefill attention (attention.hip) ----
-  int attn_fwd_hp_maxs = 1024;  // causal GQA-4 forwards up to this many query positions use the head-packed
-                                // 32-position tiles (0: always the 128-position tiles of one head)
+  int attn_fwd_hp_maxs = 1024;  // causal D = 128 forwards up to this many query positions use the head-packed
+                                // 32-position tiles (GQA-4) or 64-position tiles of one head (other
+                                // groupings); 0: always the 128-position tiles of one head
   // ---- norms (norm.hip) ----
   // threads per row of the split-K-slab norm (256, or 512 at H = 4096: 6.76 -> 6.56 us at batch 256,
   // profiles/r4/norm_slab_threads.log)

@@ -109,11 +109,15 @@ __device__ __forceinline__ int v_off(int r, int c) {
 // passed: the 128-row tile's waves ran every key tile up to the tile's LAST row. Per row the same
 // key tiles in the same order with the same arithmetic (trailing fully masked tiles change
 // nothing: alpha = 1, p = 0), so the output and lse are bitwise the 128-row form's.
-template <int D, int NU = 2, bool HP = false>
-__global__ __launch_bounds__(64 * 8 / NU, D == 128 ? 2 : (D == 64 ? 3 : 4))
+//
+// Q64 (NU = 1, 4 waves of 16 rows): 64 positions of one head per workgroup — the same causal
+// saving for heads that share no K / V (MHA, e.g. Llama-2-13B), bitwise the 128-row form too.
+template <int D, int NU = 2, bool HP = false, bool Q64 = false>
+__global__ __launch_bounds__(Q64 ? 256 : 64 * 8 / NU, D == 128 ? 2 : (D == 64 ? 3 : 4))
 void attn_fwd_kernel(AttnArgs a) {
   static_assert(!HP || NU == 2, "HP: 4 waves of 32 rows");
-  constexpr int NT = 64 * 8 / NU;  // threads per workgroup
+  static_assert(!Q64 || (NU == 1 && !HP), "Q64: 4 waves of 16 rows");
+  constexpr int NT = Q64 ? 256 : 64 * 8 / NU;  // threads per workgroup
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TILE_BYTES = 64 * D * 2;
   constexpr int OROW = D + 8;  // O staging row stride (elements)
@@ -131,7 +135,7 @@ void attn_fwd_kernel(AttnArgs a) {
   const int b = bx.z;
   const int h = HP ? bx.y * 4 + wid : bx.y;
   const int hk = HP ? bx.y : h / (a.Hq / a.Hkv);
-  constexpr int QROWS = HP ? 32 : 128;  // query positions per workgroup
+  constexpr int QROWS = HP ? 32 : (Q64 ? 64 : 128);  // query positions per workgroup
   const int qblk0 = bx.x * QROWS;
   const int q0 = HP ? qblk0 : qblk0 + wid * 16 * NU;
 
@@ -338,7 +342,7 @@ void attn_fwd_kernel(AttnArgs a) {
       for (int c = 0; c < DT; ++c) Os[row * OROW + 16 * c + r16] = f2bf(o[u][c][i] * inv);
     }
   __syncthreads();
-  for (int e = tid; e < 128 * NCH; e += NT) {
+  for (int e = tid; e < (Q64 ? 64 : 128) * NCH; e += NT) {
     const int row = e / NCH, c = e % NCH;
     // HP: staging row 32 w + r = position qblk0 + r of head 4 hk + w
     const int qq = HP ? qblk0 + (row & 31) : qblk0 + row;
@@ -1934,6 +1938,13 @@ extern "C" int rt_attn_fwd(const void* q, long ldq, const void* k, long ldk, con
   if (D == 128 && Hkv * 4 == Hq && causal && Sq <= tuning().attn_fwd_hp_maxs && !rel_bias) {
     dim3 grid((Sq + 31) / 32, Hkv, B), block(256);
     hipLaunchKernelGGL((attn_fwd_kernel<128, 2, true>), grid, block, 0, stream, a);
+    RT_LAUNCH_CHECK();
+    return 0;
+  }
+  // other head groupings (MHA), D = 128: 64-position tiles of one head (4 waves x 16 rows)
+  if (D == 128 && causal && Sq <= tuning().attn_fwd_hp_maxs && !rel_bias) {
+    dim3 grid((Sq + 63) / 64, Hq, B), block(256);
+    hipLaunchKernelGGL((attn_fwd_kernel<128, 1, false, true>), grid, block, 0, stream, a);
     RT_LAUNCH_CHECK();
     return 0;
   }

@@ -354,10 +354,12 @@ def test_flash_fwd_bwd(S, causal, window, left):
 
 @pytest.mark.parametrize("S,window,left", [(1, 0, False), (31, 0, True), (77, 0, False), (301, 0, True),
                                            (301, 100, False), (700, 0, True)])
-def test_flash_fwd_head_packed_bitwise(S, window, left):
-    """The head-packed forward (4 query heads x 32 positions per workgroup, GQA-4 causal) writes
-    bitwise the output and log-sum-exp of the 128-position-per-head form."""
-    B, Hq, Hkv, D = 3, 32, 8, 128
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (16, 16), (16, 8)])
+def test_flash_fwd_head_packed_bitwise(S, window, left, Hq, Hkv):
+    """The short-sequence causal forward tiles — head-packed (4 query heads x 32 positions per
+    workgroup, GQA-4) and 64 positions of one head (other groupings) — write bitwise the output and
+    log-sum-exp of the 128-position-per-head form."""
+    B, D = 3, 128
     torch.manual_seed(S + window)
     qkv = _qkv(B, S, Hq, Hkv, D)
     q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]

@@ -18,9 +18,11 @@ from gemv_balance_probe import t_us  # noqa: E402
 def main():
     dev = "cuda"
     C = ops.native()
-    Hq, Hkv, D = 32, 8, 128
-    for name, B, S in (("update_b32_s301", 32, 301), ("ref_b128_s301", 128, 301), ("prefill_b256_s173", 256, 173),
-                       ("answer_b1_s174", 1, 174), ("long_b1_s1024", 1, 1024)):
+    D = 128
+    for name, B, S, Hq, Hkv in (("update_b32_s301", 32, 301, 32, 8), ("ref_b128_s301", 128, 301, 32, 8),
+                                ("prefill_b256_s173", 256, 173, 32, 8), ("answer_b1_s174", 1, 174, 32, 8),
+                                ("long_b1_s1024", 1, 1024, 32, 8), ("mha13b_update_b32_s301", 32, 301, 40, 40),
+                                ("mha13b_prefill_b256_s173", 256, 173, 40, 40)):
         qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16)
         q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
         ks = torch.randint(0, 20, (B,), device=dev, dtype=torch.int32)
