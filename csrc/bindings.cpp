@@ -103,6 +103,7 @@ static const TuningField kTuningFields[] = {
     {"decode_mw_kpp", &rt::Tuning::decode_mw_kpp, nullptr},
     {"decode_mw_smax", &rt::Tuning::decode_mw_smax, nullptr},
     {"attn_fwd_hp_maxs", &rt::Tuning::attn_fwd_hp_maxs, nullptr},
+    {"attn_dq_hp_maxs", &rt::Tuning::attn_dq_hp_maxs, nullptr},
     {"norm_slab_threads", &rt::Tuning::norm_slab_threads, nullptr},
     {"gemm_variant", &rt::Tuning::gemm_variant, nullptr},
     {"gemv16", &rt::Tuning::gemv16, nullptr},

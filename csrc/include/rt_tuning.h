@@ -21,6 +21,8 @@ struct Tuning {
   int attn_fwd_hp_maxs = 1024;  // causal D = 128 forwards up to this many query positions use the head-packed
                                 // 32-position tiles (GQA-4) or 64-position tiles of one head (other
                                 // groupings); 0: always the 128-position tiles of one head
+  int attn_dq_hp_maxs = 1024;   // causal GQA-4 backward dQ up to this many positions on head-packed 16-position
+                                // workgroups (0: 64 positions of one head)
   // ---- norms (norm.hip) ----
   // threads per row of the split-K-slab norm (256, or 512 at H = 4096: 6.76 -> 6.56 us at batch 256,
   // profiles/r4/norm_slab_threads.log)

@@ -1778,7 +1778,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
 // masks; dQ += dS·K with dS (packed accumulators) as the A operand and K^T by transposed reads of
 // the same K image. Each dQ element is written once, in bf16 (the atomic form added one fp32 row
 // per key block: ~0.5 GB of atomics per Mistral-7B layer at 9.6k tokens, bound at ~1.3 TB/s).
-template <int D>
+// HP (GQA-4, causal, short sequences): a workgroup = 16 positions x the 4 query heads of one kv
+// head (wave w = head 4 hk + w), every wave on the same causal key range and one K / V staging for
+// the 4 heads; per row the same key tiles in the same order (trailing fully masked tiles add exact
+// zeros), so dQ is bitwise the 64-row form's.
+template <int D, bool HP = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TILE_BYTES = 64 * D * 2;
@@ -1788,13 +1792,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   const int3 bx = attn_block_xyz();
-  const int b = bx.z, h = bx.y;
-  const int hk = h / (a.Hq / a.Hkv);
-  const int qblk0 = bx.x * 64;
-  const int q0 = qblk0 + wid * 16;
+  const int b = bx.z;
+  const int h = HP ? bx.y * 4 + wid : bx.y;
+  const int hk = HP ? bx.y : h / (a.Hq / a.Hkv);
+  constexpr int QROWS = HP ? 16 : 64;
+  const int qblk0 = bx.x * QROWS;
+  const int q0 = HP ? qblk0 : qblk0 + wid * 16;
   const int start = a.kv_start ? a.kv_start[b] : 0;
   int kend = a.S;
-  if (a.causal) kend = min(kend, min(qblk0 + 63, a.S - 1) + 1);
+  if (a.causal) kend = min(kend, min(qblk0 + QROWS - 1, a.S - 1) + 1);
   int kbeg = start;
   if (a.window > 0) kbeg = max(kbeg, qblk0 - a.window + 1);
   kbeg = max(kbeg, 0) & ~63;
@@ -2181,13 +2187,17 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
   dim3 pgrid((unsigned)((rows + rows_per_block - 1) / rows_per_block)), grid((S + 63) / 64, Hkv, B);
   // dK / dV per 64-key block, dQ by a separate kernel per 64-query block (no atomics)
   if (D != 64 && D != 128) return -1;
-  dim3 qgrid((S + 63) / 64, Hq, B);
+  // GQA-4, causal, short sequences: dQ on head-packed 16-position workgroups
+  const bool dq_hp = D == 128 && Hkv * 4 == Hq && causal && S <= tuning().attn_dq_hp_maxs;
+  dim3 qgrid = dq_hp ? dim3((S + 15) / 16, Hkv, B) : dim3((S + 63) / 64, Hq, B);
 #define BWD_CASE(DD)                                                                              \
   hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, pgrid, dim3(256), 0, stream, a);                    \
-  hipLaunchKernelGGL(attn_bwd_kernel<DD>, grid, dim3(256), 0, stream, a);                         \
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<DD>, qgrid, dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(attn_bwd_kernel<DD>, grid, dim3(256), 0, stream, a);
   if (D == 64) { BWD_CASE(64) } else { BWD_CASE(128) }
 #undef BWD_CASE
+  if (D == 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<64>), qgrid, dim3(256), 0, stream, a);
+  else if (dq_hp) hipLaunchKernelGGL((attn_bwd_dq_kernel<128, true>), qgrid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((attn_bwd_dq_kernel<128>), qgrid, dim3(256), 0, stream, a);
   RT_LAUNCH_CHECK();
   return 0;
 }

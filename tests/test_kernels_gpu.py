@@ -375,6 +375,25 @@ def test_flash_fwd_head_packed_bitwise(S, window, left, Hq, Hkv):
     assert torch.equal(l1, l2)
 
 
+@pytest.mark.parametrize("S,window,left", [(31, 0, True), (301, 0, True), (301, 100, False), (700, 0, False)])
+def test_flash_bwd_dq_head_packed_bitwise(S, window, left):
+    """The head-packed dQ kernel (4 query heads x 16 positions per workgroup, GQA-4 causal) gives
+    bitwise the gradients of the 64-position-per-head form (dK / dV are the same kernel)."""
+    B, Hq, Hkv, D = 3, 32, 8, 128
+    torch.manual_seed(S + 3 * window)
+    qkv = _qkv(B, S, Hq, Hkv, D)
+    kv_start = torch.tensor([0, min(37, S - 1), 5], device=DEV, dtype=torch.int32) if left else None
+    go = torch.randn(B * S, Hq * D, device=DEV, dtype=torch.bfloat16)
+    grads = []
+    for maxs in (4096, 0):
+        with ops.tuning(attn_dq_hp_maxs=maxs):
+            x = qkv.clone().requires_grad_(True)
+            o = ops.flash_attention_qkv(x, B, S, Hq, Hkv, D, True, window, kv_start=kv_start)
+            (o.float() * go.float()).sum().backward()
+            grads.append(x.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+
+
 @pytest.mark.parametrize("D,H", [(32, 12), (64, 12)])
 def test_encoder_attention_relbias(D, H):
     B, S = 3, 70
