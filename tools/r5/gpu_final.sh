@@ -2,7 +2,7 @@
 # round 5: full GPU tier + smoke + headline bench (20 timed / 5 warm-up) on the final tree
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/r5final2
+O=gpurun_out/r5final3
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 || { tail -40 $O/gputests.log; exit 1; }
 tail -3 $O/gputests.log
