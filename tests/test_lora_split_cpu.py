@@ -1,0 +1,51 @@
+"""Split plans of the LoRA narrow products (ops.linear._narrow / gemm_tn) measured in round 5
+(profiles/r5/lora_narrow_split_sweep.log): the forward U = X A^T splits its reduction 3 ways, the
+token reduction of dA / dB splits 4 ways on 64 output tiles and 8 above. The plans are host code:
+checked here by intercepting the native launch."""
+import importlib
+
+import torch
+
+L = importlib.import_module("rag_tl_domainllm_optimizer_amd.ops.linear")  # the module (ops.linear is the function)
+
+
+class _Native:
+    def __init__(self):
+        self.calls = []
+
+    def gemm_small(self, a, b, la, lb, out_mode, ns, out, bm):
+        self.calls.append((la, lb, out_mode, ns, bm))
+        R = b.shape[0] if lb == L.ROW else b.shape[1]
+        return out if out is not None else torch.zeros(a.shape[0], R, dtype=a.dtype)
+
+
+def _run(monkeypatch, fn):
+    nat = _Native()
+    monkeypatch.setattr(L, "native", lambda: nat)
+    monkeypatch.setattr(L, "on_gpu", lambda t: True)
+    fn()
+    return nat.calls
+
+
+def test_forward_u_splits_three_ways(monkeypatch):
+    for K in (4096, 14336):
+        x = torch.zeros(9632, K, dtype=torch.bfloat16)
+        a = torch.zeros(64, K, dtype=torch.bfloat16)
+        calls = _run(monkeypatch, lambda: L._narrow(x, a, L.ROW))
+        assert [c[3] for c in calls] == [3], (K, calls)
+    # tiny reductions are not split
+    calls = _run(monkeypatch, lambda: L._narrow(torch.zeros(300, 256, dtype=torch.bfloat16),
+                                                torch.zeros(64, 256, dtype=torch.bfloat16), L.ROW))
+    assert [c[3] for c in calls] == [1]
+
+
+def test_adapter_gradient_token_splits(monkeypatch):
+    T = 9632
+    du = torch.zeros(T, 64, dtype=torch.bfloat16)
+    cases = [(lambda: L.gemm_tn(du, torch.zeros(T, 4096, dtype=torch.bfloat16)), 4),    # dA, 64 tiles
+             (lambda: L.gemm_tn(du, torch.zeros(T, 14336, dtype=torch.bfloat16)), 8),   # dA, 224 tiles
+             (lambda: L.gemm_tn(torch.zeros(T, 4096, dtype=torch.bfloat16), du), 4),    # dB, 64 tiles
+             (lambda: L.gemm_tn(torch.zeros(T, 6144, dtype=torch.bfloat16), du), 8)]    # dB, 96 tiles
+    for fn, ns in cases:
+        calls = _run(monkeypatch, fn)
+        assert [c[3] for c in calls] == [ns], calls

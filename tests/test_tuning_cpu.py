@@ -56,6 +56,9 @@ def test_tuning_roundtrip():
         pytest.skip("native extension not built")
     t0 = ops.get_tuning()
     assert t0["decode_mw_kpp"] == 512 and t0["gemm_variant"] == 0 and abs(t0["gemm_bn128_cost"] - 0.55) < 1e-6
+    # round-5 defaults: short-sequence attention tiles on up to 1024 positions, the small-batch
+    # decode attention unpartitioned up to 1024 cache slots
+    assert t0["attn_fwd_hp_maxs"] == 1024 and t0["attn_dq_hp_maxs"] == 1024 and t0["decode_mw_smax"] == 1024
     # only knobs with a live alternative remain (measured-slower paths left the product kernels)
     for gone in ("gemm_streamk", "gemm_ring", "attn_fwd_w8", "attn_bwd_atomic_dq", "gemm_fp8_256", "gemm_tr_builtin",
                  "decode_mw", "decode_mfma"):
