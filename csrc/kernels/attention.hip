@@ -22,8 +22,8 @@
 // Backward (attn_bwd_kernel<D>): FA2-style. One workgroup = 64 keys of one (batch, kv head);
 // waves own 16 keys each and keep dK^T, dV^T in accumulators while sweeping the group's query
 // heads x 64-row query tiles. S and dP are computed with the key on the lane so their
-// accumulators are directly the B operands of dV^T = dO^T·P and dK^T = Q^T·dS; only dS crosses
-// LDS (once) for dQ = dS·K, which is accumulated with fp32 atomics.
+// accumulators are directly the B operands of dV^T = dO^T·P and dK^T = Q^T·dS. dQ is a separate
+// kernel (attn_bwd_dq_kernel: query rows per workgroup, no atomics).
 #include "rt_common.h"
 
 #include <algorithm>
@@ -1596,13 +1596,12 @@ template <int D>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
   constexpr int NCH = D / 8, DS = D / 32, DT = D / 16;
   constexpr int TB = 64 * D * 2;
-  // LDS: K tile (block keys) | Q tile | dO tile | dS tile [64 q][64 keys] | lse[64] | delta[64]
-  __shared__ __attribute__((aligned(16))) char smem[3 * TB + 64 * 64 * 2 + 2 * 64 * 4];
-  char* Ks = smem;
-  char* Qs = smem + TB;
-  char* Os = smem + 2 * TB;  // dO
-  char* dSs = smem + 3 * TB;
-  float* lse_s = (float*)(dSs + 64 * 64 * 2);
+  // LDS: Q tile | dO tile | lse[64] | delta[64] (dQ is the separate attn_bwd_dq_kernel: no K or dS
+  // tile here)
+  __shared__ __attribute__((aligned(16))) char smem[2 * TB + 2 * 64 * 4];
+  char* Qs = smem;
+  char* Os = smem + TB;  // dO
+  float* lse_s = (float*)(smem + 2 * TB);
   float* del_s = lse_s + 64;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1615,14 +1614,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
   const int mykey = kb0 + wid * 16 + r16;  // this lane's key column
   constexpr int CPT = 64 * NCH / 256;
 
-  // block K tile -> LDS (for dQ), and this wave's K, V fragments (B operands) -> registers
-#pragma unroll
-  for (int r = 0; r < CPT; ++r) {
-    const int e = tid + 256 * r;
-    const int key = e / NCH, c = e % NCH;
-    const int kk = min(kb0 + key, a.S - 1);
-    *(uint4*)(Ks + v_off<D>(key, c)) = *(const uint4*)(a.k + ((long)b * a.S + kk) * a.ldk + (long)hk * D + c * 8);
-  }
+  // this wave's K, V fragments (B operands) -> registers
   bf16x8 kf[DS], vf[DS];
   {
     const int kk = min(mykey, a.S - 1);
