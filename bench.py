@@ -103,6 +103,9 @@ def main():
     ap.add_argument("--old-logp", default="rollout", choices=["rollout", "recompute"],
                     help="PPO ratio's theta_old log-probs: the rollout sampler's (free) or a training-numerics "
                          "forward of the policy beside the reference forward (exact ratio 1 at theta_old)")
+    ap.add_argument("--kl-in-loss", default="on", choices=["on", "off"],
+                    help="frozen-reference KL as a k3 penalty on the update forward's own log-probs (on) or as a "
+                         "-beta (old - ref) token reward (off: the pre-round-6 form)")
     ap.add_argument("--defer-splitk", default="on", choices=["on", "off"],
                     help="decode at batch > 64: split-K partials summed by the norm / attention kernels (on) or "
                          "reduced after each GEMM (off; A/B)")
@@ -203,13 +206,15 @@ def main():
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
                    lora_r=16, lora_alpha=32.0, seed=0, rollout_chunks=1, overlap_reward=True,
                    full_finetune=args.full_ft, merged_lora_rollout=args.merged_rollout == "on",
-                   old_logp=args.old_logp,
+                   old_logp=args.old_logp, kl_in_loss=args.kl_in_loss == "on",
                    **({"ref_minibatch_size": args.ref_minibatch} if args.ref_minibatch else {}))
     trainer = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
     if args.merged_rollout == "off":
         tuning_over["merged_rollout"] = "off"
     if args.old_logp != "rollout":
         tuning_over["old_logp"] = args.old_logp
+    if args.kl_in_loss != "on":
+        tuning_over["kl_in_loss"] = "off"
     if args.no_graph:
         trainer.gen.use_graph = False
     rng = random.Random(100 + di.rank)
@@ -261,8 +266,19 @@ def main():
         return
 
     # ---- PPO steps ----
+    # KL(pi_theta_old || ref) per sequence of the very first step (LoRA B = 0: policy == reference),
+    # measured on the first update minibatch in training numerics; with the KL in the loss this is
+    # what the penalty sees at init (the pre-round-6 sampler-vs-training form read 1.83 here)
+    kl_init = {}
+
+    def note_init(m):
+        if not kl_init:
+            kl_init.update(kl_ref_at_init=m["kl_ref_theta_old"], kl_old_ref_at_init=m["kl_old_ref"],
+                           clipfrac_first_mb_at_init=m["clipfrac_first_mb"])
+
     for w in range(args.warmup):
         m = trainer.step(make_batch())
+        note_init(m)
         log(f"[bench] warmup {w}: {m['step_time_s']:.2f}s tokens={m['rollout_tokens']:.0f} "
             f"reward={m['reward_mean']:.3f}")
     if args.torch_profile:
@@ -273,11 +289,13 @@ def main():
     t0 = time.perf_counter()
     tokens = 0.0
     phase = {}
-    gaps, egaps, clipf = [], [], []
+    gaps, egaps, clipf, kls = [], [], [], []
     for s in range(args.steps):
         # inside the timed region: sample the rank's queries, encode them and search the IVF index
         # (retrieval), then the full PPO iteration on the retrieved RAG prompts
         m = trainer.step(make_batch())
+        note_init(m)
+        kls.append((m["kl_ref"], m["kl_ref_theta_old"], m["kl_old_ref"]))
         tokens += m["rollout_tokens"] * di.world  # reduce_metrics averaged over ranks
         for k, v in m.items():
             if k.startswith("time/"):
@@ -333,6 +351,14 @@ def main():
         "rollout_engine_logp_gap": sum(egaps) / len(egaps),
         "old_logp_source": args.old_logp,
         "clipfrac_first_mb": sum(clipf) / len(clipf),
+        # reference KL (nats / sequence): where the penalty is applied, its value over the timed steps
+        # (update forwards vs reference; first minibatch at theta_old), sum_t (old_logp - ref) (the
+        # sampler-based quantity the reward used before round 6), and the same at the first step
+        "kl_in_loss": args.kl_in_loss == "on",
+        "kl_ref": sum(k[0] for k in kls) / len(kls),
+        "kl_ref_theta_old": sum(k[1] for k in kls) / len(kls),
+        "kl_old_ref": sum(k[2] for k in kls) / len(kls),
+        **kl_init,
         # data-parallel diagnostics: gradient payload each rank hands to RCCL per step, and the
         # spread of the per-rank step times (before the closing barrier) in seconds
         "allreduce_bytes_per_step": comm_bytes,

@@ -83,7 +83,9 @@ int rt_gae(const float*, const float*, const float*, int, int, float, float, flo
 int rt_ppo_advantages(const float*, const float*, const float*, const float*, const int*, int, int, float, float, float,
                       int, float, float*, float*, float*, float*, hipStream_t);
 int rt_ppo_loss(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
-                const float*, long, float, float, float, float, float*, float*, float*, float*, hipStream_t);
+                const float*, long, float, float, float, float, const float*, float, float*, float*, float*, float*,
+                hipStream_t);
+int rt_rowdot(const void*, long, const float*, const float*, int, long, float*, hipStream_t);
 int rt_decode_update(const long*, long*, int, float*, const float*, float*, const float*, uint8_t*, int*, int*, long*,
                      int*, int64_t*, int64_t*, int, const long*, int, long, int*, const int*, hipStream_t);
 }
@@ -1222,10 +1224,12 @@ std::vector<Tensor> gae(const Tensor& rewards, const Tensor& values, const Tenso
   return {adv, ret};
 }
 
-// fused token-level PPO objective: returns {stats[6], dlp, dv, dent} (see rl.hip)
+// fused token-level PPO objective: returns {stats[9], dlp, dv, dent} (see rl.hip); ``ref`` (optional,
+// with kl_coef): the frozen reference's log-probs for the in-loss k3 KL penalty
 std::vector<Tensor> ppo_loss(const Tensor& lp, const Tensor& old, const Tensor& adv, const Tensor& v,
                              const Tensor& ret, const optional<Tensor>& vold, const Tensor& ent, const Tensor& mask,
-                             double eps, double c_v, double c_e, double vclip) {
+                             double eps, double c_v, double c_e, double vclip, const optional<Tensor>& ref,
+                             double kl_coef) {
   for (const Tensor* t : {&lp, &old, &adv, &v, &ret, &ent, &mask}) {
     CHECK_CUDA(*t); CHECK_F32(*t);
     TORCH_CHECK(t->is_contiguous() && t->numel() == lp.numel(), "ppo_loss: operands must be contiguous, same size");
@@ -1234,15 +1238,34 @@ std::vector<Tensor> ppo_loss(const Tensor& lp, const Tensor& old, const Tensor& 
     TORCH_CHECK(vold.has_value() && vold->defined() && vold->numel() == lp.numel() && vold->is_contiguous());
     CHECK_F32(*vold);
   }
-  auto stats = at::empty({6}, lp.options());
+  const bool has_ref = ref.has_value() && ref->defined();
+  if (has_ref) {
+    CHECK_CUDA(*ref); CHECK_F32(*ref);
+    TORCH_CHECK(ref->is_contiguous() && ref->numel() == lp.numel(), "ppo_loss: ref must be contiguous, same size");
+  }
+  auto stats = at::zeros({9}, lp.options());
   auto dlp = at::empty_like(lp), dv = at::empty_like(lp), dent = at::empty_like(lp);
   check_rc(rt_ppo_loss(lp.data_ptr<float>(), old.data_ptr<float>(), adv.data_ptr<float>(), v.data_ptr<float>(),
                        ret.data_ptr<float>(), vclip > 0 ? vold->data_ptr<float>() : nullptr, ent.data_ptr<float>(),
                        mask.data_ptr<float>(), lp.numel(), (float)eps, (float)c_v, (float)c_e, (float)vclip,
-                       stats.data_ptr<float>(), dlp.data_ptr<float>(), dv.data_ptr<float>(), dent.data_ptr<float>(),
-                       cur_stream()),
+                       has_ref ? ref->data_ptr<float>() : nullptr, (float)kl_coef, stats.data_ptr<float>(),
+                       dlp.data_ptr<float>(), dv.data_ptr<float>(), dent.data_ptr<float>(), cur_stream()),
            "ppo_loss");
   return {stats, dlp, dv, dent};
+}
+
+// value head V = h . w + b per row (bf16 h [T, H], fp32 w [H], b [1]): batch-invariant row dot (loss.hip)
+Tensor rowdot(const Tensor& h, const Tensor& w, const optional<Tensor>& b) {
+  CHECK_CUDA(h); CHECK_CUDA(w); CHECK_F32(w);
+  TORCH_CHECK(h.scalar_type() == at::kBFloat16 && h.dim() == 2 && h.stride(1) == 1, "rowdot: h bf16 [T, H] rows");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == h.size(1) && h.size(1) % 8 == 0, "rowdot: w [H], H % 8 == 0");
+  TORCH_CHECK(((uintptr_t)h.data_ptr() % 16) == 0 && ((uintptr_t)w.data_ptr() % 16) == 0, "rowdot: 16-B alignment");
+  if (b.has_value() && b->defined()) { CHECK_CUDA(*b); CHECK_F32(*b); }
+  auto out = at::empty({h.size(0)}, h.options().dtype(at::kFloat));
+  check_rc(rt_rowdot(h.data_ptr(), h.stride(0), w.data_ptr<float>(), (const float*)opt_ptr(b), (int)h.size(1),
+                     h.size(0), out.data_ptr<float>(), cur_stream()),
+           "rowdot");
+  return out;
 }
 
 void decode_update(const Tensor& tok, Tensor out_tokens, const optional<Tensor>& out_logp,
@@ -1352,7 +1375,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("segment_mean", &segment_mean, "k-means update: per-segment mean of sorted rows (+ L2 normalise)");
   m.def("gae", &gae);
   m.def("ppo_advantages", &ppo_advantages, "token KL rewards + GAE + advantage whitening in one launch");
-  m.def("ppo_loss", &ppo_loss, "fused token-level PPO loss: {stats[6], dlp, dv, dent}");
+  m.def("ppo_loss", &ppo_loss, "fused token-level PPO loss: {stats[9], dlp, dv, dent}");
+  m.def("rowdot", &rowdot, "value head: batch-invariant per-row dot product");
   m.def("decode_update", &decode_update);
   ragtl::bind_tokenizer(m);
   ragtl::bind_ivf_host(m);

@@ -112,6 +112,31 @@ __global__ __launch_bounds__(256) void logprob_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// Value head V(s) = w . h + b per row (rl.py:150 nn.Linear(H, 1)): one wave per row, a
+// fixed per-lane order over 16-B chunks and a fixed butterfly, so a row's value does not depend on
+// how many rows the launch holds (torch's last-dim reduction picks its block split from the row
+// count: the PPO scoring forward must give bitwise the same value at minibatch 32 and 128).
+__global__ __launch_bounds__(256) void rowdot_kernel(const bf16_t* __restrict__ h, long ldh, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, int H, long T,
+                                                     float* __restrict__ out) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const bf16_t* x = h + row * ldh;
+  float acc = 0.f;
+  const int nv = H / 8;
+  for (int c = lane; c < nv; c += 64) {
+    float f[8];
+    unpack8(*(const uint4*)(x + c * 8), f);
+    const float4 a = *(const float4*)(w + c * 8), b = *(const float4*)(w + c * 8 + 4);
+    acc = fmaf(f[0], a.x, acc); acc = fmaf(f[1], a.y, acc); acc = fmaf(f[2], a.z, acc); acc = fmaf(f[3], a.w, acc);
+    acc = fmaf(f[4], b.x, acc); acc = fmaf(f[5], b.y, acc); acc = fmaf(f[6], b.z, acc); acc = fmaf(f[7], b.w, acc);
+  }
+  for (int c = nv * 8 + lane; c < H; c += 64) acc = fmaf(bf2f(x[c]), w[c], acc);
+  acc = wave_sum(acc);
+  if (lane == 0) out[row] = acc + (bias ? bias[0] : 0.f);
+}
+
 }  // namespace rt
 
 using namespace rt;
@@ -139,6 +164,16 @@ extern "C" int rt_logprob_bwd(const void* logits, int is_f32, long ld, const lon
   else
     hipLaunchKernelGGL(logprob_bwd_kernel<bf16_t>, dim3(T), dim3(256), 0, stream, (const bf16_t*)logits, ld, tgt,
                        inv_temp, V, lse, ex, g_lp, g_ent, (bf16_t*)dlogits, ldd);
+  RT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int rt_rowdot(const void* h, long ldh, const float* w, const float* bias, int H, long T, float* out,
+                         hipStream_t stream) {
+  if (T == 0) return 0;
+  if (ldh % 8) return -1;
+  hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, stream, (const bf16_t*)h, ldh, w, bias,
+                     H, T, out);
   RT_LAUNCH_CHECK();
   return 0;
 }

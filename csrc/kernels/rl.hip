@@ -149,6 +149,10 @@ __global__ void decode_update_kernel(const long* __restrict__ tok, long* __restr
 //                                 vc = v_old + clamp(v - v_old, +-value_clip)]
 //   ent  = mean(entropy);  loss = pg + c_v vl - c_e ent
 //   stats[0..5] = loss, pg, vl, ent, approx_kl = mean(old - lp), clipfrac = mean(|r - 1| > eps)
+//   ref != null (KL to the frozen reference in the loss, PPOConfig.kl_in_loss): with d = ref - lp,
+//   loss += kl_coef mean(k3), k3 = e^d - d - 1 (the non-negative, unbiased-in-expectation
+//   estimator of KL(pi || ref) on tokens drawn from pi); stats[6] = mean(k3), stats[7] =
+//   mean(lp - ref) (k1); stats[8] = n (masked tokens); d k3 / d lp = 1 - e^d
 //   dlp = d loss / d lp, dv = d loss / d v, dent = d loss / d entropy (per token, 0 off the mask)
 // Formulas: reference PPOTrainer.ppo_update (reinforcement_learning_optimization_after_rag.py:212-225)
 // at token level, with the SURVEY B5 true-entropy fix. Replaces ~25 tiny elementwise/reduction
@@ -157,11 +161,12 @@ __global__ __launch_bounds__(1024) void ppo_loss_kernel(
     const float* __restrict__ lp, const float* __restrict__ old, const float* __restrict__ adv,
     const float* __restrict__ v, const float* __restrict__ ret, const float* __restrict__ vold,
     const float* __restrict__ ent, const float* __restrict__ mask, long n_el, float eps, float c_v, float c_e,
-    float vclip, float* __restrict__ stats, float* __restrict__ dlp, float* __restrict__ dv,
-    float* __restrict__ dent) {
-  __shared__ float red[16][6];
+    float vclip, const float* __restrict__ ref, float kl_coef, float* __restrict__ stats, float* __restrict__ dlp,
+    float* __restrict__ dv, float* __restrict__ dent) {
+  constexpr int NA = 8;
+  __shared__ float red[16][NA];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // n, pg, vl, ent, kl, clipfrac (sums)
+  float acc[NA] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // n, pg, vl, ent, kl, clipfrac, k3, k1 (sums)
   for (long i = tid; i < n_el; i += 1024) {
     const float m = mask[i];
     if (m == 0.f) continue;
@@ -180,18 +185,23 @@ __global__ __launch_bounds__(1024) void ppo_loss_kernel(
     acc[3] += m * ent[i];
     acc[4] += m * (old[i] - lp[i]);
     acc[5] += m * (fabsf(r - 1.f) > eps ? 1.f : 0.f);
+    if (ref) {
+      const float d = ref[i] - lp[i];
+      acc[6] += m * (__expf(d) - d - 1.f);
+      acc[7] -= m * d;
+    }
   }
 #pragma unroll
-  for (int k = 0; k < 6; ++k)
+  for (int k = 0; k < NA; ++k)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, 64);
   if (lane == 0)
 #pragma unroll
-    for (int k = 0; k < 6; ++k) red[wid][k] = acc[k];
+    for (int k = 0; k < NA; ++k) red[wid][k] = acc[k];
   __syncthreads();
-  float tot[6];
+  float tot[NA];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < NA; ++k) {
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < 16; ++w) t += red[w][k];
@@ -200,12 +210,16 @@ __global__ __launch_bounds__(1024) void ppo_loss_kernel(
   const float inv_n = 1.f / fmaxf(tot[0], 1.f);
   if (tid == 0) {
     const float pg = tot[1] * inv_n, vl = 0.5f * tot[2] * inv_n, em = tot[3] * inv_n;
-    stats[0] = pg + c_v * vl - c_e * em;
+    const float k3 = tot[6] * inv_n;
+    stats[0] = pg + c_v * vl - c_e * em + (ref && kl_coef != 0.f ? kl_coef * k3 : 0.f);
     stats[1] = pg;
     stats[2] = vl;
     stats[3] = em;
     stats[4] = tot[4] * inv_n;
     stats[5] = tot[5] * inv_n;
+    stats[6] = k3;
+    stats[7] = tot[7] * inv_n;
+    stats[8] = tot[0];
   }
   for (long i = tid; i < n_el; i += 1024) {
     const float m = mask[i];
@@ -217,6 +231,7 @@ __global__ __launch_bounds__(1024) void ppo_loss_kernel(
       // -min(rA, rc A): the unclipped branch is active (or tied) -> d/dlp = -A r; the clipped branch
       // only differs when r is outside the range, where clamp has no gradient
       g_lp = (r * A <= rc * A) ? -A * r : 0.f;
+      if (ref && kl_coef != 0.f) g_lp += kl_coef * (1.f - __expf(ref[i] - lp[i]));
       const float dvv = v[i] - ret[i];
       float gv = dvv;
       if (vclip > 0.f) {
@@ -242,10 +257,10 @@ using namespace rt;
 
 extern "C" int rt_ppo_loss(const float* lp, const float* old, const float* adv, const float* v, const float* ret,
                            const float* vold, const float* ent, const float* mask, long n_el, float eps, float c_v,
-                           float c_e, float vclip, float* stats, float* dlp, float* dv, float* dent,
-                           hipStream_t stream) {
+                           float c_e, float vclip, const float* ref, float kl_coef, float* stats, float* dlp,
+                           float* dv, float* dent, hipStream_t stream) {
   hipLaunchKernelGGL(ppo_loss_kernel, dim3(1), dim3(1024), 0, stream, lp, old, adv, v, ret, vold, ent, mask, n_el,
-                     eps, c_v, c_e, vclip, stats, dlp, dv, dent);
+                     eps, c_v, c_e, vclip, ref, kl_coef, stats, dlp, dv, dent);
   RT_LAUNCH_CHECK();
   return 0;
 }

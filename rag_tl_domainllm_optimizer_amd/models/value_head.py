@@ -21,8 +21,11 @@ class ValueHead(nn.Module):
             self.linear.bias.zero_()
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:
-        # a row dot product (memory-bound, one pass over h), not a library GEMV
-        return (h.float() * self.linear.weight[0]).sum(-1) + self.linear.bias
+        # a row dot product (memory-bound, one pass over h), not a library GEMV; on the GPU one
+        # wave per row in a fixed order (ops.row_dot): a row's value is independent of the batch
+        from .. import ops
+
+        return ops.row_dot(h, self.linear.weight[0], self.linear.bias)
 
     def reference_state_dict(self):
         """{"weight": [1, H], "bias": [1]} exactly as torch.nn.Linear(H, 1).state_dict()."""

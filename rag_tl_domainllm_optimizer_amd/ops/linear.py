@@ -19,6 +19,7 @@ The reference runs these products through HF/PyTorch (reinforcement_learning_opt
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -48,14 +49,38 @@ def splitk_plan(M: int, N: int, K: int, act: int = 0):
     return max(1, min(nk // 8, (256 + tiles // 2) // tiles)), bn
 
 
+_BATCH_INVARIANT = 0
+
+
+@contextlib.contextmanager
+def batch_invariant(on: bool = True):
+    """Row-invariant GEMM numerics inside the block: every token-parallel GEMM (``gemm``) runs the
+    gemm_big kernel without a K split whatever M is, so a row's output bits do not depend on how
+    many other rows share the launch (no M-dependent split-K / skinny-kernel choice; gemm_big's
+    256- and 128-column tiles accumulate every element in the same K order). The PPO scoring
+    forwards (``train.common.score_sequences``) run under it: reference log-probs, the optional
+    theta_old recompute and the update forward then agree bitwise across minibatch sizes,
+    padding and packing. Costs nothing at scoring sizes (M in the thousands never splits)."""
+    global _BATCH_INVARIANT
+    _BATCH_INVARIANT += int(bool(on))
+    try:
+        yield
+    finally:
+        _BATCH_INVARIANT -= int(bool(on))
+
+
 def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None,
          residual=None, nsplit: int = 0):
     """Raw (non-autograd) fused GEMM on 2-D row-major operands: act(x w^T + u ub^T + bias) (+ residual).
     M <= 64: weight-streaming kernels; small M with few output tiles: split-K fp32 slabs + fused
-    reduce epilogue (``nsplit`` overrides the plan); otherwise the 256x256 MFMA kernel."""
+    reduce epilogue (``nsplit`` overrides the plan); otherwise the 256x256 MFMA kernel. Under
+    :func:`batch_invariant` always the 256x256-family kernel without a split."""
     if on_gpu(x):
         M, K = x.shape
         N = w.shape[0]
+        if _BATCH_INVARIANT and K % 8 == 0 and (act != ACT_SWIGLU or N % 256 == 0) \
+                and (residual is None or not out_f32):
+            return native().gemm_big(x, w, ROW, ROW, u, ub, bias, act, 1 if out_f32 else 0, 1, out, None, residual, 0)
         # 32 <= M <= 64 on narrow weights (qkv / o): the 256x128-tile split-K form beats the ring
         # kernel by 2-4 us (profiles/gemm_r2_m32_m64_ring_vs_splitk.log); wide / deep weights and
         # M < 32 stay on the weight-streaming ring / GEMV kernels
@@ -309,7 +334,12 @@ def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0, zero32=N
     # (measured at 9632 tokens: dU 383 -> 172 us at K = 28672, profiles/lora_narrow_r2.log). The
     # forward U (ROW adapter image) runs 3 ways split from cold activations: K = 4096 31.3 -> 28.7
     # us, K = 14336 78.0 -> 73.8 us (profiles/r5/lora_narrow_split_sweep.log)
-    auto = min(3, max(1, K // 512)) if lb == ROW else max(1, min(K // 512, (768 + tiles - 1) // tiles))
+    # The forward U (ROW adapter image) runs without a split: fp32 atomic partials land in arrival
+    # order, so a split forward is not bitwise reproducible (nor batch-invariant) — the PPO ratio and
+    # reference KL need the scoring forward to be (ops.batch_invariant). Cost: K = 4096 28.7 -> 31.3
+    # us, K = 14336 73.8 -> 78.0 us at 9632 tokens (profiles/r5/lora_narrow_split_sweep.log). The
+    # backward products (dU, dA, dB) keep their atomic splits.
+    auto = 1 if lb == ROW else max(1, min(K // 512, (768 + tiles - 1) // tiles))
     ns = nsplit or auto
     if ns == 1:
         return native().gemm_small(a, b, ROW, lb, 0, 1, None, bm)
@@ -556,6 +586,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
                     params += [a, b]
             f8 = fp8.train_cache() if (fp8 is not None and fp8.train) else None
             y = _LinearFn.apply(x2, w, None, ACT_SWIGLU, lora if use_lora else None, f8, None, *params)
+            return y.reshape(*shp[:-1], w.shape[0] // 2)
+        if on_gpu(x2) and not grad_needed and bias is None and w.shape[0] % 256 == 0 and x2.shape[1] % 8 == 0 \
+                and w.dtype == torch.bfloat16 and use_lora and not lora.use_merged and fp8 is None \
+                and (x2.shape[0] > 64 or _BATCH_INVARIANT):
+            # unmerged adapters without grad (reference / theta_old scoring): the training forward's
+            # exact product — U = X A_pad^T as K-extension steps of the [gate; up] GEMM with the
+            # SwiGLU epilogue — not the merged bf16 W + s B A (a second rounding of every weight)
+            y = gemm_big(x2, w, ROW, ROW, _narrow(x2, lora.a_pad, ROW), lora.ub, None, ACT_SWIGLU)
             return y.reshape(*shp[:-1], w.shape[0] // 2)
         if on_gpu(x2) and not grad_needed and bias is None and w.shape[0] % 64 == 0 and x2.shape[1] % 64 == 0 \
                 and (x2.shape[0] <= 64 or w.shape[0] % 256 == 0):

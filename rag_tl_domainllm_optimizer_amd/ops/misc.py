@@ -1,6 +1,8 @@
 """SwiGLU, embedding gather, token log-probs / entropy, sampler, retrieval and RL kernels."""
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 import torch.nn.functional as F
 
@@ -169,11 +171,12 @@ def segment_mean(x, order, seg, normalize: bool, out):
 # ---------------------------------------------------------------------------------------- RL
 class _PPOLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, lp, vals, ent, old, adv, ret, mask, vold, eps, c_v, c_e, vclip):
+    def forward(ctx, lp, vals, ent, old, adv, ret, mask, vold, eps, c_v, c_e, vclip, ref_lp, kl_coef):
         f = lambda t: t.detach().float().contiguous()  # noqa: E731
         stats, dlp, dv, dent = native().ppo_loss(f(lp), f(old), f(adv), f(vals), f(ret),
                                                  f(vold) if vold is not None else None, f(ent), f(mask),
-                                                 eps, c_v, c_e, vclip if vclip else 0.0)
+                                                 eps, c_v, c_e, vclip if vclip else 0.0,
+                                                 f(ref_lp) if ref_lp is not None else None, kl_coef)
         ctx.save_for_backward(dlp, dv, dent)
         ctx.mark_non_differentiable(stats)
         return stats[0], stats
@@ -181,17 +184,51 @@ class _PPOLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g, _gstats):
         dlp, dv, dent = ctx.saved_tensors
-        return dlp * g, dv * g, dent * g, None, None, None, None, None, None, None, None, None
+        return dlp * g, dv * g, dent * g, None, None, None, None, None, None, None, None, None, None, None
 
 
-def ppo_loss(lp, vals, ent, old, adv, ret, mask, eps: float, c_v: float, c_e: float, vclip=None, vold=None):
+def ppo_loss(lp, vals, ent, old, adv, ret, mask, eps: float, c_v: float, c_e: float, vclip=None, vold=None,
+             ref_lp=None, kl_coef: float = 0.0):
     """Token-level clipped PPO objective: ``(loss, stats)`` with stats = [loss,
-    policy_loss, value_loss, entropy, approx_kl, clipfrac]; one fused HIP kernel computes the loss
-    and its gradient (w.r.t. lp, vals, ent) together on the GPU."""
+    policy_loss, value_loss, entropy, approx_kl, clipfrac, kl_ref_k3, kl_ref_k1, n_tokens]; one
+    fused HIP kernel computes the loss and its gradient (w.r.t. lp, vals, ent) together on the GPU.
+    ``ref_lp`` (frozen-reference log-probs of the same tokens): adds ``kl_coef * mean(k3)`` with
+    k3 = exp(ref - lp) - (ref - lp) - 1, the reference-KL penalty on the update forward's own
+    (training-numerics) log-probs (PPOConfig.kl_in_loss)."""
     if on_gpu(lp):
         return _PPOLossFn.apply(lp, vals, ent, old, adv, ret, mask.float(), vold, float(eps), float(c_v),
-                                float(c_e), float(vclip) if vclip else 0.0)
-    return ref.ppo_loss(lp, old, adv, vals, ret, ent, mask.float(), eps, c_v, c_e, vclip, vold)
+                                float(c_e), float(vclip) if vclip else 0.0, ref_lp, float(kl_coef))
+    return ref.ppo_loss(lp, old, adv, vals, ret, ent, mask.float(), eps, c_v, c_e, vclip, vold, ref_lp, kl_coef)
+
+
+class _RowDotFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, w, b):
+        ctx.save_for_backward(h, w)
+        return native().rowdot(h, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w = ctx.saved_tensors
+        g = g.float()
+        dh = (g[:, None] * w[None, :]).to(h.dtype) if ctx.needs_input_grad[0] else None
+        dw = (g[:, None] * h.float()).sum(0) if ctx.needs_input_grad[1] else None
+        db = g.sum().reshape(1) if ctx.needs_input_grad[2] else None
+        return dh, dw, db
+
+
+def row_dot(h: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-row h . w (+ b) in fp32 (the scalar value head): on the GPU one wave per row in a fixed
+    order (``rowdot_kernel``), so a row's value is bitwise independent of the other rows in the
+    launch; h [T, H] bf16, w [H] fp32. CPU: the fp32 expression."""
+    if on_gpu(h) and h.dtype == torch.bfloat16 and h.shape[-1] % 8 == 0:
+        h2 = h.reshape(-1, h.shape[-1])
+        if h2.stride(-1) != 1 or h2.stride(0) % 8 or h2.data_ptr() % 16:
+            h2 = h2.contiguous()
+        y = _RowDotFn.apply(h2, w.contiguous(), b)
+        return y.reshape(h.shape[:-1])
+    y = (h.float() * w).sum(-1)
+    return y + b if b is not None else y
 
 
 def ppo_advantages(old_logp, ref_logp, values, scores, resp_len, kl_coef: float, gamma: float, lam: float,

@@ -238,9 +238,10 @@ def gae(rewards, values, mask, gamma, lam):
     return adv, ret
 
 
-def ppo_loss(lp, old, adv, vals, ret, ent, mask, eps, c_v, c_e, vclip=None, vold=None):
-    """Token-level PPO objective (eager oracle of the fused kernel): returns (loss, stats[6]) with
-    stats = loss, policy_loss, value_loss, entropy, approx_kl, clipfrac."""
+def ppo_loss(lp, old, adv, vals, ret, ent, mask, eps, c_v, c_e, vclip=None, vold=None, ref_lp=None, kl_coef=0.0):
+    """Token-level PPO objective (eager oracle of the fused kernel): returns (loss, stats[9]) with
+    stats = loss, policy_loss, value_loss, entropy, approx_kl, clipfrac, kl_ref_k3, kl_ref_k1,
+    n_tokens; ``ref_lp``: + kl_coef * mean(exp(ref - lp) - (ref - lp) - 1)."""
     m = mask.to(lp.dtype)
     n = m.sum().clamp(min=1.0)
     ratio = torch.exp(lp - old)
@@ -252,10 +253,19 @@ def ppo_loss(lp, old, adv, vals, ret, ent, mask, eps, c_v, c_e, vclip=None, vold
         vl = 0.5 * (((vals - ret) ** 2) * m).sum() / n
     em = (ent * m).sum() / n
     loss = pg + c_v * vl - c_e * em
+    zero = lp.new_zeros(())
+    k3 = k1 = zero
+    if ref_lp is not None:
+        d = ref_lp - lp
+        k3 = ((torch.exp(d) - d - 1) * m).sum() / n
+        k1 = (-d * m).sum() / n
+        if kl_coef:
+            loss = loss + kl_coef * k3
     with torch.no_grad():
         kl = ((old - lp) * m).sum() / n
         cf = ((((ratio - 1).abs() > eps).to(lp.dtype)) * m).sum() / n
-        stats = torch.stack([loss.detach(), pg.detach(), vl.detach(), em.detach(), kl, cf])
+        stats = torch.stack([loss.detach(), pg.detach(), vl.detach(), em.detach(), kl, cf, k3.detach(), k1.detach(),
+                             m.sum()])
     return loss, stats
 
 

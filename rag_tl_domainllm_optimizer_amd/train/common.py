@@ -35,6 +35,18 @@ def response_mask(lengths: torch.Tensor, T: int) -> torch.Tensor:
 def score_sequences(model, prompt_ids: torch.Tensor, start: torch.Tensor, resp: torch.Tensor,
                     resp_len: torch.Tensor, inv_temp: float = 1.0, value_head=None,
                     gradient_checkpointing: bool = False, lengths=None):
+    """See :func:`_score_sequences`. Runs under ``ops.batch_invariant()``: a row's log-probs /
+    entropy / value are bitwise the same whatever rows share the forward (minibatch 32 or 128,
+    padded or packed, grad or no grad) — the PPO ratio is exactly 1 at theta_old under
+    ``old_logp="recompute"`` and the reference KL is exactly 0 at LoRA B = 0."""
+    with ops.batch_invariant():
+        return _score_sequences(model, prompt_ids, start, resp, resp_len, inv_temp, value_head,
+                                gradient_checkpointing, lengths)
+
+
+def _score_sequences(model, prompt_ids: torch.Tensor, start: torch.Tensor, resp: torch.Tensor,
+                     resp_len: torch.Tensor, inv_temp: float = 1.0, value_head=None,
+                     gradient_checkpointing: bool = False, lengths=None):
     """One forward over [prompt | response] -> per-response-token (logp, entropy, values).
 
     The hidden state at position S-1+t produces the distribution of response token t and is also

@@ -55,6 +55,14 @@ class PPOConfig:
     eps: float = 1e-8
     value_clip: Optional[float] = None
     kl_coef: float = 0.05
+    # where the frozen-reference KL penalty is applied: True = in the loss, as
+    # kl_coef * mean_t k3(pi_theta || ref) on the update forward's own log-probs (training
+    # numerics, the same batch-invariant scoring forward as the reference log-probs: exactly 0 at
+    # LoRA B = 0, no extra forward); False = as a -kl_coef * (old - ref) per-token reward term,
+    # where "old" are the old_logp below (with "rollout" these are the sampler's log-probs, whose
+    # engine gap to the training forward then reads as KL: 1.83 nats / sequence at init,
+    # profiles/r5/bench_old_logp_recompute.log)
+    kl_in_loss: bool = True
     adaptive_kl: bool = False
     target_kl: float = 6.0
     kl_horizon: int = 10000
@@ -79,10 +87,11 @@ class PPOConfig:
     rollout_chunks: int = 1          # >1: score chunk i while chunk i+1 decodes
     merged_lora_rollout: bool = True  # decode/prefill rollouts on W + sBA (refreshed per update)
     # where the PPO ratio's theta_old log-probs / values come from: "rollout" = the sampler of the
-    # decode engine (free; differs from the training forward by the two engines' bf16 numerics,
-    # ~0.09 nats / token on a random-init Mistral-7B, profiles/r5/behaviour_gap_7b.log), or
-    # "recompute" = one no-grad training-numerics forward of the policy over the rollouts beside the
-    # reference forward (ratio exactly 1 at theta = theta_old; costs a forward)
+    # decode engine, i.e. the behaviour policy mu that drew the tokens (free; the importance ratio
+    # pi_theta / mu then also corrects the two engines' bf16 numerics, ~0.09 nats / token on a
+    # random-init Mistral-7B, profiles/r5/behaviour_gap_7b.log), or "recompute" = one no-grad
+    # forward of the policy over the rollouts in the update forward's exact numerics (the
+    # batch-invariant scoring forward: ratio bitwise 1 at theta = theta_old; costs a forward)
     old_logp: str = "rollout"
     lr_schedule: str = "constant"
     save_every: int = 0              # CLI: mid-epoch "latest" checkpoint every N steps (0 = epoch ends)
@@ -135,7 +144,7 @@ class Rollout:
     returns: Optional[torch.Tensor] = None
     rewards_tok: Optional[torch.Tensor] = None
     n_tokens: int = 0
-    kl_ref: float = 0.0
+    kl_old_ref: Optional[torch.Tensor] = None  # per-sequence mean of sum_t (old - ref)
     # host copies of (start, resp_len) for the varlen (packed) scoring forwards
     host_lengths: Optional[tuple] = None
 
@@ -363,13 +372,15 @@ class PPOTrainer:
             # the whole reference forward is queued and nothing above waited for the device: the
             # host detokenises now and the reward encoder runs on the side stream beside it
             self._collect_rewards(ro)
-        # token rewards (-beta * KL per token, score at the last token), GAE and whitening: one
-        # kernel on GPU (ops.ppo_advantages; the eager oracle on CPU)
+        # token rewards (-beta * KL per token unless the KL is in the loss, score at the last
+        # token), GAE and whitening: one kernel on GPU (ops.ppo_advantages; the eager oracle on CPU)
         adv, ret, rewards, kl_seq = ops.ppo_advantages(ro.old_logp, ro.ref_logp, ro.old_values, ro.scores,
-                                                       ro.resp_len, self.kl_coef, c.gamma, c.lam,
-                                                       c.whiten_advantages)
+                                                       ro.resp_len, 0.0 if c.kl_in_loss else self.kl_coef,
+                                                       c.gamma, c.lam, c.whiten_advantages)
         ro.adv, ro.returns, ro.rewards_tok = adv, ret, rewards
-        ro.kl_ref = float(kl_seq.mean())
+        # sum_t (old - ref) per sequence: the reference KL when "old" is a training-numerics forward;
+        # with sampler log-probs it also holds the decode engine's numerics gap (reported apart)
+        ro.kl_old_ref = kl_seq.mean()
         return ro
 
     # ------------------------------------------------------------------ update
@@ -392,9 +403,12 @@ class PPOTrainer:
                                                           lengths=(hl[0][rows], hl[1][rows]) if hl else None)
                     # fused token-level objective (clipped surrogate + value + entropy) and its
                     # gradient in one kernel on the GPU (ops.ppo_loss; eager oracle on CPU)
+                    # the ratio's denominator: the behaviour log-probs old_logp (sampler mu, or the
+                    # recomputed theta_old); the reference KL (kl_in_loss) on this forward's own lp
                     loss, st = ops.ppo_loss(lp, vals, ent, ro.old_logp[idx], ro.adv[idx], ro.returns[idx], mask,
                                             c.clip_range, c.value_coef, c.entropy_coef, c.value_clip,
-                                            ro.old_values[idx] if c.value_clip is not None else None)
+                                            ro.old_values[idx] if c.value_clip is not None else None,
+                                            ro.ref_logp[idx], self.kl_coef if c.kl_in_loss else 0.0)
                     if not stats:
                         # behaviour / target policy gap: the first minibatch scores the
                         # rollouts at theta = theta_old, so |logp - old_logp| is the rollout engine's
@@ -416,12 +430,29 @@ class PPOTrainer:
                     self.opt.step(lr)
                     self.policy.refresh_lora()
                     stats.append(st)
-        # stats rows: [loss, policy_loss, value_loss, entropy, approx_kl, clipfrac] (one D2H copy)
-        sm = torch.stack(stats).mean(0).tolist()
+        # stats rows: [loss, policy_loss, value_loss, entropy, approx_kl, clipfrac, kl_ref_k3,
+        # kl_ref_k1, n_tokens] (one D2H copy with the step's other device scalars)
+        sts = torch.stack(stats)
+        first_epoch = sts[: (B + c.minibatch_size - 1) // c.minibatch_size]
+        # reference KL per sequence from the first epoch's forwards (every rollout token scored once;
+        # the first minibatch at theta_old): sum_t (lp - ref) / B in training numerics
+        kl_tok_sum = (first_epoch[:, 7] * first_epoch[:, 8]).sum()
+        rows0 = min(B, c.minibatch_size)
+        dev_scalars = torch.stack([kl_tok_sum / B, ro.kl_old_ref.to(sts.device).float(), first_gap.float(),
+                                   engine_gap.float(), sts[0, 7] * sts[0, 8] / rows0]).tolist()
+        sm = sts.mean(0).tolist()
         out = {"total_loss": sm[0], "policy_loss": sm[1], "value_loss": sm[2], "entropy": sm[3],
-               "entropy_loss": -c.entropy_coef * sm[3], "approx_kl": sm[4], "clipfrac": sm[5]}
-        out["behaviour_logp_gap"] = float(first_gap)
-        out["rollout_engine_logp_gap"] = float(engine_gap)
+               "entropy_loss": -c.entropy_coef * sm[3], "approx_kl": sm[4], "clipfrac": sm[5],
+               "kl_ref_k3": sm[6]}
+        # kl_ref: nats per sequence. kl_in_loss: the update forwards' own lp vs the reference (what
+        # the penalty acts on); otherwise sum_t (old - ref), the quantity in the reward
+        out["kl_ref"] = dev_scalars[0] if c.kl_in_loss else dev_scalars[1]
+        out["kl_old_ref"] = dev_scalars[1]
+        # the first minibatch scores at theta = theta_old: KL(pi_theta_old || ref) per sequence in
+        # training numerics (exactly 0 at LoRA B = 0 / before any full-FT update)
+        out["kl_ref_theta_old"] = dev_scalars[4]
+        out["behaviour_logp_gap"] = dev_scalars[2]
+        out["rollout_engine_logp_gap"] = dev_scalars[3]
         out["clipfrac_first_mb"] = float(stats[0][5])
         out["grad_norm"] = float(self.opt.last_norm)
         out["skipped_steps"] = float(self.opt.skipped)
@@ -444,7 +475,7 @@ class PPOTrainer:
             "reward_mean": float(ro.scores.mean()), "reward_std": float(ro.scores.std(unbiased=False)),
             "factual_accuracy": float(comps["factual_accuracy"].mean()), "relevance": float(comps["relevance"].mean()),
             "conciseness": float(comps["conciseness"].mean()),
-            **upd, "kl_ref": ro.kl_ref, "kl_coef": self.kl_coef, "rollout_tokens": float(ro.n_tokens),
+            **upd, "kl_coef": self.kl_coef, "rollout_tokens": float(ro.n_tokens),
             "response_len": float(ro.resp_len.float().mean()), "step_time_s": dt,
         }
         m.update(self.timer.as_dict())

@@ -144,5 +144,5 @@ def test_full_finetune_kl_and_ratio_at_theta_old():
         for m in ms:
             assert m["behaviour_logp_gap"] < 1e-4, m["behaviour_logp_gap"]
             assert m["clipfrac_first_mb"] == 0.0
-        assert abs(ms[0]["kl_ref"]) < 1e-4  # no update yet: policy == reference
+        assert abs(ms[0]["kl_ref_theta_old"]) < 1e-4  # no update yet: policy == reference
     assert hi[1]["kl_ref"] > 5 * lo[1]["kl_ref"] > 0

@@ -825,24 +825,27 @@ def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split):
         C.set_tuning({"m64_split": 0})
 
 
+@pytest.mark.parametrize("kl", [None, 0.05])
 @pytest.mark.parametrize("vclip", [None, 0.2])
 @pytest.mark.parametrize("B,T", [(16, 128), (3, 37), (64, 300)])
-def test_ppo_loss_fused(B, T, vclip):
-    """Fused PPO objective + closed-form gradient == eager autograd of the reference formulas."""
+def test_ppo_loss_fused(B, T, vclip, kl):
+    """Fused PPO objective + closed-form gradient == eager autograd of the reference formulas
+    (with and without the in-loss k3 reference-KL term)."""
     torch.manual_seed(B * T)
     lp = (torch.randn(B, T, device=DEV) * 0.3 - 2).requires_grad_(True)
     vals = torch.randn(B, T, device=DEV).requires_grad_(True)
     ent = (torch.rand(B, T, device=DEV) * 3).requires_grad_(True)
     old = lp.detach() + torch.randn(B, T, device=DEV) * 0.2
     adv, ret, vold = torch.randn(B, T, device=DEV), torch.randn(B, T, device=DEV), torch.randn(B, T, device=DEV)
+    refl = lp.detach() + torch.randn(B, T, device=DEV) * 0.3 if kl else None
     lens = torch.randint(1, T + 1, (B,), device=DEV)
     mask = torch.arange(T, device=DEV)[None] < lens[:, None]
-    loss, st = ops.ppo_loss(lp, vals, ent, old, adv, ret, mask, 0.2, 0.5, 0.01, vclip, vold)
+    loss, st = ops.ppo_loss(lp, vals, ent, old, adv, ret, mask, 0.2, 0.5, 0.01, vclip, vold, refl, kl or 0.0)
     (2.0 * loss).backward()
     g = [t.grad.clone() for t in (lp, vals, ent)]
     for t in (lp, vals, ent):
         t.grad = None
-    rl, rst = ref.ppo_loss(lp, old, adv, vals, ret, ent, mask.float(), 0.2, 0.5, 0.01, vclip, vold)
+    rl, rst = ref.ppo_loss(lp, old, adv, vals, ret, ent, mask.float(), 0.2, 0.5, 0.01, vclip, vold, refl, kl or 0.0)
     (2.0 * rl).backward()
     torch.testing.assert_close(st, rst, rtol=1e-4, atol=1e-5)
     for a, t in zip(g, (lp, vals, ent)):

@@ -66,7 +66,7 @@ def test_decode_matches_teacher_forcing():
 
     with torch.no_grad():
         lp, _, _, _ = score_sequences(m, out.prompt_ids, out.prompt_start, out.tokens, out.lengths, 1 / 0.7)
-    torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=0.08)
+    torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=1e-2)
 
 
 def test_fused_decode_follows_adapter_updates():
@@ -87,9 +87,16 @@ def test_fused_decode_follows_adapter_updates():
                 q.normal_(0, 0.08)
         m.refresh_lora()
         out = gen.generate(prompts, p, pad_id=0, eos_ids=[-1])
-        with torch.no_grad():
-            lp, _, _, _ = score_sequences(m, out.prompt_ids, out.prompt_start, out.tokens, out.lengths, 1 / 0.7)
-        torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=0.08, msg=f"step {step}")
+        # teacher forcing on the same merged bf16 weights the decode engine reads (W + s B A rounded
+        # once): what is left is the two engines' numerics (a stale derived weight is off by far more)
+        prev = m.set_lora_merged(True)
+        try:
+            with torch.no_grad():
+                lp, _, _, _ = score_sequences(m, out.prompt_ids, out.prompt_start, out.tokens, out.lengths, 1 / 0.7)
+        finally:
+            m.set_lora_merged(prev)
+        err = float((lp - out.logprobs).abs().max())
+        assert err <= 1e-2, (step, err)
 
 
 def test_shuffled_decode_weights_match_row_major(monkeypatch):
@@ -202,7 +209,7 @@ def test_odd_vocab_generation_gpu():
     assert out.tokens.shape == (2, 6) and int(out.tokens.max()) < 514 and torch.isfinite(out.logprobs).all()
     with torch.no_grad():
         lp, _, _, _ = score_sequences(m, out.prompt_ids, out.prompt_start, out.tokens, out.lengths, 1 / 0.7)
-    torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=0.08)
+    torch.testing.assert_close(lp, out.logprobs, rtol=0.0, atol=1e-2)
 
 
 @pytest.mark.parametrize("merged_lora,batch", [(False, 160), (True, 160), (False, 100)])
@@ -242,7 +249,9 @@ def test_batched_decode_deferred_splitk_bitwise(merged_lora, batch):
 
 def test_varlen_packed_scoring_and_prefill_gpu(monkeypatch):
     """Packed (varlen) scoring and prefill on the MI355X kernels agree with the padded forms: the
-    same per-token math on fewer GEMM rows (bf16 tolerance; greedy tokens identical)."""
+    same per-token math on fewer GEMM rows — log-probs and values bitwise (the scoring forward is
+    batch-invariant), LoRA gradients to fp32-atomic reduction order, greedy prefill continuations
+    identical (prefill under ops.batch_invariant: by default its small-M GEMMs pick a split-K per M)."""
     import numpy as np
 
     from rag_tl_domainllm_optimizer_amd.models import ValueHead
@@ -277,10 +286,10 @@ def test_varlen_packed_scoring_and_prefill_gpu(monkeypatch):
         outs.append((lp.detach().float(), val.detach().float(), mask))
         grads.append(torch.cat([p.grad.float().reshape(-1) for p in m.lora_parameters()]))
     (a_lp, a_v, mask), (b_lp, b_v, _) = outs
-    assert float(((a_lp - b_lp).abs() * mask).max()) < 0.05
-    assert float(((a_v - b_v).abs() * mask).max()) < 0.05
+    assert torch.equal(a_lp * mask, b_lp * mask)
+    assert torch.equal(a_v * mask, b_v * mask)
     rel = float((grads[0] - grads[1]).norm() / grads[0].norm().clamp(min=1e-12))
-    assert rel < 0.05, rel
+    assert rel < 1e-2, rel
     # prefill: greedy continuations of variable-length prompts, packed vs padded
     prompts = [list(range(7, 7 + n)) for n in (60, 5, 33, 17)]
     toks = []
@@ -288,10 +297,10 @@ def test_varlen_packed_scoring_and_prefill_gpu(monkeypatch):
         monkeypatch.setenv("RAGTL_PACK", flag)
         gen = Generator(m, max_batch=4, max_seq=96, device=DEV)
         gen.use_graph = False
-        out = gen.generate(prompts, SamplingParams(max_new_tokens=6, do_sample=False), pad_id=0, eos_ids=[-5])
+        with ops.batch_invariant():
+            out = gen.generate(prompts, SamplingParams(max_new_tokens=6, do_sample=False), pad_id=0, eos_ids=[-5])
         toks.append(out.tokens.cpu())
-    agree = float((toks[0] == toks[1]).float().mean())
-    assert agree >= 0.9, (agree, toks)
+    assert torch.equal(toks[0], toks[1]), toks
 
 
 def test_graph_replay_eos_after_allocator_churn():
@@ -409,4 +418,4 @@ def test_continuous_batching_gpu_matches_teacher_forcing():
         with torch.no_grad():
             lp, _, _, _ = score_sequences(m, ids, torch.zeros(1, dtype=torch.long, device=DEV), resp,
                                           torch.tensor([10], device=DEV), 1 / 0.7)
-        torch.testing.assert_close(lp[0].cpu(), torch.tensor(f.logprobs), rtol=0.0, atol=0.08)
+        torch.testing.assert_close(lp[0].cpu(), torch.tensor(f.logprobs), rtol=0.0, atol=1e-2)
