@@ -2,7 +2,8 @@
 """Headline benchmark: PPO rollout tokens/sec (node) + p50 RAG answer latency, Mistral-7B.
 
 Metric and config from BASELINE.json: Mistral-7B-shaped bf16 policy (random init, LoRA r=16 on all
-linear projections — or every weight with --full-ft — value head), 256 rollouts per GPU, all-MiniLM-L6-shaped reward/retrieval encoder, 100k-doc synthetic
+linear projections — or every weight with --full-ft — value head), 256 rollouts per GPU, all-MiniLM-L6-shaped
+retrieval encoder, all-mpnet-base-v2-shaped reward encoder (the reference's default), 100k-doc synthetic
 corpus in an HBM-resident IVF index. One process per GPU (torchrun env, RCCL over xGMI), data
 parallel; per-GPU work is fixed (weak scaling).
 
@@ -51,7 +52,10 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="mistral-7b")
-    ap.add_argument("--encoder", default="minilm-l6")
+    ap.add_argument("--encoder", default="minilm-l6", help="retrieval (bi-encoder / IVF index) encoder")
+    ap.add_argument("--reward-encoder", default="mpnet-base",
+                    help="reward-model sentence encoder (the reference's RewardModel default is all-mpnet-base-v2, "
+                         "rl.py:54-55); 'same' reuses the retrieval encoder")
     ap.add_argument("--rollout-batch", type=int, default=256,
                     help="sequences per GPU per PPO step (default 256, also for --mode pipeline: "
                          "profiles/r4/pipeline13b_rollout_batch.log)")
@@ -184,7 +188,14 @@ def main():
         tuning_over["defer_splitk"] = "off"
     enc_model = build_model(args.encoder, device=dev, dtype=torch.bfloat16, seed=1, fast_init=True).eval()
     encoder = Encoder(enc_model, Tokenizer.synthetic(enc_model.cfg.vocab_size, enc_model.cfg.arch), max_length=128)
-    log(f"[bench] models ready: {args.model} ({pcfg.num_params() / 1e9:.2f} B params) + {args.encoder}")
+    if args.reward_encoder in ("same", args.encoder):
+        reward_encoder = encoder
+    else:
+        rw_model = build_model(args.reward_encoder, device=dev, dtype=torch.bfloat16, seed=2, fast_init=True).eval()
+        reward_encoder = Encoder(rw_model, Tokenizer.synthetic(rw_model.cfg.vocab_size, rw_model.cfg.arch),
+                                 max_length=128)
+    log(f"[bench] models ready: {args.model} ({pcfg.num_params() / 1e9:.2f} B params) + {args.encoder} (retrieval) + "
+        f"{args.reward_encoder} (reward)")
 
     # ---- corpus + IVF index in HBM ----
     corpus = SyntheticCorpus(tok.words(), n_docs=args.ndocs, doc_words=args.doc_words, seed=7)
@@ -198,7 +209,7 @@ def main():
     log(f"[bench] indexed {len(corpus)} docs (IVF nlist={index.nlist}) in {time.perf_counter() - t0:.1f}s")
 
     if args.mode in ("sft", "pipeline"):
-        return run_sft_pipeline(args, di, policy, tok, encoder, corpus, index, ar_probe)
+        return run_sft_pipeline(args, di, policy, tok, encoder, corpus, index, ar_probe, reward_encoder)
     if args.mode == "serve":
         return run_serve(args, di, policy, tok, encoder, corpus, index)
 
@@ -208,7 +219,7 @@ def main():
                    full_finetune=args.full_ft, merged_lora_rollout=args.merged_rollout == "on",
                    old_logp=args.old_logp, kl_in_loss=args.kl_in_loss == "on",
                    **({"ref_minibatch_size": args.ref_minibatch} if args.ref_minibatch else {}))
-    trainer = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
+    trainer = PPOTrainer(policy, tok, RewardModel(reward_encoder), pc, max_batch=args.rollout_batch)
     if args.merged_rollout == "off":
         tuning_over["merged_rollout"] = "off"
     if args.old_logp != "rollout":
@@ -330,7 +341,9 @@ def main():
         "config": {"model": args.model, "global_batch": args.rollout_batch * di.world,
                    "seq_len": args.max_prompt + args.new_tokens, "parallelism": f"dp{di.world}",
                    "new_tokens": args.new_tokens, "lora_r": None if args.full_ft else 16,
-                   "full_finetune": bool(args.full_ft), "encoder": args.encoder, "ndocs": args.ndocs,
+                   "full_finetune": bool(args.full_ft), "encoder": args.encoder,
+                   "reward_encoder": args.reward_encoder if args.reward_encoder != "same" else args.encoder,
+                   "ndocs": args.ndocs,
                    "index": f"ivf{index.nlist}/nprobe{args.nprobe}", "minibatch": args.minibatch,
                    **({"docs_per_query": f"1-{args.top_k_docs}",
                        "packed": os.environ.get("RAGTL_PACK", "1") != "0"} if args.vary_docs else {})},
@@ -484,7 +497,7 @@ def run_serve(args, di, policy, tok, encoder, corpus, index):
     parallel.shutdown()
 
 
-def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index, ar_probe=None):
+def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index, ar_probe=None, reward_encoder=None):
     """config 3 (--mode sft) and config 5 (--mode pipeline) on synthetic data / random weights."""
     import random
 
@@ -540,7 +553,7 @@ def run_sft_pipeline(args, di, policy, tok, encoder, corpus, index, ar_probe=Non
     policy.kv_fp8 = bool(args.fp8_kv)
     pc = PPOConfig(max_new_tokens=args.new_tokens, max_prompt_tokens=args.max_prompt, minibatch_size=args.minibatch,
                    lora_r=16, lora_alpha=32.0, seed=0)
-    ppo = PPOTrainer(policy, tok, RewardModel(encoder), pc, max_batch=args.rollout_batch)
+    ppo = PPOTrainer(policy, tok, RewardModel(reward_encoder or encoder), pc, max_batch=args.rollout_batch)
 
     def make_batch():
         its = corpus.sample_queries(args.rollout_batch, seed=rng.randrange(1 << 30))

@@ -119,6 +119,7 @@ static const TuningField kTuningFields[] = {
     {"gemm_bn128_cost", nullptr, &rt::Tuning::gemm_bn128_cost},
     {"gemm_group_m", &rt::Tuning::gemm_group_m, nullptr},
     {"sample_window", &rt::Tuning::sample_window, nullptr},
+    {"sample_fast64", &rt::Tuning::sample_fast64, nullptr},
 };
 
 py::dict get_tuning() {

@@ -44,6 +44,8 @@ struct Tuning {
   // ---- sampler (sampling.hip) ----
   int sample_window = 1;      // top-k: candidates from a window below the row max, k-th key in one
                               // wave (0: 16 block-wide counting passes over the whole row; same draw)
+  int sample_fast64 = 1;      // <= 64 survivors: sort / top-p / draw in wave 0's registers without a block
+                              // barrier (0: the block-wide path; same draw)
 };
 
 }  // namespace rt

@@ -450,7 +450,11 @@ __device__ __forceinline__ int block_sum_int1024(int v, int* red) {
 __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
     const bf16_t* __restrict__ logits, long ld, int V, float inv_temp, int top_k, float top_p, uint64_t seed,
     const int64_t* __restrict__ offset_ptr, const uint8_t* __restrict__ row_active, long* __restrict__ out_tok,
-    float* __restrict__ out_logp, int use_window) {
+    float* __restrict__ out_logp, int flags) {
+  // flags bit 0: candidate window (tuning sample_window); bit 1: the <= 64-survivor wave-0 fast
+  // path (tuning sample_fast64; 0 sends those rows through the block-wide sort / top-p / Gumbel
+  // path, the same arithmetic — tests pin the two bitwise)
+  const bool use_window = flags & 1, fast64 = flags & 2;
   extern __shared__ __attribute__((aligned(16))) uint16_t keys[];  // [V]
   __shared__ int lidx[TK_CAP];
   __shared__ float lval[TK_CAP];   // tempered logit of each survivor
@@ -608,6 +612,8 @@ __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
       for (int c = tid + RC * 1024; c < nv; c += 1024) cand(*(const uint4*)(keys + c * 8), c);
       __syncthreads();
       const int n = cnt;
+      // every thread has read cnt before wave 0 (compaction below) or thread 0 (retry) rewrites it
+      __syncthreads();
       if (n >= K && n <= TK_CAP) {
         done = true;
         if (wid == 0) {
@@ -644,7 +650,6 @@ __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
           if (lane == 0) cnt = ns;
         }
       } else {
-        __syncthreads();  // every thread has read cnt
         if (tid == 0) cnt = 0;
         __syncthreads();
       }
@@ -679,7 +684,7 @@ __global__ __launch_bounds__(1024) void sample_topk_search_kernel(
     __syncthreads();
     const bool overflow = cnt > TK_CAP;  // > TK_CAP - top_k ties at the k-th value: draw from the keys
     const int n = min(cnt, TK_CAP);
-    if (!overflow && n <= 64) {
+    if (!overflow && n <= 64 && fast64) {
       // <= 64 survivors (top-k 50): sort, nucleus cut and Gumbel draw in wave 0's registers, no
       // block barrier — the same arithmetic, lane assignment and reduction order as the general
       // path below, so the same token
@@ -873,7 +878,7 @@ extern "C" int rt_sample(const void* logits, int is_f32, long ld, long B, int V,
     const size_t shm = ((size_t)V * 2 + 15) / 16 * 16;
     hipLaunchKernelGGL(sample_topk_search_kernel, dim3(B), dim3(1024), shm, stream, (const bf16_t*)logits, ld, V,
                        inv_temp, top_k, top_p, seed, offset_ptr, row_active, out_tok, out_logp,
-                       tuning().sample_window);
+                       (tuning().sample_window ? 1 : 0) | (tuning().sample_fast64 ? 2 : 0));
     RT_LAUNCH_CHECK();
     return 0;
   }

@@ -131,13 +131,14 @@ def save_policy(model, path: str, dtype=torch.bfloat16, max_shard_bytes: int = 5
     _commit(tmp, path)
 
 
-def save_rank_rng(prefix: str, rank: int, rng: dict):
-    """RNG state of one data-parallel rank into {prefix}_trainer_state/rng_rank{rank}.*"""
+def save_rank_rng(prefix: str, rank: int, rng: dict, d: Optional[str] = None):
+    """RNG state of one data-parallel rank into {prefix}_trainer_state/rng_rank{rank}.* (or into
+    ``d``, the not-yet-committed trainer-state directory of :func:`save_checkpoint_dp`)."""
     from safetensors.torch import save_file
 
     from ..utils.seed import rng_state_pack
 
-    d = f"{prefix}_trainer_state"
+    d = d or f"{prefix}_trainer_state"
     os.makedirs(d, exist_ok=True)
     rt, rm = rng_state_pack(rng)
     save_file(rt, os.path.join(d, f"rng_rank{rank}.safetensors.tmp"))
@@ -171,8 +172,38 @@ def load_rank_rng(prefix: str, rank: int):
     return None
 
 
+def save_checkpoint_dp(prefix: str, model, tokenizer, value_head=None, optimizer=None,
+                       trainer_state: Optional[dict] = None, save_full_policy: bool = True):
+    """Data-parallel save (every rank calls it): rank 0 writes the artifacts and the trainer state
+    into ``{prefix}_trainer_state.tmp``; after a barrier every other rank adds its RNG state and,
+    under ZeRO-1, every rank its optimizer shard to that same directory; rank 0 renames it into
+    place only after a second barrier behind all of those writes. A crash anywhere before the
+    rename leaves the previous checkpoint of this prefix intact (never a state.json without its
+    shards or RNG files)."""
+    from ..parallel import barrier
+    from ..parallel import info as dist_info
+    from ..utils import rng_state
+
+    di = dist_info()
+    tmp = f"{prefix}_trainer_state.tmp"
+    if di.is_main:
+        save_checkpoint(prefix, model, tokenizer, value_head, optimizer, trainer_state, save_full_policy,
+                        defer_commit=True)
+    barrier()
+    if not di.is_main:
+        save_rank_rng(prefix, di.rank, rng_state(), d=tmp)
+    if optimizer is not None and getattr(optimizer, "sharded", False):
+        optimizer.save_shard(tmp)
+    barrier()
+    if di.is_main:
+        _commit(tmp, f"{prefix}_trainer_state")
+    barrier()
+
+
 def save_checkpoint(prefix: str, model, tokenizer, value_head=None, optimizer=None, trainer_state: Optional[dict] = None,
-                    save_full_policy: bool = True):
+                    save_full_policy: bool = True, defer_commit: bool = False):
+    """Rank-local save of every artifact. ``defer_commit``: leave the trainer state in
+    ``{prefix}_trainer_state.tmp`` for :func:`save_checkpoint_dp` to complete and rename."""
     os.makedirs(os.path.dirname(os.path.abspath(prefix)), exist_ok=True)
     if save_full_policy:
         save_policy(model, f"{prefix}_policy", extra=value_head.trl_state_dict() if value_head is not None else None)
@@ -197,6 +228,10 @@ def save_checkpoint(prefix: str, model, tokenizer, value_head=None, optimizer=No
 
         tmp = _atomic_dir(f"{prefix}_trainer_state")
         st = dict(trainer_state or {})
+        if optimizer is not None:
+            # how the optimizer state is laid out: 0 = one optimizer.safetensors, N = ZeRO-1 shards
+            # of a world of N (load_checkpoint refuses a mismatching optimizer)
+            st["zero_world"] = int(optimizer.world) if getattr(optimizer, "sharded", False) else 0
         if optimizer is not None and getattr(optimizer, "sharded", False):
             # ZeRO-1: metadata here, tensors per rank (ZeroAdamW.save_shard, called on every rank)
             osd = optimizer.state_dict()
@@ -219,8 +254,36 @@ def save_checkpoint(prefix: str, model, tokenizer, value_head=None, optimizer=No
                 json.dump(rm, f)
         with open(os.path.join(tmp, "state.json"), "w") as f:
             json.dump(st, f, indent=2, default=float)
-        _commit(tmp, f"{prefix}_trainer_state")
+        if not defer_commit:
+            _commit(tmp, f"{prefix}_trainer_state")
     print(f"Checkpoint saved at {prefix}")
+
+
+def _check_optimizer_layout(tsd: str, st: dict, optimizer):
+    """Refuse to resume an optimizer from a checkpoint whose optimizer state has another layout:
+    ZeRO-1 shards of a different world size, shards into an unsharded optimizer or the reverse —
+    silently skipping the moments (and, under full fine-tuning, the fp32 masters that carry the
+    weights) would resume from the initial weights with a restored step counter."""
+    import glob
+
+    sharded = bool(getattr(optimizer, "sharded", False))
+    world = int(getattr(optimizer, "world", 1)) if sharded else 0
+    if "zero_world" in st:
+        zw = int(st["zero_world"])
+    elif glob.glob(os.path.join(tsd, "optimizer_zero*_rank*.safetensors")):  # written before "zero_world"
+        zw = -1
+    else:
+        zw = 0 if os.path.exists(os.path.join(tsd, "optimizer.safetensors")) or "optimizer" not in st else -2
+    if zw == -2:
+        raise RuntimeError(f"{tsd}: state.json records optimizer state but optimizer.safetensors is missing")
+    if zw == 0 and sharded:
+        raise RuntimeError(f"{tsd}: unsharded optimizer checkpoint, but the optimizer is ZeRO-1 sharded over "
+                           f"{world} ranks; resume with zero=False (or world 1)")
+    if zw != 0 and not sharded:
+        raise RuntimeError(f"{tsd}: ZeRO-1 sharded optimizer checkpoint (world {zw if zw > 0 else '?'}), but the "
+                           f"optimizer is unsharded; resume with zero=True at the saving world size")
+    if zw > 0 and zw != world:
+        raise RuntimeError(f"{tsd}: ZeRO-1 shards of world {zw}, resuming at world {world}")
 
 
 def load_checkpoint(prefix: str, model, value_head=None, optimizer=None, load_policy_weights: bool = False):
@@ -239,6 +302,8 @@ def load_checkpoint(prefix: str, model, value_head=None, optimizer=None, load_po
     if os.path.isdir(tsd):
         with open(os.path.join(tsd, "state.json")) as f:
             st = json.load(f)
+        if optimizer is not None:
+            _check_optimizer_layout(tsd, st, optimizer)
         if optimizer is not None and getattr(optimizer, "sharded", False):
             osd = dict(st.get("optimizer", {}))
             optimizer.load_state_dict(osd)

@@ -504,23 +504,14 @@ class PPOTrainer:
 
     def save_checkpoint(self, prefix: str, epoch: int = 0, best: float = -math.inf, full_policy: bool = True,
                         batch_in_epoch: int = 0, extra_state: Optional[dict] = None):
-        """Rank 0 writes the artifacts; every other rank adds its own RNG state (rng_rank{r})."""
-        from ..parallel import barrier
-        from ..utils import rng_state
-        from .checkpoint import save_checkpoint, save_rank_rng
+        """Every rank calls this: rank 0 writes the artifacts, every other rank its RNG state, every
+        rank its ZeRO-1 optimizer shard — all inside the trainer-state directory before it is
+        renamed into place (checkpoint.save_checkpoint_dp)."""
+        from .checkpoint import save_checkpoint_dp
 
-        di = dist_info()
         st = self.trainer_state(epoch, best, batch_in_epoch)  # collective-free; every rank
         st.update(extra_state or {})
-        if di.is_main:
-            save_checkpoint(prefix, self.policy, self.tok, self.value_head, self.opt, st,
-                            save_full_policy=full_policy)
-        barrier()
-        if not di.is_main:
-            save_rank_rng(prefix, di.rank, rng_state())
-        if getattr(self.opt, "sharded", False):  # ZeRO-1: every rank writes its optimizer shard
-            self.opt.save_shard(f"{prefix}_trainer_state")
-        barrier()
+        save_checkpoint_dp(prefix, self.policy, self.tok, self.value_head, self.opt, st, save_full_policy=full_policy)
 
     def load_checkpoint(self, prefix: str) -> dict:
         from ..utils import set_rng_state

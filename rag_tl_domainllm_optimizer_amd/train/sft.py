@@ -264,20 +264,12 @@ class SFTTrainer:
         """PEFT adapter (LoRA) + optimizer moments + trainer state (position, best loss, every
         rank's RNG), and the merged HF policy when ``full_policy`` (always under full fine-tuning);
         rank 0 writes the artifacts, every other rank its RNG state."""
-        from ..parallel import barrier
-        from ..utils import rng_state
-        from .checkpoint import save_checkpoint, save_rank_rng
+        from .checkpoint import save_checkpoint_dp
 
-        di = dist_info()
         st = self.trainer_state(epoch, step_in_epoch, best_loss)
         st.update(extra_state or {})
-        if di.is_main:
-            save_checkpoint(prefix, self.model, self.tok, None, self.opt, st,
-                            save_full_policy=full_policy or self.cfg.full_finetune)
-        barrier()
-        if not di.is_main:
-            save_rank_rng(prefix, di.rank, rng_state())
-        barrier()
+        save_checkpoint_dp(prefix, self.model, self.tok, None, self.opt, st,
+                           save_full_policy=full_policy or self.cfg.full_finetune)
 
     def load_checkpoint(self, prefix: str) -> dict:
         """Inverse of :meth:`save`: adapter (or, under full fine-tuning, the fp32 master restored

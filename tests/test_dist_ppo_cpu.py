@@ -251,7 +251,7 @@ def _zero_ppo_worker(rank, world, port, out_dir, zero):
 
     parallel.init(device="cpu")
 
-    def setup():
+    def setup(zero=zero):
         torch.manual_seed(0)
         cfg = PRESETS["tiny-llama"]
         tok = Tokenizer.synthetic(cfg.vocab_size, "llama")
@@ -272,12 +272,24 @@ def _zero_ppo_worker(rank, world, port, out_dir, zero):
     m1 = tr.step(batches[0])
     ck = os.path.join(out_dir, f"ck{int(zero)}", "s1")
     tr.save_checkpoint(ck, 0, m1["reward_mean"], full_policy=True, batch_in_epoch=1)
+    d = ck + "_trainer_state"
+    files = os.listdir(d)
+    assert not os.path.exists(d + ".tmp")
+    assert all(f"rng_rank{r}.safetensors" in files for r in range(world)), files
+    if zero:
+        # every rank's shard is inside the committed directory (written before the rename)
+        assert all(f"optimizer_zero{world}_rank{r}.safetensors" in files for r in range(world)), files
     m2 = tr.step(batches[1])
     params = torch.cat([p.detach().float().reshape(-1) for p in tr.policy.parameters()])
     tr2, _ = setup()
     tr2.load_checkpoint(ck)
     m2b = tr2.step(batches[1])
     params_b = torch.cat([p.detach().float().reshape(-1) for p in tr2.policy.parameters()])
+    if zero:
+        # an unsharded optimizer refuses the sharded state instead of silently resuming without it
+        tr_rep, _ = setup(zero=False)
+        with pytest.raises(RuntimeError, match="ZeRO-1 sharded"):
+            tr_rep.load_checkpoint(ck)
     torch.save({"m1": m1, "m2": m2, "m2b": m2b, "params": params, "params_b": params_b},
                os.path.join(out_dir, f"zppo{int(zero)}_{rank}.pt"))
     parallel.barrier()

@@ -1318,6 +1318,32 @@ def test_sampler_window_path_bitwise(top_k, top_p, scale):
     assert keep.gather(1, t1[:, None]).float().mean().item() >= 0.97
 
 
+@pytest.mark.parametrize("window", [0, 1])
+@pytest.mark.parametrize("top_k,top_p,scale", [(50, 1.0, 2.0), (50, 0.9, 2.0), (64, 0.8, 1.0), (7, 0.5, 0.3),
+                                               (50, 0.9, 0.02)])
+def test_sampler_fast64_path_bitwise(top_k, top_p, scale, window):
+    """<= 64 survivors (top-k 50): the wave-0 register fast path vs the block-wide sort / nucleus /
+    Gumbel path (tuning sample_fast64=0) — the same token and behaviour log-prob bitwise, with ties
+    at the top and at the k-th value, under both candidate searches."""
+    B, V = 48, 32000
+    g = torch.Generator(device="cpu").manual_seed(top_k + 1000)
+    logits = (torch.randn(B, V, generator=g) * scale).to(torch.bfloat16).to(DEV)
+    logits[3, 100:140] = logits[3].max()  # 40-way tie at the top
+    kth = logits[5].float().topk(top_k).values[-1]
+    logits[5, 200:230] = kth.to(torch.bfloat16)  # ties at the k-th value (survivor count > k)
+    outs = []
+    for fast in (1, 0):
+        with ops.tuning(sample_window=window, sample_fast64=fast):
+            res = []
+            for o in range(3):
+                off = torch.full((1,), o, dtype=torch.long, device=DEV)
+                res.append(ops.sample(logits, 1 / 0.7, top_k=top_k, top_p=top_p, seed=11, offset=off))
+        outs.append(res)
+    for (t1, l1), (t0, l0) in zip(*outs):
+        assert torch.equal(t1, t0)
+        assert torch.equal(l1, l0)
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 15360, 5120), (256, 5120, 13824), (200, 4096, 4096), (130, 1000, 512)])
 def test_gemm_fp8_splitk_slabs(M, N, K):
     """W8A8 split-K into fp32 slabs (config-5 decode at batch > 64): the summed slabs equal the
