@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--old-logp", default="rollout", choices=["rollout", "recompute"],
                     help="PPO ratio's theta_old log-probs: the rollout sampler's (free) or a training-numerics "
                          "forward of the policy beside the reference forward (exact ratio 1 at theta_old)")
+    ap.add_argument("--lora-grad-epilogue", default="on", choices=["on", "off"],
+                    help="A/B: LoRA adapter gradients accumulated into the flat .grad buffer by one native epilogue "
+                         "per projection (on) or returned to autograd (off: zero fill + scale + one add per adapter)")
     ap.add_argument("--kl-in-loss", default="on", choices=["on", "off"],
                     help="frozen-reference KL as a k3 penalty on the update forward's own log-probs (on) or as a "
                          "-beta (old - ref) token reward (off: the pre-round-6 form)")
@@ -163,6 +166,11 @@ def main():
             tuning_over[k.strip()] = float(v) if "." in v else int(v)
         ops.set_tuning(**tuning_over)
         log(f"[bench] tuning overrides: {tuning_over}")
+    if args.lora_grad_epilogue == "off":
+        import importlib
+
+        importlib.import_module("rag_tl_domainllm_optimizer_amd.ops.linear").DIRECT_LORA_GRADS = False
+        tuning_over["lora_grad_epilogue"] = "off"
     if args.rope_fusion == "off":
         import importlib
 

@@ -74,6 +74,8 @@ int rt_adamw_mixed(float*, const void*, long, const float*, float*, float*, void
                    float, int, float, const float*, int, float*, int*, hipStream_t);
 int rt_pool_norm(const void*, const int*, int, int, int, int, float*, hipStream_t);
 int rt_scatter_scaled(const long*, int, long, hipStream_t);
+int rt_lora_grad_accum(const long*, int, long, hipStream_t);
+int rt_f32_to_bf16_zero(float*, void*, long, hipStream_t);
 int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*, hipStream_t);
 int rt_segment_mean(const float*, int, const long*, const int*, int, int, float*, hipStream_t);
 int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const int*, const void*, const long*, const float*,
@@ -1099,6 +1101,24 @@ void grad_sumsq(const Tensor& g, Tensor partials) {
 
 // Batched scaled fp32 -> bf16 scatter (LoRA compute images): tab int64 [n, 7] on the device =
 // {src, src_ld, dst, dst_ld, rows, cols, fp32 scale bits}; max_elems = max rows * cols.
+// LoRA backward epilogue: scaled accumulate of the adapter-gradient workspaces into .grad, zeroing them
+void lora_grad_accum(const Tensor& tab, int64_t max_elems) {
+  CHECK_CUDA(tab);
+  TORCH_CHECK(tab.scalar_type() == at::kLong && tab.is_contiguous() && tab.dim() == 2 && tab.size(1) == 9,
+              "lora_grad_accum: table must be contiguous int64 [n, 9]");
+  check_rc(rt_lora_grad_accum((const long*)tab.data_ptr<int64_t>(), (int)tab.size(0), (long)max_elems, cur_stream()),
+           "lora_grad_accum");
+}
+
+// bf16 copy of an fp32 accumulator that is zeroed in the same pass
+Tensor f32_to_bf16_zero(Tensor src) {
+  CHECK_CUDA(src); CHECK_F32(src);
+  TORCH_CHECK(src.is_contiguous(), "f32_to_bf16_zero: contiguous source");
+  auto out = at::empty(src.sizes(), src.options().dtype(at::kBFloat16));
+  check_rc(rt_f32_to_bf16_zero(src.data_ptr<float>(), out.data_ptr(), src.numel(), cur_stream()), "f32_to_bf16_zero");
+  return out;
+}
+
 void scatter_scaled(const Tensor& tab, int64_t max_elems) {
   CHECK_CUDA(tab);
   TORCH_CHECK(tab.scalar_type() == at::kLong && tab.dim() == 2 && tab.size(1) == 7 && tab.is_contiguous(),
@@ -1366,6 +1386,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample", &sample);
   m.def("adamw", &adamw);
   m.def("scatter_scaled", &scatter_scaled, "batched scaled fp32 -> bf16 strided scatter (LoRA images)");
+  m.def("lora_grad_accum", &lora_grad_accum, "LoRA backward: scaled accumulate of adapter-gradient workspaces into grads");
+  m.def("f32_to_bf16_zero", &f32_to_bf16_zero, "fp32 -> bf16 copy that zeroes the source");
   m.def("adamw_mixed", &adamw_mixed);
   m.def("grad_norm", &grad_norm);
   m.def("adamw_apply", &adamw_apply);

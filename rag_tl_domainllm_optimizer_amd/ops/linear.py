@@ -317,6 +317,20 @@ def refresh_lora_batched(groups: List["LoRAGroup"], dtype=torch.bfloat16) -> boo
     return True
 
 
+_WS: dict = {}
+
+
+def _persistent_zeros(key, n: int, device) -> torch.Tensor:
+    """A cached fp32 buffer of >= n elements that is ALL ZERO between uses: its consumers (the
+    native f32_to_bf16_zero / lora_grad_accum epilogues) zero what they read, so the LoRA backward
+    needs no per-call zero fill. Grows (reallocated zeroed) when a larger prefix is asked for."""
+    k = (key, str(device))
+    t = _WS.get(k)
+    if t is None or t.numel() < n:
+        t = _WS[k] = torch.zeros(max(n, 1), dtype=torch.float32, device=device)
+    return t[:n]
+
+
 def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0, zero32=None) -> torch.Tensor:
     """a [M, K] (ROW) times a narrow operand b (ROW [R, K] or KMAJ [K, R]; R = padded LoRA rank) ->
     [M, R] bf16 on the 64x64-tile kernel (U = X A_pad^T forward, dU = dY UB backward). One
@@ -343,8 +357,12 @@ def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0, zero32=N
     ns = nsplit or auto
     if ns == 1:
         return native().gemm_small(a, b, ROW, lb, 0, 1, None, bm)
-    # ``zero32``: a caller-provided zeroed fp32 [M, R] accumulator (shared fill)
-    out = zero32 if zero32 is not None else torch.zeros(M, R, dtype=torch.float32, device=a.device)
+    # ``zero32``: a caller-provided zeroed fp32 [M, R] accumulator; it is consumed here (rounded to
+    # bf16 and zeroed in one pass: a persistent workspace stays zero for the next call)
+    if zero32 is not None:
+        native().gemm_small(a, b, ROW, lb, 2, ns, zero32, bm)
+        return native().f32_to_bf16_zero(zero32)
+    out = torch.zeros(M, R, dtype=torch.float32, device=a.device)
     native().gemm_small(a, b, ROW, lb, 2, ns, out, bm)
     return out.to(a.dtype)
 
@@ -445,22 +463,77 @@ class _LinearFn(torch.autograd.Function):
         return (dx, dw, db, None, None, None, None, *lora_grads)
 
 
+# the LoRA backward's direct-to-.grad epilogue (A/B switch for tests)
+DIRECT_LORA_GRADS = True
+
+
+def _direct_grads_ok(lora: "LoRAGroup") -> bool:
+    """The adapter gradients can be accumulated straight into the parameters' .grad buffers (fp32
+    contiguous tensors already allocated on the device, e.g. views of a flat gradient buffer,
+    ops.FlatParams) instead of being returned to autograd for an accumulate-add each."""
+    if not DIRECT_LORA_GRADS or torch.is_grad_enabled():  # create_graph: gradients stay differentiable
+        return False
+    for p in lora.a + lora.b:
+        g = p.grad
+        if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.device != p.device:
+            return False
+    return True
+
+
+def _grad_table(lora: "LoRAGroup", ga: torch.Tensor, gb: torch.Tensor):
+    """Device descriptor table of lora_grad_accum for this group's workspaces and .grad buffers
+    (cached per address set): dA rows of each adapter (scaled) -> a.grad, each adapter's rows of
+    dB_all (its own rank columns) -> b.grad, other dB_all rows zeroed only."""
+    import struct
+
+    key = (ga.data_ptr(), gb.data_ptr(), tuple(p.grad.data_ptr() for p in lora.a + lora.b), tuple(lora.scale))
+    ent = getattr(lora, "_grad_tab", None)
+    if ent is not None and ent[0] == key:
+        return ent[1], ent[2]
+    Rp, K = ga.shape
+    N = gb.shape[0]
+    rows, cov = [], []
+    f = lambda x: struct.unpack("<i", struct.pack("<f", float(x)))[0]  # noqa: E731
+    for a, b, r0, c0, sc in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
+        ri, ni = a.shape[0], b.shape[0]
+        rows.append((ga.data_ptr() + 4 * r0 * K, K, a.grad.data_ptr(), K, ri, K, 0, K, f(sc)))
+        rows.append((gb.data_ptr() + 4 * c0 * Rp, Rp, b.grad.data_ptr(), ri, ni, Rp, r0, r0 + ri, f(1.0)))
+        cov.append((c0, c0 + ni))
+    cov.sort()
+    r = 0
+    for lo, hi in cov + [(N, N)]:  # dB_all rows no adapter owns: zero them
+        if lo > r:
+            rows.append((gb.data_ptr() + 4 * r * Rp, Rp, 0, 0, lo - r, Rp, 0, 0, f(1.0)))
+        r = max(r, hi)
+    tab = torch.tensor(rows, dtype=torch.int64).to(ga.device)
+    mx = max(rw[4] * rw[5] for rw in rows)
+    lora._grad_tab = (key, tab, mx)
+    return tab, mx
+
+
 def _linear_bwd(dy, x2, w, u, lora, mask, need_x: bool, need_w: bool, dx_act: int = 0, dx_aux=None, dx_out=None):
     """Gradients of y = x W^T (+ s (drop(x) A^T) B^T) given dL/dy: (dX, dW, [dA_i, dB_i, ...]).
     ``dx_act`` = ACT_DSWIGLU: dX is the down projection's input gradient dF and goes through the
     SwiGLU backward in the dX GEMM's epilogue (``dx_aux`` = the [gate | up] pre-activation,
-    ``dx_out`` = the d[gate | up] buffer it writes)."""
+    ``dx_out`` = the d[gate | up] buffer it writes). On the GPU with .grad buffers in place
+    (:func:`_direct_grads_ok`) the adapter gradients are accumulated into them by one native
+    epilogue and returned as None (the parameter's ``_rt_grad_ready`` hook, set by
+    parallel.GradSync, is called instead of autograd's post-accumulate hook)."""
     dx = dw = None
     gpu = on_gpu(dy)
     ws = None
+    direct = gpu and lora is not None and _direct_grads_ok(lora)
     if lora is not None and gpu:
-        # one zero fill for the three fp32 accumulators of the adapter products: dU [M, Rp]
-        # (split-K over N), dA_all [Rp, K], dB_all [N, Rp]
+        # fp32 accumulators of the adapter products: dU [M, Rp] (split-K over N) always from a
+        # persistent zeroed workspace (rounded to bf16 and re-zeroed in one pass); dA_all [Rp, K] /
+        # dB_all [N, Rp] from another one in the direct mode (consumed by lora_grad_accum), else
+        # from one fresh zero fill (their slices are handed to autograd)
         Mr, Kr, Nr, Rp = dy.shape[0], x2.shape[1], dy.shape[1], lora.ub.shape[1]
-        ws = torch.zeros(Mr * Rp + Rp * Kr + Nr * Rp, dtype=torch.float32, device=dy.device)
-        du32 = ws[:Mr * Rp].view(Mr, Rp)
-        ga_out = ws[Mr * Rp:Mr * Rp + Rp * Kr].view(Rp, Kr)
-        gb_out = ws[Mr * Rp + Rp * Kr:].view(Nr, Rp)
+        du32 = _persistent_zeros("lora_du", Mr * Rp, dy.device).view(Mr, Rp)
+        ws = _persistent_zeros(("lora_gab", Rp, Kr, Nr), Rp * Kr + Nr * Rp, dy.device) if direct else \
+            torch.zeros(Rp * Kr + Nr * Rp, dtype=torch.float32, device=dy.device)
+        ga_out = ws[:Rp * Kr].view(Rp, Kr)
+        gb_out = ws[Rp * Kr:].view(Nr, Rp)
     du = _narrow(dy, lora.ub, KMAJ, zero32=du32 if ws is not None else None) if lora is not None else None
     if need_x:
         if dx_act == ACT_DSWIGLU:
@@ -486,6 +559,14 @@ def _linear_bwd(dy, x2, w, u, lora, mask, need_x: bool, need_w: bool, dx_act: in
         xd = x2 * mask if mask is not None else x2
         ga_all = gemm_tn(du, xd, out=ga_out, zeroed=True) if ws is not None else gemm_tn(du, xd)
         gb_all = gemm_tn(dy, u, out=gb_out, zeroed=True) if ws is not None else gemm_tn(dy, u)
+        if direct:
+            tab, mx = _grad_table(lora, ga_all, gb_all)
+            native().lora_grad_accum(tab, mx)
+            for p in lora.a + lora.b:
+                hook = getattr(p, "_rt_grad_ready", None)
+                if hook is not None:
+                    hook(p)
+            return dx, dw, [None] * (2 * len(lora.a))
         one_scale = len(set(lora.scale)) == 1
         if one_scale:
             ga_all.mul_(lora.scale[0])  # one launch for every adapter of the projection

@@ -107,6 +107,49 @@ def test_linear_lora_mixed_scales_grads():
         _close(p.grad, q.grad, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("M", [200, 3000])
+def test_linear_lora_direct_grads(M):
+    """LoRA backward with .grad buffers in place (ops.FlatParams): the adapter gradients go straight
+    into them through the native epilogue (scaled dA rows, each adapter's dB block, other dB rows
+    zeroed only; persistent workspaces left zero) — equal to the autograd-returned gradients,
+    accumulating across backwards, calling a parameter's ``_rt_grad_ready`` hook. Three adapters
+    with an uncovered middle block of output rows and two scales."""
+    torch.manual_seed(5)
+    K, N, r = 256, 384, 8
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.nn.Parameter((torch.randn(N, K, device=DEV) / 16).to(torch.bfloat16), requires_grad=False)
+    shapes = ((r, K), (128, r), (r, K), (64, r), (r, K), (128, r))
+    base = [torch.randn(*shp, device=DEV) * 0.05 for shp in shapes]
+    import importlib
+
+    L = importlib.import_module("rag_tl_domainllm_optimizer_amd.ops.linear")
+    g = None
+    grads = {}
+    for mode in ("returned", "direct"):
+        L.DIRECT_LORA_GRADS = mode == "direct"
+        ps = [torch.nn.Parameter(t.clone()) for t in base]
+        # adapters on rows [0, 128), [192, 256) and [256, 384): rows [128, 192) have none
+        grp = ops.LoRAGroup(["q", "k", "v"], ps[0::2], ps[1::2], [0, 192, 256], [2.0, 2.0, 0.5], N)
+        calls = []
+        if mode == "direct":
+            for p in ps:
+                p.grad = torch.zeros_like(p)
+                p._rt_grad_ready = calls.append
+        for _ in range(2):
+            y = ops.linear(x, w, lora=grp)
+            if g is None:
+                g = torch.randn_like(y)
+            (y.float() * g.float()).sum().backward()
+        grads[mode] = [p.grad.clone() for p in ps]
+        if mode == "direct":
+            assert len(calls) == 2 * len(ps)
+    L.DIRECT_LORA_GRADS = True
+    for a, b in zip(grads["returned"], grads["direct"]):
+        _close(b, a, rtol=1e-4, atol=1e-5)
+    for k, t in L._WS.items():
+        assert int((t != 0).sum()) == 0, k
+
+
 def test_refresh_lora_batched_matches_per_group():
     """One-launch rebuild of every group's bf16 images (scaled A rows, B blocks) is bitwise the
     per-group torch refresh."""
