@@ -184,7 +184,7 @@ def test_reward_stream_overlap_matches_serial(monkeypatch):
         t = {k: e["ref_start"].elapsed_time(v) for k, v in e.items()}
         evs.append(t)
         upd = tr.update(ro)
-        res.append({"reward_mean": float(ro.scores.mean()), "kl_ref": ro.kl_ref,
+        res.append({"reward_mean": float(ro.scores.mean()), "kl_ref": float(ro.kl_old_ref),
                     "factual_accuracy": float(ro.components["factual_accuracy"].mean()), **upd})
     ov, ser = evs
     assert ov["reward_end"] < ov["ref_end"], ov        # encoder finished while the reference ran

@@ -149,3 +149,35 @@ def test_ppo_old_logp_recompute_ratio_is_one_at_theta_old():
         assert m["behaviour_logp_gap"] < 1e-5, m["behaviour_logp_gap"]
         assert m["clipfrac_first_mb"] == 0.0
         assert math.isfinite(m["rollout_engine_logp_gap"]) and m["rollout_engine_logp_gap"] >= 0.0
+
+
+def test_kl_in_loss_exact_zero_at_init_and_oracle():
+    """The reference KL in the loss (PPOConfig.kl_in_loss): at LoRA B = 0 the policy IS the reference,
+    so the first minibatch's KL at theta_old is 0 (up to the CPU GEMMs' batch-size-dependent
+    blocking; exactly 0 on the GPU, tests/test_batch_invariance_gpu.py; the sampler-based sum
+    (old - ref) is reported apart); the loss oracle adds kl_coef * mean(exp(d) - d - 1), d = ref - lp, whose
+    gradient is kl_coef * (1 - exp(d)) / n per masked token."""
+    from rag_tl_domainllm_optimizer_amd.ops import reference as ref
+
+    tr, recs = _setup(seed=4)
+    assert tr.cfg.kl_in_loss
+    m = tr.step(next(iter(RecordLoader(recs, batch_size=8, seed=1))))
+    assert abs(m["kl_ref_theta_old"]) < 1e-5
+    assert m["kl_ref_k3"] >= 0.0 and math.isfinite(m["kl_old_ref"])
+    torch.manual_seed(0)
+    B, T, beta = 3, 7, 0.05
+    lp = (torch.randn(B, T) * 0.3 - 2).requires_grad_(True)
+    refl = lp.detach() + torch.randn(B, T) * 0.2
+    z = torch.zeros(B, T)
+    mask = torch.ones(B, T)
+    mask[0, 5:] = 0
+    loss0, st0 = ref.ppo_loss(lp, lp.detach(), z, z, z, z, mask, 0.2, 0.5, 0.0)
+    loss1, st1 = ref.ppo_loss(lp, lp.detach(), z, z, z, z, mask, 0.2, 0.5, 0.0, None, None, refl, beta)
+    d = refl - lp.detach()
+    n = mask.sum()
+    k3 = ((torch.exp(d) - d - 1) * mask).sum() / n
+    torch.testing.assert_close(loss1 - loss0, beta * k3)
+    torch.testing.assert_close(st1[6], k3)
+    torch.testing.assert_close(st1[7], ((-d) * mask).sum() / n)
+    (g,) = torch.autograd.grad(loss1 - loss0, lp)
+    torch.testing.assert_close(g, beta * (1 - torch.exp(d)) * mask / n)
