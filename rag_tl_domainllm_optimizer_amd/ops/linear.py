@@ -517,8 +517,7 @@ def _linear_bwd(dy, x2, w, u, lora, mask, need_x: bool, need_w: bool, dx_act: in
     SwiGLU backward in the dX GEMM's epilogue (``dx_aux`` = the [gate | up] pre-activation,
     ``dx_out`` = the d[gate | up] buffer it writes). On the GPU with .grad buffers in place
     (:func:`_direct_grads_ok`) the adapter gradients are accumulated into them by one native
-    epilogue and returned as None (the parameter's ``_rt_grad_ready`` hook, set by
-    parallel.GradSync, is called instead of autograd's post-accumulate hook)."""
+    epilogue and returned as None."""
     dx = dw = None
     gpu = on_gpu(dy)
     ws = None
@@ -562,10 +561,10 @@ def _linear_bwd(dy, x2, w, u, lora, mask, need_x: bool, need_w: bool, dx_act: in
         if direct:
             tab, mx = _grad_table(lora, ga_all, gb_all)
             native().lora_grad_accum(tab, mx)
-            for p in lora.a + lora.b:
-                hook = getattr(p, "_rt_grad_ready", None)
-                if hook is not None:
-                    hook(p)
+            # None to autograd: the parameters' AccumulateGrad nodes still run (with no gradient)
+            # and fire their post-accumulate hooks after this backward returns, i.e. behind the
+            # epilogue on the stream — parallel.GradSync's bucket readiness needs nothing else
+            # (tests/test_zz_dist_gpu.py: ranks hold the same reduced gradient)
             return dx, dw, [None] * (2 * len(lora.a))
         one_scale = len(set(lora.scale)) == 1
         if one_scale:

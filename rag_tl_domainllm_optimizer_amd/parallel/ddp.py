@@ -70,7 +70,6 @@ class GradSync:
         self._ready = [0] * len(bounds)
         self._handles: List[Optional[object]] = [None] * len(bounds)
         self._hooks = []
-        self._direct = []
         self.sync_enabled = True
         self.wait_s = 0.0  # host time blocked in finish() (exposed all-reduce tail), reset by the caller
         self.comm_bytes = 0  # payload bytes handed to collectives (per rank), reset by the caller
@@ -83,12 +82,9 @@ class GradSync:
         self.rs32_inflight = max(1, int(os.environ.get("RAGTL_RS32_INFLIGHT", "2")))
         if self.overlap:
             for p, bi in zip(flat.params, self.param_bucket):
-                hook = self._make_hook(bi)
-                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
-                # kernels that accumulate straight into .grad (the LoRA backward epilogue,
-                # ops.linear._linear_bwd) return no gradient to autograd and call this instead
-                p._rt_grad_ready = hook
-                self._direct.append(p)
+                # also fires when a backward accumulated straight into .grad and returned None
+                # (the LoRA epilogue, ops.linear._linear_bwd): AccumulateGrad still runs
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
 
     def _make_hook(self, bi):
         def hook(_p):
@@ -191,10 +187,6 @@ class GradSync:
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        for p in self._direct:
-            if hasattr(p, "_rt_grad_ready"):
-                del p._rt_grad_ready
-        self._direct = []
 
 
 class _Done:

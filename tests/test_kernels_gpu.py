@@ -112,8 +112,9 @@ def test_linear_lora_direct_grads(M):
     """LoRA backward with .grad buffers in place (ops.FlatParams): the adapter gradients go straight
     into them through the native epilogue (scaled dA rows, each adapter's dB block, other dB rows
     zeroed only; persistent workspaces left zero) — equal to the autograd-returned gradients,
-    accumulating across backwards, calling a parameter's ``_rt_grad_ready`` hook. Three adapters
-    with an uncovered middle block of output rows and two scales."""
+    accumulating across backwards; autograd still fires the parameters' post-accumulate hooks
+    (parallel.GradSync's bucket readiness) exactly once per backward. Three adapters with an
+    uncovered middle block of output rows and two scales."""
     torch.manual_seed(5)
     K, N, r = 256, 384, 8
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -134,7 +135,7 @@ def test_linear_lora_direct_grads(M):
         if mode == "direct":
             for p in ps:
                 p.grad = torch.zeros_like(p)
-                p._rt_grad_ready = calls.append
+                p.register_post_accumulate_grad_hook(calls.append)
         for _ in range(2):
             y = ops.linear(x, w, lora=grp)
             if g is None:
@@ -142,7 +143,7 @@ def test_linear_lora_direct_grads(M):
             (y.float() * g.float()).sum().backward()
         grads[mode] = [p.grad.clone() for p in ps]
         if mode == "direct":
-            assert len(calls) == 2 * len(ps)
+            assert len(calls) == 2 * len(ps)  # one post-accumulate hook per parameter and backward
     L.DIRECT_LORA_GRADS = True
     for a, b in zip(grads["returned"], grads["direct"]):
         _close(b, a, rtol=1e-4, atol=1e-5)
