@@ -20,6 +20,7 @@ The reference runs these products through HF/PyTorch (reinforcement_learning_opt
 from __future__ import annotations
 
 import contextlib
+import threading
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -49,7 +50,11 @@ def splitk_plan(M: int, N: int, K: int, act: int = 0):
     return max(1, min(nk // 8, (256 + tiles // 2) // tiles)), bn
 
 
-_BATCH_INVARIANT = 0
+_BI = threading.local()  # per-thread nesting depth of batch_invariant() (a serving thread keeps its plans)
+
+
+def _batch_invariant_on() -> bool:
+    return getattr(_BI, "depth", 0) > 0
 
 
 @contextlib.contextmanager
@@ -61,12 +66,12 @@ def batch_invariant(on: bool = True):
     forwards (``train.common.score_sequences``) run under it: reference log-probs, the optional
     theta_old recompute and the update forward then agree bitwise across minibatch sizes,
     padding and packing. Costs nothing at scoring sizes (M in the thousands never splits)."""
-    global _BATCH_INVARIANT
-    _BATCH_INVARIANT += int(bool(on))
+    d = int(bool(on))
+    _BI.depth = getattr(_BI, "depth", 0) + d
     try:
         yield
     finally:
-        _BATCH_INVARIANT -= int(bool(on))
+        _BI.depth -= d
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, out_f32=False, out=None,
@@ -78,7 +83,7 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
     if on_gpu(x):
         M, K = x.shape
         N = w.shape[0]
-        if _BATCH_INVARIANT and K % 8 == 0 and (act != ACT_SWIGLU or N % 256 == 0) \
+        if _batch_invariant_on() and K % 8 == 0 and (act != ACT_SWIGLU or N % 256 == 0) \
                 and (residual is None or not out_f32):
             return native().gemm_big(x, w, ROW, ROW, u, ub, bias, act, 1 if out_f32 else 0, 1, out, None, residual, 0)
         # 32 <= M <= 64 on narrow weights (qkv / o): the 256x128-tile split-K form beats the ring
@@ -669,7 +674,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act=None, lora: Optional
             return y.reshape(*shp[:-1], w.shape[0] // 2)
         if on_gpu(x2) and not grad_needed and bias is None and w.shape[0] % 256 == 0 and x2.shape[1] % 8 == 0 \
                 and w.dtype == torch.bfloat16 and use_lora and not lora.use_merged and fp8 is None \
-                and (x2.shape[0] > 64 or _BATCH_INVARIANT):
+                and (x2.shape[0] > 64 or _batch_invariant_on()):
             # unmerged adapters without grad (reference / theta_old scoring): the training forward's
             # exact product — U = X A_pad^T as K-extension steps of the [gate; up] GEMM with the
             # SwiGLU epilogue — not the merged bf16 W + s B A (a second rounding of every weight)

@@ -52,3 +52,50 @@ def test_adapter_gradient_token_splits(monkeypatch):
     for fn, ns in cases:
         calls = _run(monkeypatch, fn)
         assert [c[3] for c in calls] == [ns], calls
+
+
+class _NativeGemm:
+    def __init__(self):
+        self.calls = []
+
+    def gemm(self, x, w, *a):
+        self.calls.append("skinny")
+        return torch.zeros(x.shape[0], w.shape[0], dtype=x.dtype)
+
+    def gemm_splitk(self, x, w, s, *a):
+        self.calls.append(f"splitk{s}")
+        return torch.zeros(x.shape[0], w.shape[0], dtype=x.dtype)
+
+    def gemm_big(self, a, b, la, lb, a2, b2, bias, act, out_mode, nsplit, out, out2, residual, bn):
+        self.calls.append(f"big{nsplit}")
+        return torch.zeros(a.shape[0], b.shape[0], dtype=a.dtype)
+
+
+def test_batch_invariant_dispatch(monkeypatch):
+    """ops.batch_invariant(): every token-parallel GEMM takes the unsplit 256-row kernel whatever M
+    is (the per-M plan picks skinny kernels at M <= 64 and split-K at M <= 512 otherwise), per
+    thread, nesting."""
+    import threading
+
+    nat = _NativeGemm()
+    monkeypatch.setattr(L, "native", lambda: nat)
+    monkeypatch.setattr(L, "on_gpu", lambda t: True)
+    w = torch.zeros(4096, 4096, dtype=torch.bfloat16)
+    for M in (8, 48, 300, 2000):
+        L.gemm(torch.zeros(M, 4096, dtype=torch.bfloat16), w)
+    assert nat.calls[0] == "skinny" and nat.calls[2].startswith("splitk") and nat.calls[3] == "big1", nat.calls
+    nat.calls.clear()
+    with L.batch_invariant():
+        with L.batch_invariant():
+            L.gemm(torch.zeros(8, 4096, dtype=torch.bfloat16), w)
+        for M in (48, 300, 2000):
+            L.gemm(torch.zeros(M, 4096, dtype=torch.bfloat16), w)
+        other = []
+        th = threading.Thread(target=lambda: (L.gemm(torch.zeros(8, 4096, dtype=torch.bfloat16), w),
+                                              other.append(nat.calls[-1])))
+        th.start()
+        th.join()
+    assert nat.calls[:4] == ["big1"] * 4, nat.calls
+    assert other == ["skinny"]  # another thread keeps its own (default) plans
+    L.gemm(torch.zeros(8, 4096, dtype=torch.bfloat16), w)
+    assert nat.calls[-1] == "skinny"
