@@ -488,13 +488,16 @@ Tensor gemm_small(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t la
   const int64_t N = layout_b ? b.size(1) : b.size(0), Kb = layout_b ? b.size(0) : b.size(1);
   TORCH_CHECK(K == Kb, "gemm_small: K mismatch");
   const auto odt = out_mode == 0 ? at::kBFloat16 : at::kFloat;
+  // out_mode 3: split-K slabs [nsplit * M, N] (row stride N), one per split
+  const int64_t rows = out_mode == 3 ? nsplit * M : M;
   Tensor c;
   if (out.has_value() && out->defined()) {
     c = *out;
-    TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.scalar_type() == odt, "gemm_small: out");
+    TORCH_CHECK(c.size(0) == rows && c.size(1) == N && c.stride(1) == 1 && c.scalar_type() == odt &&
+                (out_mode != 3 || c.is_contiguous()), "gemm_small: out");
   } else {
     TORCH_CHECK(out_mode != 2, "gemm_small: atomic accumulation needs an initialised out");
-    c = at::empty({M, N}, a.options().dtype(odt));
+    c = at::empty({rows, N}, a.options().dtype(odt));
   }
   if (M == 0 || N == 0) return c;
   check_rc(rt_gemm_small((int)layout_a, (int)layout_b, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),

@@ -781,6 +781,8 @@ __global__ __launch_bounds__(256, 2) void gemm_small_kernel(Args p) {
                                    __HIP_MEMORY_SCOPE_AGENT);
           else if constexpr (OUT == O_F32)
             ((float*)p.C)[(long)row * p.ldc + col] = acc[i][j][r];
+          else if constexpr (OUT == O_F32_SLAB)  // split ks -> slab ks ([nsplit][M][ldc]); summed in a fixed order
+            ((float*)p.C)[((long)blockIdx.y * p.M + row) * p.ldc + col] = acc[i][j][r];
           else
             ((bf16_t*)p.C)[(long)row * p.ldc + col] = f2bf(acc[i][j][r]);
         }
@@ -1124,7 +1126,8 @@ extern "C" int rt_gemm_splitk_reduce(const float* slabs, int nsplit, int M, int 
   return 0;
 }
 
-// 64x64-tile GEMM (narrow LoRA products). out: 0 bf16, 1 fp32 store, 2 fp32 atomic add (split-K).
+// 64x64-tile GEMM (narrow LoRA products). out: 0 bf16, 1 fp32 store, 2 fp32 atomic add (split-K),
+// 3 fp32 split-K slabs [nsplit][M][ldc] (ROW / ROW: the deterministic forward U product).
 extern "C" int rt_gemm_small(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb, void* C,
                              long ldc, int M, int N, int K, int out, int nsplit, const void* zpage, int bm,
                              hipStream_t stream) {
@@ -1132,7 +1135,7 @@ extern "C" int rt_gemm_small(int layout_a, int layout_b, const void* A, long lda
   if (!zpage || ((layout_a == ROW || layout_b == ROW) && K % 8)) return -1;
   if ((layout_a == KMAJ && M % 8) || (layout_b == KMAJ && N % 8)) return -1;
   if (nsplit < 1) nsplit = 1;
-  if (nsplit > 1 && out != O_F32_ATOMIC) return -2;
+  if (nsplit > 1 && out != O_F32_ATOMIC && out != O_F32_SLAB) return -2;
   Args p{};
   p.A = (const bf16_t*)A; p.lda = lda; p.B = (const bf16_t*)B; p.ldb = ldb;
   p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K; p.nsplit = nsplit; p.zpage = (const bf16_t*)zpage;
@@ -1148,6 +1151,7 @@ extern "C" int rt_gemm_small(int layout_a, int layout_b, const void* A, long lda
     case 0: GS_LAUNCH(ROW, ROW, O_BF16); break;
     case 1: GS_LAUNCH(ROW, ROW, O_F32); break;
     case 2: GS_LAUNCH(ROW, ROW, O_F32_ATOMIC); break;
+    case 3: GS_LAUNCH(ROW, ROW, O_F32_SLAB); break;
     case 10: GS_LAUNCH(ROW, KMAJ, O_BF16); break;
     case 11: GS_LAUNCH(ROW, KMAJ, O_F32); break;
     case 12: GS_LAUNCH(ROW, KMAJ, O_F32_ATOMIC); break;

@@ -353,15 +353,18 @@ def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0, zero32=N
     # (measured at 9632 tokens: dU 383 -> 172 us at K = 28672, profiles/lora_narrow_r2.log). The
     # forward U (ROW adapter image) runs 3 ways split from cold activations: K = 4096 31.3 -> 28.7
     # us, K = 14336 78.0 -> 73.8 us (profiles/r5/lora_narrow_split_sweep.log)
-    # The forward U (ROW adapter image) runs without a split: fp32 atomic partials land in arrival
-    # order, so a split forward is not bitwise reproducible (nor batch-invariant) — the PPO ratio and
-    # reference KL need the scoring forward to be (ops.batch_invariant). Cost: K = 4096 28.7 -> 31.3
-    # us, K = 14336 73.8 -> 78.0 us at 9632 tokens (profiles/r5/lora_narrow_split_sweep.log). The
-    # backward products (dU, dA, dB) keep their atomic splits.
-    auto = 1 if lb == ROW else max(1, min(K // 512, (768 + tiles - 1) // tiles))
+    # The forward U (ROW adapter image) splits 3 ways into fp32 SLABS summed in a fixed order (fp32
+    # atomics land in arrival order: not bitwise reproducible, nor batch-invariant — the PPO ratio
+    # and reference KL need the scoring forward to be, ops.batch_invariant): K = 4096 31.3 -> 28.7
+    # us, K = 14336 78.0 -> 73.8 us at 9632 tokens (profiles/r5/lora_narrow_split_sweep.log, atomic
+    # form). The backward products (dU, dA, dB) keep their atomic splits.
+    auto = min(3, max(1, K // 512)) if lb == ROW else max(1, min(K // 512, (768 + tiles - 1) // tiles))
     ns = nsplit or auto
     if ns == 1:
         return native().gemm_small(a, b, ROW, lb, 0, 1, None, bm)
+    if lb == ROW and zero32 is None and R % 8 == 0:
+        slabs = native().gemm_small(a, b, ROW, ROW, 3, ns, None, bm)
+        return native().splitk_reduce(slabs, ns, M, R, torch.empty(M, R, dtype=a.dtype, device=a.device))
     # ``zero32``: a caller-provided zeroed fp32 [M, R] accumulator; it is consumed here (rounded to
     # bf16 and zeroed in one pass: a persistent workspace stays zero for the next call)
     if zero32 is not None:

@@ -1,5 +1,5 @@
 """Split plans of the LoRA narrow products (ops.linear._narrow / gemm_tn) measured in round 5
-(profiles/r5/lora_narrow_split_sweep.log): the forward U = X A^T runs unsplit (round 6: deterministic), the
+(profiles/r5/lora_narrow_split_sweep.log): the forward U = X A^T splits 3 ways into fixed-order fp32 slabs (round 6: deterministic), the
 token reduction of dA / dB splits 4 ways on 64 output tiles and 8 above. The plans are host code:
 checked here by intercepting the native launch."""
 import importlib
@@ -16,7 +16,12 @@ class _Native:
     def gemm_small(self, a, b, la, lb, out_mode, ns, out, bm):
         self.calls.append((la, lb, out_mode, ns, bm))
         R = b.shape[0] if lb == L.ROW else b.shape[1]
+        if out_mode == 3:
+            return torch.zeros(ns * a.shape[0], R, dtype=torch.float32)
         return out if out is not None else torch.zeros(a.shape[0], R, dtype=a.dtype)
+
+    def splitk_reduce(self, slabs, ns, M, N, out):
+        return out
 
 
 def _run(monkeypatch, fn):
@@ -27,15 +32,15 @@ def _run(monkeypatch, fn):
     return nat.calls
 
 
-def test_forward_u_is_not_split(monkeypatch):
-    """The forward adapter product U = X A_pad^T runs unsplit (bf16 out, no fp32 atomics): a split's
-    atomic partials land in arrival order, which would make the scoring forward non-reproducible
-    and batch-variant (ops.batch_invariant, PPO ratio / reference KL exactness)."""
+def test_forward_u_splits_into_slabs(monkeypatch):
+    """The forward adapter product U = X A_pad^T splits 3 ways into fp32 slabs (out mode 3) summed in a
+    fixed order — never fp32 atomics, whose arrival-order sums would make the scoring forward
+    non-reproducible and batch-variant (ops.batch_invariant, PPO ratio / reference KL exactness)."""
     for K in (4096, 14336):
         x = torch.zeros(9632, K, dtype=torch.bfloat16)
         a = torch.zeros(64, K, dtype=torch.bfloat16)
         calls = _run(monkeypatch, lambda: L._narrow(x, a, L.ROW))
-        assert [c[3] for c in calls] == [1], (K, calls)
+        assert [(c[2], c[3]) for c in calls] == [(3, 3)], (K, calls)
     # tiny reductions are not split
     calls = _run(monkeypatch, lambda: L._narrow(torch.zeros(300, 256, dtype=torch.bfloat16),
                                                 torch.zeros(64, 256, dtype=torch.bfloat16), L.ROW))
