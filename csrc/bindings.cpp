@@ -75,7 +75,6 @@ int rt_adamw_mixed(float*, const void*, long, const float*, float*, float*, void
 int rt_pool_norm(const void*, const int*, int, int, int, int, float*, hipStream_t);
 int rt_scatter_scaled(const long*, int, long, hipStream_t);
 int rt_lora_grad_accum(const long*, int, long, hipStream_t);
-int rt_f32_to_bf16_zero(float*, void*, long, hipStream_t);
 int rt_topk(const float*, long, long, int, int, const long*, long, float*, long*, hipStream_t);
 int rt_segment_mean(const float*, int, const long*, const int*, int, int, float*, hipStream_t);
 int rt_ivf_scan(const void*, int, int, const int*, int, const int*, const int*, const void*, const long*, const float*,
@@ -476,7 +475,7 @@ Tensor gemm_rope(const Tensor& a, const Tensor& w, const optional<Tensor>& u, co
 }
 
 // 64x64-tile GEMM for narrow products (LoRA U / dU / dA / dB): same operand layouts as gemm_big;
-// out_mode 0 bf16 / 1 fp32 / 2 fp32 atomic accumulate into `out` (split-K over `nsplit`).
+// out_mode 0 bf16 / 1 fp32 / 2 fp32 atomic accumulate into `out` / 3 fp32 slabs [nsplit * M, N] (split-K over `nsplit`).
 // bm: 64 (64x64 tiles) or 128 (128x64 tiles: the narrow B image staged once per 128 A rows).
 Tensor gemm_small(const Tensor& a, const Tensor& b, int64_t layout_a, int64_t layout_b, int64_t out_mode,
                   int64_t nsplit, optional<Tensor> out, int64_t bm) {
@@ -1102,9 +1101,8 @@ void grad_sumsq(const Tensor& g, Tensor partials) {
            "grad_sumsq");
 }
 
-// Batched scaled fp32 -> bf16 scatter (LoRA compute images): tab int64 [n, 7] on the device =
-// {src, src_ld, dst, dst_ld, rows, cols, fp32 scale bits}; max_elems = max rows * cols.
-// LoRA backward epilogue: scaled accumulate of the adapter-gradient workspaces into .grad, zeroing them
+// LoRA backward epilogue: tab int64 [n, 9] on the device = {src, src_ld, dst, dst_ld, rows, cols,
+// fp32 scale bits, slabs, slab stride}: dst += scale * (sum of the split-K slabs, fixed order)
 void lora_grad_accum(const Tensor& tab, int64_t max_elems) {
   CHECK_CUDA(tab);
   TORCH_CHECK(tab.scalar_type() == at::kLong && tab.is_contiguous() && tab.dim() == 2 && tab.size(1) == 9,
@@ -1113,15 +1111,8 @@ void lora_grad_accum(const Tensor& tab, int64_t max_elems) {
            "lora_grad_accum");
 }
 
-// bf16 copy of an fp32 accumulator that is zeroed in the same pass
-Tensor f32_to_bf16_zero(Tensor src) {
-  CHECK_CUDA(src); CHECK_F32(src);
-  TORCH_CHECK(src.is_contiguous(), "f32_to_bf16_zero: contiguous source");
-  auto out = at::empty(src.sizes(), src.options().dtype(at::kBFloat16));
-  check_rc(rt_f32_to_bf16_zero(src.data_ptr<float>(), out.data_ptr(), src.numel(), cur_stream()), "f32_to_bf16_zero");
-  return out;
-}
-
+// Batched scaled fp32 -> bf16 scatter (LoRA compute images): tab int64 [n, 7] on the device =
+// {src, src_ld, dst, dst_ld, rows, cols, fp32 scale bits}; max_elems = max rows * cols.
 void scatter_scaled(const Tensor& tab, int64_t max_elems) {
   CHECK_CUDA(tab);
   TORCH_CHECK(tab.scalar_type() == at::kLong && tab.dim() == 2 && tab.size(1) == 7 && tab.is_contiguous(),
@@ -1389,8 +1380,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample", &sample);
   m.def("adamw", &adamw);
   m.def("scatter_scaled", &scatter_scaled, "batched scaled fp32 -> bf16 strided scatter (LoRA images)");
-  m.def("lora_grad_accum", &lora_grad_accum, "LoRA backward: scaled accumulate of adapter-gradient workspaces into grads");
-  m.def("f32_to_bf16_zero", &f32_to_bf16_zero, "fp32 -> bf16 copy that zeroes the source");
+  m.def("lora_grad_accum", &lora_grad_accum, "LoRA backward: scaled sum of adapter-gradient slabs into grads");
   m.def("adamw_mixed", &adamw_mixed);
   m.def("grad_norm", &grad_norm);
   m.def("adamw_apply", &adamw_apply);

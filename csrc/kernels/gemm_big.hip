@@ -1127,7 +1127,8 @@ extern "C" int rt_gemm_splitk_reduce(const float* slabs, int nsplit, int M, int 
 }
 
 // 64x64-tile GEMM (narrow LoRA products). out: 0 bf16, 1 fp32 store, 2 fp32 atomic add (split-K),
-// 3 fp32 split-K slabs [nsplit][M][ldc] (ROW / ROW: the deterministic forward U product).
+// 3 fp32 split-K slabs [nsplit][M][ldc] summed in a fixed order by their consumer (the forward U,
+// the backward dU, dA and dB: bitwise-reproducible LoRA products).
 extern "C" int rt_gemm_small(int layout_a, int layout_b, const void* A, long lda, const void* B, long ldb, void* C,
                              long ldc, int M, int N, int K, int out, int nsplit, const void* zpage, int bm,
                              hipStream_t stream) {
@@ -1155,7 +1156,9 @@ extern "C" int rt_gemm_small(int layout_a, int layout_b, const void* A, long lda
     case 10: GS_LAUNCH(ROW, KMAJ, O_BF16); break;
     case 11: GS_LAUNCH(ROW, KMAJ, O_F32); break;
     case 12: GS_LAUNCH(ROW, KMAJ, O_F32_ATOMIC); break;
+    case 13: GS_LAUNCH(ROW, KMAJ, O_F32_SLAB); break;
     case 112: GS_LAUNCH(KMAJ, KMAJ, O_F32_ATOMIC); break;
+    case 113: GS_LAUNCH(KMAJ, KMAJ, O_F32_SLAB); break;
     case 111: GS_LAUNCH(KMAJ, KMAJ, O_F32); break;
     default: return -4;
   }

@@ -193,41 +193,26 @@ __global__ __launch_bounds__(256) void scatter_scaled_kernel(const long* __restr
     dst[r * dld + c] = f2bf(src[r * sld + c] * scale);
   }
 }
-// LoRA backward epilogue (ops.linear._linear_bwd): the projection's fp32 adapter-gradient
-// workspaces (dA_all [Rp, K], dB_all [N, Rp], filled by the split-K TN GEMMs with atomics) are
-// accumulated, scaled, into the parameters' .grad (views of the flat gradient buffer) and left
-// zeroed for the next backward — one launch instead of a zero fill, a scale pass and one autograd
-// accumulate-add per adapter parameter. Entry (9 int64): src, src ld, dst (0: zero only), dst ld,
-// rows, src cols, first / end source column copied to dst (dst col = src col - first), scale bits.
-// Every source element belongs to exactly one entry.
+
+// LoRA backward epilogue: per descriptor (9 int64: src, src row stride, dst, dst row stride, rows,
+// cols, fp32 scale bits, slabs, slab stride) dst[r][c] += scale * sum_s src[s][r][c], the split-K
+// slabs of dA_all / dB_all summed in a fixed order (bitwise-reproducible gradients) straight into
+// the parameters' .grad buffers. One blockIdx.y per descriptor.
 __global__ __launch_bounds__(256) void lora_grad_accum_kernel(const long* __restrict__ tab) {
   const long* t = tab + (long)blockIdx.y * 9;
-  float* src = (float*)t[0];
+  const float* src = (const float*)t[0];
   float* dst = (float*)t[2];
-  const long sld = t[1], dld = t[3], rows = t[4], cols = t[5], c0 = t[6], c1 = t[7];
-  const float scale = __int_as_float((int)t[8]);
+  const long sld = t[1], dld = t[3], rows = t[4], cols = t[5];
+  const float scale = __int_as_float((int)t[6]);
+  const int ns = (int)t[7];
+  const long sst = t[8];
   const long n = rows * cols;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
     const long r = e / cols, c = e - r * cols;
-    float* sp = src + r * sld + c;
-    const float v = *sp;
-    *sp = 0.f;
-    if (dst && c >= c0 && c < c1) dst[r * dld + (c - c0)] += scale * v;
-  }
-}
-
-// fp32 -> bf16 and zero the source (the split-K dU accumulator, kept zeroed between backwards)
-__global__ __launch_bounds__(256) void f32_to_bf16_zero_kernel(float* __restrict__ src, bf16_t* __restrict__ dst, long n) {
-  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i + 4 <= n) {
-    float4 v = *(float4*)(src + i);
-    *(float4*)(src + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-    *(uint2*)(dst + i) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
-  } else {
-    for (long j = i; j < n; ++j) {
-      dst[j] = f2bf(src[j]);
-      src[j] = 0.f;
-    }
+    const float* sp = src + r * sld + c;
+    float v = 0.f;
+    for (int k = 0; k < ns; ++k) v += sp[(long)k * sst];
+    dst[r * dld + c] += scale * v;
   }
 }
 }  // namespace rt
@@ -239,16 +224,6 @@ extern "C" int rt_lora_grad_accum(const long* tab, int n, long max_elems, hipStr
   if (bx > 256) bx = 256;
   if (bx < 1) bx = 1;
   hipLaunchKernelGGL(lora_grad_accum_kernel, dim3((unsigned)bx, (unsigned)n), dim3(256), 0, stream, tab);
-  RT_LAUNCH_CHECK();
-  return 0;
-}
-
-extern "C" int rt_f32_to_bf16_zero(float* src, void* dst, long n, hipStream_t stream) {
-  if (n <= 0) return 0;
-  if (((uintptr_t)src % 16) || ((uintptr_t)dst % 8)) return -1;
-  const long threads = (n + 3) / 4;
-  hipLaunchKernelGGL(f32_to_bf16_zero_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, src,
-                     (bf16_t*)dst, n);
   RT_LAUNCH_CHECK();
   return 0;
 }

@@ -325,23 +325,38 @@ def refresh_lora_batched(groups: List["LoRAGroup"], dtype=torch.bfloat16) -> boo
 _WS: dict = {}
 
 
-def _persistent_zeros(key, n: int, device) -> torch.Tensor:
-    """A cached fp32 buffer of >= n elements that is ALL ZERO between uses: its consumers (the
-    native f32_to_bf16_zero / lora_grad_accum epilogues) zero what they read, so the LoRA backward
-    needs no per-call zero fill. Grows (reallocated zeroed) when a larger prefix is asked for."""
+def _workspace(key, n: int, device) -> torch.Tensor:
+    """A cached fp32 buffer of >= n elements (split-K slabs of the LoRA backward products: fully
+    overwritten by every producer, consumed in stream order before the next one reuses it)."""
     k = (key, str(device))
     t = _WS.get(k)
     if t is None or t.numel() < n:
-        t = _WS[k] = torch.zeros(max(n, 1), dtype=torch.float32, device=device)
+        t = _WS[k] = torch.empty(max(n, 1), dtype=torch.float32, device=device)
     return t[:n]
 
 
-def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0, zero32=None) -> torch.Tensor:
+def _tn_slabs(a: torch.Tensor, b: torch.Tensor, key):
+    """Narrow a^T b (a [T, P], b [T, Q], min(P, Q) <= 128: the LoRA dA / dB products) as fp32
+    split-K slabs [ns, P, Q] in a cached workspace: every token split stores its partial tile with
+    plain stores and the consumer sums the ns slabs in a fixed order — bitwise reproducible, unlike
+    the fp32 atomics of gemm_tn (partials added in arrival order). Same tiles and token splits as
+    gemm_tn (profiles/r5/lora_narrow_split_sweep.log). Returns (slabs [ns * P, Q], ns)."""
+    T, P = a.shape
+    Q = b.shape[1]
+    bm = 128 if P >= 16384 else 64
+    tiles = ((P + bm - 1) // bm) * ((Q + 63) // 64)
+    ns = max(1, min(T // 256, 4 if tiles <= 64 else 8))
+    ws = _workspace(key, ns * P * Q, a.device).view(ns * P, Q)
+    native().gemm_small(a, b, KMAJ, KMAJ, 3, ns, ws, bm)
+    return ws, ns
+
+
+def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0) -> torch.Tensor:
     """a [M, K] (ROW) times a narrow operand b (ROW [R, K] or KMAJ [K, R]; R = padded LoRA rank) ->
     [M, R] bf16 on the 64x64-tile kernel (U = X A_pad^T forward, dU = dY UB backward). One
     workgroup per 64 tokens leaves most CUs idle at a few thousand tokens (151 workgroups at 9632
     tokens, each over a K of up to 28672), so the reduction is split until ~3 workgroups per CU
-    are in flight: fp32 atomic partials, rounded to bf16 once."""
+    are in flight: fp32 split-K slabs summed in a fixed order and rounded to bf16 once."""
     if not on_gpu(a):
         B = b.float().t() if lb == ROW else b.float()
         return (a.float() @ B).to(a.dtype)
@@ -357,19 +372,14 @@ def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0, zero32=N
     # atomics land in arrival order: not bitwise reproducible, nor batch-invariant — the PPO ratio
     # and reference KL need the scoring forward to be, ops.batch_invariant): K = 4096 31.3 -> 28.7
     # us, K = 14336 78.0 -> 73.8 us at 9632 tokens (profiles/r5/lora_narrow_split_sweep.log, atomic
-    # form). The backward products (dU, dA, dB) keep their atomic splits.
+    # form). The backward dU (KMAJ adapter image) splits the same way into slabs.
     auto = min(3, max(1, K // 512)) if lb == ROW else max(1, min(K // 512, (768 + tiles - 1) // tiles))
     ns = nsplit or auto
     if ns == 1:
         return native().gemm_small(a, b, ROW, lb, 0, 1, None, bm)
-    if lb == ROW and zero32 is None and R % 8 == 0:
-        slabs = native().gemm_small(a, b, ROW, ROW, 3, ns, None, bm)
+    if R % 8 == 0:
+        slabs = native().gemm_small(a, b, ROW, lb, 3, ns, None, bm)
         return native().splitk_reduce(slabs, ns, M, R, torch.empty(M, R, dtype=a.dtype, device=a.device))
-    # ``zero32``: a caller-provided zeroed fp32 [M, R] accumulator; it is consumed here (rounded to
-    # bf16 and zeroed in one pass: a persistent workspace stays zero for the next call)
-    if zero32 is not None:
-        native().gemm_small(a, b, ROW, lb, 2, ns, zero32, bm)
-        return native().f32_to_bf16_zero(zero32)
     out = torch.zeros(M, R, dtype=torch.float32, device=a.device)
     native().gemm_small(a, b, ROW, lb, 2, ns, out, bm)
     return out.to(a.dtype)
@@ -488,31 +498,27 @@ def _direct_grads_ok(lora: "LoRAGroup") -> bool:
     return True
 
 
-def _grad_table(lora: "LoRAGroup", ga: torch.Tensor, gb: torch.Tensor):
-    """Device descriptor table of lora_grad_accum for this group's workspaces and .grad buffers
-    (cached per address set): dA rows of each adapter (scaled) -> a.grad, each adapter's rows of
-    dB_all (its own rank columns) -> b.grad, other dB_all rows zeroed only."""
+def _grad_table(lora: "LoRAGroup", ga: torch.Tensor, nsa: int, gb: torch.Tensor, nsb: int):
+    """Device descriptor table of lora_grad_accum for this group's slab workspaces and .grad
+    buffers (cached per address set): each adapter's dA rows (scaled, summed over the nsa slabs of
+    dA_all [Rp, K]) -> a.grad and its dB block (its own output rows and rank columns of the nsb slabs
+    of dB_all [N, Rp]) -> b.grad. Entry: src, src row stride, dst, dst row stride, rows, cols,
+    scale bits, slabs, slab stride (elements)."""
     import struct
 
-    key = (ga.data_ptr(), gb.data_ptr(), tuple(p.grad.data_ptr() for p in lora.a + lora.b), tuple(lora.scale))
+    Rp, K = lora.a_pad.shape
+    N = lora.ub.shape[0]
+    key = (ga.data_ptr(), nsa, gb.data_ptr(), nsb, tuple(p.grad.data_ptr() for p in lora.a + lora.b),
+           tuple(lora.scale))
     ent = getattr(lora, "_grad_tab", None)
     if ent is not None and ent[0] == key:
         return ent[1], ent[2]
-    Rp, K = ga.shape
-    N = gb.shape[0]
-    rows, cov = [], []
+    rows = []
     f = lambda x: struct.unpack("<i", struct.pack("<f", float(x)))[0]  # noqa: E731
     for a, b, r0, c0, sc in zip(lora.a, lora.b, lora.r0, lora.col0, lora.scale):
         ri, ni = a.shape[0], b.shape[0]
-        rows.append((ga.data_ptr() + 4 * r0 * K, K, a.grad.data_ptr(), K, ri, K, 0, K, f(sc)))
-        rows.append((gb.data_ptr() + 4 * c0 * Rp, Rp, b.grad.data_ptr(), ri, ni, Rp, r0, r0 + ri, f(1.0)))
-        cov.append((c0, c0 + ni))
-    cov.sort()
-    r = 0
-    for lo, hi in cov + [(N, N)]:  # dB_all rows no adapter owns: zero them
-        if lo > r:
-            rows.append((gb.data_ptr() + 4 * r * Rp, Rp, 0, 0, lo - r, Rp, 0, 0, f(1.0)))
-        r = max(r, hi)
+        rows.append((ga.data_ptr() + 4 * r0 * K, K, a.grad.data_ptr(), K, ri, K, f(sc), nsa, Rp * K))
+        rows.append((gb.data_ptr() + 4 * (c0 * Rp + r0), Rp, b.grad.data_ptr(), ri, ni, ri, f(1.0), nsb, N * Rp))
     tab = torch.tensor(rows, dtype=torch.int64).to(ga.device)
     mx = max(rw[4] * rw[5] for rw in rows)
     lora._grad_tab = (key, tab, mx)
@@ -528,20 +534,9 @@ def _linear_bwd(dy, x2, w, u, lora, mask, need_x: bool, need_w: bool, dx_act: in
     epilogue and returned as None."""
     dx = dw = None
     gpu = on_gpu(dy)
-    ws = None
     direct = gpu and lora is not None and _direct_grads_ok(lora)
-    if lora is not None and gpu:
-        # fp32 accumulators of the adapter products: dU [M, Rp] (split-K over N) always from a
-        # persistent zeroed workspace (rounded to bf16 and re-zeroed in one pass); dA_all [Rp, K] /
-        # dB_all [N, Rp] from another one in the direct mode (consumed by lora_grad_accum), else
-        # from one fresh zero fill (their slices are handed to autograd)
-        Mr, Kr, Nr, Rp = dy.shape[0], x2.shape[1], dy.shape[1], lora.ub.shape[1]
-        du32 = _persistent_zeros("lora_du", Mr * Rp, dy.device).view(Mr, Rp)
-        ws = _persistent_zeros(("lora_gab", Rp, Kr, Nr), Rp * Kr + Nr * Rp, dy.device) if direct else \
-            torch.zeros(Rp * Kr + Nr * Rp, dtype=torch.float32, device=dy.device)
-        ga_out = ws[:Rp * Kr].view(Rp, Kr)
-        gb_out = ws[Rp * Kr:].view(Nr, Rp)
-    du = _narrow(dy, lora.ub, KMAJ, zero32=du32 if ws is not None else None) if lora is not None else None
+    # dU = dY UB [M, Rp]: split over N into fp32 slabs, summed in a fixed order and rounded once
+    du = _narrow(dy, lora.ub, KMAJ) if lora is not None else None
     if need_x:
         if dx_act == ACT_DSWIGLU:
             assert mask is None
@@ -564,10 +559,19 @@ def _linear_bwd(dy, x2, w, u, lora, mask, need_x: bool, need_w: bool, dx_act: in
         # accumulate): dA_all = dU^T drop(X) [Rp, K]; dB_all = dY^T U [N, Rp] (adapter i uses
         # its diagonal block)
         xd = x2 * mask if mask is not None else x2
-        ga_all = gemm_tn(du, xd, out=ga_out, zeroed=True) if ws is not None else gemm_tn(du, xd)
-        gb_all = gemm_tn(dy, u, out=gb_out, zeroed=True) if ws is not None else gemm_tn(dy, u)
+        Rp, Kr, Nr = lora.ub.shape[1], x2.shape[1], dy.shape[1]
+        if gpu and Rp <= 128:
+            # token-split fp32 slabs (bitwise reproducible): summed by lora_grad_accum straight into
+            # .grad (direct), else by one torch reduction each
+            ga_s, nsa = _tn_slabs(du, xd, ("lora_ga", Rp, Kr))
+            gb_s, nsb = _tn_slabs(dy, u, ("lora_gb", Nr, Rp))
+            if not direct:
+                ga_all, gb_all = ga_s.view(nsa, Rp, Kr).sum(0), gb_s.view(nsb, Nr, Rp).sum(0)
+        else:
+            ga_s, nsa, gb_s, nsb = gemm_tn(du, xd), 1, gemm_tn(dy, u), 1
+            ga_all, gb_all = ga_s, gb_s
         if direct:
-            tab, mx = _grad_table(lora, ga_all, gb_all)
+            tab, mx = _grad_table(lora, ga_s, nsa, gb_s, nsb)
             native().lora_grad_accum(tab, mx)
             # None to autograd: the parameters' AccumulateGrad nodes still run (with no gradient)
             # and fire their post-accumulate hooks after this backward returns, i.e. behind the

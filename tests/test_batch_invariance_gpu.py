@@ -99,7 +99,7 @@ def test_score_sequences_bitwise_across_batches(B, S, T):
                 assert torch.equal(a[idx] * mask[idx], b * mask[idx]), (size, rows)
 
 
-def _ppo(old_logp, kl_in_loss=True, lora_std=0.0):
+def _ppo(old_logp, kl_in_loss=True, lora_std=0.0, trainer=False):
     from rag_tl_domainllm_optimizer_amd.data import RecordLoader, SyntheticCorpus
     from rag_tl_domainllm_optimizer_amd.retrieval import Encoder
     from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
@@ -124,7 +124,8 @@ def _ppo(old_logp, kl_in_loss=True, lora_std=0.0):
                 p.normal_(0, lora_std)
         policy.refresh_lora()
     batch = next(iter(RecordLoader(recs, batch_size=16, seed=0)))
-    return [tr.step(batch) for _ in range(2)]
+    ms = [tr.step(batch) for _ in range(2)]
+    return (ms, tr) if trainer else ms
 
 
 def test_ppo_recompute_ratio_exactly_one():
@@ -145,3 +146,25 @@ def test_ppo_kl_in_loss_zero_at_init():
     assert ms[0]["kl_ref_theta_old"] == 0.0
     assert ms[0]["kl_ref_k3"] >= 0.0
     assert ms[1]["kl_ref_theta_old"] != 0.0
+
+
+def test_ppo_steps_bitwise_reproducible():
+    """Two PPO steps (rollout, reference / reward, GAE, minibatch updates with AdamW) from the same
+    seeds end in bitwise-identical adapters, value head and metrics: every reduction on the path is
+    fixed-order — split-K slabs instead of fp32 atomics in the LoRA forward / backward products (the
+    arrival order of atomic partials changed the gradient bits run to run)."""
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        ms, tr = _ppo("rollout", lora_std=0.02, trainer=True)
+        params = [p.detach().clone() for p in tr.policy.lora_parameters()]
+        params += [p.detach().clone() for p in tr.value_head.parameters()]
+        runs.append((ms, params))
+    (m0, p0), (m1, p1) = runs
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
+    for s0, s1 in zip(m0, m1):
+        for k, v in s0.items():
+            if "time" in k or "per_s" in k or k.endswith("_s") or not isinstance(v, (int, float)):
+                continue
+            assert v == s1[k] or (v != v and s1[k] != s1[k]), (k, v, s1[k])

@@ -45,6 +45,25 @@ def test_forward_u_splits_into_slabs(monkeypatch):
     calls = _run(monkeypatch, lambda: L._narrow(torch.zeros(300, 256, dtype=torch.bfloat16),
                                                 torch.zeros(64, 256, dtype=torch.bfloat16), L.ROW))
     assert [c[3] for c in calls] == [1]
+    # the backward dU = dY UB (KMAJ adapter image [N, Rp]): slabs too, ~3 workgroups per CU
+    calls = _run(monkeypatch, lambda: L._narrow(torch.zeros(9632, 28672, dtype=torch.bfloat16),
+                                                torch.zeros(28672, 64, dtype=torch.bfloat16), L.KMAJ))
+    assert calls == [(L.ROW, L.KMAJ, 3, 11, 128)], calls
+
+
+def test_backward_tn_products_into_slabs(monkeypatch):
+    """dA_all = dU^T X and dB_all = dY^T U of the LoRA backward: token-split fp32 slabs (out mode 3,
+    KMAJ x KMAJ) in a cached workspace, same tiles / splits as the atomic gemm_tn form."""
+    T = 9632
+    du = torch.zeros(T, 64, dtype=torch.bfloat16)
+    for a, b, ns, bm in ((du, torch.zeros(T, 4096, dtype=torch.bfloat16), 4, 64),
+                         (torch.zeros(T, 28672, dtype=torch.bfloat16), du, 8, 128)):
+        out = []
+        calls = _run(monkeypatch, lambda: out.append(L._tn_slabs(a, b, ("t", a.shape[1], b.shape[1]))))
+        assert calls == [(L.KMAJ, L.KMAJ, 3, ns, bm)], calls
+        ws, n = out[0]
+        assert n == ns and ws.shape == (ns * a.shape[1], b.shape[1])
+    L._WS.clear()
 
 
 def test_adapter_gradient_token_splits(monkeypatch):
