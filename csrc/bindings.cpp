@@ -42,6 +42,7 @@ int rt_norm_fwd(int, const void*, const void*, const void*, const void*, void*, 
                 const float*, int, hipStream_t);
 int rt_norm_bwd(int, const void*, const void*, const void*, const float*, const float*, const void*, void*, float*,
                 float*, int, int, hipStream_t);
+int rt_norm_bwd_blocks(int);
 int rt_rope_qkv(void*, long, const int*, const float*, const float*, int, int, int, int, int, float, void*, void*,
                 const int*, int, int, hipStream_t);
 int rt_swiglu_fwd(const void*, void*, long, int, hipStream_t);
@@ -734,8 +735,11 @@ std::vector<Tensor> norm_bwd(bool layernorm, const Tensor& dy, const Tensor& h, 
   TORCH_CHECK(dy.is_contiguous() && h.is_contiguous(), "norm_bwd: contiguous inputs required");
   const int64_t H = dy.size(-1), T = dy.numel() / H;
   auto dh = at::empty_like(dy);
-  Tensor dw = need_dw ? at::zeros({H}, dy.options().dtype(at::kFloat)) : Tensor();
-  Tensor db = need_db ? at::zeros({H}, dy.options().dtype(at::kFloat)) : Tensor();
+  // dw / db: one fp32 partial row per workgroup (plain stores), summed in a fixed order below — no
+  // arrival-order atomics (bitwise-reproducible full fine-tuning)
+  const int64_t nb = rt_norm_bwd_blocks((int)T);
+  Tensor dw = need_dw ? at::empty({nb, H}, dy.options().dtype(at::kFloat)) : Tensor();
+  Tensor db = need_db ? at::empty({nb, H}, dy.options().dtype(at::kFloat)) : Tensor();
   if (dh_res.has_value() && dh_res->defined()) {
     CHECK_BF16(*dh_res);
     TORCH_CHECK(dh_res->is_contiguous(), "norm_bwd: dh_res contiguous");
@@ -745,7 +749,7 @@ std::vector<Tensor> norm_bwd(bool layernorm, const Tensor& dy, const Tensor& h, 
                        need_dw ? dw.data_ptr<float>() : nullptr, need_db ? db.data_ptr<float>() : nullptr, (int)T,
                        (int)H, cur_stream()),
            "norm_bwd");
-  return {dh, dw, db};
+  return {dh, need_dw ? dw.sum(0) : dw, need_db ? db.sum(0) : db};
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1198,13 +1202,14 @@ std::vector<Tensor> ivf_scan(const Tensor& q, const Tensor& probes, const Tensor
   return {cand, cid};
 }
 
-Tensor segment_mean(const Tensor& x, const Tensor& order, const Tensor& seg, bool normalize, Tensor out) {
+// mode bit 0: L2-normalise each segment mean; bit 1: segment sums instead of means
+Tensor segment_mean(const Tensor& x, const Tensor& order, const Tensor& seg, int64_t mode, Tensor out) {
   CHECK_CUDA(x); CHECK_F32(x); CHECK_I64(order); CHECK_I32(seg); CHECK_F32(out);
   TORCH_CHECK(x.is_contiguous() && order.is_contiguous() && seg.is_contiguous() && out.is_contiguous());
   const int64_t k = seg.numel() - 1, d = x.size(1);
   TORCH_CHECK(out.size(0) == k && out.size(1) == d, "segment_mean: out shape");
   check_rc(rt_segment_mean(x.data_ptr<float>(), (int)d, (const long*)order.data_ptr(), seg.data_ptr<int>(), (int)k,
-                           normalize ? 1 : 0, out.data_ptr<float>(), cur_stream()),
+                           (int)mode, out.data_ptr<float>(), cur_stream()),
            "segment_mean");
   return out;
 }

@@ -103,7 +103,8 @@ __global__ __launch_bounds__(MAXT) void norm_fwd_kernel(const bf16_t* __restrict
 }
 
 // Backward. Each workgroup walks `rows_per_block` rows, accumulating dw (and db) in registers,
-// then adds its partial into fp32 dw/db with one atomic per element per workgroup.
+// then stores its partial as row blockIdx.x of the fp32 dw / db slabs [gridDim.x, H] (the caller
+// sums the rows in a fixed order: no arrival-order atomics).
 //   xhat = (h - mean) * rstd ; y = xhat*w (+b)
 //   g = dy*w ; dh = rstd * (g - mean(g) [LN only] - xhat * mean(g*xhat))  (+ dh_res)
 template <bool LAYERNORM, int NV>
@@ -165,15 +166,15 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const bf16_t* __restrict_
       }
     }
   }
-  if (dw) {
+  if (dw || db) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = threadIdx.x + i * blockDim.x;
       if (c < nv)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          atomicAdd(dw + c * 8 + k, dwacc[i][k]);
-          if (LAYERNORM && db) atomicAdd(db + c * 8 + k, dbacc[i][k]);
+          if (dw) dw[(long)blockIdx.x * H + c * 8 + k] = dwacc[i][k];
+          if (LAYERNORM && db) db[(long)blockIdx.x * H + c * 8 + k] = dbacc[i][k];
         }
     }
   }
@@ -240,6 +241,15 @@ extern "C" int rt_norm_fwd(int layernorm, const void* x, const void* res, const 
   return 0;
 }
 
+// workgroups of rt_norm_bwd for T rows (= the rows of its dw / db partial slabs)
+extern "C" int rt_norm_bwd_blocks(int T) {
+  if (T <= 0) return 0;
+  const int nblk = T < 1024 ? T : 1024;
+  const int rpb = (T + nblk - 1) / nblk;
+  return (T + rpb - 1) / rpb;
+}
+
+// dw / db (optional): fp32 [rt_norm_bwd_blocks(T), H] partial slabs, every row written
 extern "C" int rt_norm_bwd(int layernorm, const void* dy, const void* h, const void* w, const float* rstd,
                            const float* mean, const void* dh_res, void* dh, float* dw, float* db, int T, int H,
                            hipStream_t stream) {
@@ -249,7 +259,7 @@ extern "C" int rt_norm_bwd(int layernorm, const void* dy, const void* h, const v
   norm_geom(H, threads, nvpt);
   const int nblk = T < 1024 ? T : 1024;
   const int rpb = (T + nblk - 1) / nblk;
-  const int grid = (T + rpb - 1) / rpb;
+  const int grid = rt_norm_bwd_blocks(T);
   if (layernorm) {
     NORM_DISPATCH(true, norm_bwd_kernel, dim3(grid), dim3(threads), 0, stream, (const bf16_t*)dy, (const bf16_t*)h,
                   (const bf16_t*)w, rstd, mean, (const bf16_t*)dh_res, (bf16_t*)dh, dw, db, T, H, rpb)

@@ -162,16 +162,18 @@ __global__ __launch_bounds__(256) void ivf_scan_kernel(const bf16_t* __restrict_
 // k-means update: centroid c = mean of the rows order[seg[c] .. seg[c+1]) of x (rows sorted by
 // assigned centroid), L2-normalised for the inner-product metric. One workgroup per centroid, a
 // column per thread, rows summed in a fixed order (deterministic, no atomics). Empty clusters are
-// left untouched (the caller reseeds them).
+// left untouched (the caller reseeds them). mode bit 0: L2-normalise; bit 1: the plain segment sum
+// (the deterministic embedding-table gradient, ops.misc._EmbedFn).
 __global__ __launch_bounds__(256) void segment_mean_kernel(const float* __restrict__ x, int d,
                                                            const long* __restrict__ order, const int* __restrict__ seg,
-                                                           int normalize, float* __restrict__ out) {
+                                                           int mode, float* __restrict__ out) {
   extern __shared__ float col[];  // [d]
   __shared__ float sb[4];
   const int c = blockIdx.x;
   const int r0 = seg[c], r1 = seg[c + 1];
   if (r1 <= r0) return;  // uniform over the block
-  const float inv = 1.f / (float)(r1 - r0);
+  const bool normalize = mode & 1;
+  const float inv = (mode & 2) ? 1.f : 1.f / (float)(r1 - r0);  // bit 1: plain sum
   float ss = 0.f;
   for (int j = threadIdx.x; j < d; j += 256) {
     float a = 0.f;
@@ -219,11 +221,10 @@ extern "C" int rt_ivf_scan(const void* q, int nq, int d, const int* probes, int 
   return 0;
 }
 
-extern "C" int rt_segment_mean(const float* x, int d, const long* order, const int* seg, int k, int normalize,
+extern "C" int rt_segment_mean(const float* x, int d, const long* order, const int* seg, int k, int mode,
                                float* out, hipStream_t stream) {
   if (k == 0) return 0;
-  hipLaunchKernelGGL(segment_mean_kernel, dim3(k), dim3(256), d * sizeof(float), stream, x, d, order, seg, normalize,
-                     out);
+  hipLaunchKernelGGL(segment_mean_kernel, dim3(k), dim3(256), d * sizeof(float), stream, x, d, order, seg, mode, out);
   RT_LAUNCH_CHECK();
   return 0;
 }

@@ -55,9 +55,20 @@ class _EmbedFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        """Table gradient without arrival-order atomics: the rows are sorted by id (stable) and each
+        distinct id's rows summed in that fixed order (segment_mean kernel, sum mode), then added
+        once per distinct id — bitwise reproducible (full fine-tuning trains the table)."""
         (ids,) = ctx.saved_tensors
         d = torch.zeros(ctx.shape, dtype=torch.float32, device=g.device)
-        d.index_add_(0, ids.reshape(-1), g.reshape(-1, ctx.shape[1]).float())
+        flat = ids.reshape(-1)
+        g2 = g.reshape(-1, ctx.shape[1]).float().contiguous()
+        order = torch.argsort(flat, stable=True)
+        uniq, counts = torch.unique_consecutive(flat[order], return_counts=True)
+        seg = torch.zeros(uniq.numel() + 1, dtype=torch.int32, device=g.device)
+        seg[1:] = counts.cumsum(0)
+        sums = torch.empty(uniq.numel(), ctx.shape[1], dtype=torch.float32, device=g.device)
+        native().segment_mean(g2, order, seg, 2, sums)
+        d.index_add_(0, uniq, sums)  # distinct rows: one add per element
         return d.to(g.dtype), None
 
 
@@ -164,7 +175,7 @@ def segment_mean(x, order, seg, normalize: bool, out):
     """out[c] = mean(x[order[seg[c]:seg[c+1]]]) (L2-normalised if asked); empty segments untouched."""
     if on_gpu(x):
         return native().segment_mean(x.float().contiguous(), order.long().contiguous(), seg.int().contiguous(),
-                                     normalize, out)
+                                     int(bool(normalize)), out)
     return ref.segment_mean(x, order, seg, normalize, out)
 
 

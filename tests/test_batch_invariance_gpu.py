@@ -99,7 +99,7 @@ def test_score_sequences_bitwise_across_batches(B, S, T):
                 assert torch.equal(a[idx] * mask[idx], b * mask[idx]), (size, rows)
 
 
-def _ppo(old_logp, kl_in_loss=True, lora_std=0.0, trainer=False):
+def _ppo(old_logp, kl_in_loss=True, lora_std=0.0, trainer=False, full=False):
     from rag_tl_domainllm_optimizer_amd.data import RecordLoader, SyntheticCorpus
     from rag_tl_domainllm_optimizer_amd.retrieval import Encoder
     from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
@@ -117,7 +117,8 @@ def _ppo(old_logp, kl_in_loss=True, lora_std=0.0, trainer=False):
             for it in corpus.sample_queries(16)]
     tr = PPOTrainer(policy, tok, RewardModel(enc),
                     PPOConfig(max_new_tokens=12, max_prompt_tokens=64, minibatch_size=4, ref_minibatch_size=16,
-                              lr=1e-3, old_logp=old_logp, kl_in_loss=kl_in_loss, lora_r=8), max_batch=16)
+                              lr=1e-3, old_logp=old_logp, kl_in_loss=kl_in_loss, lora_r=8, full_finetune=full),
+                    max_batch=16)
     if lora_std:
         with torch.no_grad():
             for p in policy.lora_parameters():
@@ -148,16 +149,20 @@ def test_ppo_kl_in_loss_zero_at_init():
     assert ms[1]["kl_ref_theta_old"] != 0.0
 
 
-def test_ppo_steps_bitwise_reproducible():
+@pytest.mark.parametrize("full", [False, True])
+def test_ppo_steps_bitwise_reproducible(full):
     """Two PPO steps (rollout, reference / reward, GAE, minibatch updates with AdamW) from the same
-    seeds end in bitwise-identical adapters, value head and metrics: every reduction on the path is
-    fixed-order — split-K slabs instead of fp32 atomics in the LoRA forward / backward products (the
-    arrival order of atomic partials changed the gradient bits run to run)."""
+    seeds end in bitwise-identical trainable weights, value head and metrics: every reduction on the
+    path is fixed-order — split-K slabs instead of fp32 atomics in the LoRA forward / backward
+    products (the arrival order of atomic partials changed the gradient bits run to run); under
+    full fine-tuning also the RMSNorm weight and embedding-table gradients."""
     runs = []
     for _ in range(2):
         torch.manual_seed(0)
-        ms, tr = _ppo("rollout", lora_std=0.02, trainer=True)
-        params = [p.detach().clone() for p in tr.policy.lora_parameters()]
+        ms, tr = _ppo("rollout", lora_std=0.0 if full else 0.02, trainer=True, full=full)
+        train = [p for p in tr.policy.parameters() if p.requires_grad] if full else list(tr.policy.lora_parameters())
+        assert train
+        params = [p.detach().clone() for p in train]
         params += [p.detach().clone() for p in tr.value_head.parameters()]
         runs.append((ms, params))
     (m0, p0), (m1, p1) = runs

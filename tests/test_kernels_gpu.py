@@ -369,6 +369,57 @@ def test_embed():
     _close(out, (table[ids].float() + ptable[pids].float()), rtol=1e-2, atol=1e-2)
 
 
+def test_embed_grad_fixed_order():
+    """Trainable table (full fine-tuning): the gradient is the per-id sum of the output gradient rows
+    (fp32 oracle: index_add), summed in a fixed order — two backwards give the same bits."""
+    torch.manual_seed(2)
+    V, H = 500, 384
+    ids = torch.randint(0, V, (7, 300), device=DEV)
+    ids[:, :50] = 3  # a heavily repeated id
+    g = torch.randn(7, 300, H, device=DEV).to(torch.bfloat16)
+    grads = []
+    for _ in range(2):
+        table = torch.randn(V, H, device=DEV, generator=torch.Generator(device=DEV).manual_seed(0)).to(
+            torch.bfloat16).requires_grad_(True)
+        out = ops.embedding(table, ids)
+        (out.float() * g.float()).sum().backward()
+        grads.append(table.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    expect = torch.zeros(V, H, device=DEV).index_add_(0, ids.reshape(-1), g.reshape(-1, H).float())
+    _close(grads[0], expect, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("layernorm", [False, True])
+def test_norm_weight_grad_fixed_order(layernorm):
+    """RMSNorm / LayerNorm weight (and bias) gradients over many rows per workgroup: per-workgroup
+    partial rows summed in a fixed order — equal to the fp32 oracle and bitwise repeatable."""
+    torch.manual_seed(3)
+    T, H = 5000, 4096
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16) if layernorm else None
+    gy = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    runs = []
+    for _ in range(2):
+        wg = w.clone().requires_grad_(True)
+        bg = b.clone().requires_grad_(True) if layernorm else None
+        y, _ = ops.layer_norm(x, wg, bg, 1e-5) if layernorm else ops.rms_norm(x, wg, 1e-5)
+        (y.float() * gy.float()).sum().backward()
+        runs.append((wg.grad.clone(), bg.grad.clone() if layernorm else None))
+    assert torch.equal(runs[0][0], runs[1][0])
+    if layernorm:
+        assert torch.equal(runs[0][1], runs[1][1])
+    wf = w.float().requires_grad_(True)
+    bf = b.float().requires_grad_(True) if layernorm else None
+    xf = x.float()
+    yf = torch.nn.functional.layer_norm(xf, (H,), wf, bf, 1e-5) if layernorm else \
+        xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    (yf * gy.float()).sum().backward()
+    _close(runs[0][0], wf.grad, rtol=3e-2, atol=0.5)
+    if layernorm:
+        _close(runs[0][1], bf.grad, rtol=3e-2, atol=0.5)
+
+
 def _qkv(B, S, Hq, Hkv, D):
     return torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
 
