@@ -99,7 +99,7 @@ def test_score_sequences_bitwise_across_batches(B, S, T):
                 assert torch.equal(a[idx] * mask[idx], b * mask[idx]), (size, rows)
 
 
-def _ppo(old_logp, kl_in_loss=True, lora_std=0.0, trainer=False, full=False):
+def _ppo_trainer(old_logp, kl_in_loss=True, lora_std=0.0, full=False):
     from rag_tl_domainllm_optimizer_amd.data import RecordLoader, SyntheticCorpus
     from rag_tl_domainllm_optimizer_amd.retrieval import Encoder
     from rag_tl_domainllm_optimizer_amd.rewards import RewardModel
@@ -124,9 +124,18 @@ def _ppo(old_logp, kl_in_loss=True, lora_std=0.0, trainer=False, full=False):
             for p in policy.lora_parameters():
                 p.normal_(0, lora_std)
         policy.refresh_lora()
-    batch = next(iter(RecordLoader(recs, batch_size=16, seed=0)))
+    return tr, next(iter(RecordLoader(recs, batch_size=16, seed=0)))
+
+
+def _ppo(old_logp, kl_in_loss=True, lora_std=0.0, trainer=False, full=False):
+    tr, batch = _ppo_trainer(old_logp, kl_in_loss, lora_std, full)
     ms = [tr.step(batch) for _ in range(2)]
     return (ms, tr) if trainer else ms
+
+
+def _trainable(tr, full):
+    ps = [p for p in tr.policy.parameters() if p.requires_grad] if full else list(tr.policy.lora_parameters())
+    return [p.detach().clone() for p in ps] + [p.detach().clone() for p in tr.value_head.parameters()]
 
 
 def test_ppo_recompute_ratio_exactly_one():
@@ -160,11 +169,7 @@ def test_ppo_steps_bitwise_reproducible(full):
     for _ in range(2):
         torch.manual_seed(0)
         ms, tr = _ppo("rollout", lora_std=0.0 if full else 0.02, trainer=True, full=full)
-        train = [p for p in tr.policy.parameters() if p.requires_grad] if full else list(tr.policy.lora_parameters())
-        assert train
-        params = [p.detach().clone() for p in train]
-        params += [p.detach().clone() for p in tr.value_head.parameters()]
-        runs.append((ms, params))
+        runs.append((ms, _trainable(tr, full)))
     (m0, p0), (m1, p1) = runs
     for a, b in zip(p0, p1):
         assert torch.equal(a, b)
@@ -173,3 +178,30 @@ def test_ppo_steps_bitwise_reproducible(full):
             if "time" in k or "per_s" in k or k.endswith("_s") or not isinstance(v, (int, float)):
                 continue
             assert v == s1[k] or (v != v and s1[k] != s1[k]), (k, v, s1[k])
+
+
+@pytest.mark.parametrize("full", [False, True])
+def test_ppo_resume_bitwise(tmp_path, full):
+    """Checkpoint after one PPO step, resume in a fresh trainer, take the next step: the weights,
+    value head, optimizer-driven update and metrics are bitwise those of the uninterrupted run (the
+    checkpoint carries everything the step depends on: adapters / weights, AdamW state, step
+    counter, sampler RNG position)."""
+    prefix = str(tmp_path / "ck" / "s1")
+    torch.manual_seed(0)
+    tr, batch = _ppo_trainer("rollout", lora_std=0.0 if full else 0.02, full=full)
+    tr.step(batch)
+    tr.save_checkpoint(prefix, full_policy=full)
+    m_a = tr.step(batch)
+    p_a = _trainable(tr, full)
+    torch.manual_seed(0)
+    tr2, batch2 = _ppo_trainer("rollout", lora_std=0.0 if full else 0.02, full=full)
+    tr2.load_checkpoint(prefix)
+    m_b = tr2.step(batch2)
+    p_b = _trainable(tr2, full)
+    assert len(p_a) == len(p_b)
+    for a, b in zip(p_a, p_b):
+        assert torch.equal(a, b)
+    for k, v in m_a.items():
+        if "time" in k or "per_s" in k or k.endswith("_s") or not isinstance(v, (int, float)):
+            continue
+        assert v == m_b[k] or (v != v and m_b[k] != m_b[k]), (k, v, m_b[k])
