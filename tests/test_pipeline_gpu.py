@@ -58,6 +58,42 @@ def test_raft_sft_lora_gpu(tmp_path):
     assert (a - b).abs().max().item() < 0.1 * a.abs().max().item() + 0.05
 
 
+@pytest.mark.parametrize("full", [False, True])
+def test_sft_resume_bitwise(tmp_path, full):
+    """RAFT SFT: checkpoint after two steps, resume in a fresh trainer, take two more — the trainable
+    weights and losses equal the uninterrupted run bit for bit (fixed-order reductions everywhere:
+    LoRA slab products, norm weight / embedding gradients; AdamW moments and step counters restored)."""
+    from rag_tl_domainllm_optimizer_amd.train import SFTConfig, SFTTrainer, build_raft_examples
+
+    def make():
+        pol, tok, enc, corpus = _tiny_stack()
+        items = corpus.sample_queries(16, seed=5)
+        recs = [{"query": i.query, "ground_truth": i.ground_truth, "gold_doc": i.gold_doc} for i in items]
+        ex = build_raft_examples(recs, corpus.docs)
+        tr = SFTTrainer(pol, tok, SFTConfig(batch_size=8, lr=1e-3, lora_r=8, warmup_steps=0, lr_schedule="constant",
+                                            max_seq=192, full_finetune=full))
+        return tr, ex
+
+    def trainable(tr):
+        return [p.detach().clone() for p in tr.model.parameters() if p.requires_grad]
+
+    torch.manual_seed(0)
+    tr, ex = make()
+    for i in range(2):
+        tr.step(ex[8 * i:8 * i + 8])
+    prefix = str(tmp_path / "sft_ck")
+    tr.save(prefix, full_policy=full)
+    la = [tr.step(ex[8 * i:8 * i + 8])["loss"] for i in (0, 1)]
+    pa = trainable(tr)
+    torch.manual_seed(0)
+    tr2, ex2 = make()
+    tr2.load_checkpoint(prefix)
+    lb = [tr2.step(ex2[8 * i:8 * i + 8])["loss"] for i in (0, 1)]
+    pb = trainable(tr2)
+    assert la == lb, (la, lb)
+    assert len(pa) == len(pb) and all(torch.equal(a, b) for a, b in zip(pa, pb))
+
+
 def test_rag_pipeline_gpu():
     from rag_tl_domainllm_optimizer_amd.generation import SamplingParams
     from rag_tl_domainllm_optimizer_amd.rag import RagPipeline
