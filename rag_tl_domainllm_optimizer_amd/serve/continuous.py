@@ -35,6 +35,7 @@ class ContinuousEngine:
         self._dead: Optional[BaseException] = None  # the error that ended the worker, if any
         self._lock = threading.Lock()  # submit's closed-check + put vs the worker's final drain
         self.stats = {"admitted": 0, "finished": 0, "steps": 0, "max_active": 0}
+        self._row_steps = 0  # sum over decode steps of the active rows (an answer's mean batch)
         self._ready = threading.Event()
         self._init_error = None
         self._worker = threading.Thread(target=self._loop, name="rag-continuous", daemon=True)
@@ -104,7 +105,8 @@ class ContinuousEngine:
                 continue
             prompts.append(prompt)
             metas.append({"query": it[0], "fut": it[2], "t_submit": it[3], "t_admit": time.perf_counter(),
-                          "retrieve_s": t1 - t0, "doc_ids": row_ids, "docs": docs, "scores": row_sc})
+                          "retrieve_s": t1 - t0, "doc_ids": row_ids, "docs": docs, "scores": row_sc,
+                          "rows0": (self._row_steps, self.stats["steps"])})
         if not prompts:
             return
         try:
@@ -123,9 +125,12 @@ class ContinuousEngine:
             if m["fut"].done():  # failed or cancelled elsewhere: nothing to deliver
                 continue
             text = extract_answer(p.tok.decode(r.tokens))
+            rs0, st0 = m["rows0"]
+            steps = self.stats["steps"] - st0
             tim = {"queue_s": m["t_admit"] - m["t_submit"], "retrieve_s": m["retrieve_s"],
                    "total_s": now - m["t_submit"], "new_tokens": len(r.tokens), "prompt_tokens": r.prompt_len,
-                   "decode_steps": r.steps_waited}
+                   "decode_steps": r.steps_waited,
+                   "batch_size": (self._row_steps - rs0) / steps if steps > 0 else 0.0}
             m["fut"].set_result(RagAnswer(m["query"], text, m["doc_ids"], m["docs"], m["scores"], tim))
             self.stats["finished"] += 1
 
@@ -161,6 +166,7 @@ class ContinuousEngine:
                             break
                         continue
                     self.stats["max_active"] = max(self.stats["max_active"], cb.active_rows())
+                    self._row_steps += cb.active_rows() * self.chunk
                     cb.step(self.chunk)
                     self.stats["steps"] += self.chunk
                     self._finish(cb.collect())

@@ -162,6 +162,8 @@ def test_continuous_engine_answers_like_direct_pipeline():
     assert [a.answer for a in got] == [a.answer for a in direct]
     assert [a.doc_ids for a in got] == [a.doc_ids for a in direct]
     assert all(a.timings["new_tokens"] == 5 and a.timings["queue_s"] >= 0 for a in got)
+    # mean decode batch over each answer's lifetime: between 1 and the 2 serving rows
+    assert all(1.0 <= a.timings["batch_size"] <= 2.0 for a in got), [a.timings["batch_size"] for a in got]
 
 
 def test_continuous_admit_many_batches_consecutive_rows():
