@@ -118,6 +118,7 @@ static const TuningField kTuningFields[] = {
     {"decode_depth", &rt::Tuning::decode_depth, nullptr},
     {"m64_split", &rt::Tuning::m64_split, nullptr},
     {"wide_split", &rt::Tuning::wide_split, nullptr},
+    {"m64_wide", &rt::Tuning::m64_wide, nullptr},
     {"gemm_bn128_cost", nullptr, &rt::Tuning::gemm_bn128_cost},
     {"gemm_group_m", &rt::Tuning::gemm_group_m, nullptr},
     {"sample_window", &rt::Tuning::sample_window, nullptr},

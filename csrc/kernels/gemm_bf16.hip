@@ -792,10 +792,19 @@ __global__ __launch_bounds__(256, 2) void gemm_m64_kernel(GemmArgs p, float* __r
 constexpr int WD_SLOTS = 5;             // 4 K-steps (96 KiB) in flight per workgroup, one workgroup per CU
 constexpr int WD_SLOT = 8192 + 16384;  // X (64 x 128 B) + 16 fp8 image groups (1 KiB each)
 constexpr int WD_SLAB = 64 * 256 + 64;  // split-K partial tile + row sums of squares
+// W8 = false: the same workgroup over ROW-MAJOR bf16 weights (serving / rollout decode at 16 < M <=
+// 64): each wave stages its 32 weight rows x 128 B per K-step with four 16-B LDS-DMAs per lane
+// (swizzled like X), one 40-KiB slot per K-step, 4 slots = the whole 160 KiB (3 K-steps, 120 KiB,
+// in flight). X is read from L2 N / 256 times — the 64-column ring (gemm_m64_kernel) reads it
+// N / 64 times, as many bytes again as the weights at M = 64.
+constexpr int WB_SLOTS = 4;
+constexpr int WB_SLOT = 8192 + 32768;  // X (64 x 128 B) + 256 weight rows x 128 B
 
-template <bool OUT_F32>
+template <bool OUT_F32, bool W8 = true>
 __global__ __launch_bounds__(512, 1) void gemm_w8_wide_kernel(GemmArgs p, float* __restrict__ slabs, int split) {
-  __shared__ __attribute__((aligned(16))) char smem[WD_SLOTS * WD_SLOT];  // the only __shared__ object
+  constexpr int SLOTS = W8 ? WD_SLOTS : WB_SLOTS, SLOT = W8 ? WD_SLOT : WB_SLOT;
+  constexpr int PER = W8 ? 3 : 5;  // LDS-DMAs per lane per K-step
+  __shared__ __attribute__((aligned(16))) char smem[SLOTS * SLOT];  // the only __shared__ object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int frow = lane & 15, fq = lane >> 4;
@@ -814,16 +823,34 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_wide_kernel(GemmArgs p, float*
   const long gstride = (long)(p.K / 128) * 2048;  // bytes per image group
   const char* wsrc0 = (const char*)p.B + (long)group_of(0) * gstride + lane * 16;
   const char* wsrc1 = (const char*)p.B + (long)group_of(1) * gstride + lane * 16;
+  // bf16 row-major: instruction q stages local weight rows 32 wid + 16 (q >> 1) + 8 (q & 1) + lane / 8
+  // (group group_of(q >> 1)), 16-B slot lane % 8 holding k-chunk slot ^ lds_swz(local row)
+  const bf16_t* wrow[4];
+  if constexpr (!W8) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 8 * (q & 1) + (lane >> 3);
+      const int lr = 32 * wid + 16 * (q >> 1) + r;
+      wrow[q] = p.B + (long)(group_of(q >> 1) * 16 + r) * p.ldb + ((lane & 7) ^ lds_swz(lr)) * 8;
+    }
+  }
   const int xr = wid * 8 + (lane >> 3);  // X row this lane stages
   const int xck = (lane & 7) ^ lds_swz(xr);
   const bf16_t* xsrc = p.A + (long)min(xr, p.M - 1) * p.lda + xck * 8;
 
   auto stage = [&](int t) {
-    char* slot = smem + ((t - t0) % WD_SLOTS) * WD_SLOT;
+    char* slot = smem + ((t - t0) % SLOTS) * SLOT;
     __builtin_amdgcn_global_load_lds((const void*)(xsrc + (long)t * 64), (lds_void*)(slot + wid * 1024), 16, 0, 0);
-    const long woff = (long)(t >> 1) * 2048 + (t & 1) * 1024;
-    __builtin_amdgcn_global_load_lds((const void*)(wsrc0 + woff), (lds_void*)(slot + 8192 + (2 * wid) * 1024), 16, 0, 2);
-    __builtin_amdgcn_global_load_lds((const void*)(wsrc1 + woff), (lds_void*)(slot + 8192 + (2 * wid + 1) * 1024), 16, 0, 2);
+    if constexpr (W8) {
+      const long woff = (long)(t >> 1) * 2048 + (t & 1) * 1024;
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc0 + woff), (lds_void*)(slot + 8192 + (2 * wid) * 1024), 16, 0, 2);
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc1 + woff), (lds_void*)(slot + 8192 + (2 * wid + 1) * 1024), 16, 0, 2);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_global_load_lds((const void*)(wrow[q] + (long)t * 64),
+                                         (lds_void*)(slot + 8192 + (32 * wid + 8 * q) * 128), 16, 0, 0);
+    }
   };
 
   // SWAP: the weight fragment is the MFMA's A operand, so acc[rr][j][r] = C[X row 16 rr + frow]
@@ -836,25 +863,35 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_wide_kernel(GemmArgs p, float*
   float sq[4] = {0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
-  for (int i = 0; i < WD_SLOTS - 1; ++i)
+  for (int i = 0; i < SLOTS - 1; ++i)
     if (i < nt) stage(t0 + i);
   for (int i = 0; i < nt; ++i) {
-    // retire step i (3 LDS-DMAs per lane per step); the later staged steps stay in flight
-    const int ahead = min(WD_SLOTS - 2, nt - 1 - i);
-    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    // retire step i (PER LDS-DMAs per lane per step); the later staged steps stay in flight
+    const int ahead = min(SLOTS - 2, nt - 1 - i);
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * PER) : "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
-    if (i + WD_SLOTS - 1 < nt) stage(t0 + i + WD_SLOTS - 1);  // the slot every wave finished reading
-    const char* slot = smem + (i % WD_SLOTS) * WD_SLOT;
-    rt_u32x2 w8[4];  // [j * 2 + kk]: row frow, k [32 kk + 8 fq, +8) of group 2 wid + j
-    ds_read_b64_x4_512(lds_addr(slot + 8192 + (2 * wid) * 1024 + ((fq >> 1) * 16 + frow) * 16 + (fq & 1) * 8), w8);
+    if (i + SLOTS - 1 < nt) stage(t0 + i + SLOTS - 1);  // the slot every wave finished reading
+    const char* slot = smem + (i % SLOTS) * SLOT;
     bf16x8 b[2][2], a[4][2];
+    if constexpr (W8) {
+      rt_u32x2 w8[4];  // [j * 2 + kk]: row frow, k [32 kk + 8 fq, +8) of group 2 wid + j
+      ds_read_b64_x4_512(lds_addr(slot + 8192 + (2 * wid) * 1024 + ((fq >> 1) * 16 + frow) * 16 + (fq & 1) * 8), w8);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) b[j][kk] = fp8x8_to_bf16(w8[2 * j + kk][0], w8[2 * j + kk][1]);
+        for (int kk = 0; kk < 2; ++kk) b[j][kk] = fp8x8_to_bf16(w8[2 * j + kk][0], w8[2 * j + kk][1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int lr = 32 * wid + 16 * j + frow;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          b[j][kk] = *(const bf16x8*)(slot + 8192 + lr * 128 + (((kk * 4 + fq) ^ lds_swz(lr)) << 4));
+      }
+    }
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int row = rr * 16 + frow;
@@ -915,7 +952,8 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_wide_kernel(GemmArgs p, float*
   // ---- epilogue from registers: row 16 rr + frow, 4 consecutive columns per fragment ----
   if (pair) {
     const int col = 16 * (8 * cg + wid) + 4 * fq;  // first of 4 F-columns
-    const float4 sg = *(const float4*)(p.sb + col), su = *(const float4*)(p.sb + F + col);
+    const float4 one4 = make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 sg = W8 ? *(const float4*)(p.sb + col) : one4, su = W8 ? *(const float4*)(p.sb + F + col) : one4;
     const float sgv[4] = {sg.x, sg.y, sg.z, sg.w}, suv[4] = {su.x, su.y, su.z, su.w};
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
@@ -938,7 +976,7 @@ __global__ __launch_bounds__(512, 1) void gemm_w8_wide_kernel(GemmArgs p, float*
   for (int j = 0; j < 2; ++j) {
     const int col = 16 * (16 * cg + 2 * wid + j) + 4 * fq;
     if (col >= p.N) continue;
-    const float4 sc4 = *(const float4*)(p.sb + col);
+    const float4 sc4 = W8 ? *(const float4*)(p.sb + col) : make_float4(1.f, 1.f, 1.f, 1.f);
     const float scv[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
@@ -1000,11 +1038,11 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(GemmArgs p, const floa
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     if (pair) {
-      float gt = gv[r] * rs * p.sb[col + r], up = uv[r] * rs * p.sb[F + col + r];
+      float gt = gv[r] * rs * (p.sb ? p.sb[col + r] : 1.f), up = uv[r] * rs * (p.sb ? p.sb[F + col + r] : 1.f);
       if (p.bias) { gt += bf2f(p.bias[col + r]); up += bf2f(p.bias[F + col + r]); }
       y[r] = gt / (1.f + __expf(-gt)) * up;
     } else {
-      float v = gv[r] * rs * p.sb[col + r];
+      float v = gv[r] * rs * (p.sb ? p.sb[col + r] : 1.f);
       if (p.bias) v += bf2f(p.bias[col + r]);
       y[r] = apply_act(v, p.act);
       if (p.R) y[r] += bf2f(p.R[(long)row * p.ldr + col + r]);
@@ -1130,7 +1168,25 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   if (wshuf && (M > 64 || N % 16 != 0 || K % 64 != 0)) return -4;  // shuffled weights: decode kernel only
   if (act == ACT_SWIGLU && (M > 64 || N % 64 != 0 || (U && UB))) return -2;
   if (M > 64) return -5;  // token-parallel GEMMs: rt_gemm_big
-  if (M > 16 && M <= 64 && p.Rp == 0 && !wshuf) {
+  if (M > 16 && M <= 64 && p.Rp == 0 && !wshuf && tuning().m64_wide && act != ACT_SWIGLU && N % 256 == 0 &&
+      K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && (!R || ldr % 4 == 0)) {
+    // 256 weight rows per workgroup over the row-major weights (X from L2 N / 256 times). Cold-weight
+    // probe at M = 24..64 (profiles/r6/m64_wide_probe.log): qkv 24 -> 17-19 us, o 18-19 -> 13-15,
+    // down 32-37 -> 28-31 vs the 64-column ring; the SwiGLU gate / up (112 groups: split 2 + reduce)
+    // stays on the ring (51-54 vs 58-65 us)
+    int split = slabs ? fit_split(wide_split(N, K), N / 256, WD_SLAB) : 1;
+    split = std::min(split, std::max(1, K / 64));
+    dim3 grid((N / 256) * split), block(512);
+    if (out_f32) hipLaunchKernelGGL((gemm_w8_wide_kernel<true, false>), grid, block, 0, stream, p, slabs, split);
+    else hipLaunchKernelGGL((gemm_w8_wide_kernel<false, false>), grid, block, 0, stream, p, slabs, split);
+    if (split > 1) {
+      const long work = (long)M * (act == ACT_SWIGLU ? N / 2 : N) / 4;
+      if (out_f32) hipLaunchKernelGGL((wide_reduce_kernel<true>), dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream,
+                                      p, slabs, split);
+      else hipLaunchKernelGGL((wide_reduce_kernel<false>), dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream,
+                              p, slabs, split);
+    }
+  } else if (M > 16 && M <= 64 && p.Rp == 0 && !wshuf) {
     const int split = (slabs && tickets) ? fit_split(m64_split(N, K), (N + 63) / 64, 64 * 64 + 64) : 1;
     dim3 grid(((N + 63) / 64) * split), block(256);
     if (out_f32) hipLaunchKernelGGL((gemm_m64_kernel<true>), grid, block, 0, stream, p, slabs, tickets, split);

@@ -205,13 +205,15 @@ class CausalLM(nn.Module):
         self._rope = None
         self._head_shuf = None  # ShufCache of the LM head for decode at batch <= 16
         # decode steps run the fused 4-GEMM layer (norms folded into GEMMs, residual epilogues) up to
-        # this batch: bf16 on the no-split tile-ordered GEMVs (M <= 16); above it the bf16 decode
-        # layer uses the token-parallel 256x128 split-K GEMMs with the split-K partials summed inside
-        # the norm and attention-prologue kernels (``defer_splitk``). With fp8 weights (config 5)
-        # the fused layer runs up to batch 64: W8A16 tile-ordered GEMVs to 16 rows, then the fp8
-        # LDS-DMA ring with the same folded-norm / SwiGLU / residual epilogues
+        # this batch: bf16 on the no-split tile-ordered GEMVs (M <= 16), then (17..64, serving) on
+        # the 256-row wide kernel / 64-column LDS-DMA ring with the in-GEMM RMS norm — 3 % faster
+        # decode steps than separate norm kernels (profiles/r6/decode_fused_max_ab.log); above it the
+        # bf16 decode layer uses the token-parallel 256x128 split-K GEMMs with the split-K partials
+        # summed inside the norm and attention-prologue kernels (``defer_splitk``). With fp8 weights
+        # (config 5) the same up to batch 64: W8A16 tile-ordered GEMVs to 16 rows, then the fp8
+        # LDS-DMA kernels with the same folded-norm / SwiGLU / residual epilogues
         self.fused_decode = True
-        self.fused_decode_max_batch = 16
+        self.fused_decode_max_batch = 64
         self.fused_decode_max_batch_fp8 = 64
         # decode at batch > 64: leave split-K partials for the consumer kernels to sum
         self.defer_splitk = True

@@ -87,10 +87,11 @@ def gemm(x: torch.Tensor, w: torch.Tensor, u=None, ub=None, bias=None, act=0, ou
                 and (residual is None or not out_f32):
             return native().gemm_big(x, w, ROW, ROW, u, ub, bias, act, 1 if out_f32 else 0, 1, out, None, residual, 0)
         # 32 <= M <= 64 on narrow weights (qkv / o): the 256x128-tile split-K form beats the ring
-        # kernel by 2-4 us (profiles/gemm_r2_m32_m64_ring_vs_splitk.log); wide / deep weights and
-        # M < 32 stay on the weight-streaming ring / GEMV kernels
+        # kernel by 2-4 us (profiles/gemm_r2_m32_m64_ring_vs_splitk.log), and the 256-row wide kernel
+        # beats both where it applies (N % 256 == 0: qkv 22.4 -> 19.0, o 18.2 -> 15.4 us at M = 64,
+        # profiles/r6/m64_wide_probe.log); wide / deep weights and M < 32 stay on the native kernels
         narrow_split = 32 <= M <= 64 and N <= 8192 and K <= 8192 and N % 16 == 0 and act == 0 and u is None \
-            and not out_f32 and bias is None and residual is None and nsplit == 0
+            and not out_f32 and bias is None and residual is None and nsplit == 0 and (N % 256 or K % 64)
         if M <= 64 and residual is None and N % 8 == 0 and not narrow_split:
             return native().gemm(x, w, u, ub, bias, act, out_f32, out)
         s, bn = splitk_plan(M, N, K, act)

@@ -895,14 +895,16 @@ def test_gemm_decode_norm_residual(M, N, K):
     _close(ops.gemm_decode(x, wf, residual=res, norm_eps=1e-5, fp8=c8), yr8)
 
 
+@pytest.mark.parametrize("wide", [0, 1])
 @pytest.mark.parametrize("M,N,K,split", [(64, 6144, 4096, 0), (64, 4096, 14336, 8), (33, 28672, 4096, 1),
                                          (64, 4096, 4096, 4), (17, 1152, 384, 0), (64, 32000, 4096, 2),
                                          (48, 4096, 512, 3)])
-def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split):
-    """16 < M <= 64 ring kernel with every split-K and epilogue (plain, in-GEMM RMS norm, residual,
-    SwiGLU pair) against fp32 references; tickets re-arm across launches."""
+def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split, wide):
+    """16 < M <= 64 kernels — the 64-column ring (wide = 0) and the 256-row wide kernel over
+    row-major weights (wide = 1, N % 256 == 0) — with every split-K and epilogue (plain, fp32 out,
+    in-GEMM RMS norm, residual, SwiGLU pair) against fp32 references; tickets re-arm across launches."""
     C = ops.native()
-    C.set_tuning({"m64_split": split})
+    C.set_tuning({"m64_split": split, "m64_wide": wide, "wide_split": split})
     try:
         torch.manual_seed(M + N + K)
         x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2
@@ -911,6 +913,8 @@ def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split):
         yr = x.float() @ w.float().t()
         for _ in range(2):
             _close(ops.gemm(x, w), yr)
+            _close(C.gemm(x, w, None, None, None, 0, False, None), yr)
+        _close(C.gemm(x, w, None, None, None, 0, True, None), yr, rtol=1e-4, atol=1e-3)
         rstd = torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
         _close(ops.gemm_decode(x, w, residual=res, norm_eps=1e-5), yr * rstd + res.float())
         if N % 64 == 0:
@@ -918,7 +922,7 @@ def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split):
             g, u = (x.float() * rstd) @ w[:F].float().t(), (x.float() * rstd) @ w[F:].float().t()
             _close(ops.gemm_decode(x, w, act=ops.ACT_SWIGLU, norm_eps=1e-5), torch.nn.functional.silu(g) * u)
     finally:
-        C.set_tuning({"m64_split": 0})
+        C.set_tuning({"m64_split": 0, "m64_wide": 1, "wide_split": 0})
 
 
 @pytest.mark.parametrize("kl", [None, 0.05])

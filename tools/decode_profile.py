@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--depths", default="0", help="M<=16 GEMM weight-pipeline depths to A/B (0 = auto)")
     ap.add_argument("--iters", type=int, default=3, help="generations per depth")
     ap.add_argument("--no-graph", action="store_true", help="eager decode steps (counter collection)")
+    ap.add_argument("--fused-max", type=int, default=-1, help="bf16 fused decode layer up to this batch (-1: model default)")
     a = ap.parse_args()
     from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
     from rag_tl_domainllm_optimizer_amd.models import build_model
@@ -33,6 +34,8 @@ def main():
         m.add_lora(16, 32.0, "all")
     if a.fp8:
         m.set_fp8(True)
+    if a.fused_max >= 0:
+        m.fused_decode_max_batch = a.fused_max
     g = torch.Generator().manual_seed(0)
     prompts = [torch.randint(5, m.cfg.vocab_size, (a.prompt - (i % 7) * 3,), generator=g).tolist()
                for i in range(a.batch)]
