@@ -104,6 +104,7 @@ struct TuningField {
   float rt::Tuning::*f;
 };
 static const TuningField kTuningFields[] = {
+    {"decode_mw_bh", &rt::Tuning::decode_mw_bh, nullptr},
     {"decode_mw_kpp", &rt::Tuning::decode_mw_kpp, nullptr},
     {"decode_mw_smax", &rt::Tuning::decode_mw_smax, nullptr},
     {"attn_fwd_hp_maxs", &rt::Tuning::attn_fwd_hp_maxs, nullptr},

@@ -14,6 +14,10 @@ namespace rt {
 
 struct Tuning {
   // ---- decode attention (attention.hip) ----
+  int decode_mw_bh = 320;     // (batch x kv heads) below which decode attention runs multi-wave workgroups:
+                              // 8 waves per (row, kv head) below 256, 4 waves from 256 up to this bound
+                              // (decode step at batch 32 4.35 -> 4.20 ms; at 48 / 64 / 96 the one-wave
+                              // kernel is 2-9 % faster: profiles/r6/decode_attn_4wave_ab.log)
   int decode_mw_kpp = 512;    // keys per partition of the 8-wave small-batch kernel past decode_mw_smax cache slots
   int decode_mw_smax = 1024;  // cache slots up to which it runs one partition per kv head (fewer: measured slower
                               // at 456 slots, profiles/r5/decode_b1_deferred_partition_merge.log)

@@ -1992,7 +1992,7 @@ extern "C" int rt_attn_decode_fused_ps(int D, int nk) { return 4 * (64 / (D / 8)
 constexpr int DEC_MW = 8;
 static bool rt_attn_decode_mw_ok(int B, int Hq, int Hkv, int D, int Smax) {
   const int G = Hkv ? Hq / Hkv : 0;
-  return D == 128 && (long)B * Hkv < 256 && (G == 1 || G == 2 || G == 4 || G == 8);
+  return D == 128 && (long)B * Hkv < std::max(256, tuning().decode_mw_bh) && (G == 1 || G == 2 || G == 4 || G == 8);
 }
 static int rt_attn_decode_mw_np(int Smax, int np_ws) {
   const int kpp = std::max(16, tuning().decode_mw_kpp);
@@ -2001,7 +2001,8 @@ static int rt_attn_decode_mw_np(int Smax, int np_ws) {
 }
 extern "C" int rt_attn_decode_mfma_ok(int B, int Hq, int Hkv, int D, int NP) {
   const int G = Hkv ? Hq / Hkv : 0;
-  return NP == 1 && D == 128 && (long)B * Hkv >= 256 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
+  return NP == 1 && D == 128 && (long)B * Hkv >= std::max(256, tuning().decode_mw_bh) &&
+         (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
 }
 
 // Prompt K / V (rows [b * S + s] of the rotated qkv) -> fp8 cache slots [0, S): one 16-lane group
@@ -2125,12 +2126,24 @@ extern "C" int rt_attn_decode_fused(const void* qkv, long ldq, void* kc, void* v
     const int npm = rt_attn_decode_mw_np(Smax, NP);
     a.NP = npm;
     a.PS = npm > 1 ? ((Smax + npm - 1) / npm + 15) / 16 * 16 : Smax;
-    dim3 mgrid((unsigned)(B * Hkv * npm)), mblock(64 * DEC_MW);
-    switch (G) {
-      case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, DEC_MW>), mgrid, mblock, 0, stream, a); break;
-      case 2: hipLaunchKernelGGL((attn_decode_mfma_kernel<2, DEC_MW>), mgrid, mblock, 0, stream, a); break;
-      case 4: hipLaunchKernelGGL((attn_decode_mfma_kernel<4, DEC_MW>), mgrid, mblock, 0, stream, a); break;
-      default: hipLaunchKernelGGL((attn_decode_mfma_kernel<8, DEC_MW>), mgrid, mblock, 0, stream, a); break;
+    // 8 waves per (row, kv head) up to 256 pairs (one 512-thread workgroup per CU); 4 waves above
+    // (serving at batch 32..127: 1024-2048 waves instead of one chain of tiles per pair)
+    const bool w4 = (long)B * Hkv >= 256;
+    dim3 mgrid((unsigned)(B * Hkv * npm)), mblock(64 * (w4 ? 4 : DEC_MW));
+    if (w4) {
+      switch (G) {
+        case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, 4>), mgrid, mblock, 0, stream, a); break;
+        case 2: hipLaunchKernelGGL((attn_decode_mfma_kernel<2, 4>), mgrid, mblock, 0, stream, a); break;
+        case 4: hipLaunchKernelGGL((attn_decode_mfma_kernel<4, 4>), mgrid, mblock, 0, stream, a); break;
+        default: hipLaunchKernelGGL((attn_decode_mfma_kernel<8, 4>), mgrid, mblock, 0, stream, a); break;
+      }
+    } else {
+      switch (G) {
+        case 1: hipLaunchKernelGGL((attn_decode_mfma_kernel<1, DEC_MW>), mgrid, mblock, 0, stream, a); break;
+        case 2: hipLaunchKernelGGL((attn_decode_mfma_kernel<2, DEC_MW>), mgrid, mblock, 0, stream, a); break;
+        case 4: hipLaunchKernelGGL((attn_decode_mfma_kernel<4, DEC_MW>), mgrid, mblock, 0, stream, a); break;
+        default: hipLaunchKernelGGL((attn_decode_mfma_kernel<8, DEC_MW>), mgrid, mblock, 0, stream, a); break;
+      }
     }
     RT_LAUNCH_CHECK();
     return 0;

@@ -24,11 +24,16 @@ def main():
     ap.add_argument("--iters", type=int, default=3, help="generations per depth")
     ap.add_argument("--no-graph", action="store_true", help="eager decode steps (counter collection)")
     ap.add_argument("--fused-max", type=int, default=-1, help="bf16 fused decode layer up to this batch (-1: model default)")
+    ap.add_argument("--set", default="", help="native tuning knobs for the run, k=v[,k=v]")
     a = ap.parse_args()
     from rag_tl_domainllm_optimizer_amd.generation import Generator, SamplingParams
     from rag_tl_domainllm_optimizer_amd.models import build_model
 
     dev = torch.device("cuda")
+    if a.set:
+        from rag_tl_domainllm_optimizer_amd import ops as _ops
+
+        _ops.native().set_tuning({k: int(v) for k, v in (kv.split("=") for kv in a.set.split(","))})
     m = build_model(a.model, device=dev, dtype=torch.bfloat16, seed=0, fast_init=True)
     if not a.no_lora:
         m.add_lora(16, 32.0, "all")
