@@ -42,7 +42,7 @@ struct Tuning {
   int decode_depth = 0;       // force weight-pipeline depth (2 / 4) of the M <= 16 decode kernel
   int m64_split = 0;          // force split-K of the 16 < M <= 64 ring kernel
   int wide_split = 0;         // force split-K of the wide W8A16 kernel
-  int m64_wide = 1;           // bf16 16 < M <= 64, N % 256 == 0, no SwiGLU: 256 weight rows per workgroup
+  int m64_wide = 1;           // bf16 16 < M <= 64, N % 256 == 0, N <= 16384, no SwiGLU: 256 weight rows per workgroup
                               // (the wide kernel over row-major weights); 0: the 64-column ring gemm_m64_kernel
   // ---- token-parallel GEMMs (gemm_big.hip) ----
   float gemm_bn128_cost = 0.55f;  // planner: time of a 256x128 tile / a 256x256 tile

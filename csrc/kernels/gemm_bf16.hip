@@ -1169,11 +1169,11 @@ extern "C" int rt_gemm_nt(const void* A, long lda, const void* B, long ldb, cons
   if (act == ACT_SWIGLU && (M > 64 || N % 64 != 0 || (U && UB))) return -2;
   if (M > 64) return -5;  // token-parallel GEMMs: rt_gemm_big
   if (M > 16 && M <= 64 && p.Rp == 0 && !wshuf && tuning().m64_wide && act != ACT_SWIGLU && N % 256 == 0 &&
-      K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && (!R || ldr % 4 == 0)) {
+      N <= 16384 && K % 64 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 && (!R || ldr % 4 == 0)) {
     // 256 weight rows per workgroup over the row-major weights (X from L2 N / 256 times). Cold-weight
     // probe at M = 24..64 (profiles/r6/m64_wide_probe.log): qkv 24 -> 17-19 us, o 18-19 -> 13-15,
-    // down 32-37 -> 28-31 vs the 64-column ring; the SwiGLU gate / up (112 groups: split 2 + reduce)
-    // stays on the ring (51-54 vs 58-65 us)
+    // down 32-37 -> 28-31 vs the 64-column ring. Wide outputs (>= 64 groups: split 2 + a reduce) stay
+    // on the ring: SwiGLU gate / up 51-54 vs 58-65 us, the LM head (N 32000) 58-60 vs 77-80 us
     int split = slabs ? fit_split(wide_split(N, K), N / 256, WD_SLAB) : 1;
     split = std::min(split, std::max(1, K / 64));
     dim3 grid((N / 256) * split), block(512);

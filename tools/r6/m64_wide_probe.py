@@ -31,8 +31,8 @@ def main():
     C = ops.native()
     dev = torch.device("cuda")
     shapes = [("qkv", 6144, 4096, 0), ("o", 4096, 4096, 0), ("gate_up", 28672, 4096, ops.ACT_SWIGLU),
-              ("down", 4096, 14336, 0)]
-    for M in (24, 32, 48, 64):
+              ("down", 4096, 14336, 0), ("lm_head", 32000, 4096, 0)]
+    for M in [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "24,32,48,64").split(",")]:
         x = torch.randn(M, 14336, device=dev).to(torch.bfloat16)
         tot = {"ring": 0.0, "wide": 0.0, "ops.gemm": 0.0}
         for name, N, K, act in shapes:
