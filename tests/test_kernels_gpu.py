@@ -898,7 +898,7 @@ def test_gemm_decode_norm_residual(M, N, K):
 @pytest.mark.parametrize("wide", [0, 1])
 @pytest.mark.parametrize("M,N,K,split", [(64, 6144, 4096, 0), (64, 4096, 14336, 8), (33, 28672, 4096, 1),
                                          (64, 4096, 4096, 4), (17, 1152, 384, 0), (64, 32000, 4096, 2),
-                                         (48, 4096, 512, 3)])
+                                         (48, 4096, 512, 3), (17, 4096, 1024, 0), (40, 6144, 4096, 8)])
 def test_m64_kernel_plain_norm_residual_swiglu(M, N, K, split, wide):
     """16 < M <= 64 kernels — the 64-column ring (wide = 0) and the 256-row wide kernel over
     row-major weights (wide = 1, N % 256 == 0) — with every split-K and epilogue (plain, fp32 out,
