@@ -73,27 +73,17 @@ def main():
                 "lib_nt": lambda: torch.matmul(x, w.t()),
                 "nt256": lambda: ops.gemm_big(x, w, 0, 0, bn=256),
                 "nt128": lambda: ops.gemm_big(x, w, 0, 0, bn=128),
-                "w4_192": lambda: ops.gemm_big(x, w, 0, 0, bn=3),
-                "w4_256": lambda: ops.gemm_big(x, w, 0, 0, bn=4),
                 "nn256": lambda: ops.gemm_big(dy, w, 0, 1, bn=256),
                 "nn128": lambda: ops.gemm_big(dy, w, 0, 1, bn=128),
                 "nn_lora256": lambda: ops.gemm_big(dy, w, 0, 1, du, ap_, bn=256),
                 "nn": lambda: ops.gemm_big(dy, w, 0, 1),
                 "nn_lora": lambda: ops.gemm_big(dy, w, 0, 1, du, ap_),
                 "lib_nn": lambda: torch.matmul(dy, w),
-                # stream-K tail off (the wave planner alone) / forced
-                "nt_nosk": tuned(lambda: ops.gemm_big(x, w, 0, 0), gemm_streamk=0),
-                "nn_nosk": tuned(lambda: ops.gemm_big(dy, w, 0, 1), gemm_streamk=0),
-                "nt_sk": tuned(lambda: ops.gemm_big(x, w, 0, 0), gemm_streamk=2),
-                "nn_sk": tuned(lambda: ops.gemm_big(dy, w, 0, 1), gemm_streamk=2),
             }
             if name == "gate_up":
                 cases["nt_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5)
-                cases["nt_swiglu_nosk"] = tuned(lambda: ops.gemm_big(x, w, 0, 0, act=5), gemm_streamk=0)
             if name == "gate_up":
                 cases["nt128_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5, bn=128)
-                cases["w4_192_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5, bn=3)
-                cases["w4_256_swiglu"] = lambda: ops.gemm_big(x, w, 0, 0, act=5, bn=4)
             for sp in (1, 2, 4, 5, 8, 12, 16):
                 cases[f"split{sp}"] = (lambda sp=sp: ops.gemm(x, w, nsplit=sp))
                 if name == "gate_up":
