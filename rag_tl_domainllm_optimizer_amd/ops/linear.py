@@ -341,12 +341,16 @@ def _tn_slabs(a: torch.Tensor, b: torch.Tensor, key):
     split-K slabs [ns, P, Q] in a cached workspace: every token split stores its partial tile with
     plain stores and the consumer sums the ns slabs in a fixed order — bitwise reproducible, unlike
     the fp32 atomics of gemm_tn (partials added in arrival order). Same tiles and token splits as
-    gemm_tn (profiles/r5/lora_narrow_split_sweep.log). Returns (slabs [ns * P, Q], ns)."""
+    gemm_tn's tiles. Returns (slabs [ns * P, Q], ns)."""
     T, P = a.shape
     Q = b.shape[1]
     bm = 128 if P >= 16384 else 64
-    tiles = ((P + bm - 1) // bm) * ((Q + 63) // 64)
-    ns = max(1, min(T // 256, 4 if tiles <= 64 else 8))
+    # token splits re-swept with slabs (no atomic cost; profiles/r6/lora_narrow_sweep.log, 9632
+    # tokens): 8 on the 64x64-tile products (dA at K = 4096, dB of o / down: 19.4 -> 17.8 us), 2 on
+    # the 128x64-tile dB of gate_up (130.9 -> 118.5 us: its 224 tiles fill the chip; 8 slabs of
+    # 7.3 MB each were the cost). Whole PPO step: same within noise (update 2.137-2.140 vs 2.138-2.145
+    # s, same box, profiles/r6/bench_lora_slab_splits_ab.log)
+    ns = max(1, min(T // 256, 2 if bm == 128 else 8))
     ws = _workspace(key, ns * P * Q, a.device).view(ns * P, Q)
     native().gemm_small(a, b, KMAJ, KMAJ, 3, ns, ws, bm)
     return ws, ns
@@ -375,6 +379,8 @@ def _narrow(a: torch.Tensor, b: torch.Tensor, lb: int, nsplit: int = 0) -> torch
     # us, K = 14336 78.0 -> 73.8 us at 9632 tokens (profiles/r5/lora_narrow_split_sweep.log, atomic
     # form). The backward dU (KMAJ adapter image) splits the same way into slabs.
     auto = min(3, max(1, K // 512)) if lb == ROW else max(1, min(K // 512, (768 + tiles - 1) // tiles))
+    if lb == KMAJ and bm == 128:
+        auto = min(auto, 6)  # dU of gate_up (K = 28672): 6 slabs 115 vs 11 at 127-129 us (lora_narrow_sweep.log)
     ns = nsplit or auto
     if ns == 1:
         return native().gemm_small(a, b, ROW, lb, 0, 1, None, bm)

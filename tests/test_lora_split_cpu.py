@@ -48,16 +48,17 @@ def test_forward_u_splits_into_slabs(monkeypatch):
     # the backward dU = dY UB (KMAJ adapter image [N, Rp]): slabs too, ~3 workgroups per CU
     calls = _run(monkeypatch, lambda: L._narrow(torch.zeros(9632, 28672, dtype=torch.bfloat16),
                                                 torch.zeros(28672, 64, dtype=torch.bfloat16), L.KMAJ))
-    assert calls == [(L.ROW, L.KMAJ, 3, 11, 128)], calls
+    assert calls == [(L.ROW, L.KMAJ, 3, 6, 128)], calls
 
 
 def test_backward_tn_products_into_slabs(monkeypatch):
     """dA_all = dU^T X and dB_all = dY^T U of the LoRA backward: token-split fp32 slabs (out mode 3,
-    KMAJ x KMAJ) in a cached workspace, same tiles / splits as the atomic gemm_tn form."""
+    KMAJ x KMAJ) in a cached workspace, gemm_tn's tiles; 8 splits on 64x64 tiles, 2 on the 128x64
+    tiles of gate_up's dB (profiles/r6/lora_narrow_sweep.log)."""
     T = 9632
     du = torch.zeros(T, 64, dtype=torch.bfloat16)
-    for a, b, ns, bm in ((du, torch.zeros(T, 4096, dtype=torch.bfloat16), 4, 64),
-                         (torch.zeros(T, 28672, dtype=torch.bfloat16), du, 8, 128)):
+    for a, b, ns, bm in ((du, torch.zeros(T, 4096, dtype=torch.bfloat16), 8, 64),
+                         (torch.zeros(T, 28672, dtype=torch.bfloat16), du, 2, 128)):
         out = []
         calls = _run(monkeypatch, lambda: out.append(L._tn_slabs(a, b, ("t", a.shape[1], b.shape[1]))))
         assert calls == [(L.KMAJ, L.KMAJ, 3, ns, bm)], calls
