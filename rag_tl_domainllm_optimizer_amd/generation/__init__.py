@@ -318,7 +318,7 @@ class Generator:
         h_last = self.model.prefill(ids, self.kv_start[:B], sub, packed=packed) if packed is not None else \
             self.model.prefill(ids, self.kv_start[:B], sub)
         if hasattr(self.model, "refresh_decode_weights"):
-            self.model.refresh_decode_weights()  # merged / folded / fp8 images used by graph replays
+            self.model.refresh_decode_weights(self._bucket(B))  # folded / tile-ordered / fp8 images of graph replays
         self._nb = self._bucket(B)
         h = torch.zeros(self._nb, cfg.hidden_size, dtype=h_last.dtype, device=dev)
         h[:B] = h_last
@@ -563,7 +563,7 @@ class ContinuousBatcher:
         g._nb = 1
         self._prev_merged = g.model.set_lora_merged(g.merge_lora) if hasattr(g.model, "set_lora_merged") else None
         if hasattr(g.model, "refresh_decode_weights"):
-            g.model.refresh_decode_weights()
+            g.model.refresh_decode_weights(MB)
         if T > 1:
             g._ensure_graph(params, self.eos, self.eos_list, pad_id, T)  # captured while no row is active
         self.rows = {}  # row -> (tag, prompt_len, steps at admission)

@@ -451,7 +451,16 @@ class CausalLM(nn.Module):
                 g.use_merged = on
         return prev
 
-    def refresh_decode_weights(self):
+    def refresh_decode_weights(self, batch: Optional[int] = None):
+        """Eagerly refresh the images the fused decode layer's graph replays read (norm-folded /
+        tile-ordered / fp8 weights). ``batch``: the decode batch about to run — above the fused
+        layer's limit none of them is read, so batch-256 rollouts skip the refresh (a later
+        small-batch generation refreshes them before its replays). Same-box A/B: within noise
+        (profiles/r6/bench_decode_refresh_gating_ab.log)."""
+        if batch is not None:
+            fp8 = bool(self.layers) and self.layers[0].fp8_enabled
+            if batch > (self.fused_decode_max_batch_fp8 if fp8 else self.fused_decode_max_batch):
+                return
         if self.fused_decode:
             for layer in self.layers:
                 layer.refresh_decode_weights()
