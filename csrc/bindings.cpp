@@ -105,6 +105,7 @@ struct TuningField {
 };
 static const TuningField kTuningFields[] = {
     {"decode_mw_bh", &rt::Tuning::decode_mw_bh, nullptr},
+    {"attn_lpt", &rt::Tuning::attn_lpt, nullptr},
     {"decode_mw_kpp", &rt::Tuning::decode_mw_kpp, nullptr},
     {"decode_mw_smax", &rt::Tuning::decode_mw_smax, nullptr},
     {"attn_fwd_hp_maxs", &rt::Tuning::attn_fwd_hp_maxs, nullptr},

@@ -27,6 +27,8 @@ struct Tuning {
                                 // groupings); 0: always the 128-position tiles of one head
   int attn_dq_hp_maxs = 1024;   // causal GQA-4 backward dQ up to this many positions on head-packed 16-position
                                 // workgroups (0: 64 positions of one head)
+  int attn_lpt = 8192;          // causal forward / backward grids of at most this many workgroups dispatch their
+                                // heaviest tiles first within each XCD (attention.hip attn_block_xyz); 0: tile order
   // ---- norms (norm.hip) ----
   // threads per row of the split-K-slab norm (256, or 512 at H = 4096: 6.76 -> 6.56 us at batch 256,
   // profiles/r4/norm_slab_threads.log)

@@ -59,10 +59,36 @@ __device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
 // share a K / V head (the query tiles of the G query heads of one kv head, or a kv head's key
 // blocks) are consecutive in (x, y, z) order and land on ONE XCD's L2 instead of being dealt round
 // robin over all eight (each of which would fetch the K / V / Q tiles from memory again)
-__device__ __forceinline__ int3 attn_block_xyz() {
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int lin = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), nx * ny * gridDim.z);
-  return make_int3(lin % nx, (lin / nx) % ny, lin / (nx * ny));
+//
+// lpt != 0 (causal grids, tuning().attn_lpt): the same XCD gets the same set of workgroups, but
+// dispatches them heaviest first (longest-processing-time order): a causal tile's work grows with x
+// (lpt = 1: query tiles) or shrinks with it (lpt = 2: key blocks of the backward). With ~5
+// workgroups per slot and a 1:5 light:heavy spread, x-ascending order leaves the heavy tiles of the
+// last groups as the launch's tail. A bijection of the XCD's contiguous range [base, base + cnt):
+// dispatch position s walks the x values heaviest first, within one x the groups in order.
+__device__ __forceinline__ int3 attn_block_xyz(int lpt = 0) {
+  const int nx = gridDim.x, ny = gridDim.y, nwg = nx * ny * gridDim.z;
+  const int orig = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  if (lpt == 0 || nx == 1) {
+    const int lin = xcd_remap(orig, nwg);
+    return make_int3(lin % nx, (lin / nx) % ny, lin / (nx * ny));
+  }
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int end = base + (xcd < r ? q + 1 : q);
+  int s = orig / 8;  // dispatch position within the XCD
+  const int bmod = base % nx;
+  for (int i = 0; i < nx; ++i) {
+    const int v = lpt == 1 ? nx - 1 - i : i;
+    const int first = base + (v - bmod + nx) % nx;  // first lin >= base with lin % nx == v
+    const int c = first < end ? (end - 1 - first) / nx + 1 : 0;
+    if (s < c) {
+      const int lin = first + s * nx;
+      return make_int3(v, (lin / nx) % ny, lin / (nx * ny));
+    }
+    s -= c;
+  }
+  return make_int3(0, 0, 0);  // not reached: the counts over v sum to the range length
 }
 
 struct AttnArgs {
@@ -78,6 +104,7 @@ struct AttnArgs {
   int B, Sq, Sk, Hq, Hkv;
   int causal, window;
   float scale_log2;           // softmax scale * log2(e)
+  int lpt;                    // heaviest-first dispatch order (attn_block_xyz; causal grids)
 };
 
 // byte offset of 16-B chunk c of row r in a K-style (row-read) tile image
@@ -131,7 +158,7 @@ void attn_fwd_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int3 bx = attn_block_xyz();
+  const int3 bx = attn_block_xyz(a.lpt);
   const int b = bx.z;
   const int h = HP ? bx.y * 4 + wid : bx.y;
   const int hk = HP ? bx.y : h / (a.Hq / a.Hkv);
@@ -1546,6 +1573,7 @@ struct AttnBwdArgs {
   int causal, window;
   float scale_log2;            // scale * log2 e
   float scale;
+  int lpt;                     // heaviest-first dispatch order (attn_block_xyz; causal grids)
   // RoPE backward fused into the dQ / dK stores (null: none): q / k were rotated by angle row
   // rope_pos[b * S + s] of the [positions, D / 2] tables; dq / dk are inverse-rotated from their
   // bf16-rounded values with rope_qkv_kernel's arithmetic (sign -1): bitwise the separate pass
@@ -1606,7 +1634,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int3 bx = attn_block_xyz();
+  const int3 bx = attn_block_xyz(a.lpt ? 2 : 0);  // key blocks: the lowest sees the most queries
   const int b = bx.z, hk = bx.y;
   const int kb0 = bx.x * 64;
   const int G = a.Hq / a.Hkv;
@@ -1783,7 +1811,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   char* Vs = smem + TILE_BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int3 bx = attn_block_xyz();
+  const int3 bx = attn_block_xyz(a.lpt);
   const int b = bx.z;
   const int h = HP ? bx.y * 4 + wid : bx.y;
   const int hk = HP ? bx.y : h / (a.Hq / a.Hkv);
@@ -1921,6 +1949,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 
 using namespace rt;
 
+// heaviest-first dispatch (attn_block_xyz) on causal grids of at most tuning().attn_lpt workgroups
+// (32 per CU): at the PPO update's minibatch it trims the launch tail (profiles/r6/attn_lpt_ab.log:
+// forward -3..5 %, backward -7..9 %); on 4x larger grids (reference scoring, prefill) it was slower
+// (+1..7 %): consecutive workgroups of an XCD then span too many kv heads for its L2
+static int attn_lpt_on(dim3 grid, int causal) {
+  const long nwg = (long)grid.x * grid.y * grid.z;
+  return causal && grid.x > 1 && nwg <= tuning().attn_lpt ? 1 : 0;
+}
+
 extern "C" int rt_attn_fwd(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv, void* o, long ldo,
                            float* lse, const int* kv_start, const int* kv_len, const float* rel_bias, int rb_L, int B,
                            int Sq, int Sk, int Hq, int Hkv, int D, int causal, int window, float scale,
@@ -1930,11 +1967,13 @@ extern "C" int rt_attn_fwd(const void* q, long ldq, const void* k, long ldk, con
   a.o = (bf16_t*)o; a.ldo = ldo; a.lse = lse; a.kv_start = kv_start; a.kv_len = kv_len; a.rel_bias = rel_bias;
   a.rb_L = rb_L; a.B = B; a.Sq = Sq; a.Sk = Sk; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.window = window;
   a.scale_log2 = scale * 1.4426950408889634f;
+  a.lpt = 0;
   if (B == 0 || Sq == 0) return 0;
   // GQA (4 query heads per kv head), D = 128, short sequences: the head-packed 32-position tiles
   // (every wave of a workgroup on the same causal key range)
   if (D == 128 && Hkv * 4 == Hq && causal && Sq <= tuning().attn_fwd_hp_maxs && !rel_bias) {
     dim3 grid((Sq + 31) / 32, Hkv, B), block(256);
+    a.lpt = attn_lpt_on(grid, causal);
     hipLaunchKernelGGL((attn_fwd_kernel<128, 2, true>), grid, block, 0, stream, a);
     RT_LAUNCH_CHECK();
     return 0;
@@ -1942,11 +1981,13 @@ extern "C" int rt_attn_fwd(const void* q, long ldq, const void* k, long ldk, con
   // other head groupings (MHA), D = 128: 64-position tiles of one head (4 waves x 16 rows)
   if (D == 128 && causal && Sq <= tuning().attn_fwd_hp_maxs && !rel_bias) {
     dim3 grid((Sq + 63) / 64, Hq, B), block(256);
+    a.lpt = attn_lpt_on(grid, causal);
     hipLaunchKernelGGL((attn_fwd_kernel<128, 1, false, true>), grid, block, 0, stream, a);
     RT_LAUNCH_CHECK();
     return 0;
   }
   dim3 grid((Sq + 127) / 128, Hq, B), block(256);
+  a.lpt = attn_lpt_on(grid, causal);
   switch (D) {
     case 32: hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, block, 0, stream, a); break;
     case 64: hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, block, 0, stream, a); break;
@@ -2183,6 +2224,7 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
   a.dq = dq_f32; a.dk = (bf16_t*)dk; a.lddk = lddk; a.dv = (bf16_t*)dv; a.lddv = lddv; a.kv_start = kv_start;
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.causal = causal; a.window = window;
   a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
+  a.lpt = 0;
   if ((rope_pos != nullptr) != (rope_cos != nullptr) || (rope_cos != nullptr) != (rope_sin != nullptr)) return -2;
   a.rope_pos = rope_pos; a.rope_cos = rope_cos; a.rope_sin = rope_sin;
   if (B == 0 || S == 0) return 0;
@@ -2198,8 +2240,10 @@ extern "C" int rt_attn_bwd(const void* q, long ldq, const void* k, long ldk, con
 #define BWD_CASE(DD)                                                                              \
   hipLaunchKernelGGL(attn_bwd_pre_kernel<DD>, pgrid, dim3(256), 0, stream, a);                    \
   hipLaunchKernelGGL(attn_bwd_kernel<DD>, grid, dim3(256), 0, stream, a);
+  a.lpt = attn_lpt_on(grid, causal);
   if (D == 64) { BWD_CASE(64) } else { BWD_CASE(128) }
 #undef BWD_CASE
+  a.lpt = attn_lpt_on(qgrid, causal);
   if (D == 64) hipLaunchKernelGGL((attn_bwd_dq_kernel<64>), qgrid, dim3(256), 0, stream, a);
   else if (dq_hp) hipLaunchKernelGGL((attn_bwd_dq_kernel<128, true>), qgrid, dim3(256), 0, stream, a);
   else hipLaunchKernelGGL((attn_bwd_dq_kernel<128>), qgrid, dim3(256), 0, stream, a);

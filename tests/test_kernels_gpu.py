@@ -490,6 +490,39 @@ def test_flash_bwd_dq_head_packed_bitwise(S, window, left):
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("S,Hq,Hkv,D,window,left,hp", [(301, 32, 8, 128, 0, True, 1), (301, 32, 8, 128, 0, True, 0),
+                                                       (700, 32, 8, 128, 100, False, 1), (301, 12, 12, 64, 0, True, 1),
+                                                       (97, 8, 8, 128, 0, False, 1), (1100, 16, 4, 128, 0, True, 1)])
+def test_flash_heaviest_first_order_bitwise(S, Hq, Hkv, D, window, left, hp):
+    """attn_lpt (causal grids dispatch their heaviest tiles first within each XCD) only permutes
+    which workgroup runs when: forward output / LSE and every gradient are bitwise the tile-order
+    launch's, on the head-packed, 64-position, 128-position and D = 64 forms and both dQ forms."""
+    B = 3
+    torch.manual_seed(S + Hq + D + window)
+    qkv = _qkv(B, S, Hq, Hkv, D)
+    kv_start = torch.tensor([0, min(37, S - 1), 5], device=DEV, dtype=torch.int32) if left else None
+    go = torch.randn(B * S, Hq * D, device=DEV, dtype=torch.bfloat16)
+    maxs = 4096 if hp else 0
+    res = []
+    for lpt in (0, 1 << 30):  # tile order / heaviest first whatever the grid size
+        with ops.tuning(attn_lpt=lpt, attn_fwd_hp_maxs=maxs, attn_dq_hp_maxs=maxs):
+            x = qkv.clone().requires_grad_(True)
+            o = ops.flash_attention_qkv(x, B, S, Hq, Hkv, D, True, window, kv_start=kv_start)
+            (o.float() * go.float()).sum().backward()
+            res.append((o.detach().clone(), x.grad.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    # and the heaviest-first launch still matches the fp32 oracle
+    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    orf, _ = ref.attention(q, k, v, B, S, S, Hq, Hkv, D, True, window, None, kv_start, None, None, 0)
+    rows = torch.ones(B, S, dtype=torch.bool, device=DEV)
+    if kv_start is not None:
+        for b in range(B):
+            rows[b, :int(kv_start[b])] = False  # query rows left of a row's start are padding
+    rows = rows.reshape(-1)
+    _close(res[1][0][rows], orf[rows])
+
+
 @pytest.mark.parametrize("D,H", [(32, 12), (64, 12)])
 def test_encoder_attention_relbias(D, H):
     B, S = 3, 70
